@@ -1,0 +1,207 @@
+// Paged grouped-query attention for decode (and prefill expressed as per-token
+// causal decode), gfx950. SURVEY.md §2F attn_decode_paged.
+//
+// KV cache (one layer): k/v [num_slots][Hkv][D] bf16, slot = block_table[seq][pos / BS] * BS + pos % BS.
+// Grid: (tokens, Hkv, n_split). A workgroup handles the G = Hq/Hkv query heads that
+// share one KV head over one context chunk (split-K / flash-decoding), so a KV row
+// is read from HBM once per (token, kv head, chunk) and used by all G heads.
+// Lane map: D/8 lanes per key (16 B each = 8 dims), 64/(D/8) keys per wave in flight;
+// every lane group keeps its own online-softmax state (m, l, o) which the workgroup
+// merges through LDS at the end. With n_split > 1 unnormalised partials go to a
+// workspace and attn_combine merges them (log-sum-exp in base 2).
+#include "common.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_decode_kernel(
+    const __bf16* __restrict__ q, long ldq, const __bf16* __restrict__ kc, const __bf16* __restrict__ vc,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
+    const int* __restrict__ ctx_len, int Hkv, int bs, float scale, int chunk, int n_split,
+    __bf16* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml) {
+  constexpr int LPT = D / 8;          // lanes per key
+  constexpr int TPW = 64 / LPT;       // keys per wave per step
+  constexpr int NSTREAM = 4 * TPW;    // independent softmax streams per workgroup
+  const int t = blockIdx.x, kh = blockIdx.y, split = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int dl = lane % LPT, ts = lane / LPT;
+  const int stream = wave * TPW + ts;
+  const int Hq = Hkv * G;
+
+  const int ctx = ctx_len[t];
+  if (chunk <= 0) chunk = max(16, ((ctx + n_split - 1) / n_split + 15) / 16 * 16);   // balanced splits
+  const int start = split * chunk;
+  const int end = min(ctx, start + chunk);
+  const int* bt = block_tables + (size_t)tok_seq[t] * bt_stride;
+
+  // q for the G heads of this kv head, this lane's 8 dims, pre-scaled for exp2
+  float qf[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const u32x4 raw = ld16(q + (size_t)t * ldq + (size_t)(kh * G + h) * D + 8 * dl);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      qf[h][2 * i] = bf2f(raw[i] & 0xFFFF) * scale * LOG2E;
+      qf[h][2 * i + 1] = bf2f(raw[i] >> 16) * scale * LOG2E;
+    }
+  }
+  float m[G], l[G], o[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    m[h] = -INFINITY;
+    l[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[h][i] = 0.f;
+  }
+
+  for (int base = start; base < end; base += NSTREAM) {
+    const int pos = base + stream;
+    const bool valid = pos < end;
+    const int pc = valid ? pos : start;
+    const long slot = (long)bt[pc / bs] * bs + (pc % bs);
+    const size_t off = ((size_t)slot * Hkv + kh) * D + 8 * dl;
+    const u32x4 kr = ld16(kc + off);
+    const u32x4 vr = ld16(vc + off);
+    float kf[8], vf[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      kf[2 * i] = bf2f(kr[i] & 0xFFFF);
+      kf[2 * i + 1] = bf2f(kr[i] >> 16);
+      vf[2 * i] = bf2f(vr[i] & 0xFFFF);
+      vf[2 * i + 1] = bf2f(vr[i] >> 16);
+    }
+    float s[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += qf[h][i] * kf[i];
+#pragma unroll
+      for (int o2 = LPT / 2; o2 > 0; o2 >>= 1) acc += __shfl_xor(acc, o2, 64);
+      s[h] = valid ? acc : -INFINITY;
+    }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float mn = fmaxf(m[h], s[h]);
+      if (mn == -INFINITY) continue;
+      const float c = exp2f(m[h] - mn);
+      const float p = exp2f(s[h] - mn);
+      m[h] = mn;
+      l[h] = l[h] * c + p;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * c + p * vf[i];
+    }
+  }
+
+  // ---- merge the NSTREAM streams through LDS ----------------------------------
+  __shared__ float sml[NSTREAM][G][2];
+  __shared__ float so[NSTREAM][G][D];
+  if (dl == 0) {
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      sml[stream][h][0] = m[h];
+      sml[stream][h][1] = l[h];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) so[stream][h][8 * dl + i] = o[h][i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < G * D; e += 256) {
+    const int h = e / D, d = e - h * D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int s2 = 0; s2 < NSTREAM; ++s2) M = fmaxf(M, sml[s2][h][0]);
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int s2 = 0; s2 < NSTREAM; ++s2) {
+        const float ms = sml[s2][h][0];
+        if (ms == -INFINITY) continue;
+        const float f = exp2f(ms - M);
+        L += sml[s2][h][1] * f;
+        O += so[s2][h][d] * f;
+      }
+    }
+    const int qh = kh * G + h;
+    if (n_split == 1) {
+      out[(size_t)t * ldo + (size_t)qh * D + d] = (__bf16)(L > 0.f ? O / L : 0.f);
+    } else {
+      const size_t pi = ((size_t)t * Hq + qh) * n_split + split;
+      part_o[pi * D + d] = O;
+      if (d == 0) {
+        part_ml[2 * pi] = M;
+        part_ml[2 * pi + 1] = L;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ void attn_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
+                                    int Hq, int n_split, __bf16* __restrict__ out, long ldo) {
+  const int t = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  const size_t pb = ((size_t)t * Hq + h) * n_split;
+  float M = -INFINITY;
+  for (int s = 0; s < n_split; ++s) M = fmaxf(M, part_ml[2 * (pb + s)]);
+  float L = 0.f, O = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < n_split; ++s) {
+      const float ms = part_ml[2 * (pb + s)];
+      if (ms == -INFINITY) continue;
+      const float f = exp2f(ms - M);
+      L += part_ml[2 * (pb + s) + 1] * f;
+      O += part_o[(pb + s) * D + d] * f;
+    }
+  }
+  out[(size_t)t * ldo + (size_t)h * D + d] = (__bf16)(L > 0.f ? O / L : 0.f);
+}
+
+template <int D, int G>
+void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const __bf16* kc, const __bf16* vc,
+                 const int* bt, int bts, const int* ts, const int* cl, int Hkv, int bs, float scale, int chunk,
+                 int ns, __bf16* out, long ldo, float* po, float* pml) {
+  hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, q, ldq, kc, vc, bt, bts, ts, cl, Hkv, bs,
+                     scale, chunk, ns, out, ldo, po, pml);
+}
+
+}  // namespace
+
+extern "C" {
+
+// workspace: part_o [T*Hq*n_split*D] f32, part_ml [T*Hq*n_split*2] f32 (only if n_split > 1)
+int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                    int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
+                    int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
+                    float* part_ml, void* stream) {
+  if (Hq % Hkv || chunk % 16 || n_split < 1) return -1;
+  const int G = Hq / Hkv;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(T, Hkv, n_split);
+  const __bf16* qq = (const __bf16*)q;
+  const __bf16* k = (const __bf16*)kc;
+  const __bf16* v = (const __bf16*)vc;
+  __bf16* o = (__bf16*)out;
+#define NLS_ATTN_CASE(DD, GG)                                                                                 \
+  if (D == DD && G == GG) {                                                                                  \
+    launch_attn<DD, GG>(grid, st, qq, ldq, k, v, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \
+                        scale, chunk, n_split, o, ldo, part_o, part_ml);                                     \
+  } else
+  NLS_ATTN_CASE(128, 1) NLS_ATTN_CASE(128, 2) NLS_ATTN_CASE(128, 4) NLS_ATTN_CASE(128, 8)
+  NLS_ATTN_CASE(64, 1) NLS_ATTN_CASE(64, 2) NLS_ATTN_CASE(64, 4) NLS_ATTN_CASE(64, 8) { return -1; }
+#undef NLS_ATTN_CASE
+  if (n_split > 1) {
+    if (D == 128)
+      hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, Hq, n_split, o,
+                         ldo);
+    else
+      hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(T, Hq), dim3(64), 0, st, part_o, part_ml, Hq, n_split, o,
+                         ldo);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

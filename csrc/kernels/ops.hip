@@ -1,0 +1,307 @@
+// Elementwise / normalisation / positional / gather kernels (gfx950), SURVEY.md §2F:
+// embed_gather_q, rmsnorm, rope (+ paged KV append), dequant_* (prefill + tests),
+// logits argmax. All bf16/f32 traffic is 16-B vectorised where rows allow it
+// (cdna_hip_programming.md Guideline 13).
+#include "common.h"
+
+namespace {
+
+DEVI float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int BS>
+DEVI float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < BS / 64; ++i) t += sh[i];
+  __syncthreads();
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// RMSNorm: out_bf16[m] = x[m] * rsqrt(mean(x^2) + eps) * w      (x f32, fp32 accumulate)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, long ldx,
+                                                      const float* __restrict__ w,
+                                                      __bf16* __restrict__ out, long ldo, int D,
+                                                      float eps) {
+  __shared__ float sh[4];
+  const float* xr = x + (size_t)blockIdx.x * ldx;
+  float ss = 0.f;
+  for (int i = threadIdx.x * 4; i < D; i += 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + i);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = block_sum<256>(ss, sh);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  __bf16* o = out + (size_t)blockIdx.x * ldo;
+  for (int i = threadIdx.x * 4; i < D; i += 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + i);
+    const float4 ww = *reinterpret_cast<const float4*>(w + i);
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 r = {(__bf16)(v.x * inv * ww.x), (__bf16)(v.y * inv * ww.y), (__bf16)(v.z * inv * ww.z),
+                (__bf16)(v.w * inv * ww.w)};
+    *reinterpret_cast<bf16x4*>(o + i) = r;
+  }
+}
+
+// f32 -> f32 variant (final norm feeding an fp32 reference / lm-head in f32)
+__global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restrict__ x, long ldx,
+                                                          const float* __restrict__ w,
+                                                          float* __restrict__ out, long ldo, int D,
+                                                          float eps) {
+  __shared__ float sh[4];
+  const float* xr = x + (size_t)blockIdx.x * ldx;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < D; i += 256) ss += xr[i] * xr[i];
+  ss = block_sum<256>(ss, sh);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  for (int i = threadIdx.x; i < D; i += 256) out[(size_t)blockIdx.x * ldo + i] = xr[i] * inv * w[i];
+}
+
+// ---------------------------------------------------------------------------
+// RoPE on q,k (+ write k,v to the paged cache slot) for each token.
+// qkv row: [Hq*D | Hkv*D | Hkv*D] f32. cs: [max_pos][D/2][2] (cos, sin) f32.
+// neox=0: adjacent pairs (2i, 2i+1) -- GGUF llama "NORM" rope; neox=1: (i, i+D/2).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, long ldqkv,
+                                                      const int* __restrict__ pos,
+                                                      const int* __restrict__ slot,
+                                                      const float* __restrict__ cs,
+                                                      __bf16* __restrict__ q_out, long ldq,
+                                                      __bf16* __restrict__ kc, __bf16* __restrict__ vc,
+                                                      int Hq, int Hkv, int D, int neox) {
+  const int t = blockIdx.x;
+  const float* row = qkv + (size_t)t * ldqkv;
+  const int p = pos[t];
+  const long s = slot[t];  // int32 slot index, widened
+  const int half = D >> 1;
+  const float* c = cs + (size_t)p * D;
+  for (int idx = threadIdx.x; idx < (Hq + Hkv) * half; idx += blockDim.x) {
+    const int h = idx / half, i = idx - h * half;
+    const int i0 = neox ? i : 2 * i, i1 = neox ? i + half : 2 * i + 1;
+    const float x0 = row[h * D + i0], x1 = row[h * D + i1];
+    const float cc = c[2 * i], ss = c[2 * i + 1];
+    const float y0 = x0 * cc - x1 * ss, y1 = x0 * ss + x1 * cc;
+    if (h < Hq) {
+      q_out[(size_t)t * ldq + h * D + i0] = (__bf16)y0;
+      q_out[(size_t)t * ldq + h * D + i1] = (__bf16)y1;
+    } else if (s >= 0) {
+      __bf16* kd = kc + ((size_t)s * Hkv + (h - Hq)) * D;
+      kd[i0] = (__bf16)y0;
+      kd[i1] = (__bf16)y1;
+    }
+  }
+  if (s >= 0) {
+    const float* vr = row + (size_t)(Hq + Hkv) * D;
+    __bf16* vd = vc + (size_t)s * Hkv * D;
+    for (int i = threadIdx.x; i < Hkv * D; i += blockDim.x) vd[i] = (__bf16)vr[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Embedding gather + dequant: out[t, :] = scale * W[ids[t], :]
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids, WDesc W, int type,
+                                                    float* __restrict__ out, long ldo, float scale) {
+  const int t = blockIdx.x;
+  const int id = ids[t];
+  for (int k = threadIdx.x; k < W.K; k += 256)
+    out[(size_t)t * ldo + k] = scale * dequant_elem(W, type, id, k);
+}
+
+// ---------------------------------------------------------------------------
+// Whole-tensor dequant to bf16 (prefill GEMM operand, tests). One wave = 16 rows
+// x one 256 super-block, using the same register dequant as the GEMV.
+// ---------------------------------------------------------------------------
+template <int T>
+__global__ __launch_bounds__(256) void dequant_kernel(WDesc W, __bf16* __restrict__ out, long ldo) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int row = blockIdx.x * 16 + r;
+  const int sb = blockIdx.y * 4 + wave;
+  if (sb >= (W.K >> 8)) return;
+  const int rowc = min(row, W.rows - 1);
+  auto raw = load_raw<T, false>(W, rowc, sb, g);
+  bf16x8 wf[8];
+  dequant<T>(raw, g, wf);
+  if (row >= W.rows) return;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    *reinterpret_cast<bf16x8*>(out + (size_t)row * ldo + sb * 256 + xoff<T>(t, g)) = wf[t];
+}
+
+// ---------------------------------------------------------------------------
+// Greedy argmax over logits rows (standalone; the lm-head GEMV can also fuse it)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ logits, long ld, int V,
+                                                      int* __restrict__ out) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const float* row = logits + (size_t)blockIdx.x * ld;
+  float bv = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  for (int i = threadIdx.x; i < V; i += 1024) {
+    const float v = row[i];
+    if (v > bv) { bv = v; bi = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bv = sv[0]; bi = si[0];
+    for (int i = 1; i < 16; ++i)
+      if (sv[i] > bv || (sv[i] == bv && si[i] < bi)) { bv = sv[i]; bi = si[i]; }
+    out[blockIdx.x] = bi;
+  }
+}
+
+// unpack the fused-argmax u64 keys into token ids
+__global__ void argmax_unpack_kernel(const unsigned long long* __restrict__ keys, int n,
+                                     int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int)(0xFFFFFFFFu - (uint32_t)(keys[i] & 0xFFFFFFFFull));
+}
+
+// residual += sum_k w[t,k] * y[t*topk + k]   (MoE combine, deterministic order)
+__global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ y, const float* __restrict__ w,
+                                                          int topk, float* __restrict__ resid, long ldr,
+                                                          int D, float alpha) {
+  const int t = blockIdx.x;
+  for (int i = threadIdx.x; i < D; i += 256) {
+    float s = 0.f;
+    for (int k = 0; k < topk; ++k) s += w[t * topk + k] * y[((size_t)t * topk + k) * D + i];
+    resid[(size_t)t * ldr + i] += alpha * s;
+  }
+}
+
+// MoE router: softmax over E logits -> top-k (renormalised) -> per-expert row lists.
+// logits [T][E] f32; outputs: topw [T][k], counts [E] (must be zeroed), rows [E][T*k]
+// (segment-local x row = token t, y row = t*k + j).
+__global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k, int renorm,
+                                 float* __restrict__ topw, int* __restrict__ counts,
+                                 int* __restrict__ xrows, int* __restrict__ yrows, int cap) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const float* l = logits + (size_t)t * E;
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) mx = fmaxf(mx, l[e]);
+  float p[64];
+  float sum = 0.f;
+  for (int e = 0; e < E; ++e) { p[e] = __expf(l[e] - mx); sum += p[e]; }
+  unsigned long long used = 0;
+  float wsum = 0.f;
+  int sel[8];
+  float sw[8];
+  for (int j = 0; j < k; ++j) {
+    int be = -1;
+    float bv = -1.f;
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1) && p[e] > bv) { bv = p[e]; be = e; }
+    used |= 1ull << be;
+    sel[j] = be;
+    sw[j] = bv / sum;
+    wsum += sw[j];
+  }
+  for (int j = 0; j < k; ++j) {
+    topw[t * k + j] = renorm ? sw[j] / wsum : sw[j];
+    const int e = sel[j];
+    const int pos = atomicAdd(counts + e, 1);
+    xrows[e * cap + pos] = t;
+    yrows[e * cap + pos] = t * k + j;
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// Paged attention (decode and prefill-as-decode): see attention.hip
+// ===========================================================================
+
+extern "C" {
+
+int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, int M, int D, float eps,
+                int out_f32, void* stream) {
+  if (D % 4) return -1;
+  if (out_f32)
+    hipLaunchKernelGGL(rmsnorm_f32_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, x, ldx, w,
+                       (float*)out, ldo, D, eps);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, x, ldx, w,
+                       (__bf16*)out, ldo, D, eps);
+  return (int)hipGetLastError();
+}
+
+int nls_rope_kv(const float* qkv, long ldqkv, const int* pos, const int* slot, const float* cs, void* q_out,
+                long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox, void* stream) {
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, pos, slot, cs,
+                     (__bf16*)q_out, ldq, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, D, neox);
+  return (int)hipGetLastError();
+}
+
+int nls_embed(const int* ids, int T, const void* w, int type, int rows, int K, float* out, long ldo,
+              float scale, void* stream) {
+  WDesc W{(const uint8_t*)w, rows, K};
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, ids, W, type, out, ldo, scale);
+  return (int)hipGetLastError();
+}
+
+int nls_dequant(const void* w, int type, int rows, int K, void* out, long ldo, void* stream) {
+  if (K % 256) return -1;
+  WDesc W{(const uint8_t*)w, rows, K};
+  dim3 grid((rows + 15) / 16, ((K >> 8) + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+  __bf16* o = (__bf16*)out;
+  switch (type) {
+    case QT_Q4_K: hipLaunchKernelGGL(dequant_kernel<QT_Q4_K>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_Q5_K: hipLaunchKernelGGL(dequant_kernel<QT_Q5_K>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_Q6_K: hipLaunchKernelGGL(dequant_kernel<QT_Q6_K>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_Q8_0: hipLaunchKernelGGL(dequant_kernel<QT_Q8_0>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_F16: hipLaunchKernelGGL(dequant_kernel<QT_F16>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_BF16: hipLaunchKernelGGL(dequant_kernel<QT_BF16>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_F32: hipLaunchKernelGGL(dequant_kernel<QT_F32>, grid, dim3(256), 0, st, W, o, ldo); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+int nls_argmax(const float* logits, long ld, int M, int V, int* out, void* stream) {
+  hipLaunchKernelGGL(argmax_kernel, dim3(M), dim3(1024), 0, (hipStream_t)stream, logits, ld, V, out);
+  return (int)hipGetLastError();
+}
+
+int nls_argmax_unpack(const void* keys, int n, int* out, void* stream) {
+  hipLaunchKernelGGL(argmax_unpack_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     (const unsigned long long*)keys, n, out);
+  return (int)hipGetLastError();
+}
+
+int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* topw, int* counts, int* xrows,
+                  int* yrows, int cap, void* stream) {
+  if (E > 64 || k > 8) return -1;
+  hipLaunchKernelGGL(moe_route_kernel, dim3((T + 63) / 64), dim3(64), 0, (hipStream_t)stream, logits, T, E, k,
+                     renorm, topw, counts, xrows, yrows, cap);
+  return (int)hipGetLastError();
+}
+
+int nls_moe_combine(const float* y, const float* w, int T, int topk, float* resid, long ldr, int D, float alpha,
+                    void* stream) {
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr, D,
+                     alpha);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+"""Build the native parts in-tree (no JIT cache, no site-packages):
+
+* `_kernels.so`  -- gfx950 HIP kernels (hipcc --offload-arch=gfx950)
+* `_natscore.*.so` -- C++ NATS wire core (client + embedded server + JetStream object store), pybind11
+
+    python -m nats_llm_studio_amd.build [--force]
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(ROOT, "csrc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _stale(out: str, srcs) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def build_kernels(force: bool = False) -> str:
+    out = os.path.join(PKG, "_kernels.so")
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    if force or _stale(out, deps):
+        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+        tmp = out + ".tmp"
+        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics",
+              *srcs, "-o", tmp])
+        os.replace(tmp, out)
+    return out
+
+
+def natscore_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG, "natsio", "_natscore" + suffix)
+
+
+def build_natscore(force: bool = False) -> str:
+    out = natscore_path()
+    srcs = sorted(glob.glob(os.path.join(CSRC, "natscore", "*.cpp")))
+    if not srcs:
+        return ""
+    deps = srcs + glob.glob(os.path.join(CSRC, "natscore", "*.h"))
+    if force or _stale(out, deps):
+        import pybind11
+        inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{os.path.join(CSRC, 'natscore')}"]
+        tmp = out + ".tmp"
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden", *inc, *srcs,
+              "-o", tmp])
+        os.replace(tmp, out)
+    return out
+
+
+def build_all(force: bool = False):
+    k = build_kernels(force)
+    n = build_natscore(force)
+    return k, n
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

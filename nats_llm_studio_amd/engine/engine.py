@@ -1,0 +1,444 @@
+"""Continuous-batching inference engine with a paged KV cache and hipGraph-captured decode.
+
+Replaces LM Studio's request path behind `lmstudio.chat_model`
+(`/root/reference/nats_llm_studio.go:327-364` -> `:158-179`), where the reference
+serialises one generation per subscription. Here every in-flight request shares
+each decode step:
+
+  admission (KV blocks reserved for prompt + max_tokens)
+   -> chunked prefill (eager; quantised GEMVs in 64-row chunks + paged attention)
+   -> decode loop: one hipGraph replay per step for the padded batch bucket
+      + ONE host<-device copy of the next-token ids
+   -> stop checks (eos / stop ids / stop strings / max_tokens / deadline) -> Future
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import threading
+import time
+from collections import deque
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Callable, Deque, Dict, List, Optional, Sequence as Seq
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.llama import LlamaModel
+from .sampling import SamplingParams, sample_rows
+
+BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64)
+
+
+@dataclass
+class GenRequest:
+    prompt_ids: List[int]
+    params: SamplingParams = field(default_factory=SamplingParams)
+    request_id: str = ""
+    on_token: Optional[Callable[[int], None]] = None
+    deadline: Optional[float] = None       # time.monotonic() deadline
+
+
+@dataclass
+class GenResult:
+    request_id: str
+    token_ids: List[int]
+    text: str
+    prompt_tokens: int
+    completion_tokens: int
+    finish_reason: str                     # stop | length | timeout | cancelled | error
+    stop_reason: str                       # eosFound | stopStringFound | maxPredictedTokensReached | ...
+    time_to_first_token: float
+    generation_time: float
+    error: Optional[str] = None
+
+    @property
+    def tokens_per_second(self) -> float:
+        return self.completion_tokens / self.generation_time if self.generation_time > 0 else 0.0
+
+
+class BlockAllocator:
+    def __init__(self, n: int):
+        self.n = n
+        self.free: Deque[int] = deque(range(n))
+
+    def alloc(self, k: int) -> Optional[List[int]]:
+        if k > len(self.free):
+            return None
+        return [self.free.popleft() for _ in range(k)]
+
+    def release(self, blocks: Seq[int]):
+        self.free.extend(blocks)
+
+    @property
+    def n_free(self) -> int:
+        return len(self.free)
+
+
+class _Seq:
+    __slots__ = ("req", "fut", "tokens", "n_prompt", "n_prefilled", "blocks", "t_submit", "t_first", "t_done",
+                 "gen", "max_new", "done", "text_cache")
+
+    def __init__(self, req: GenRequest, fut: Future):
+        self.req = req
+        self.fut = fut
+        self.tokens = list(req.prompt_ids)
+        self.n_prompt = len(req.prompt_ids)
+        self.n_prefilled = 0
+        self.blocks: List[int] = []
+        self.t_submit = time.monotonic()
+        self.t_first = None
+        self.t_done = None
+        self.gen = None
+        self.max_new = req.params.max_tokens
+        self.done = False
+
+    @property
+    def generated(self) -> List[int]:
+        return self.tokens[self.n_prompt:]
+
+
+class Engine:
+    def __init__(self, model: LlamaModel, tokenizer=None, max_batch: int = 64, block_size: int = 16,
+                 num_blocks: Optional[int] = None, max_prefill_tokens: int = 2048, use_graphs: bool = True,
+                 ctx: Optional[int] = None, kv_mem_fraction: float = 0.5, eos_ids: Seq[int] = ()):
+        self.model = model
+        self.tok = tokenizer
+        self.cfg = model.cfg
+        self.dev = model.device
+        self.bs = block_size
+        self.max_batch = min(max_batch, BUCKETS[-1])
+        self.ctx = min(ctx or self.cfg.ctx, self.cfg.ctx)
+        self.max_blocks = math.ceil(self.ctx / block_size)
+        if num_blocks is None:
+            num_blocks = self.max_batch * self.max_blocks
+            if self.dev.type == "cuda":
+                per_block = 2 * self.cfg.n_layer * block_size * model.Hkv * model.D * 2
+                free, _ = torch.cuda.mem_get_info(self.dev)
+                num_blocks = int(min(num_blocks, kv_mem_fraction * free // per_block))
+        self.num_blocks = num_blocks
+        self.kc, self.vc = model.kv_cache(num_blocks, block_size)
+        self.alloc = BlockAllocator(num_blocks)
+        self.max_prefill = max_prefill_tokens
+        self.db = model.step_buffers(self.max_batch, self.max_batch, self.max_blocks)
+        self.pb = model.step_buffers(max_prefill_tokens, self.max_batch, self.max_blocks)
+        pin = self.dev.type == "cuda"
+        self.h_meta_d = torch.zeros(self.db.meta.numel(), dtype=torch.int32, pin_memory=pin)
+        self.h_meta_p = torch.zeros(self.pb.meta.numel(), dtype=torch.int32, pin_memory=pin)
+        self.h_next = torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin)
+        self.use_graphs = use_graphs and self.dev.type == "cuda"
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.eos = set(int(e) for e in eos_ids)
+        if tokenizer is not None and getattr(tokenizer, "eos_id", None) is not None:
+            self.eos.add(int(tokenizer.eos_id))
+        if tokenizer is not None:
+            for name in ("<|eot_id|>", "<|end_of_text|>", "<|eom_id|>", "</s>"):
+                tid = tokenizer.vocab.get(name) if hasattr(tokenizer, "vocab") else None
+                if tid is not None:
+                    self.eos.add(int(tid))
+        self.waiting: Deque[_Seq] = deque()
+        self.running: List[_Seq] = []
+        self.lock = threading.Condition()
+        self.thread: Optional[threading.Thread] = None
+        self.stop_flag = False
+        self._ids = itertools.count()
+        self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0)
+
+    # ------------------------------------------------------------------ API
+    def submit(self, req: GenRequest) -> Future:
+        fut: Future = Future()
+        if not req.request_id:
+            req.request_id = f"req-{next(self._ids)}"
+        s = _Seq(req, fut)
+        if s.n_prompt == 0:
+            fut.set_exception(ValueError("empty prompt"))
+            return fut
+        if s.n_prompt >= self.ctx:
+            fut.set_exception(ValueError(f"prompt ({s.n_prompt} tokens) exceeds the context length ({self.ctx})"))
+            return fut
+        s.max_new = max(1, min(req.params.max_tokens, self.ctx - s.n_prompt))
+        if req.params.seed is not None and not req.params.greedy:
+            s.gen = torch.Generator(device="cpu").manual_seed(int(req.params.seed))
+        with self.lock:
+            self.waiting.append(s)
+            self.counters["requests"] += 1
+            self.lock.notify_all()
+        return fut
+
+    def generate(self, prompt_ids: List[int], params: SamplingParams = None, timeout: float = None) -> GenResult:
+        fut = self.submit(GenRequest(list(prompt_ids), params or SamplingParams()))
+        if self.thread is None:
+            while not fut.done():
+                self.step()
+        return fut.result(timeout)
+
+    def start(self):
+        if self.thread is None:
+            self.stop_flag = False
+            self.thread = threading.Thread(target=self._loop, name="nls-engine", daemon=True)
+            self.thread.start()
+        return self
+
+    def shutdown(self):
+        with self.lock:
+            self.stop_flag = True
+            self.lock.notify_all()
+        if self.thread is not None:
+            self.thread.join()
+            self.thread = None
+        for s in list(self.running) + list(self.waiting):
+            self._finish(s, "cancelled", "engineShutdown")
+        self.running.clear()
+        self.waiting.clear()
+
+    def unload(self):
+        """Free device memory (KV cache, graphs, weights)."""
+        self.shutdown()
+        self.graphs.clear()
+        self.kc = self.vc = None
+        self.db = self.pb = None
+        self.model = None
+        if self.dev.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def _loop(self):
+        while True:
+            with self.lock:
+                while not self.stop_flag and not self.waiting and not self.running:
+                    self.lock.wait(0.5)
+                if self.stop_flag:
+                    return
+            try:
+                self.step()
+            except Exception as e:  # fail every in-flight request rather than hang them
+                import traceback
+                traceback.print_exc()
+                for s in list(self.running):
+                    self._finish(s, "error", "engineError", error=str(e))
+                self.running.clear()
+
+    # ------------------------------------------------------------------ scheduling
+    def step(self):
+        self._expire()
+        self._admit()
+        if any(s.n_prefilled < s.n_prompt for s in self.running):
+            self._prefill()
+        dec = [s for s in self.running if s.n_prefilled >= s.n_prompt and not s.done]
+        if dec:
+            self._decode(dec)
+        self.running = [s for s in self.running if not s.done]
+        self.counters["steps"] += 1
+
+    def _expire(self):
+        now = time.monotonic()
+        for s in list(self.running):
+            if s.req.deadline is not None and now > s.req.deadline:
+                self._finish(s, "timeout", "timeout")
+        with self.lock:
+            keep = deque()
+            for s in self.waiting:
+                if s.req.deadline is not None and now > s.req.deadline:
+                    self._finish(s, "timeout", "timeout")
+                else:
+                    keep.append(s)
+            self.waiting = keep
+        self.running = [s for s in self.running if not s.done]
+
+    def _admit(self):
+        with self.lock:
+            while self.waiting and len(self.running) < self.max_batch:
+                s = self.waiting[0]
+                need = math.ceil((s.n_prompt + s.max_new) / self.bs)
+                blocks = self.alloc.alloc(need)
+                if blocks is None:
+                    break
+                s.blocks = blocks
+                self.waiting.popleft()
+                self.running.append(s)
+
+    def _slot(self, s: _Seq, p: int) -> int:
+        return s.blocks[p // self.bs] * self.bs + p % self.bs
+
+    def _prefill(self):
+        b, pad = self.pb, self.pb.pad
+        h = self.h_meta_p.numpy()
+        ids, pos, slot, tseq, ctxl = (h[i * pad:(i + 1) * pad] for i in range(5))
+        bt = h[5 * pad:].reshape(self.max_batch, self.max_blocks)
+        budget = self.max_prefill
+        T = 0
+        rows, finishing = [], []
+        batch = [s for s in self.running if s.n_prefilled < s.n_prompt]
+        for si, s in enumerate(batch):
+            if budget <= 0:
+                break
+            n = min(budget, s.n_prompt - s.n_prefilled)
+            p0 = s.n_prefilled
+            ids[T:T + n] = s.tokens[p0:p0 + n]
+            pr = np.arange(p0, p0 + n)
+            pos[T:T + n] = pr
+            blk = np.asarray(s.blocks, dtype=np.int64)
+            slot[T:T + n] = blk[pr // self.bs] * self.bs + pr % self.bs
+            tseq[T:T + n] = si
+            ctxl[T:T + n] = pr + 1
+            bt[si, :len(s.blocks)] = s.blocks
+            s.n_prefilled += n
+            T += n
+            budget -= n
+            if s.n_prefilled >= s.n_prompt:
+                rows.append(T - 1)
+                finishing.append(s)
+        b.meta.copy_(self.h_meta_p, non_blocking=self.dev.type == "cuda")
+        nrows = max(1, len(rows))
+        lr = torch.tensor(rows + [0] * (nrows - len(rows)), dtype=torch.int32, device=self.dev)
+        self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
+                           logit_rows=lr, n_logits=nrows)
+        self.counters["prefill_tokens"] += T
+        if finishing:
+            toks = self._pick(finishing, b, list(range(len(finishing))))
+            now = time.monotonic()
+            for s, t in zip(finishing, toks):
+                s.t_first = now
+                self._append(s, t)
+
+    def _pick(self, seqs: List[_Seq], b, rows: List[int]) -> List[int]:
+        greedy = b.next_ids[:len(rows)].cpu().tolist() if self.dev.type != "cuda" else None
+        if greedy is None:
+            self.h_next[:len(rows)].copy_(b.next_ids[:len(rows)])
+            greedy = self.h_next[:len(rows)].tolist()
+        out = list(greedy)
+        sampled = [i for i, s in enumerate(seqs) if not s.req.params.greedy]
+        if sampled:
+            toks = sample_rows(b.logits[[rows[i] for i in sampled]], [seqs[i].req.params for i in sampled],
+                               [seqs[i].tokens for i in sampled], [seqs[i].gen for i in sampled])
+            for i, t in zip(sampled, toks):
+                out[i] = t
+        return out
+
+    def _bucket(self, B: int) -> int:
+        for k in BUCKETS:
+            if k >= B and k <= self.max_batch:
+                return k
+        return self.max_batch
+
+    def _decode(self, seqs: List[_Seq]):
+        b, pad = self.db, self.db.pad
+        B = len(seqs)
+        Bp = self._bucket(B)
+        h = self.h_meta_d.numpy()
+        ids, pos, slot, tseq, ctxl = (h[i * pad:(i + 1) * pad] for i in range(5))
+        bt = h[5 * pad:].reshape(self.max_batch, self.max_blocks)
+        for i, s in enumerate(seqs):
+            p = len(s.tokens) - 1
+            ids[i] = s.tokens[-1]
+            pos[i] = p
+            slot[i] = self._slot(s, p)
+            tseq[i] = i
+            ctxl[i] = p + 1
+            bt[i, :len(s.blocks)] = s.blocks
+        ids[B:Bp] = 0
+        pos[B:Bp] = 0
+        slot[B:Bp] = -1
+        tseq[B:Bp] = 0
+        ctxl[B:Bp] = 0
+        if self.dev.type == "cuda":
+            b.meta.copy_(self.h_meta_d, non_blocking=True)
+        else:
+            b.meta.copy_(self.h_meta_d)
+        self._run_decode(Bp)
+        toks = self._pick(seqs, b, list(range(B)))
+        self.counters["decode_tokens"] += B
+        for s, t in zip(seqs, toks):
+            self._append(s, t)
+
+    def _run_decode(self, Bp: int):
+        ns = LlamaModel.attn_splits(Bp, self.model.Hkv)
+        if not self.use_graphs:
+            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
+            return
+        g = self.graphs.get(Bp)
+        if g is None:
+            g = self._capture(Bp, ns)
+        g.replay()
+        self.counters["graph_replays"] += 1
+
+    def _capture(self, Bp: int, ns: int):
+        # eager warm-up allocates every lazily sized workspace before capture
+        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
+        torch.cuda.synchronize(self.dev)
+        self.graphs[Bp] = g
+        return g
+
+    def capture_all(self, buckets: Seq[int] = None):
+        """Pre-capture decode graphs (padded rows have ctx 0 / slot -1: no KV writes)."""
+        if not self.use_graphs:
+            return
+        pad = self.db.pad
+        h = self.h_meta_d.numpy()
+        h[:] = 0
+        h[2 * pad:3 * pad] = -1
+        self.db.meta.copy_(self.h_meta_d)
+        for Bp in buckets or [k for k in BUCKETS if k <= self.max_batch]:
+            if Bp not in self.graphs:
+                self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv))
+
+    # ------------------------------------------------------------------ completion
+    def _append(self, s: _Seq, t: int):
+        s.tokens.append(int(t))
+        p = s.req.params
+        if s.req.on_token is not None:
+            try:
+                s.req.on_token(int(t))
+            except Exception:
+                pass
+        ng = len(s.tokens) - s.n_prompt
+        if not p.ignore_eos and int(t) in self.eos:
+            self._finish(s, "stop", "eosFound")
+        elif int(t) in p.stop_token_ids:
+            self._finish(s, "stop", "stopTokenFound")
+        elif p.stop and self.tok is not None and self._stop_string(s):
+            self._finish(s, "stop", "stopStringFound")
+        elif ng >= s.max_new:
+            self._finish(s, "length", "maxPredictedTokensReached")
+        elif len(s.tokens) >= self.ctx:
+            self._finish(s, "length", "contextLengthReached")
+
+    def _stop_string(self, s: _Seq) -> bool:
+        text = self.tok.decode(s.generated)
+        for st in s.req.params.stop:
+            if st and st in text:
+                return True
+        return False
+
+    def _finish(self, s: _Seq, finish: str, reason: str, error: str = None):
+        if s.done:
+            return
+        s.done = True
+        s.t_done = time.monotonic()
+        if s.blocks:
+            self.alloc.release(s.blocks)
+            s.blocks = []
+        gen = s.generated
+        text = ""
+        if self.tok is not None:
+            text = self.tok.decode(gen)
+            if reason == "stopStringFound":
+                cut = min((text.find(st) for st in s.req.params.stop if st and st in text), default=-1)
+                if cut >= 0:
+                    text = text[:cut]
+        gen_ids = gen
+        t_first = s.t_first or s.t_done
+        res = GenResult(s.req.request_id, gen_ids, text, s.n_prompt, len(gen), finish, reason,
+                        t_first - s.t_submit, max(s.t_done - t_first, 1e-9), error)
+        if not s.fut.done():
+            s.fut.set_result(res)
+
+    def stats(self) -> dict:
+        return dict(self.counters, running=len(self.running), waiting=len(self.waiting),
+                    kv_blocks_free=self.alloc.n_free, kv_blocks_total=self.num_blocks,
+                    graphs=sorted(self.graphs))

@@ -1,0 +1,315 @@
+"""Llama-family decoder (Llama-3, Mistral/Mixtral MoE, Granite) executing on GGUF
+quantised weights with the gfx950 kernels of `nats_llm_studio_amd.ops`.
+
+This is the co-located engine that replaces LM Studio's llama.cpp runtime behind
+`POST /api/v0/chat/completions` (`/root/reference/nats_llm_studio.go:158-179`).
+
+Per layer the decode step is 8 launches (7 for a dense FFN with fused epilogues):
+  rmsnorm -> QKV GEMV (Q|K|V segments, per-tensor quant type) -> RoPE + paged KV append
+  -> paged GQA attention -> O GEMV (+residual, fused) -> rmsnorm
+  -> gate|up GEMV with fused SwiGLU -> down GEMV (+residual, fused)
+and the whole step is captured once per batch bucket in a hipGraph by the engine.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..gguf.constants import GGMLType, GGML_BLOCK
+from ..gguf.reader import GGUFReader
+from ..ops import QWeight, Seg
+from .config import ModelConfig
+
+
+@dataclass
+class ShardSpec:
+    """Tensor-parallel shard of this process (rank of size); size 1 = whole model."""
+    rank: int = 0
+    size: int = 1
+
+
+def _raw_rows(raw: np.ndarray, ggml_type: int, rows: int, K: int, r0: int, r1: int) -> np.ndarray:
+    rb = ops.row_bytes(ggml_type, K)
+    return np.asarray(raw).view(np.uint8).reshape(rows, rb)[r0:r1].reshape(-1)
+
+
+def _raw_cols(raw: np.ndarray, ggml_type: int, rows: int, K: int, k0: int, k1: int) -> np.ndarray:
+    blk, nbytes = GGML_BLOCK[GGMLType(ggml_type)]
+    if k0 % 256 or k1 % 256:
+        raise ValueError("column shards must be multiples of 256")
+    b = np.asarray(raw).view(np.uint8).reshape(rows, K // blk, nbytes)
+    return np.ascontiguousarray(b[:, k0 // blk:k1 // blk]).reshape(-1)
+
+
+@dataclass
+class LayerWeights:
+    attn_norm: torch.Tensor
+    ffn_norm: torch.Tensor
+    qkv: List[Seg]
+    wo: QWeight
+    gateup: Optional[QWeight] = None
+    down: Optional[QWeight] = None
+    # MoE
+    router: Optional[QWeight] = None
+    exp_gateup: List[QWeight] = field(default_factory=list)
+    exp_down: List[QWeight] = field(default_factory=list)
+
+
+@dataclass
+class StepBuffers:
+    """Device buffers for one forward of up to `cap` tokens (static for hipGraph capture)."""
+    cap: int
+    ids: torch.Tensor
+    pos: torch.Tensor
+    slot: torch.Tensor
+    tok_seq: torch.Tensor
+    ctx_len: torch.Tensor
+    block_tables: torch.Tensor
+    x: torch.Tensor
+    h: torch.Tensor
+    qkv: torch.Tensor
+    q: torch.Tensor
+    ao: torch.Tensor
+    act: torch.Tensor
+    logits: torch.Tensor
+    keys: torch.Tensor
+    next_ids: torch.Tensor
+    attn_ws: torch.Tensor
+    moe: Dict[str, torch.Tensor] = field(default_factory=dict)
+    meta: Optional[torch.Tensor] = None
+    pad: int = 0
+
+
+class LlamaModel:
+    def __init__(self, reader: GGUFReader, device="cpu", shard: ShardSpec = ShardSpec(), comm=None):
+        self.reader = reader
+        self.device = torch.device(device)
+        self.cfg = cfg = ModelConfig.from_gguf(reader.metadata, reader.tensors.keys())
+        self.shard = shard
+        self.comm = comm
+        n = shard.size
+        if cfg.n_head % n or cfg.n_kv_head % n:
+            raise ValueError(f"TP={n} must divide head counts ({cfg.n_head}/{cfg.n_kv_head})")
+        self.Hq = cfg.n_head // n
+        self.Hkv = cfg.n_kv_head // n
+        self.D = cfg.head_dim
+        self.ffn = cfg.d_ff // n
+        if (self.Hq * self.D) % 256 or self.ffn % 256:
+            raise ValueError("TP shard widths must be multiples of 256 (K-quant super-blocks)")
+        self.vocab_lo, self.vocab_hi = self._vocab_range()
+        self.weight_bytes = 0
+        self._load()
+        self.cs = ops.rope_table(cfg.ctx, self.D, cfg.rope_base, self.device)
+
+    # ------------------------------------------------------------------ loading
+    def _vocab_range(self):
+        n, r, V = self.shard.size, self.shard.rank, self.cfg.vocab
+        per = (V + n - 1) // n
+        per = (per + 15) // 16 * 16
+        return min(V, r * per), min(V, (r + 1) * per)
+
+    def _t(self, name):
+        return self.reader.tensor(name)
+
+    def _qw(self, raw, gt, rows, K, name) -> QWeight:
+        w = QWeight(raw, gt, rows, K, self.device, name)
+        self.weight_bytes += w.nbytes
+        return w
+
+    def _matrix(self, name, rows_sl=None, cols_sl=None, expert=None) -> QWeight:
+        ti = self._t(name)
+        shape = ti.np_shape
+        raw = ti.data
+        if expert is not None:
+            E = shape[0]
+            per = ti.nbytes // E
+            raw = np.asarray(raw)[expert * per:(expert + 1) * per]
+            shape = shape[1:]
+        rows, K = shape
+        if rows_sl is not None:
+            raw = _raw_rows(raw, ti.ggml_type, rows, K, *rows_sl)
+            rows = rows_sl[1] - rows_sl[0]
+        if cols_sl is not None:
+            raw = _raw_cols(raw, ti.ggml_type, rows, K, *cols_sl)
+            K = cols_sl[1] - cols_sl[0]
+        return self._qw(raw, ti.ggml_type, rows, K, name)
+
+    def _vec(self, name) -> torch.Tensor:
+        return torch.from_numpy(self.reader.dequantized(name).astype(np.float32).copy()).to(self.device)
+
+    def _gateup(self, gname, uname, expert=None) -> QWeight:
+        cfg, r = self.cfg, self.shard.rank
+        sl = (r * self.ffn, (r + 1) * self.ffn)
+        gt, ut = self._t(gname).ggml_type, self._t(uname).ggml_type
+        if gt != ut:
+            raise NotImplementedError("gate/up with different quant types")
+        raw = ops.interleave_gate_up(self._raw_of(gname, sl, expert), self._raw_of(uname, sl, expert), gt,
+                                     self.ffn, cfg.d_model)
+        return self._qw(raw, gt, 2 * self.ffn, cfg.d_model, gname + "|up")
+
+    def _raw_of(self, name, rows_sl, expert=None):
+        ti = self._t(name)
+        shape = ti.np_shape
+        raw = ti.data
+        if expert is not None:
+            per = ti.nbytes // shape[0]
+            raw = np.asarray(raw)[expert * per:(expert + 1) * per]
+            shape = shape[1:]
+        return _raw_rows(raw, ti.ggml_type, shape[0], shape[1], *rows_sl)
+
+    def _load(self):
+        cfg, r = self.cfg, self.shard.rank
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        self.tok_embd = self._matrix("token_embd.weight")
+        self.layers: List[LayerWeights] = []
+        for i in range(cfg.n_layer):
+            p = f"blk.{i}."
+            wq = self._matrix(p + "attn_q.weight", (r * Hq * D, (r + 1) * Hq * D))
+            wk = self._matrix(p + "attn_k.weight", (r * Hkv * D, (r + 1) * Hkv * D))
+            wv = self._matrix(p + "attn_v.weight", (r * Hkv * D, (r + 1) * Hkv * D))
+            qkv = [Seg(wq, 0), Seg(wk, Hq * D), Seg(wv, (Hq + Hkv) * D)]
+            wo = self._matrix(p + "attn_output.weight", None, (r * Hq * D, (r + 1) * Hq * D))
+            lw = LayerWeights(self._vec(p + "attn_norm.weight"), self._vec(p + "ffn_norm.weight"), qkv, wo)
+            if cfg.n_expert:
+                lw.router = self._matrix(p + "ffn_gate_inp.weight")
+                for e in range(cfg.n_expert):
+                    lw.exp_gateup.append(self._gateup(p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", e))
+                    lw.exp_down.append(self._matrix(p + "ffn_down_exps.weight", None,
+                                                    (r * self.ffn, (r + 1) * self.ffn), expert=e))
+            else:
+                lw.gateup = self._gateup(p + "ffn_gate.weight", p + "ffn_up.weight")
+                lw.down = self._matrix(p + "ffn_down.weight", None, (r * self.ffn, (r + 1) * self.ffn))
+            self.layers.append(lw)
+        self.out_norm = self._vec("output_norm.weight")
+        head = "token_embd.weight" if cfg.tied_embeddings else "output.weight"
+        self.lm_head = self._matrix(head, (self.vocab_lo, self.vocab_hi))
+
+    # ------------------------------------------------------------------ buffers
+    def kv_cache(self, num_blocks: int, block_size: int = 16):
+        L, slots = self.cfg.n_layer, num_blocks * block_size
+        k = torch.zeros(L, slots, self.Hkv, self.D, dtype=torch.bfloat16, device=self.device)
+        v = torch.zeros_like(k)
+        return k, v
+
+    def step_buffers(self, cap: int, max_seqs: int, max_blocks: int) -> StepBuffers:
+        """All int32 step metadata lives in ONE tensor (`meta`) so the engine refreshes it
+        with a single host->device copy per step: [ids|pos|slot|tok_seq|ctx_len|block_tables]."""
+        cfg, dev = self.cfg, self.device
+        pad = (cap + 63) // 64 * 64
+        Vs = self.vocab_hi - self.vocab_lo
+        nq = self.Hq * self.D
+        k = max(1, cfg.n_expert_used)
+        meta = torch.zeros(5 * pad + max_seqs * max_blocks, dtype=torch.int32, device=dev)
+        f = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        b = StepBuffers(
+            cap=cap,
+            ids=meta[0:pad], pos=meta[pad:2 * pad], slot=meta[2 * pad:3 * pad],
+            tok_seq=meta[3 * pad:4 * pad], ctx_len=meta[4 * pad:5 * pad],
+            block_tables=meta[5 * pad:].view(max_seqs, max_blocks),
+            x=torch.zeros(pad, cfg.d_model, **f),
+            h=torch.zeros(pad, cfg.d_model, **bf),
+            qkv=torch.zeros(pad, (self.Hq + 2 * self.Hkv) * self.D, **f),
+            q=torch.zeros(pad, nq, **bf),
+            ao=torch.zeros(pad, nq, **bf),
+            act=torch.zeros(pad * (k if cfg.n_expert else 1), self.ffn, **bf),
+            logits=torch.zeros(min(pad, max(64, max_seqs)), Vs, **f),
+            keys=torch.zeros(pad, dtype=torch.int64, device=dev),
+            next_ids=torch.zeros(pad, dtype=torch.int32, device=dev),
+            attn_ws=torch.zeros(1, **f),
+        )
+        b.meta = meta
+        b.pad = pad
+        b.slot.fill_(-1)
+        if cfg.n_expert:
+            E = cfg.n_expert
+            b.moe = dict(
+                rlogits=torch.zeros(pad, E, dtype=torch.float32, device=dev),
+                topw=torch.zeros(pad * k, dtype=torch.float32, device=dev),
+                counts=torch.zeros(E, dtype=torch.int32, device=dev),
+                xrows=torch.zeros(E * pad, dtype=torch.int32, device=dev),
+                yrows=torch.zeros(E * pad, dtype=torch.int32, device=dev),
+                yexp=torch.zeros(pad * k, cfg.d_model, dtype=torch.float32, device=dev),
+            )
+        return b
+
+    @staticmethod
+    def attn_splits(T: int, Hkv: int) -> int:
+        wg = T * Hkv
+        if wg >= 512:
+            return 1
+        return int(min(32, max(1, 512 // wg)))
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, b: StepBuffers, kc: torch.Tensor, vc: torch.Tensor, T: int, block_size: int,
+                n_split: int = 1, logit_rows: Optional[torch.Tensor] = None, n_logits: Optional[int] = None):
+        """Runs T tokens through the model; leaves greedy ids in b.next_ids[:n] and logits in b.logits[:n]."""
+        cfg = self.cfg
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        x = b.x
+        ops.embed(b.ids, self.tok_embd, x, T, cfg.embedding_scale)
+        need = T * Hq * n_split * (D + 2)
+        if n_split > 1 and b.attn_ws.numel() < need:
+            b.attn_ws = torch.zeros(need, dtype=torch.float32, device=self.device)
+        for L, lw in enumerate(self.layers):
+            ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
+            ops.qgemv(lw.qkv, b.h, b.qkv, T)
+            ops.rope_kv(b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D, cfg.rope_neox)
+            ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
+                          block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws)
+            self._row_parallel(lw.wo, b.ao, x, T, cfg.residual_scale)
+            ops.rmsnorm(x, lw.ffn_norm, b.h, T, cfg.eps)
+            if cfg.n_expert:
+                self._moe(lw, b, T)
+            else:
+                ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
+                self._row_parallel(lw.down, b.act, x, T, cfg.residual_scale)
+        ops.rmsnorm(x, self.out_norm, b.h, T, cfg.eps)
+        h = b.h
+        n = T
+        if logit_rows is not None:
+            n = int(n_logits)
+            h = b.h.index_select(0, logit_rows[:n].long())
+            h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
+        ops.argmax_reset(b.keys)
+        ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale,
+                  argmax=b.keys if self.shard.size == 1 else None)
+        if self.shard.size == 1:
+            ops.argmax_unpack(b.keys, n, b.next_ids)
+        else:
+            self.comm.vocab_parallel_argmax(b.logits, n, self.vocab_lo, b.next_ids)
+        return n
+
+    def _row_parallel(self, w: QWeight, xin: torch.Tensor, resid: torch.Tensor, T: int, alpha: float):
+        if self.shard.size == 1:
+            ops.qgemv([Seg(w)], xin, resid, T, alpha=alpha, epi="add")
+        else:
+            self.comm.row_parallel_add(w, xin, resid, T, alpha)
+
+    def _moe(self, lw: LayerWeights, b: StepBuffers, T: int):
+        """Top-k routed experts: router GEMV -> route kernel (per-expert row lists on device)
+        -> grouped expert GEMVs (tiles of experts with no routed rows exit before reading
+        weights) -> deterministic weighted combine into the residual."""
+        cfg = self.cfg
+        m = b.moe
+        k, E = cfg.n_expert_used, cfg.n_expert
+        cap = b.x.shape[0]
+        ops.qgemv([Seg(lw.router)], b.h, m["rlogits"], T)
+        for c0 in range(0, T, 64):
+            n = min(64, T - c0)
+            ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap)
+            segs = [Seg(lw.exp_gateup[e], 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1])
+                    for e in range(E)]
+            for s0 in range(0, E, 8):
+                ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu")
+            segs = [Seg(lw.exp_down[e], 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1])
+                    for e in range(E)]
+            for s0 in range(0, E, 8):
+                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32")
+            if self.shard.size > 1:
+                self.comm.all_reduce(m["yexp"][:n * k])
+            ops.moe_combine(m["yexp"], m["topw"], n, k, b.x[c0:], cfg.residual_scale)

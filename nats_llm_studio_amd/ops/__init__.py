@@ -1,0 +1,331 @@
+"""Device ops. CUDA(HIP) tensors -> hand-written gfx950 kernels in `_kernels.so`;
+CPU tensors -> the pure-torch fp32 reference of the same op (tests, CPU stub runs).
+
+The CPU branch is never taken for GPU tensors: a missing kernel library on a GPU
+box raises instead of silently running eager PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import warnings
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..gguf.constants import GGMLType, GGML_BLOCK
+from ..gguf.quants import dequantize
+from . import _lib
+
+EPI = {"f32": 0, "bf16": 1, "add": 2, "swiglu": 3}
+
+
+def _stream_ptr(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# ---------------------------------------------------------------------------
+# Quantised weights
+# ---------------------------------------------------------------------------
+
+def to_device_layout(raw: np.ndarray, ggml_type: int, rows: int, K: int) -> np.ndarray:
+    """ggml block bytes -> the kernel's device layout (see csrc/kernels/common.h)."""
+    t = GGMLType(ggml_type)
+    raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)
+    if t == GGMLType.Q6_K:
+        b = raw.reshape(-1, 210)
+        return np.concatenate([b[:, 0:128].reshape(-1), b[:, 128:192].reshape(-1), b[:, 192:208].reshape(-1),
+                               b[:, 208:210].reshape(-1)])
+    if t == GGMLType.Q8_0:
+        b = raw.reshape(-1, 34)
+        return np.concatenate([b[:, 2:34].reshape(-1), b[:, 0:2].reshape(-1)])
+    return raw
+
+
+def row_bytes(ggml_type: int, K: int) -> int:
+    blk, nb = GGML_BLOCK[GGMLType(ggml_type)]
+    return K // blk * nb
+
+
+class QWeight:
+    """A [rows, K] weight matrix resident on `device` in its quantised form."""
+
+    def __init__(self, raw: np.ndarray, ggml_type: int, rows: int, K: int, device, name: str = ""):
+        self.type = int(ggml_type)
+        self.rows = int(rows)
+        self.K = int(K)
+        self.name = name
+        self.device = torch.device(device)
+        if K % 256:
+            raise ValueError(f"{name}: K={K} is not a multiple of 256")
+        dev = np.ascontiguousarray(to_device_layout(raw, ggml_type, rows, K))
+        with warnings.catch_warnings():     # read-only mmap views: .to(device) copies anyway
+            warnings.simplefilter("ignore", UserWarning)
+            t = torch.from_numpy(dev)
+        self.data = t.to(self.device) if self.device.type != "cpu" else t.clone()
+        self._raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1) if self.device.type == "cpu" else None
+        self._dense = None
+
+    @property
+    def nbytes(self) -> int:
+        return self.data.numel()
+
+    def dense(self, dtype=torch.float32) -> torch.Tensor:
+        """Dequantised [rows, K] (CPU: numpy ggml codec; GPU: HIP dequant kernel, bf16)."""
+        if self.device.type == "cpu":
+            if self._dense is None:
+                self._dense = torch.from_numpy(dequantize(self._raw, self.type, (self.rows, self.K)).copy())
+            return self._dense.to(dtype)
+        out = torch.empty(self.rows, self.K, dtype=torch.bfloat16, device=self.device)
+        _lib.check(_lib.lib().nls_dequant(self.data.data_ptr(), self.type, self.rows, self.K, out.data_ptr(),
+                                          self.K, _stream_ptr(out)), "nls_dequant")
+        return out.to(dtype)
+
+
+def interleave_gate_up(gate_raw: np.ndarray, up_raw: np.ndarray, ggml_type: int, rows: int, K: int,
+                       group: int = 8) -> np.ndarray:
+    """Rows [g0..g7, u0..u7, g8..g15, u8..u15, ...] so one 16-row MFMA tile yields 8 SwiGLU outputs."""
+    rb = row_bytes(ggml_type, K)
+    g = np.asarray(gate_raw).view(np.uint8).reshape(rows // group, group, rb)
+    u = np.asarray(up_raw).view(np.uint8).reshape(rows // group, group, rb)
+    return np.ascontiguousarray(np.concatenate([g, u], axis=1)).reshape(-1)
+
+
+@dataclass
+class Seg:
+    w: QWeight
+    ycol: int = 0
+    xmap: Optional[torch.Tensor] = None     # int32 [max rows]
+    ymap: Optional[torch.Tensor] = None     # int32 [max rows]
+    mcount: Optional[torch.Tensor] = None   # int32 [1]
+
+
+def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
+          argmax: Optional[torch.Tensor] = None, waves: int = 8, rt: int = 1):
+    """y (epilogue) alpha * x[:M] @ W^T for each segment. x: bf16 [>=pad16(M), K]."""
+    if x.is_cuda:
+        L = _lib.lib()
+        mapped = any(s.xmap is not None for s in segs)
+        if M > 64 and not mapped:
+            for m0 in range(0, M, 64):
+                mm = min(64, M - m0)
+                qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt)
+            return y
+        arr = (_lib.NlsSeg * len(segs))()
+        for i, s in enumerate(segs):
+            arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
+                                 s.w.K, s.ycol)
+        rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
+                         EPI[epi], _p(argmax), waves, rt, _stream_ptr(x))
+        _lib.check(rc, "nls_qgemv")
+        return y
+    # ---- CPU reference ----
+    for s in segs:
+        W = s.w.dense()
+        if s.xmap is not None:
+            cnt = int(s.mcount.item()) if s.mcount is not None else M
+            cnt = min(cnt, M)
+            xi = s.xmap[:cnt].long()
+            yi = s.ymap[:cnt].long() if s.ymap is not None else torch.arange(cnt)
+            xs = x.index_select(0, xi).float()
+        else:
+            cnt = M
+            xs = x[:M].float()
+            yi = torch.arange(M)
+        if cnt == 0:
+            continue
+        acc = alpha * (xs @ W.t())
+        n = W.shape[0]
+        if epi == "swiglu":
+            a4 = acc.view(cnt, n // 16, 2, 8)
+            g, u = a4[:, :, 0, :], a4[:, :, 1, :]
+            out = (torch.nn.functional.silu(g) * u).reshape(cnt, n // 2)
+            y[yi, s.ycol:s.ycol + n // 2] = out.to(y.dtype)
+        elif epi == "add":
+            y[yi, s.ycol:s.ycol + n] += acc.to(y.dtype)
+        else:
+            y[yi, s.ycol:s.ycol + n] = acc.to(y.dtype)
+        if argmax is not None:
+            v, idx = acc.max(dim=1)
+            key = _argmax_keys(v, idx + s.ycol)
+            argmax[yi] = torch.maximum(argmax[yi], key)
+    return y
+
+
+def _argmax_keys(v: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    u = v.float().view(torch.int32).long() & 0xFFFFFFFF
+    neg = (u & 0x80000000) != 0
+    u = torch.where(neg, (~u) & 0xFFFFFFFF, u | 0x80000000)
+    # GPU keys are unsigned u64; on CPU flip the top bit so signed int64 order == unsigned order
+    return ((u ^ 0x80000000) << 32) | (0xFFFFFFFF - idx.long())
+
+
+def argmax_reset(keys: torch.Tensor):
+    """Initial value of a fused-argmax key buffer (smaller than every key)."""
+    if keys.is_cuda:
+        keys.zero_()
+    else:
+        keys.fill_(torch.iinfo(torch.int64).min)
+
+
+# ---------------------------------------------------------------------------
+# Normalisation, RoPE + KV append, embedding, attention, sampling, MoE routing
+# ---------------------------------------------------------------------------
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, M: int, eps: float):
+    D = x.shape[1]
+    if x.is_cuda:
+        _lib.check(_lib.lib().nls_rmsnorm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), M,
+                                          D, float(eps), int(out.dtype == torch.float32), _stream_ptr(x)),
+                   "nls_rmsnorm")
+        return out
+    xs = x[:M].float()
+    r = xs * torch.rsqrt(xs.pow(2).mean(dim=1, keepdim=True) + eps) * w.float()
+    out[:M] = r.to(out.dtype)
+    return out
+
+
+def rope_table(max_pos: int, head_dim: int, base: float, device) -> torch.Tensor:
+    inv = 1.0 / (base ** (np.arange(0, head_dim, 2, dtype=np.float64) / head_dim))
+    ang = np.arange(max_pos, dtype=np.float64)[:, None] * inv[None, :]
+    cs = np.stack([np.cos(ang), np.sin(ang)], axis=-1).astype(np.float32)   # [P, D/2, 2]
+    return torch.from_numpy(cs).to(device)
+
+
+def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.Tensor, q_out: torch.Tensor,
+            kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, neox: bool = False):
+    """kc/vc: [slots, Hkv, D] bf16 for one layer. slot (int32) < 0 skips the cache write."""
+    if qkv.is_cuda:
+        _lib.check(_lib.lib().nls_rope_kv(qkv.data_ptr(), qkv.stride(0), pos.data_ptr(), slot.data_ptr(),
+                                          cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(),
+                                          vc.data_ptr(), T, Hq, Hkv, D, int(neox), _stream_ptr(qkv)), "nls_rope_kv")
+        return
+    x = qkv[:T].float()
+    p = pos[:T].long()
+    c, s = cs[p, :, 0], cs[p, :, 1]                      # [T, D/2]
+
+    def rot(h):                                          # h: [T, H, D]
+        if neox:
+            x0, x1 = h[..., :D // 2], h[..., D // 2:]
+        else:
+            x0, x1 = h[..., 0::2], h[..., 1::2]
+        cc, ss = c[:, None, :], s[:, None, :]
+        y0, y1 = x0 * cc - x1 * ss, x0 * ss + x1 * cc
+        if neox:
+            return torch.cat([y0, y1], dim=-1)
+        return torch.stack([y0, y1], dim=-1).flatten(-2)
+
+    q = rot(x[:, :Hq * D].view(T, Hq, D))
+    k = rot(x[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D))
+    v = x[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].view(T, Hkv, D)
+    q_out[:T, :Hq * D] = q.reshape(T, Hq * D).to(q_out.dtype)
+    sl = slot[:T].long()
+    ok = sl >= 0
+    kc[sl[ok]] = k[ok].to(kc.dtype)
+    vc[sl[ok]] = v[ok].to(vc.dtype)
+
+
+def embed(ids: torch.Tensor, w: QWeight, out: torch.Tensor, T: int, scale: float = 1.0):
+    if ids.is_cuda:
+        _lib.check(_lib.lib().nls_embed(ids.data_ptr(), T, w.data.data_ptr(), w.type, w.rows, w.K, out.data_ptr(),
+                                        out.stride(0), float(scale), _stream_ptr(ids)), "nls_embed")
+        return out
+    out[:T] = scale * w.dense()[ids[:T].long()]
+    return out
+
+
+def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables: torch.Tensor,
+              tok_seq: torch.Tensor, ctx_len: torch.Tensor, out: torch.Tensor, T: int, Hq: int, Hkv: int, D: int,
+              block_size: int, scale: float, chunk: int = 256, n_split: int = 1,
+              workspace: Optional[torch.Tensor] = None):
+    """Paged GQA attention; query t attends to the first ctx_len[t] positions of sequence tok_seq[t]."""
+    if q.is_cuda:
+        po = pml = None
+        if n_split > 1:
+            need = T * Hq * n_split * (D + 2)
+            if workspace is None or workspace.numel() < need:
+                workspace = torch.empty(need, dtype=torch.float32, device=q.device)
+            po = workspace.data_ptr()
+            pml = po + T * Hq * n_split * D * 4
+        _lib.check(_lib.lib().nls_attn_decode(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
+                                              block_tables.data_ptr(), block_tables.stride(0), tok_seq.data_ptr(),
+                                              ctx_len.data_ptr(), T, Hq, Hkv, D, block_size, float(scale), chunk,
+                                              n_split, out.data_ptr(), out.stride(0), po, pml, _stream_ptr(q)),
+                   "nls_attn_decode")
+        return out
+    G = Hq // Hkv
+    for t in range(T):
+        n = int(ctx_len[t])
+        if n <= 0:
+            out[t, :Hq * D] = 0
+            continue
+        bt = block_tables[int(tok_seq[t])].long()
+        p = torch.arange(n)
+        slots = bt[p // block_size] * block_size + p % block_size
+        k = kc[slots].float()                                  # [n, Hkv, D]
+        v = vc[slots].float()
+        qq = q[t, :Hq * D].float().view(Hkv, G, D)
+        s = torch.einsum("hgd,nhd->hgn", qq, k) * scale
+        pr = torch.softmax(s, dim=-1)
+        o = torch.einsum("hgn,nhd->hgd", pr, v)
+        out[t, :Hq * D] = o.reshape(Hq * D).to(out.dtype)
+    return out
+
+
+def argmax(logits: torch.Tensor, M: int, out: torch.Tensor):
+    V = logits.shape[1]
+    if logits.is_cuda:
+        _lib.check(_lib.lib().nls_argmax(logits.data_ptr(), logits.stride(0), M, V, out.data_ptr(),
+                                         _stream_ptr(logits)), "nls_argmax")
+        return out
+    out[:M] = logits[:M].float().argmax(dim=1).to(out.dtype)
+    return out
+
+
+def argmax_unpack(keys: torch.Tensor, n: int, out: torch.Tensor):
+    if keys.is_cuda:
+        _lib.check(_lib.lib().nls_argmax_unpack(keys.data_ptr(), n, out.data_ptr(), _stream_ptr(keys)),
+                   "nls_argmax_unpack")
+        return out
+    out[:n] = (0xFFFFFFFF - (keys[:n] & 0xFFFFFFFF)).to(out.dtype)
+    return out
+
+
+def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
+              yrows: torch.Tensor, cap: int, renorm: bool = True):
+    E = logits.shape[1]
+    if logits.is_cuda:
+        counts.zero_()
+        _lib.check(_lib.lib().nls_moe_route(logits.data_ptr(), T, E, k, int(renorm), topw.data_ptr(),
+                                            counts.data_ptr(), xrows.data_ptr(), yrows.data_ptr(), cap,
+                                            _stream_ptr(logits)), "nls_moe_route")
+        return
+    p = torch.softmax(logits[:T].float(), dim=-1)
+    w, e = torch.topk(p, k, dim=-1)
+    if renorm:
+        w = w / w.sum(dim=-1, keepdim=True)
+    topw[:T * k] = w.reshape(-1)
+    counts.zero_()
+    for t in range(T):
+        for j in range(k):
+            ex = int(e[t, j])
+            c = int(counts[ex])
+            xrows[ex * cap + c] = t
+            yrows[ex * cap + c] = t * k + j
+            counts[ex] += 1
+
+
+def moe_combine(y: torch.Tensor, topw: torch.Tensor, T: int, k: int, resid: torch.Tensor, alpha: float = 1.0):
+    D = resid.shape[1]
+    if y.is_cuda:
+        _lib.check(_lib.lib().nls_moe_combine(y.data_ptr(), topw.data_ptr(), T, k, resid.data_ptr(),
+                                              resid.stride(0), D, float(alpha), _stream_ptr(y)), "nls_moe_combine")
+        return
+    yy = y[:T * k].float().view(T, k, D)
+    resid[:T] += alpha * (topw[:T * k].view(T, k, 1) * yy).sum(dim=1)

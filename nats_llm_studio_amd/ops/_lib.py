@@ -1,0 +1,61 @@
+"""ctypes binding of the in-tree HIP kernel library (`_kernels.so`, built for gfx950
+by `nats_llm_studio_amd/build.py`). On a GPU tensor every op goes through this
+library; if it is missing we raise -- there is no silent eager fallback."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_kernels.so")
+
+_lib = None
+
+c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+
+
+class NlsSeg(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("xmap", c_void_p), ("ymap", c_void_p), ("mcount", c_void_p),
+                ("type", c_int), ("rows", c_int), ("K", c_int), ("ycol", c_int)]
+
+
+_SIGS = {
+    "nls_qgemv": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_float, c_int,
+                  c_void_p, c_int, c_int, c_void_p],
+    "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
+    "nls_rope_kv": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
+                    c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nls_embed": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_float, c_void_p],
+    "nls_dequant": [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p],
+    "nls_argmax": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
+    "nls_argmax_unpack": [c_void_p, c_int, c_void_p, c_void_p],
+    "nls_moe_route": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                      c_void_p],
+    "nls_moe_combine": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p],
+    "nls_attn_decode": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
+                        c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p,
+                        c_void_p],
+}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP kernel library missing: {LIB_PATH} (run `python -m nats_llm_studio_amd.build`)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        _lib = L
+    return _lib
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)

@@ -1,0 +1,199 @@
+"""HIP kernel numerics vs the fp32 PyTorch reference of the same op (MI355X only)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from nats_llm_studio_amd import ops
+from nats_llm_studio_amd.gguf import quants as Q
+from nats_llm_studio_amd.gguf.constants import GGMLType
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16, GGMLType.BF16, GGMLType.F32]
+
+
+def _qw(rows, K, t, dev, seed=0):
+    rng = np.random.default_rng(seed)
+    raw = Q.random_blocks(t, rows * K, 0.05, rng)
+    cpu = ops.QWeight(raw, t, rows, K, "cpu")
+    return ops.QWeight(raw, t, rows, K, dev), cpu.dense()
+
+
+def _x(M, K, dev, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    pad = (M + 63) // 64 * 64
+    x = torch.zeros(pad, K, dtype=torch.bfloat16)
+    x[:M] = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    return x.to(dev)
+
+
+def _close(a, b, rtol=2e-2):
+    err = (a.float().cpu() - b.float().cpu()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= rtol * scale, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("t", TYPES)
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+def test_qgemv_types(gpu, t, M):
+    rows, K = 96, 1024
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    y = torch.zeros(64, rows, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+
+
+def test_dequant_kernel_exact(gpu):
+    for t in TYPES:
+        w, Wd = _qw(48, 512, t, gpu, seed=3)
+        d = w.dense().float().cpu()
+        torch.testing.assert_close(d, Wd.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("rt,waves", [(1, 8), (2, 8), (1, 4), (2, 4)])
+def test_qgemv_multiseg_add_argmax(gpu, rt, waves):
+    K = 768
+    a, Ad = _qw(64, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(40, K, GGMLType.Q6_K, gpu, 2)     # rows not a multiple of 16
+    c, Cd = _qw(32, K, GGMLType.Q8_0, gpu, 3)
+    M = 5
+    x = _x(M, K, gpu)
+    base = torch.randn(64, 136, device=gpu)
+    y = base.clone()
+    ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 64), ops.Seg(c, 104)], x, y, M, alpha=0.5, epi="add", waves=waves, rt=rt)
+    W = torch.cat([Ad, Bd, Cd])
+    ref = base[:M].cpu() + 0.5 * (x[:M].float().cpu() @ W.t())
+    _close(y[:M], ref)
+    # fused argmax on a single segment
+    keys = torch.zeros(64, dtype=torch.int64, device=gpu)
+    logits = torch.zeros(64, 40, device=gpu)
+    ops.qgemv([ops.Seg(b)], x, logits, M, argmax=keys, waves=waves, rt=rt)
+    ids = torch.zeros(64, dtype=torch.int32, device=gpu)
+    ops.argmax_unpack(keys, M, ids)
+    assert ids[:M].cpu().tolist() == logits[:M].argmax(1).cpu().tolist()
+
+
+def test_qgemv_swiglu(gpu):
+    K, F = 512, 256
+    rng = np.random.default_rng(5)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    raw = ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K)
+    w = ops.QWeight(raw, GGMLType.Q4_K, 2 * F, K, gpu)
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    for M in (1, 20):
+        x = _x(M, K, gpu)
+        y = torch.zeros(64, F, dtype=torch.bfloat16, device=gpu)
+        ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu")
+        xf = x[:M].float().cpu()
+        ref = torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t())
+        _close(y[:M], ref, 3e-2)
+
+
+def test_qgemv_mapped_rows(gpu):
+    """MoE-style: per-segment x/y row maps and a device row count (0 -> tile skipped)."""
+    K = 512
+    w0, W0 = _qw(32, K, GGMLType.Q4_K, gpu, 7)
+    w1, W1 = _qw(32, K, GGMLType.Q4_K, gpu, 8)
+    x = _x(6, K, gpu)
+    xm0 = torch.tensor([4, 1, 0, 0], dtype=torch.int32, device=gpu)
+    ym0 = torch.tensor([0, 3, 0, 0], dtype=torch.int32, device=gpu)
+    c0 = torch.tensor([2], dtype=torch.int32, device=gpu)
+    c1 = torch.tensor([0], dtype=torch.int32, device=gpu)
+    y = torch.full((64, 32), 7.0, device=gpu)
+    ops.qgemv([ops.Seg(w0, 0, xm0, ym0, c0), ops.Seg(w1, 0, xm0, ym0, c1)], x, y, 6)
+    xf = x.float().cpu()
+    _close(y[0], xf[4] @ W0.t())
+    _close(y[3], xf[1] @ W0.t())
+    assert (y[1].cpu() == 7.0).all()
+
+
+def test_rmsnorm_embed(gpu):
+    x = torch.randn(5, 1024, device=gpu)
+    w = torch.randn(1024, device=gpu)
+    out = torch.zeros(64, 1024, dtype=torch.bfloat16, device=gpu)
+    ops.rmsnorm(x, w, out, 5, 1e-5)
+    ref = x * torch.rsqrt(x.pow(2).mean(1, keepdim=True) + 1e-5) * w
+    _close(out[:5], ref, 1e-2)
+    for t in TYPES:
+        qw, Wd = _qw(50, 512, t, gpu, 11)
+        ids = torch.tensor([0, 49, 7], dtype=torch.int32, device=gpu)
+        e = torch.zeros(3, 512, device=gpu)
+        ops.embed(ids, qw, e, 3, 2.0)
+        torch.testing.assert_close(e.cpu(), 2.0 * Wd[[0, 49, 7]], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("neox", [False, True])
+def test_rope_kv(gpu, neox):
+    T, Hq, Hkv, D = 3, 8, 2, 128
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=gpu)
+    pos = torch.tensor([0, 5, 100], dtype=torch.int32, device=gpu)
+    slot = torch.tensor([3, -1, 7], dtype=torch.int32, device=gpu)
+    cs = ops.rope_table(256, D, 10000.0, gpu)
+    outs = []
+    for dev in (gpu, "cpu"):
+        q = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=dev)
+        kc = torch.zeros(16, Hkv, D, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        ops.rope_kv(qkv.to(dev), pos.to(dev), slot.to(dev), cs.to(dev), q, kc, vc, T, Hq, Hkv, D, neox)
+        outs.append((q.cpu().float(), kc.cpu().float(), vc.cpu().float()))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1)])
+@pytest.mark.parametrize("n_split", [1, 4, 32])
+def test_attention_paged(gpu, D, G, n_split):
+    Hkv = 2
+    Hq = Hkv * G
+    bs = 16
+    ctx = [1, 17, 300, 0, 64]
+    T = len(ctx)
+    nblk = 64
+    kc = torch.randn(nblk * bs, Hkv, D).to(torch.bfloat16)
+    vc = torch.randn(nblk * bs, Hkv, D).to(torch.bfloat16)
+    perm = torch.randperm(nblk).to(torch.int32)
+    bt = torch.zeros(T, 20, dtype=torch.int32)
+    for i in range(T):
+        bt[i] = perm[(i * 7) % 40:(i * 7) % 40 + 20]
+    q = torch.randn(T, Hq * D).to(torch.bfloat16)
+    ts = torch.arange(T, dtype=torch.int32)
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    ref = torch.zeros(T, Hq * D, dtype=torch.bfloat16)
+    ops.attention(q, kc, vc, bt, ts, cl, ref, T, Hq, Hkv, D, bs, D ** -0.5)
+    out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=gpu)
+    ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), ts.to(gpu), cl.to(gpu), out, T, Hq, Hkv, D, bs,
+                  D ** -0.5, chunk=0, n_split=n_split)
+    torch.testing.assert_close(out.cpu().float(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_argmax_kernel(gpu):
+    lg = torch.randn(3, 128256, device=gpu)
+    lg[1, 777] = 100.0
+    out = torch.zeros(3, dtype=torch.int32, device=gpu)
+    ops.argmax(lg, 3, out)
+    assert out.cpu().tolist() == lg.argmax(1).cpu().tolist()
+
+
+def test_moe_route(gpu):
+    T, E, k = 10, 8, 2
+    lg = torch.randn(T, E, device=gpu)
+    topw = torch.zeros(T * k, device=gpu)
+    counts = torch.zeros(E, dtype=torch.int32, device=gpu)
+    xr = torch.zeros(E * 64, dtype=torch.int32, device=gpu)
+    yr = torch.zeros(E * 64, dtype=torch.int32, device=gpu)
+    ops.moe_route(lg, T, k, topw, counts, xr, yr, 64)
+    p = torch.softmax(lg, -1)
+    w, e = torch.topk(p, k, -1)
+    w = w / w.sum(-1, keepdim=True)
+    torch.testing.assert_close(topw.view(T, k), w, rtol=1e-5, atol=1e-6)
+    assert counts.sum().item() == T * k
+    c = counts.cpu()
+    for ex in range(E):
+        toks = sorted(xr[ex * 64:ex * 64 + c[ex]].cpu().tolist())
+        assert toks == sorted([t for t in range(T) if ex in e[t].tolist()])

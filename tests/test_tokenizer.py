@@ -1,0 +1,45 @@
+"""Tokenizer + chat template from GGUF metadata (CPU)."""
+import pytest
+
+from nats_llm_studio_amd.gguf.reader import GGUFReader
+from nats_llm_studio_amd.tokenizer.bpe import tokenizer_from_metadata
+from nats_llm_studio_amd.tokenizer.chat_template import ChatTemplate
+
+TEXTS = ["Hello world!", "The capital of France is Paris.", "  spaces  and\nnewlines\n\n", "naïve café 😀",
+         "def main(): return 42", ""]
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite"])
+def test_roundtrip(tiny_models, name):
+    md = GGUFReader(tiny_models[name]).metadata
+    tok = tokenizer_from_metadata(md)
+    for t in TEXTS:
+        ids = tok.encode(t, add_bos=False)
+        assert tok.decode(ids) == t, (name, t, ids)
+
+
+def test_special_tokens_and_template(tiny_models):
+    md = GGUFReader(tiny_models["tiny-llama"]).metadata
+    tok = tokenizer_from_metadata(md)
+    ct = ChatTemplate(md["tokenizer.chat_template"], tok.tokens[tok.bos_id])
+    s = ct.render([{"role": "system", "content": "Be brief."}, {"role": "user", "content": "Hi"}])
+    assert s.startswith("<|begin_of_text|><|start_header_id|>system<|end_header_id|>")
+    assert s.endswith("<|start_header_id|>assistant<|end_header_id|>\n\n")
+    ids = tok.encode(s, add_bos=False)
+    assert ids[0] == tok.bos_id
+    assert tok.vocab["<|eot_id|>"] in ids
+    assert tok.decode(ids, skip_special=False) == s
+
+
+def test_bpe_merges_applied(tiny_models):
+    md = GGUFReader(tiny_models["tiny-llama"]).metadata
+    tok = tokenizer_from_metadata(md)
+    ids = tok.encode("the the the", add_bos=False)
+    assert len(ids) < len("the the the")
+
+
+def test_multipart_content(tiny_models):
+    md = GGUFReader(tiny_models["tiny-granite"]).metadata
+    ct = ChatTemplate(md["tokenizer.chat_template"])
+    s = ct.render([{"role": "user", "content": [{"type": "text", "text": "a"}, {"type": "text", "text": "b"}]}])
+    assert "<|start_of_role|>user<|end_of_role|>ab" in s
