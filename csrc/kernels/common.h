@@ -347,8 +347,11 @@ DEVI void deq_f32(const RawF32& r, int g, bf16x8* wf) {
   for (int t = 0; t < 8; ++t) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      v[i] = __builtin_bit_cast(float, r.v[2 * t][i]);
-      v[4 + i] = __builtin_bit_cast(float, r.v[2 * t + 1][i]);
+      // NB: copy the vector element out first; __builtin_bit_cast on an ext_vector
+      // element lvalue returns element 0 with hipcc (ROCm 7.2).
+      const uint32_t u0 = r.v[2 * t][i], u1 = r.v[2 * t + 1][i];
+      v[i] = __uint_as_float(u0);
+      v[4 + i] = __uint_as_float(u1);
     }
     wf[t] = pack8(v);
   }

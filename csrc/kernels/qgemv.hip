@@ -26,7 +26,7 @@ struct Seg {
   const int* xmap;     // optional: segment-local batch row -> x row (-1: none)
   const int* ymap;     // optional: segment-local batch row -> y row
   const int* mcount;   // optional: device count of valid rows (tiles skip when 0)
-  int type, rows, K, tile_begin, ycol, pad;
+  int type, rows, K, tile_begin, ycol, tile_begin_col;
 };
 struct SegList { Seg s[8]; int nseg; int pad[3]; };
 
@@ -36,7 +36,7 @@ struct GemvArgs {
   int M;               // rows of x / y (or max rows per segment when mapped)
   int epi;
   float alpha;
-  int pad;
+  int pad;            // path B split-K: total raw output columns
   unsigned long long* argmax;   // optional [M] packed (ordered value << 32 | ~idx)
 };
 
@@ -64,7 +64,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int m = mt * 16 + r;
-    int src = m;
+    int src = m < mcount ? m : -1;           // padded batch rows: no loads, zero fragment
     if (S.xmap) src = (m < mcount) ? S.xmap[m] : -1;
     xr[mt] = src >= 0 ? a.x + (size_t)src * a.ldx : nullptr;
   }
@@ -177,7 +177,10 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   }
 }
 
-template <int WAVES, int RT, int MT>
+// KSET 0: Q4_K/Q6_K (the Q4_K_M mix); KSET 1: Q5_K/Q6_K/Q8_0; KSET 2: plain F16/BF16/F32. Splitting the format
+// switch keeps the register budget of the quantised kernels small (a switch case's
+// VGPR demand is paid by every case).
+template <int WAVES, int RT, int MT, int KSET>
 __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tile = blockIdx.x;
@@ -187,32 +190,289 @@ __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArg
     if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
   if (S.mcount && *S.mcount <= 0) return;     // MoE expert with no routed tokens
   const int row0 = (tile - S.tile_begin) * RT * 16;
-  switch (S.type) {
-    case QT_Q4_K: gemv_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, a, lds); break;
-    case QT_Q5_K: gemv_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, a, lds); break;
-    case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
-    case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, a, lds); break;
-    case QT_F16: gemv_tile<QT_F16, WAVES, RT, MT>(S, row0, a, lds); break;
-    case QT_BF16: gemv_tile<QT_BF16, WAVES, RT, MT>(S, row0, a, lds); break;
-    case QT_F32: gemv_tile<QT_F32, WAVES, RT, MT>(S, row0, a, lds); break;
-    default: break;
+  if constexpr (KSET == 0) {
+    switch (S.type) {
+      case QT_Q4_K: gemv_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
+      default: break;
+    }
+  } else if constexpr (KSET == 1) {
+    switch (S.type) {
+      case QT_Q5_K: gemv_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, a, lds); break;
+      default: break;
+    }
+  } else {
+    switch (S.type) {
+      case QT_F16: gemv_tile<QT_F16, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_BF16: gemv_tile<QT_BF16, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_F32: gemv_tile<QT_F32, WAVES, RT, MT>(S, row0, a, lds); break;
+      default: break;
+    }
+  }
+}
+
+// ===========================================================================
+// Path B (batch >= ~16): waves split ROWS, not K. The activation tile of the current
+// 256-wide super-block (M x 256 bf16, XOR-swizzled 16-B chunks) is staged once per
+// workgroup in LDS (double-buffered) and read by every wave with ds_read_b128, so x is
+// fetched from L2 once per WAVES*RT*16 weight rows instead of once per 16. Optional
+// split-K over workgroups (KS > 1) writes fp32 partial slabs; splitk_reduce applies
+// the epilogue in a fixed order (deterministic, no float atomics).
+// ===========================================================================
+DEVI int lds_off(int row, int k) {            // element offset in a [rows][256] bf16 tile
+  const int ch = (k >> 3) ^ (row & 15);
+  return row * 256 + ch * 8 + (k & 7);
+}
+
+template <int T, int WAVES, int RT, int MT>
+DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, __bf16* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const WDesc W{S.w, S.rows, S.K};
+  const int nb = S.K >> 8;
+  const int sb0 = (nb * kslice) / ks, sb1 = (nb * (kslice + 1)) / ks;
+  const int M = a.M;
+  const int base = row0 + wave * RT * 16;
+  int rowc[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(base + rt * 16 + r, S.rows - 1);
+
+  constexpr int NT = WAVES * 64;
+  constexpr int NCH = (MT * 16 * 32 + NT - 1) / NT;     // 16-B chunks staged per thread
+  u32x4 xst[NCH];
+  auto load_x = [&](int sb) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int idx = threadIdx.x + c * NT;
+      const int row = idx >> 5, ch = idx & 31;
+      xst[c] = (row < M && idx < MT * 512) ? ld16(a.x + (size_t)row * a.ldx + sb * 256 + ch * 8) : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int idx = threadIdx.x + c * NT;
+      if (idx < MT * 512) {
+        const int row = idx >> 5, ch = idx & 31;
+        *reinterpret_cast<u32x4*>(lds + buf * (MT * 16 * 256) + lds_off(row, ch * 8)) = xst[c];
+      }
+    }
+  };
+
+  f32x4 acc[RT][MT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  typedef typename RawOf<T>::type Raw;
+  Raw cur[RT];
+  if (sb0 < sb1) {
+    load_x(sb0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) cur[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
+    store_x(0);
+  }
+  __syncthreads();
+  for (int sb = sb0; sb < sb1; ++sb) {
+    const int buf = (sb - sb0) & 1;
+    const bool more = sb + 1 < sb1;
+    Raw nxt[RT];
+    if (more) {
+      load_x(sb + 1);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) nxt[rt] = load_raw<T, true>(W, rowc[rt], sb + 1, g);
+    }
+    bf16x8 wf[RT][8];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) dequant<T>(cur[rt], g, wf[rt]);
+    const __bf16* xb = lds + buf * (MT * 16 * 256);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int ko = xoff<T>(t, g);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
+      }
+    }
+    if (more) {
+      store_x(buf ^ 1);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue straight from the accumulators ---------------------------------
+  // lane holds rows (base + rt*16 + r), batch rows mt*16 + 4g + i
+  if (ks > 1) {
+    const int ntot = a.pad;      // total output columns (all segments, raw rows)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = base + rt * 16 + r;
+      if (row >= S.rows) continue;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int b = mt * 16 + 4 * g + i;
+          if (b < M) ws[((size_t)kslice * M + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][i];
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int row = base + rt * 16 + r;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = mt * 16 + 4 * g + i;
+        const float v = acc[rt][mt][i] * a.alpha;
+        if (a.epi == EPI_SWIGLU_BF16) {
+          const float u = __shfl_xor(v, 8, 64);
+          if (r < 8 && b < M && row < S.rows) {
+            const int n = S.ycol + ((base + rt * 16) >> 1) + r;
+            reinterpret_cast<__bf16*>(a.y)[(size_t)b * a.ldy + n] = (__bf16)(silu(v) * u);
+          }
+          continue;
+        }
+        if (b < M && row < S.rows) {
+          const size_t off = (size_t)b * a.ldy + S.ycol + row;
+          if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
+          else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
+          else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+        }
+        if (a.argmax) {
+          unsigned long long k = (row < S.rows) ? argmax_key(v, S.ycol + row) : 0ull;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            const unsigned long long ok = __shfl_xor(k, o, 64);
+            k = ok > k ? ok : k;
+          }
+          if (r == 0 && b < M) atomicMax(a.argmax + b, k);
+        }
+      }
+    }
+  }
+}
+
+template <int WAVES, int RT, int MT, int KSET>
+__global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs a, int ks, float* ws) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 xlds[];
+  const int tile = blockIdx.x / ks, kslice = blockIdx.x % ks;
+  Seg S = segs.s[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i)
+    if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
+  const int row0 = (tile - S.tile_begin) * WAVES * RT * 16;
+  if constexpr (KSET == 0) {
+    switch (S.type) {
+      case QT_Q4_K: mm_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      default: break;
+    }
+  } else if constexpr (KSET == 1) {
+    switch (S.type) {
+      case QT_Q5_K: mm_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q8_0: mm_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      default: break;
+    }
+  } else {
+    switch (S.type) {
+      case QT_F16: mm_tile<QT_F16, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_BF16: mm_tile<QT_BF16, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_F32: mm_tile<QT_F32, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      default: break;
+    }
+  }
+}
+
+// Split-K reduction + epilogue. ws: [ks][M][ntot] fp32 (ntot = raw output rows over all segments)
+struct RedSeg { int col0, rows, ycol, pad; };
+struct RedList { RedSeg s[8]; int nseg, pad[3]; };
+
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks, int M, int ntot, RedList rl,
+                                     GemvArgs a) {
+  const int b = blockIdx.y;
+  const bool swiglu = a.epi == EPI_SWIGLU_BF16;
+  const int nout = swiglu ? ntot / 2 : ntot;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nout; j += gridDim.x * blockDim.x) {
+    int col = swiglu ? (j >> 3) * 16 + (j & 7) : j;
+    RedSeg S = rl.s[0];
+    for (int i = 1; i < rl.nseg; ++i)
+      if (col >= rl.s[i].col0) S = rl.s[i];
+    float v = 0.f, u = 0.f;
+    for (int k = 0; k < ks; ++k) {
+      v += ws[((size_t)k * M + b) * ntot + col];
+      if (swiglu) u += ws[((size_t)k * M + b) * ntot + col + 8];
+    }
+    v *= a.alpha;
+    u *= a.alpha;
+    const int row = col - S.col0;
+    if (swiglu) {
+      const int n = S.ycol + (row >> 4) * 8 + (row & 7);
+      reinterpret_cast<__bf16*>(a.y)[(size_t)b * a.ldy + n] = (__bf16)(silu(v) * u);
+      continue;
+    }
+    const size_t off = (size_t)b * a.ldy + S.ycol + row;
+    if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
+    else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
+    else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+    if (a.argmax) atomicMax(a.argmax + b, argmax_key(v, S.ycol + row));
   }
 }
 
 template <int WAVES, int RT, int MT>
-int launch_t(const SegList& sl, int ntiles, const GemvArgs& a, hipStream_t st) {
+int launch_t(const SegList& sl, int ntiles, const GemvArgs& a, hipStream_t st, int kset) {
   const size_t lds = (size_t)(WAVES + 1) * RT * MT * 256 * sizeof(float);
-  hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
+  if (kset == 0)
+    hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, 0>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
+  else if (kset == 1)
+    hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, 1>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
+  else
+    hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, 2>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
   return (int)hipGetLastError();
 }
 
 template <int WAVES, int RT>
-int launch_mt(int mt, const SegList& sl, int nt, const GemvArgs& a, hipStream_t st) {
+int launch_mt(int mt, const SegList& sl, int nt, const GemvArgs& a, hipStream_t st, int kset) {
   switch (mt) {
-    case 1: return launch_t<WAVES, RT, 1>(sl, nt, a, st);
-    case 2: return launch_t<WAVES, RT, 2>(sl, nt, a, st);
-    case 3: return launch_t<WAVES, RT, 3>(sl, nt, a, st);
-    case 4: return launch_t<WAVES, RT, 4>(sl, nt, a, st);
+    case 1: return launch_t<WAVES, RT, 1>(sl, nt, a, st, kset);
+    case 2: return launch_t<WAVES, RT, 2>(sl, nt, a, st, kset);
+    case 3: return launch_t<WAVES, RT, 3>(sl, nt, a, st, kset);
+    case 4: return launch_t<WAVES, RT, 4>(sl, nt, a, st, kset);
+  }
+  return -1;
+}
+
+template <int WAVES, int RT, int MT>
+int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st, int kset) {
+  const size_t lds = (size_t)2 * MT * 16 * 256 * sizeof(__bf16);
+  if (kset == 0)
+    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, 0>), dim3(ntiles * ks), dim3(WAVES * 64), lds, st, sl, a, ks, ws);
+  else if (kset == 1)
+    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, 1>), dim3(ntiles * ks), dim3(WAVES * 64), lds, st, sl, a, ks, ws);
+  else
+    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, 2>), dim3(ntiles * ks), dim3(WAVES * 64), lds, st, sl, a, ks, ws);
+  return (int)hipGetLastError();
+}
+
+template <int WAVES, int RT>
+int launch_b_mt(int mt, const SegList& sl, int nt, int ks, float* ws, const GemvArgs& a, hipStream_t st,
+                int kset) {
+  switch (mt) {
+    case 1: return launch_b<WAVES, RT, 1>(sl, nt, ks, ws, a, st, kset);
+    case 2: return launch_b<WAVES, RT, 2>(sl, nt, ks, ws, a, st, kset);
+    case 3: return launch_b<WAVES, RT, 3>(sl, nt, ks, ws, a, st, kset);
+    case 4: return launch_b<WAVES, RT, 4>(sl, nt, ks, ws, a, st, kset);
   }
   return -1;
 }
@@ -230,16 +490,22 @@ struct NlsSeg {
   int type, rows, K, ycol;
 };
 
-// Returns 0 on success, a hipError_t otherwise, -1 on bad arguments.
+// mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
+// mode 1: path B (waves split rows, LDS-staged activations, optional split-K `ks` with workspace
+//         `ws` of ks*M*sum(rows) floats). Returns 0 on success, a hipError_t, or -1 on bad arguments.
 int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
-              float alpha, int epi, void* argmax, int waves, int rt, void* stream) {
+              float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
+              void* stream) {
   if (nseg < 1 || nseg > 8 || M < 1 || M > 64 || (rt != 1 && rt != 2) || (waves != 4 && waves != 8))
     return -1;
+  if (mode == 1 && ks > 1 && !ws) return -1;
   SegList sl{};
-  int tiles = 0;
+  int tiles = 0, cols = 0;
+  const int tile_rows = (mode == 1 ? waves : 1) * rt * 16;
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU_BF16 && segs[i].rows % 16) return -1;
+    if (mode == 1 && segs[i].xmap) return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;
     sl.s[i].ymap = segs[i].ymap;
@@ -249,14 +515,44 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
     sl.s[i].K = segs[i].K;
     sl.s[i].ycol = segs[i].ycol;
     sl.s[i].tile_begin = tiles;
-    tiles += (segs[i].rows + rt * 16 - 1) / (rt * 16);
+    sl.s[i].tile_begin_col = cols;
+    tiles += (segs[i].rows + tile_rows - 1) / tile_rows;
+    cols += segs[i].rows;
   }
   sl.nseg = nseg;
-  GemvArgs a{(const __bf16*)x, ldx, y, ldy, M, epi, alpha, 0, (unsigned long long*)argmax};
+  // pick the smallest kernel type-set that covers every segment (Q6_K is in sets 0 and 1)
+  bool has[3] = {false, false, false}, bad = false;
+  for (int i = 0; i < nseg; ++i) {
+    const int t = segs[i].type;
+    if (t == QT_Q4_K) has[0] = true;
+    else if (t == QT_Q5_K || t == QT_Q8_0) has[1] = true;
+    else if (t == QT_F16 || t == QT_BF16 || t == QT_F32) has[2] = true;
+    else if (t != QT_Q6_K) bad = true;
+  }
+  if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
+  const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
+  GemvArgs a{(const __bf16*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax};
   const int mt = (M + 15) / 16;
   hipStream_t st = (hipStream_t)stream;
-  if (waves == 8) return rt == 1 ? launch_mt<8, 1>(mt, sl, tiles, a, st) : launch_mt<8, 2>(mt, sl, tiles, a, st);
-  return rt == 1 ? launch_mt<4, 1>(mt, sl, tiles, a, st) : launch_mt<4, 2>(mt, sl, tiles, a, st);
+  if (mode == 1) {
+    if (ks < 1) ks = 1;
+    int rc;
+    if (waves == 8) rc = rt == 1 ? launch_b_mt<8, 1>(mt, sl, tiles, ks, (float*)ws, a, st, kset)
+                                 : launch_b_mt<8, 2>(mt, sl, tiles, ks, (float*)ws, a, st, kset);
+    else rc = rt == 1 ? launch_b_mt<4, 1>(mt, sl, tiles, ks, (float*)ws, a, st, kset)
+                      : launch_b_mt<4, 2>(mt, sl, tiles, ks, (float*)ws, a, st, kset);
+    if (rc || ks == 1) return rc;
+    RedList rl{};
+    for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};
+    rl.nseg = nseg;
+    const int nout = epi == EPI_SWIGLU_BF16 ? cols / 2 : cols;
+    dim3 grid((nout + 255) / 256, M);
+    hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, ks, M, cols, rl, a);
+    return (int)hipGetLastError();
+  }
+  if (waves == 8)
+    return rt == 1 ? launch_mt<8, 1>(mt, sl, tiles, a, st, kset) : launch_mt<8, 2>(mt, sl, tiles, a, st, kset);
+  return rt == 1 ? launch_mt<4, 1>(mt, sl, tiles, a, st, kset) : launch_mt<4, 2>(mt, sl, tiles, a, st, kset);
 }
 
 }  // extern "C"

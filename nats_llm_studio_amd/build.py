@@ -32,14 +32,22 @@ def _run(cmd):
 
 
 def build_kernels(force: bool = False) -> str:
+    """Compile each .hip translation unit to an object in parallel, then link one .so."""
     out = os.path.join(PKG, "_kernels.so")
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     if force or _stale(out, deps):
+        from concurrent.futures import ThreadPoolExecutor
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+        bdir = os.path.join(ROOT, "build", "kernels")
+        os.makedirs(bdir, exist_ok=True)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics"]
+        objs = [os.path.join(bdir, os.path.basename(s) + ".o") for s in srcs]
+        jobs = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + glob.glob(os.path.join(CSRC, "kernels", "*.h")))]
+        with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+            list(ex.map(lambda so: _run([hipcc, *flags, "-c", so[0], "-o", so[1]]), jobs))
         tmp = out + ".tmp"
-        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics",
-              *srcs, "-o", tmp])
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp])
         os.replace(tmp, out)
     return out
 

@@ -106,8 +106,30 @@ class Seg:
     mcount: Optional[torch.Tensor] = None   # int32 [1]
 
 
+_WS = {}
+_WS_OLD = []   # superseded workspaces stay alive: captured hipGraphs may still point at them
+
+
+def _workspace(dev, n: int) -> torch.Tensor:
+    """Split-K partial-slab workspace (64 MiB minimum; only grows, never freed)."""
+    w = _WS.get(dev)
+    if w is None or w.numel() < n:
+        if w is not None:
+            _WS_OLD.append(w)
+        w = torch.empty(max(n, 16 << 20), dtype=torch.float32, device=dev)
+        _WS[dev] = w
+    return w
+
+
+def gemv_config(segs: Sequence[Seg], M: int):
+    """(mode, waves, rt, ks) for a launch. mode 0 = waves split K (small batch, mapped rows);
+    mode 1 = waves split rows over an LDS-staged activation tile (+ split-K across workgroups)."""
+    from . import tuning
+    return tuning.select(segs, M)
+
+
 def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
-          argmax: Optional[torch.Tensor] = None, waves: int = 8, rt: int = 1):
+          argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1):
     """y (epilogue) alpha * x[:M] @ W^T for each segment. x: bf16 [>=pad16(M), K]."""
     if x.is_cuda:
         L = _lib.lib()
@@ -115,14 +137,20 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         if M > 64 and not mapped:
             for m0 in range(0, M, 64):
                 mm = min(64, M - m0)
-                qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt)
+                qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt,
+                      mode, ks)
             return y
+        if mode < 0 or waves == 0:
+            mode, waves, rt, ks = gemv_config(segs, M) if not mapped else (0, 8, 1, 1)
         arr = (_lib.NlsSeg * len(segs))()
         for i, s in enumerate(segs):
             arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
                                  s.w.K, s.ycol)
+        ws = None
+        if mode == 1 and ks > 1:
+            ws = _workspace(x.device, ks * M * sum(s.w.rows for s in segs)).data_ptr()
         rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
-                         EPI[epi], _p(argmax), waves, rt, _stream_ptr(x))
+                         EPI[epi], _p(argmax), waves, rt, mode, ks, ws, _stream_ptr(x))
         _lib.check(rc, "nls_qgemv")
         return y
     # ---- CPU reference ----

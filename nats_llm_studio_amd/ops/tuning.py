@@ -1,0 +1,56 @@
+"""Launch-configuration selection for the quantised GEMV/GEMM kernels.
+
+Measured per-shape winners (tools/tune_gemv.py on MI355X) live in `gemv_tuning.json`
+next to this file: {"<type>:<rows>:<K>:<Mbucket>": [mode, waves, rt, ks]}. Shapes not in
+the table use the heuristic below.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+_TABLE = None
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemv_tuning.json")
+MBUCKETS = (1, 2, 4, 8, 16, 32, 48, 64)
+
+
+def _mb(M: int) -> int:
+    for b in MBUCKETS:
+        if M <= b:
+            return b
+    return 64
+
+
+def key(segs, M: int) -> str:
+    t = "+".join(str(s.w.type) for s in segs)
+    rows = sum(s.w.rows for s in segs)
+    return f"{t}:{rows}:{segs[0].w.K}:{_mb(M)}"
+
+
+def table():
+    global _TABLE
+    if _TABLE is None:
+        _TABLE = {}
+        if os.path.exists(_PATH):
+            with open(_PATH) as f:
+                _TABLE = {k: tuple(v) for k, v in json.load(f).items()}
+    return _TABLE
+
+
+def heuristic(segs, M: int):
+    rows = sum(s.w.rows for s in segs)
+    K = segs[0].w.K
+    if M <= 8:
+        return (0, 8, 1, 1)
+    waves, rt = 8, 1
+    tiles = sum((s.w.rows + waves * rt * 16 - 1) // (waves * rt * 16) for s in segs)
+    ks = 1
+    nb = K // 256
+    while tiles * ks < 256 and ks * 2 <= max(1, nb // 2):
+        ks *= 2
+    return (1, waves, rt, ks)
+
+
+def select(segs, M: int):
+    hit = table().get(key(segs, M))
+    return hit if hit is not None else heuristic(segs, M)

@@ -35,14 +35,19 @@ def _close(a, b, rtol=2e-2):
     assert err <= rtol * scale, f"max err {err} vs scale {scale}"
 
 
+CFGS = [(0, 8, 1, 1), (0, 4, 2, 1), (1, 8, 1, 1), (1, 4, 2, 2), (1, 8, 1, 4)]
+
+
 @pytest.mark.parametrize("t", TYPES)
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
-def test_qgemv_types(gpu, t, M):
-    rows, K = 96, 1024
+@pytest.mark.parametrize("cfg", CFGS)
+def test_qgemv_types(gpu, t, M, cfg):
+    rows, K = 200, 1024
     w, Wd = _qw(rows, K, t, gpu)
     x = _x(M, K, gpu)
     y = torch.zeros(64, rows, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M)
+    mode, waves, rt, ks = cfg
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=mode, waves=waves, rt=rt, ks=ks)
     ref = x[:M].float().cpu() @ Wd.t()
     _close(y[:M], ref)
 
@@ -54,8 +59,9 @@ def test_dequant_kernel_exact(gpu):
         torch.testing.assert_close(d, Wd.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-6)
 
 
-@pytest.mark.parametrize("rt,waves", [(1, 8), (2, 8), (1, 4), (2, 4)])
-def test_qgemv_multiseg_add_argmax(gpu, rt, waves):
+@pytest.mark.parametrize("cfg", CFGS)
+def test_qgemv_multiseg_add_argmax(gpu, cfg):
+    mode, waves, rt, ks = cfg
     K = 768
     a, Ad = _qw(64, K, GGMLType.Q4_K, gpu, 1)
     b, Bd = _qw(40, K, GGMLType.Q6_K, gpu, 2)     # rows not a multiple of 16
@@ -64,20 +70,23 @@ def test_qgemv_multiseg_add_argmax(gpu, rt, waves):
     x = _x(M, K, gpu)
     base = torch.randn(64, 136, device=gpu)
     y = base.clone()
-    ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 64), ops.Seg(c, 104)], x, y, M, alpha=0.5, epi="add", waves=waves, rt=rt)
+    ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 64)], x, y, M, alpha=0.5, epi="add", waves=waves, rt=rt, mode=mode, ks=ks)
+    ops.qgemv([ops.Seg(c, 104)], x, y, M, alpha=0.5, epi="add", waves=waves, rt=rt, mode=mode, ks=ks)
     W = torch.cat([Ad, Bd, Cd])
     ref = base[:M].cpu() + 0.5 * (x[:M].float().cpu() @ W.t())
     _close(y[:M], ref)
     # fused argmax on a single segment
     keys = torch.zeros(64, dtype=torch.int64, device=gpu)
     logits = torch.zeros(64, 40, device=gpu)
-    ops.qgemv([ops.Seg(b)], x, logits, M, argmax=keys, waves=waves, rt=rt)
+    ops.qgemv([ops.Seg(b)], x, logits, M, argmax=keys, waves=waves, rt=rt, mode=mode, ks=ks)
     ids = torch.zeros(64, dtype=torch.int32, device=gpu)
     ops.argmax_unpack(keys, M, ids)
     assert ids[:M].cpu().tolist() == logits[:M].argmax(1).cpu().tolist()
 
 
-def test_qgemv_swiglu(gpu):
+@pytest.mark.parametrize("cfg", CFGS)
+def test_qgemv_swiglu(gpu, cfg):
+    mode, waves, rt, ks = cfg
     K, F = 512, 256
     rng = np.random.default_rng(5)
     g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
@@ -89,7 +98,7 @@ def test_qgemv_swiglu(gpu):
     for M in (1, 20):
         x = _x(M, K, gpu)
         y = torch.zeros(64, F, dtype=torch.bfloat16, device=gpu)
-        ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu")
+        ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=mode, waves=waves, rt=rt, ks=ks)
         xf = x[:M].float().cpu()
         ref = torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t())
         _close(y[:M], ref, 3e-2)

@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Sweep launch configs of the quantised GEMV/GEMM kernels on the real model shapes and
+write the per-shape winners to nats_llm_studio_amd/ops/gemv_tuning.json.
+
+Each config is timed as a hipGraph of REPS back-to-back launches (so host launch cost is
+excluded), median of 5 replays. Usage: python tools/tune_gemv.py [--model llama-3-8b] [--out f.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np
+import torch
+
+from nats_llm_studio_amd import ops
+from nats_llm_studio_amd.gguf import quants as Q
+from nats_llm_studio_amd.gguf.constants import GGMLType
+from nats_llm_studio_amd.gguf.synth import SPECS
+from nats_llm_studio_amd.ops import tuning
+
+REPS = 20
+
+
+def shapes(spec, base=GGMLType.Q4_K, more=GGMLType.Q6_K):
+    d, hd = spec.d_model, spec.head_dim
+    nq, nkv = spec.n_head * hd, spec.n_kv_head * hd
+    out = [
+        ("qkv", [(base, nq), (base, nkv), (base, nkv)], d, "f32"),
+        ("qkv6", [(base, nq), (base, nkv), (more, nkv)], d, "f32"),
+        ("o", [(base, d)], nq, "add"),
+        ("gateup", [(base, 2 * spec.d_ff)], d, "swiglu"),
+        ("down", [(base, d)], spec.d_ff, "add"),
+        ("down6", [(more, d)], spec.d_ff, "add"),
+        ("lm_head", [(more, spec.vocab)], d, "argmax"),
+    ]
+    return out
+
+
+def configs(K):
+    nb = K // 256
+    c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
+    for waves in (4, 8):
+        for rt in (1, 2):
+            for ks in (1, 2, 4, 8, 16):
+                if ks <= max(1, nb // 2):
+                    c.append((1, waves, rt, ks))
+    return c
+
+
+def time_cfg(segs, x, y, M, epi, keys, cfg):
+    mode, waves, rt, ks = cfg
+    kw = dict(mode=mode, waves=waves, rt=rt, ks=ks)
+    e = "f32" if epi == "argmax" else epi
+    am = keys if epi == "argmax" else None
+    try:
+        ops.qgemv(segs, x, y, M, epi=e, argmax=am, **kw)      # warm (allocates workspace)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(REPS):
+                ops.qgemv(segs, x, y, M, epi=e, argmax=am, **kw)
+        g.replay()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            g.replay()
+            t.record()
+            t.synchronize()
+            ts.append(s.elapsed_time(t) / REPS * 1e3)
+        del g
+        return sorted(ts)[2]
+    except RuntimeError as ex:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--ms", default="1,2,4,8,16,32,48,64")
+    ap.add_argument("--out", default=tuning._PATH)
+    ap.add_argument("--log", default="gpurun_out/tune_gemv.log")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    spec = SPECS[args.model]
+    rng = np.random.default_rng(0)
+    table = {}
+    if os.path.exists(args.out):
+        table = json.load(open(args.out))
+    os.makedirs(os.path.dirname(args.log) or ".", exist_ok=True)
+    log = open(args.log, "a")
+    Ms = [int(m) for m in args.ms.split(",")]
+    for name, segdef, K, epi in shapes(spec):
+        segs, col = [], 0
+        nbytes = 0
+        for t, rows in segdef:
+            raw = Q.random_blocks(t, rows * K, 0.02, rng)
+            w = ops.QWeight(raw, t, rows, K, dev)
+            nbytes += w.nbytes
+            segs.append(ops.Seg(w, col))
+            col += rows
+        ncol = col // 2 if epi == "swiglu" else col
+        x = torch.randn(64, K, device=dev).to(torch.bfloat16)
+        y = torch.zeros(64, ncol, dtype=torch.bfloat16 if epi == "swiglu" else torch.float32, device=dev)
+        keys = torch.zeros(64, dtype=torch.int64, device=dev)
+        for M in Ms:
+            res = []
+            for cfg in configs(K):
+                us = time_cfg(segs, x, y, M, epi, keys, cfg)
+                if us is not None:
+                    res.append((us, cfg))
+            res.sort()
+            best_us, best = res[0]
+            k = tuning.key(segs, M)
+            table[k] = list(best)
+            line = (f"{name:8s} M={M:3d} best={best} {best_us:8.2f}us {nbytes / best_us / 1e3:7.1f} GB/s | "
+                    + " ".join(f"{c}:{u:.1f}" for u, c in res[:4]))
+            print(line, flush=True)
+            log.write(line + "\n")
+            log.flush()
+        del segs
+        torch.cuda.empty_cache()
+    with open(args.out, "w") as f:
+        json.dump(table, f, indent=0, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
