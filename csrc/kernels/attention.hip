@@ -31,8 +31,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int Hq = Hkv * G;
 
   const int ctx = ctx_len[t];
-  if (chunk <= 0) chunk = max(16, ((ctx + n_split - 1) / n_split + 15) / 16 * 16);   // balanced splits
+  // chunk > 0: fixed; chunk <= 0: balanced over n_split with a minimum of (chunk ? -chunk : 64) keys
+  if (chunk <= 0) {
+    const int mn = chunk ? -chunk : 64;
+    chunk = max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
+  }
   const int start = split * chunk;
+  if (n_split > 1 && start >= ctx && ctx > 0) return;       // inactive split: combine skips it
   const int end = min(ctx, start + chunk);
   const int* bt = block_tables + (size_t)tok_seq[t] * bt_stride;
 
@@ -56,14 +61,43 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int i = 0; i < 8; ++i) o[h][i] = 0.f;
   }
 
+  // Block-table entries are prefetched 64 at a time (one per lane) and broadcast with
+  // shuffles; the K/V rows of step i+1 are in flight while step i is computed.
+  const int b0 = start / bs;
+  const int nblk = (end + bs - 1) / bs;
+  int btw = -1, btreg = 0;
+  // base is wave-uniform, pos = base + stream (per lane)
+  auto slot_of = [&](int pos, int base) -> long {
+    const int win = (base / bs - b0) >> 6;
+    if (win != btw) {
+      btw = win;
+      const int e = b0 + win * 64 + lane;
+      btreg = e < nblk ? bt[e] : 0;
+    }
+    const int bi = pos / bs - b0;
+    int blk = __shfl(btreg, bi & 63, 64);
+    if ((bi >> 6) != win) blk = bt[b0 + bi];      // key straddles the next 64-block window
+    return (long)blk * bs + (pos % bs);
+  };
+  auto kv_off = [&](int pos, int base) -> size_t { return ((size_t)slot_of(pos, base) * Hkv + kh) * D + 8 * dl; };
+
+  u32x4 kr = {0, 0, 0, 0}, vr = {0, 0, 0, 0};
+  if (start < end) {
+    const int p0 = min(start + stream, end - 1);
+    const size_t off = kv_off(p0, start);
+    kr = ld16(kc + off);
+    vr = ld16(vc + off);
+  }
   for (int base = start; base < end; base += NSTREAM) {
     const int pos = base + stream;
     const bool valid = pos < end;
-    const int pc = valid ? pos : start;
-    const long slot = (long)bt[pc / bs] * bs + (pc % bs);
-    const size_t off = ((size_t)slot * Hkv + kh) * D + 8 * dl;
-    const u32x4 kr = ld16(kc + off);
-    const u32x4 vr = ld16(vc + off);
+    u32x4 kn = kr, vn = vr;
+    if (base + NSTREAM < end) {
+      const int pn = min(pos + NSTREAM, end - 1);
+      const size_t off = kv_off(pn, base + NSTREAM);
+      kn = ld16(kc + off);
+      vn = ld16(vc + off);
+    }
     float kf[8], vf[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -93,6 +127,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * c + p * vf[i];
     }
+    kr = kn;
+    vr = vn;
   }
 
   // ---- merge the NSTREAM streams through LDS ----------------------------------
@@ -142,14 +178,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 
 template <int D>
 __global__ void attn_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
-                                    int Hq, int n_split, __bf16* __restrict__ out, long ldo) {
+                                    const int* __restrict__ ctx_len, int Hq, int n_split, int chunk, int bs,
+                                    __bf16* __restrict__ out, long ldo) {
   const int t = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  const int ctx = ctx_len[t];
+  if (chunk <= 0) {
+    const int mn = chunk ? -chunk : 64;
+    chunk = max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
+  }
+  const int na = min(n_split, (ctx + chunk - 1) / chunk);   // active splits (others never wrote)
   const size_t pb = ((size_t)t * Hq + h) * n_split;
   float M = -INFINITY;
-  for (int s = 0; s < n_split; ++s) M = fmaxf(M, part_ml[2 * (pb + s)]);
+  for (int s = 0; s < na; ++s) M = fmaxf(M, part_ml[2 * (pb + s)]);
   float L = 0.f, O = 0.f;
   if (M != -INFINITY) {
-    for (int s = 0; s < n_split; ++s) {
+    for (int s = 0; s < na; ++s) {
       const float ms = part_ml[2 * (pb + s)];
       if (ms == -INFINITY) continue;
       const float f = exp2f(ms - M);
@@ -177,7 +220,9 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
                     int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
                     int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
                     float* part_ml, void* stream) {
-  if (Hq % Hkv || chunk % 16 || n_split < 1) return -1;
+  if (Hq % Hkv || n_split < 1 || (chunk > 0 && chunk % block_size) || 64 % (64 / (D / 8)) ||
+      (4 * 64 / (D / 8)) > 64 * block_size)
+    return -1;
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(T, Hkv, n_split);
@@ -195,11 +240,11 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
 #undef NLS_ATTN_CASE
   if (n_split > 1) {
     if (D == 128)
-      hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, Hq, n_split, o,
-                         ldo);
+      hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
+                         n_split, chunk, block_size, o, ldo);
     else
-      hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(T, Hq), dim3(64), 0, st, part_o, part_ml, Hq, n_split, o,
-                         ldo);
+      hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(T, Hq), dim3(64), 0, st, part_o, part_ml, ctx_len, Hq,
+                         n_split, chunk, block_size, o, ldo);
   }
   return (int)hipGetLastError();
 }

@@ -27,28 +27,36 @@ DEVI float block_sum(float v, float* sh) {
 
 // ---------------------------------------------------------------------------
 // RMSNorm: out_bf16[m] = x[m] * rsqrt(mean(x^2) + eps) * w      (x f32, fp32 accumulate)
+// Single pass: each of the 512 threads keeps its <= 4 float4 of the row in registers
+// (D <= 8192), so the row is read once and the kernel is one reduction deep.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, long ldx,
+__global__ __launch_bounds__(512) void rmsnorm_kernel(const float* __restrict__ x, long ldx,
                                                       const float* __restrict__ w,
                                                       __bf16* __restrict__ out, long ldo, int D,
                                                       float eps) {
-  __shared__ float sh[4];
+  __shared__ float sh[8];
   const float* xr = x + (size_t)blockIdx.x * ldx;
+  float4 v[4];
   float ss = 0.f;
-  for (int i = threadIdx.x * 4; i < D; i += 1024) {
-    const float4 v = *reinterpret_cast<const float4*>(xr + i);
-    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = (threadIdx.x + j * 512) * 4;
+    v[j] = i < D ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    ss += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
   }
-  ss = block_sum<256>(ss, sh);
+  ss = block_sum<512>(ss, sh);
   const float inv = rsqrtf(ss / (float)D + eps);
   __bf16* o = out + (size_t)blockIdx.x * ldo;
-  for (int i = threadIdx.x * 4; i < D; i += 1024) {
-    const float4 v = *reinterpret_cast<const float4*>(xr + i);
-    const float4 ww = *reinterpret_cast<const float4*>(w + i);
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    bf16x4 r = {(__bf16)(v.x * inv * ww.x), (__bf16)(v.y * inv * ww.y), (__bf16)(v.z * inv * ww.z),
-                (__bf16)(v.w * inv * ww.w)};
-    *reinterpret_cast<bf16x4*>(o + i) = r;
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = (threadIdx.x + j * 512) * 4;
+    if (i < D) {
+      const float4 ww = *reinterpret_cast<const float4*>(w + i);
+      bf16x4 r = {(__bf16)(v[j].x * inv * ww.x), (__bf16)(v[j].y * inv * ww.y), (__bf16)(v[j].z * inv * ww.z),
+                  (__bf16)(v[j].w * inv * ww.w)};
+      *reinterpret_cast<bf16x4*>(o + i) = r;
+    }
   }
 }
 
@@ -57,7 +65,7 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
                                                           const float* __restrict__ w,
                                                           float* __restrict__ out, long ldo, int D,
                                                           float eps) {
-  __shared__ float sh[4];
+  __shared__ float sh[8];
   const float* xr = x + (size_t)blockIdx.x * ldx;
   float ss = 0.f;
   for (int i = threadIdx.x; i < D; i += 256) ss += xr[i] * xr[i];
@@ -235,12 +243,12 @@ extern "C" {
 
 int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, int M, int D, float eps,
                 int out_f32, void* stream) {
-  if (D % 4) return -1;
+  if (D % 4 || D > 8192) return -1;
   if (out_f32)
     hipLaunchKernelGGL(rmsnorm_f32_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, x, ldx, w,
                        (float*)out, ldo, D, eps);
   else
-    hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, x, ldx, w,
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, x, ldx, w,
                        (__bf16*)out, ldo, D, eps);
   return (int)hipGetLastError();
 }

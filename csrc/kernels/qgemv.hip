@@ -78,18 +78,23 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // weight stream: two super-blocks in flight ahead of the one being computed
   typedef typename RawOf<T>::type Raw;
-  Raw cur[RT];
+  Raw cur[RT], nx1[RT];
   if (sb0 < sb1) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) cur[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
   }
+  if (sb0 + 1 < sb1) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) nx1[rt] = load_raw<T, true>(W, rowc[rt], sb0 + 1, g);
+  }
   const bf16x8 zero8 = {};
   for (int sb = sb0; sb < sb1; ++sb) {
-    Raw nxt[RT];
-    if (sb + 1 < sb1) {
+    Raw nx2[RT];
+    if (sb + 2 < sb1) {
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) nxt[rt] = load_raw<T, true>(W, rowc[rt], sb + 1, g);
+      for (int rt = 0; rt < RT; ++rt) nx2[rt] = load_raw<T, true>(W, rowc[rt], sb + 2, g);
     }
     bf16x8 wf[RT][8];
 #pragma unroll
@@ -105,9 +110,10 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
           acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
       }
     }
-    if (sb + 1 < sb1) {
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
+    for (int rt = 0; rt < RT; ++rt) {
+      cur[rt] = nx1[rt];
+      nx1[rt] = nx2[rt];
     }
   }
 
@@ -268,22 +274,26 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   typedef typename RawOf<T>::type Raw;
-  Raw cur[RT];
+  Raw cur[RT], nx1[RT];
   if (sb0 < sb1) {
     load_x(sb0);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) cur[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
     store_x(0);
   }
+  if (sb0 + 1 < sb1) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) nx1[rt] = load_raw<T, true>(W, rowc[rt], sb0 + 1, g);
+  }
   __syncthreads();
   for (int sb = sb0; sb < sb1; ++sb) {
     const int buf = (sb - sb0) & 1;
     const bool more = sb + 1 < sb1;
-    Raw nxt[RT];
-    if (more) {
-      load_x(sb + 1);
+    Raw nx2[RT];
+    if (more) load_x(sb + 1);
+    if (sb + 2 < sb1) {
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) nxt[rt] = load_raw<T, true>(W, rowc[rt], sb + 1, g);
+      for (int rt = 0; rt < RT; ++rt) nx2[rt] = load_raw<T, true>(W, rowc[rt], sb + 2, g);
     }
     bf16x8 wf[RT][8];
 #pragma unroll
@@ -300,10 +310,11 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
       }
     }
-    if (more) {
-      store_x(buf ^ 1);
+    if (more) store_x(buf ^ 1);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
+    for (int rt = 0; rt < RT; ++rt) {
+      cur[rt] = nx1[rt];
+      nx1[rt] = nx2[rt];
     }
     __syncthreads();
   }

@@ -156,28 +156,28 @@ def test_rope_kv(gpu, neox):
 
 
 @pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1)])
-@pytest.mark.parametrize("n_split", [1, 4, 32])
-def test_attention_paged(gpu, D, G, n_split):
+@pytest.mark.parametrize("n_split,chunk", [(1, 0), (4, 0), (32, 0), (8, -16), (3, 128)])
+def test_attention_paged(gpu, D, G, n_split, chunk):
     Hkv = 2
     Hq = Hkv * G
     bs = 16
-    ctx = [1, 17, 300, 0, 64]
+    ctx = [1, 17, 300, 0, 64, 1500]
     T = len(ctx)
-    nblk = 64
-    kc = torch.randn(nblk * bs, Hkv, D).to(torch.bfloat16)
-    vc = torch.randn(nblk * bs, Hkv, D).to(torch.bfloat16)
-    perm = torch.randperm(nblk).to(torch.int32)
-    bt = torch.zeros(T, 20, dtype=torch.int32)
+    nblk = 256
+    g = torch.Generator().manual_seed(0)
+    kc = torch.randn(nblk * bs, Hkv, D, generator=g).to(torch.bfloat16)
+    vc = torch.randn(nblk * bs, Hkv, D, generator=g).to(torch.bfloat16)
+    bt = torch.zeros(T, 100, dtype=torch.int32)
     for i in range(T):
-        bt[i] = perm[(i * 7) % 40:(i * 7) % 40 + 20]
-    q = torch.randn(T, Hq * D).to(torch.bfloat16)
+        bt[i] = torch.randperm(nblk, generator=g)[:100].to(torch.int32)
+    q = torch.randn(T, Hq * D, generator=g).to(torch.bfloat16)
     ts = torch.arange(T, dtype=torch.int32)
     cl = torch.tensor(ctx, dtype=torch.int32)
     ref = torch.zeros(T, Hq * D, dtype=torch.bfloat16)
     ops.attention(q, kc, vc, bt, ts, cl, ref, T, Hq, Hkv, D, bs, D ** -0.5)
     out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=gpu)
     ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), ts.to(gpu), cl.to(gpu), out, T, Hq, Hkv, D, bs,
-                  D ** -0.5, chunk=0, n_split=n_split)
+                  D ** -0.5, chunk=chunk, n_split=n_split)
     torch.testing.assert_close(out.cpu().float(), ref.float(), rtol=2e-2, atol=2e-2)
 
 
