@@ -156,7 +156,7 @@ def test_rope_kv(gpu, neox):
 
 
 @pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1)])
-@pytest.mark.parametrize("n_split,chunk", [(1, 0), (4, 0), (32, 0), (8, -16), (3, 128)])
+@pytest.mark.parametrize("n_split,chunk", [(1, 0), (4, 0), (32, 0), (8, -16), (3, 512)])
 def test_attention_paged(gpu, D, G, n_split, chunk):
     Hkv = 2
     Hq = Hkv * G
