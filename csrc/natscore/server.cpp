@@ -1,0 +1,672 @@
+#include "server.h"
+
+#include <dirent.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <ctime>
+#include <fstream>
+
+namespace natscore {
+
+namespace {
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
+std::string rfc3339(int64_t ns);   // defined in objstore.cpp
+
+struct Server::Conn {
+  int fd = -1;
+  uint64_t id = 0;
+  std::mutex wmu;
+  std::atomic<bool> alive{true};
+  bool headers = false, no_responders = false, verbose = false, echo = true;
+  std::thread th;
+  bool write(const std::string& s) {
+    std::lock_guard<std::mutex> g(wmu);
+    if (!alive) return false;
+    if (!send_all(fd, s.data(), s.size())) {
+      alive = false;
+      ::shutdown(fd, SHUT_RDWR);   // unblock the reader so the connection can be reaped
+      return false;
+    }
+    return true;
+  }
+};
+
+struct Server::Sub {
+  std::shared_ptr<Conn> conn;
+  std::string subject, queue, sid;
+  long max = 0;
+  std::atomic<long> delivered{0};
+};
+
+Server::Server(ServerOptions o) : opt_(std::move(o)) { server_id_ = "N" + nuid_next(); }
+
+Server::~Server() { stop(); }
+
+int Server::start() {
+  if (running_) return port_;
+  if (!opt_.store_dir.empty()) {
+    mkdir(opt_.store_dir.c_str(), 0755);
+    load_store();
+  }
+  lfd_ = tcp_listen(opt_.host, opt_.port, &port_);
+  if (lfd_ < 0) throw std::runtime_error("natscore server: cannot listen on " + opt_.host + ":" +
+                                         std::to_string(opt_.port));
+  running_ = true;
+  accept_th_ = std::thread([this] { accept_loop(); });
+  return port_;
+}
+
+void Server::stop() {
+  if (!running_.exchange(false)) return;
+  ::shutdown(lfd_, SHUT_RDWR);
+  ::close(lfd_);
+  if (accept_th_.joinable()) accept_th_.join();
+  std::vector<std::shared_ptr<Conn>> cs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    cs = conns_;
+  }
+  for (auto& c : cs) {
+    c->alive = false;
+    ::shutdown(c->fd, SHUT_RDWR);
+  }
+  for (auto& c : cs)
+    if (c->th.joinable()) c->th.join();
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& c : conns_) ::close(c->fd);
+  conns_.clear();
+  subs_.clear();
+}
+
+void Server::set_fault(double drop_rate, int delay_ms) {
+  drop_rate_ = drop_rate;
+  delay_ms_ = delay_ms;
+}
+
+void Server::disconnect_all() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& c : conns_) ::shutdown(c->fd, SHUT_RDWR);
+}
+
+std::string Server::stats_json() {
+  Json j = Json::O();
+  size_t nc, ns;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    nc = conns_.size();
+    ns = subs_.size();
+  }
+  j.set("server_id", Json::S(server_id_));
+  j.set("port", Json::N(port_));
+  j.set("connections", Json::N((double)nc));
+  j.set("subscriptions", Json::N((double)ns));
+  j.set("in_msgs", Json::N((double)in_msgs_));
+  j.set("out_msgs", Json::N((double)out_msgs_));
+  j.set("in_bytes", Json::N((double)in_bytes_));
+  j.set("out_bytes", Json::N((double)out_bytes_));
+  std::lock_guard<std::mutex> g(js_mu_);
+  j.set("streams", Json::N((double)streams_.size()));
+  return j.dump();
+}
+
+void Server::accept_loop() {
+  while (running_) {
+    int fd = ::accept(lfd_, nullptr, nullptr);
+    if (fd < 0) {
+      if (!running_) break;
+      continue;
+    }
+    auto c = std::make_shared<Conn>();
+    c->fd = fd;
+    c->id = next_cid_++;
+    std::vector<std::shared_ptr<Conn>> dead;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto it = conns_.begin(); it != conns_.end();) {
+        if (!(*it)->alive) { dead.push_back(*it); it = conns_.erase(it); }
+        else ++it;
+      }
+      conns_.push_back(c);
+    }
+    for (auto& d : dead) {      // reap finished connection threads
+      if (d->th.joinable()) d->th.join();
+      ::close(d->fd);
+    }
+    Json info = Json::O();
+    info.set("server_id", Json::S(server_id_));
+    info.set("server_name", Json::S(opt_.server_name));
+    info.set("version", Json::S("2.10.12-natscore"));
+    info.set("proto", Json::N(1));
+    info.set("host", Json::S(opt_.host));
+    info.set("port", Json::N(port_));
+    info.set("headers", Json::B(true));
+    info.set("max_payload", Json::N((double)opt_.max_payload));
+    info.set("jetstream", Json::B(opt_.jetstream));
+    info.set("client_id", Json::N((double)c->id));
+    c->write("INFO " + info.dump() + "\r\n");
+    c->th = std::thread([this, c] { conn_loop(c); });
+  }
+}
+
+void Server::conn_loop(std::shared_ptr<Conn> c) {
+  Parser p(opt_.max_payload);
+  char buf[256 * 1024];
+  while (c->alive && running_) {
+    ssize_t n = ::recv(c->fd, buf, sizeof buf, 0);
+    if (n <= 0) break;
+    bool ok = p.feed(buf, (size_t)n, [&](Op& op) { handle(c, op); });
+    if (!ok) {
+      c->write("-ERR '" + p.error() + "'\r\n");
+      break;
+    }
+  }
+  c->alive = false;
+  ::shutdown(c->fd, SHUT_RDWR);
+  std::lock_guard<std::mutex> g(mu_);
+  subs_.erase(std::remove_if(subs_.begin(), subs_.end(), [&](const std::shared_ptr<Sub>& s) { return s->conn == c; }),
+              subs_.end());
+  // the Conn object stays in conns_ until stop() (its thread handle must be joined there)
+}
+
+void Server::handle(const std::shared_ptr<Conn>& c, Op& op) {
+  switch (op.kind) {
+    case Op::CONNECT: {
+      try {
+        Json j = Json::parse(op.arg);
+        c->headers = j.boolean("headers", false);
+        c->no_responders = j.boolean("no_responders", false);
+        c->verbose = j.boolean("verbose", false);
+        c->echo = j.boolean("echo", true);
+      } catch (...) {
+        c->write("-ERR 'Invalid CONNECT'\r\n");
+        return;
+      }
+      if (c->verbose) c->write("+OK\r\n");
+      break;
+    }
+    case Op::PING: c->write("PONG\r\n"); break;
+    case Op::PONG: break;
+    case Op::SUB: {
+      if (!valid_subject(op.subject, true)) {
+        c->write("-ERR 'Invalid Subject'\r\n");
+        return;
+      }
+      auto s = std::make_shared<Sub>();
+      s->conn = c;
+      s->subject = op.subject;
+      s->queue = op.queue;
+      s->sid = op.sid;
+      std::lock_guard<std::mutex> g(mu_);
+      subs_.push_back(s);
+      if (c->verbose) c->write("+OK\r\n");
+      break;
+    }
+    case Op::UNSUB: {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto it = subs_.begin(); it != subs_.end(); ++it) {
+        if ((*it)->conn == c && (*it)->sid == op.sid) {
+          if (op.max_msgs > 0 && (*it)->delivered < op.max_msgs) (*it)->max = op.max_msgs;
+          else subs_.erase(it);
+          break;
+        }
+      }
+      if (c->verbose) c->write("+OK\r\n");
+      break;
+    }
+    case Op::PUB:
+    case Op::HPUB: {
+      if (!valid_subject(op.subject, false)) {
+        c->write("-ERR 'Invalid Publish Subject'\r\n");
+        return;
+      }
+      in_msgs_++;
+      in_bytes_ += op.payload.size() + op.hdr.size();
+      if (c->verbose) c->write("+OK\r\n");
+      const double dr = drop_rate_;
+      if (dr > 0) {
+        std::uniform_real_distribution<double> u(0, 1);
+        double x;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          x = u(rng_);
+        }
+        if (x < dr) return;   // fault injection: message lost in transit
+      }
+      const int dl = delay_ms_;
+      if (dl > 0) std::this_thread::sleep_for(std::chrono::milliseconds(dl));
+      route(op.subject, op.reply, op.hdr, op.payload, c.get());
+      break;
+    }
+    default: break;
+  }
+}
+
+void Server::respond(const std::string& reply, const std::string& body) {
+  if (!reply.empty()) route(reply, "", "", body, nullptr);
+}
+
+void Server::route(const std::string& subj, const std::string& reply, const std::string& hdr,
+                   const std::string& payload, Conn* from) {
+  bool handled = false;
+  if (opt_.jetstream) {
+    if (subj.rfind("$JS.API.", 0) == 0) handled = js_handle(subj, reply, hdr, payload);
+    else handled = js_capture(subj, reply, hdr, payload);
+  }
+  std::vector<std::shared_ptr<Sub>> targets;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    std::map<std::string, std::vector<std::shared_ptr<Sub>>> groups;
+    for (auto& s : subs_) {
+      if (!s->conn->alive || !subject_matches(s->subject, subj)) continue;
+      if (from && !s->conn->echo && s->conn.get() == from) continue;
+      if (s->queue.empty()) targets.push_back(s);
+      else groups[s->queue].push_back(s);
+    }
+    for (auto& kv : groups) {
+      std::uniform_int_distribution<size_t> d(0, kv.second.size() - 1);
+      targets.push_back(kv.second[d(rng_)]);
+    }
+  }
+  for (auto& s : targets) {
+    std::string m;
+    const bool h = !hdr.empty() && s->conn->headers;
+    const size_t total = (h ? hdr.size() : 0) + payload.size();
+    m.reserve(total + subj.size() + reply.size() + 64);
+    if (h) {
+      m = "HMSG " + subj + " " + s->sid + (reply.empty() ? "" : " " + reply) + " " + std::to_string(hdr.size()) +
+          " " + std::to_string(total) + "\r\n";
+      m += hdr;
+    } else {
+      m = "MSG " + subj + " " + s->sid + (reply.empty() ? "" : " " + reply) + " " + std::to_string(payload.size()) +
+          "\r\n";
+    }
+    m += payload;
+    m += "\r\n";
+    if (s->conn->write(m)) {
+      out_msgs_++;
+      out_bytes_ += total;
+    }
+    long d = ++s->delivered;
+    if (s->max > 0 && d >= s->max) {
+      std::lock_guard<std::mutex> g(mu_);
+      subs_.erase(std::remove(subs_.begin(), subs_.end(), s), subs_.end());
+    }
+  }
+  if (targets.empty() && !handled && !reply.empty() && from && from->headers && from->no_responders)
+    route(reply, "", "NATS/1.0 503\r\n\r\n", "", nullptr);
+}
+
+// ============================ JetStream subset ================================
+
+Json Server::stream_info(const Stream& s) {
+  Json j = Json::O();
+  j.set("config", s.config);
+  j.set("created", Json::S(rfc3339(s.created_ns)));
+  Json st = Json::O();
+  st.set("messages", Json::N((double)s.msgs.size()));
+  st.set("bytes", Json::N((double)s.bytes));
+  st.set("first_seq", Json::N(s.msgs.empty() ? (double)(s.last_seq + 1) : (double)s.msgs.begin()->first));
+  st.set("last_seq", Json::N((double)s.last_seq));
+  st.set("consumer_count", Json::N(0));
+  j.set("state", st);
+  return j;
+}
+
+static std::string js_error(int code, int err_code, const std::string& desc, const std::string& type) {
+  Json j = Json::O();
+  j.set("type", Json::S(type));
+  Json e = Json::O();
+  e.set("code", Json::N(code));
+  e.set("err_code", Json::N(err_code));
+  e.set("description", Json::S(desc));
+  j.set("error", e);
+  return j.dump();
+}
+
+void Server::store_msg(Stream& s, const std::string& subj, const std::string& hdr, const std::string& data,
+                       bool log) {
+  StoredMsg m{++s.last_seq, subj, hdr, data, now_ns()};
+  s.bytes += subj.size() + hdr.size() + data.size();
+  auto it = s.msgs.emplace(m.seq, std::move(m)).first;
+  if (log) persist(s, 'M', &it->second, "");
+}
+
+void Server::purge(Stream& s, const std::string& filter, uint64_t* n, bool log) {
+  uint64_t cnt = 0;
+  for (auto it = s.msgs.begin(); it != s.msgs.end();) {
+    if (filter.empty() || subject_matches(filter, it->second.subject)) {
+      s.bytes -= it->second.subject.size() + it->second.hdr.size() + it->second.data.size();
+      it = s.msgs.erase(it);
+      ++cnt;
+    } else {
+      ++it;
+    }
+  }
+  if (n) *n = cnt;
+  if (log) persist(s, 'P', nullptr, filter);
+}
+
+bool Server::js_capture(const std::string& subj, const std::string& reply, const std::string& hdr,
+                        const std::string& payload) {
+  std::string ack;
+  {
+    std::lock_guard<std::mutex> g(js_mu_);
+    for (auto& kv : streams_) {
+      Stream& s = *kv.second;
+      bool match = false;
+      for (auto& p : s.subjects)
+        if (subject_matches(p, subj)) { match = true; break; }
+      if (!match) continue;
+      if (!hdr.empty()) {
+        Headers h = parse_headers(hdr);
+        if (h.get("Nats-Rollup") == "sub") {
+          // rollup replaces every earlier message on this exact subject
+          for (auto it = s.msgs.begin(); it != s.msgs.end();) {
+            if (it->second.subject == subj) {
+              s.bytes -= it->second.subject.size() + it->second.hdr.size() + it->second.data.size();
+              it = s.msgs.erase(it);
+            } else {
+              ++it;
+            }
+          }
+          persist(s, 'P', nullptr, subj);
+        }
+      }
+      store_msg(s, subj, hdr, payload, true);
+      Json a = Json::O();
+      a.set("stream", Json::S(s.name));
+      a.set("seq", Json::N((double)s.last_seq));
+      ack = a.dump();
+      break;
+    }
+  }
+  if (ack.empty()) return false;
+  respond(reply, ack);
+  return true;
+}
+
+bool Server::js_handle(const std::string& subj, const std::string& reply, const std::string& hdr,
+                       const std::string& payload) {
+  (void)hdr;
+  const std::string api = subj.substr(8);   // after "$JS.API."
+  auto tail = [&](const std::string& pre) -> std::string {
+    return api.rfind(pre, 0) == 0 ? api.substr(pre.size()) : std::string();
+  };
+  Json req;
+  if (!payload.empty()) {
+    try {
+      req = Json::parse(payload);
+    } catch (...) {
+      respond(reply, js_error(400, 10025, "bad request", "io.nats.jetstream.api.v1.error"));
+      return true;
+    }
+  }
+  std::string out;
+  {
+    std::lock_guard<std::mutex> g(js_mu_);
+    if (api == "INFO") {
+      Json j = Json::O();
+      j.set("type", Json::S("io.nats.jetstream.api.v1.account_info_response"));
+      uint64_t bytes = 0;
+      for (auto& kv : streams_) bytes += kv.second->bytes;
+      j.set("memory", Json::N(opt_.store_dir.empty() ? (double)bytes : 0));
+      j.set("storage", Json::N(opt_.store_dir.empty() ? 0 : (double)bytes));
+      j.set("streams", Json::N((double)streams_.size()));
+      j.set("consumers", Json::N(0));
+      out = j.dump();
+    } else if (!tail("STREAM.CREATE.").empty() || !tail("STREAM.UPDATE.").empty()) {
+      const bool create = !tail("STREAM.CREATE.").empty();
+      std::string name = create ? tail("STREAM.CREATE.") : tail("STREAM.UPDATE.");
+      if (req.str("name", name) != name) {
+        out = js_error(400, 10058, "stream name in subject does not match request",
+                       "io.nats.jetstream.api.v1.stream_create_response");
+      } else {
+        auto it = streams_.find(name);
+        bool did = false;
+        if (it == streams_.end()) {
+          if (!create) {
+            out = js_error(404, 10059, "stream not found", "io.nats.jetstream.api.v1.stream_update_response");
+          } else {
+            auto s = std::make_unique<Stream>();
+            s->name = name;
+            s->created_ns = now_ns();
+            it = streams_.emplace(name, std::move(s)).first;
+            did = true;
+          }
+        }
+        if (out.empty()) {
+          Stream& s = *it->second;
+          Json cfg = req.t == Json::OBJ ? req : Json::O();
+          cfg.set("name", Json::S(name));
+          s.subjects.clear();
+          if (auto* sj = cfg.get("subjects"))
+            for (auto& v : sj->a)
+              if (v.t == Json::STR) s.subjects.push_back(v.s);
+          if (s.subjects.empty()) {
+            s.subjects.push_back(name);
+            Json arr = Json::A();
+            arr.a.push_back(Json::S(name));
+            cfg.set("subjects", arr);
+          }
+          s.config = cfg;
+          persist_config(s);
+          Json j = stream_info(s);
+          j.set("type", Json::S(create ? "io.nats.jetstream.api.v1.stream_create_response"
+                                       : "io.nats.jetstream.api.v1.stream_update_response"));
+          j.set("did_create", Json::B(did));
+          out = j.dump();
+        }
+      }
+    } else if (!tail("STREAM.INFO.").empty()) {
+      auto it = streams_.find(tail("STREAM.INFO."));
+      if (it == streams_.end()) {
+        out = js_error(404, 10059, "stream not found", "io.nats.jetstream.api.v1.stream_info_response");
+      } else {
+        Json j = stream_info(*it->second);
+        j.set("type", Json::S("io.nats.jetstream.api.v1.stream_info_response"));
+        out = j.dump();
+      }
+    } else if (api == "STREAM.NAMES" || api == "STREAM.LIST") {
+      Json j = Json::O();
+      j.set("type", Json::S(api == "STREAM.NAMES" ? "io.nats.jetstream.api.v1.stream_names_response"
+                                                  : "io.nats.jetstream.api.v1.stream_list_response"));
+      Json arr = Json::A();
+      for (auto& kv : streams_) arr.a.push_back(api == "STREAM.NAMES" ? Json::S(kv.first) : stream_info(*kv.second));
+      j.set("total", Json::N((double)streams_.size()));
+      j.set("offset", Json::N(0));
+      j.set("limit", Json::N(1024));
+      j.set("streams", arr);
+      out = j.dump();
+    } else if (!tail("STREAM.DELETE.").empty()) {
+      auto it = streams_.find(tail("STREAM.DELETE."));
+      if (it == streams_.end()) {
+        out = js_error(404, 10059, "stream not found", "io.nats.jetstream.api.v1.stream_delete_response");
+      } else {
+        persist(*it->second, 'X', nullptr, "");
+        streams_.erase(it);
+        out = "{\"type\":\"io.nats.jetstream.api.v1.stream_delete_response\",\"success\":true}";
+      }
+    } else if (!tail("STREAM.PURGE.").empty()) {
+      auto it = streams_.find(tail("STREAM.PURGE."));
+      if (it == streams_.end()) {
+        out = js_error(404, 10059, "stream not found", "io.nats.jetstream.api.v1.stream_purge_response");
+      } else {
+        uint64_t n = 0;
+        purge(*it->second, req.str("filter"), &n, true);
+        out = "{\"type\":\"io.nats.jetstream.api.v1.stream_purge_response\",\"success\":true,\"purged\":" +
+              std::to_string(n) + "}";
+      }
+    } else if (!tail("STREAM.MSG.GET.").empty()) {
+      auto it = streams_.find(tail("STREAM.MSG.GET."));
+      const std::string T = "io.nats.jetstream.api.v1.stream_msg_get_response";
+      if (it == streams_.end()) {
+        out = js_error(404, 10059, "stream not found", T);
+      } else {
+        Stream& s = *it->second;
+        const StoredMsg* found = nullptr;
+        const std::string last = req.str("last_by_subj"), next = req.str("next_by_subj");
+        const uint64_t seq = (uint64_t)req.num("seq", 0);
+        if (!last.empty()) {
+          for (auto r = s.msgs.rbegin(); r != s.msgs.rend(); ++r)
+            if (subject_matches(last, r->second.subject)) { found = &r->second; break; }
+        } else if (!next.empty()) {
+          for (auto f = s.msgs.lower_bound(seq); f != s.msgs.end(); ++f)
+            if (subject_matches(next, f->second.subject)) { found = &f->second; break; }
+        } else {
+          auto f = s.msgs.find(seq);
+          if (f != s.msgs.end()) found = &f->second;
+        }
+        if (!found) {
+          out = js_error(404, 10037, "no message found", T);
+        } else {
+          Json m = Json::O();
+          m.set("subject", Json::S(found->subject));
+          m.set("seq", Json::N((double)found->seq));
+          if (!found->hdr.empty()) m.set("hdrs", Json::S(b64encode(found->hdr)));
+          m.set("data", Json::S(b64encode(found->data)));
+          m.set("time", Json::S(rfc3339(found->time_ns)));
+          Json j = Json::O();
+          j.set("type", Json::S(T));
+          j.set("message", m);
+          out = j.dump();
+        }
+      }
+    } else if (!tail("STREAM.MSG.DELETE.").empty()) {
+      auto it = streams_.find(tail("STREAM.MSG.DELETE."));
+      if (it == streams_.end()) {
+        out = js_error(404, 10059, "stream not found", "io.nats.jetstream.api.v1.stream_msg_delete_response");
+      } else {
+        Stream& s = *it->second;
+        uint64_t seq = (uint64_t)req.num("seq", 0);
+        auto f = s.msgs.find(seq);
+        if (f == s.msgs.end()) {
+          out = js_error(400, 10057, "no message found", "io.nats.jetstream.api.v1.stream_msg_delete_response");
+        } else {
+          s.bytes -= f->second.subject.size() + f->second.hdr.size() + f->second.data.size();
+          s.msgs.erase(f);
+          persist(s, 'D', nullptr, std::to_string(seq));
+          out = "{\"type\":\"io.nats.jetstream.api.v1.stream_msg_delete_response\",\"success\":true}";
+        }
+      }
+    } else {
+      out = js_error(501, 10000, "not supported by the embedded server: " + api, "io.nats.jetstream.api.v1.error");
+    }
+  }
+  respond(reply, out);
+  return true;
+}
+
+// ---- persistence: <store_dir>/<stream>.cfg (JSON) + <stream>.log (binary records) ----
+static void put_u64(std::string& b, uint64_t v) { b.append((const char*)&v, 8); }
+static void put_str(std::string& b, const std::string& s) {
+  put_u64(b, s.size());
+  b += s;
+}
+
+void Server::persist_config(const Stream& s) {
+  if (opt_.store_dir.empty()) return;
+  std::ofstream f(opt_.store_dir + "/" + s.name + ".cfg", std::ios::trunc);
+  f << s.config.dump();
+}
+
+void Server::persist(const Stream& s, char kind, const StoredMsg* m, const std::string& arg) {
+  if (opt_.store_dir.empty()) return;
+  const std::string base = opt_.store_dir + "/" + s.name;
+  if (kind == 'X') {
+    ::unlink((base + ".cfg").c_str());
+    ::unlink((base + ".log").c_str());
+    return;
+  }
+  std::string rec(1, kind);
+  if (m) {
+    put_u64(rec, m->seq);
+    put_u64(rec, (uint64_t)m->time_ns);
+    put_str(rec, m->subject);
+    put_str(rec, m->hdr);
+    put_str(rec, m->data);
+  } else {
+    put_str(rec, arg);
+  }
+  FILE* f = fopen((base + ".log").c_str(), "ab");
+  if (f) {
+    fwrite(rec.data(), 1, rec.size(), f);
+    fclose(f);
+  }
+}
+
+void Server::load_store() {
+  std::string cmd_dir = opt_.store_dir;
+  // enumerate *.cfg files
+  std::vector<std::string> names;
+  if (auto* d = opendir(cmd_dir.c_str())) {
+    while (auto* e = readdir(d)) {
+      std::string n = e->d_name;
+      if (n.size() > 4 && n.substr(n.size() - 4) == ".cfg") names.push_back(n.substr(0, n.size() - 4));
+    }
+    closedir(d);
+  }
+  for (auto& name : names) {
+    std::ifstream cf(cmd_dir + "/" + name + ".cfg");
+    std::string txt((std::istreambuf_iterator<char>(cf)), std::istreambuf_iterator<char>());
+    auto s = std::make_unique<Stream>();
+    s->name = name;
+    s->created_ns = now_ns();
+    try {
+      s->config = Json::parse(txt);
+    } catch (...) {
+      continue;
+    }
+    if (auto* sj = s->config.get("subjects"))
+      for (auto& v : sj->a) s->subjects.push_back(v.s);
+    FILE* f = fopen((cmd_dir + "/" + name + ".log").c_str(), "rb");
+    if (f) {
+      auto rd64 = [&](uint64_t& v) { return fread(&v, 8, 1, f) == 1; };
+      auto rds = [&](std::string& out) {
+        uint64_t n;
+        if (!rd64(n)) return false;
+        out.resize(n);
+        return n == 0 || fread(&out[0], 1, n, f) == n;
+      };
+      int kind;
+      while ((kind = fgetc(f)) != EOF) {
+        if (kind == 'M') {
+          StoredMsg m;
+          uint64_t t;
+          if (!rd64(m.seq) || !rd64(t) || !rds(m.subject) || !rds(m.hdr) || !rds(m.data)) break;
+          m.time_ns = (int64_t)t;
+          s->last_seq = std::max(s->last_seq, m.seq);
+          s->bytes += m.subject.size() + m.hdr.size() + m.data.size();
+          s->msgs.emplace(m.seq, std::move(m));
+        } else if (kind == 'P') {
+          std::string filt;
+          if (!rds(filt)) break;
+          purge(*s, filt, nullptr, false);
+        } else if (kind == 'D') {
+          std::string a;
+          if (!rds(a)) break;
+          auto it = s->msgs.find(std::stoull(a));
+          if (it != s->msgs.end()) {
+            s->bytes -= it->second.subject.size() + it->second.hdr.size() + it->second.data.size();
+            s->msgs.erase(it);
+          }
+        } else {
+          break;
+        }
+      }
+      fclose(f);
+    }
+    streams_.emplace(name, std::move(s));
+  }
+}
+
+}  // namespace natscore

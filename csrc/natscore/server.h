@@ -1,0 +1,96 @@
+// Embedded NATS server (tests, single-box benchmarks, the GPU box which has no
+// nats-server binary): core pub/sub with `*`/`>` wildcards, queue groups, request-reply
+// with no-responders (503) status, headers, max_payload enforcement, PING/PONG, and a
+// JetStream subset sufficient for the Object Store (streams, publish acks, rollup,
+// purge, direct message get incl. next_by_subj, optional file persistence).
+// Fault-injection hooks (drop/delay/disconnect) back the failure-detection tests.
+#pragma once
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "proto.h"
+#include "util.h"
+
+namespace natscore {
+
+struct ServerOptions {
+  std::string host = "127.0.0.1";
+  int port = 0;                       // 0 = ephemeral
+  size_t max_payload = 1 << 20;       // nats-server default 1 MiB
+  bool jetstream = true;
+  std::string store_dir;              // "" = memory only
+  std::string server_name = "natscore";
+};
+
+class Server {
+ public:
+  explicit Server(ServerOptions o);
+  ~Server();
+  int start();
+  void stop();
+  int port() const { return port_; }
+  bool running() const { return running_; }
+  void set_fault(double drop_rate, int delay_ms);
+  void disconnect_all();
+  std::string stats_json();
+
+ private:
+  struct Conn;
+  struct Sub;
+  struct StoredMsg {
+    uint64_t seq;
+    std::string subject, hdr, data;
+    int64_t time_ns;
+  };
+  struct Stream {
+    std::string name;
+    Json config;
+    std::vector<std::string> subjects;
+    std::map<uint64_t, StoredMsg> msgs;
+    uint64_t last_seq = 0;
+    uint64_t bytes = 0;
+    int64_t created_ns = 0;
+  };
+
+  void accept_loop();
+  void conn_loop(std::shared_ptr<Conn> c);
+  void handle(const std::shared_ptr<Conn>& c, Op& op);
+  void route(const std::string& subj, const std::string& reply, const std::string& hdr,
+             const std::string& payload, Conn* from);
+  bool js_handle(const std::string& subj, const std::string& reply, const std::string& hdr,
+                 const std::string& payload);
+  bool js_capture(const std::string& subj, const std::string& reply, const std::string& hdr,
+                  const std::string& payload);
+  void respond(const std::string& reply, const std::string& body);
+  Json stream_info(const Stream& s);
+  void persist(const Stream& s, char kind, const StoredMsg* m, const std::string& arg);
+  void persist_config(const Stream& s);
+  void load_store();
+  void store_msg(Stream& s, const std::string& subj, const std::string& hdr, const std::string& data, bool log);
+  void purge(Stream& s, const std::string& filter, uint64_t* n, bool log);
+
+  ServerOptions opt_;
+  int lfd_ = -1;
+  int port_ = 0;
+  std::atomic<bool> running_{false};
+  std::thread accept_th_;
+  std::mutex mu_;                                 // conns + subs
+  std::vector<std::shared_ptr<Conn>> conns_;
+  std::vector<std::shared_ptr<Sub>> subs_;
+  std::mutex js_mu_;
+  std::map<std::string, std::unique_ptr<Stream>> streams_;
+  std::mt19937 rng_{12345};
+  std::atomic<uint64_t> next_cid_{1};
+  std::atomic<double> drop_rate_{0.0};
+  std::atomic<int> delay_ms_{0};
+  std::atomic<uint64_t> in_msgs_{0}, out_msgs_{0}, in_bytes_{0}, out_bytes_{0};
+  std::string server_id_;
+};
+
+}  // namespace natscore

@@ -1,0 +1,219 @@
+"""Chat backends behind `lmstudio.chat_model`.
+
+* `EngineBackend` -- the co-located GPU engine (JIT load on first chat like LM Studio,
+  LRU unload, continuous batching across concurrent requests).
+* `StubBackend`  -- CPU echo backend (BASELINE config 1: "embedded nats-server with CPU stub
+  backend (granite-3.0-2b echo), no GPU"), same response shape, no model weights.
+
+Both produce LM Studio `/api/v0/chat/completions` bodies (what the reference embeds raw
+under data.response, `/root/reference/nats_llm_studio.go:356-363`).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+import time
+import uuid
+from typing import Callable, Dict, Optional
+
+from .. import __version__
+from .registry import ModelEntry
+
+Done = Callable[[int, dict], None]      # (http_status, body)
+
+
+def _error_body(msg: str) -> dict:
+    return {"error": msg}
+
+
+def chat_response(model_id: str, entry: Optional[ModelEntry], text: str, prompt_tokens: int,
+                  completion_tokens: int, finish_reason: str, stop_reason: str, ttft: float, gen_time: float,
+                  ctx: int, arch: str = "", quant: str = "") -> dict:
+    tps = completion_tokens / gen_time if gen_time > 0 else 0.0
+    return {
+        "id": f"chatcmpl-{uuid.uuid4().hex[:24]}",
+        "object": "chat.completion",
+        "created": int(time.time()),
+        "model": model_id,
+        "choices": [{"index": 0, "logprobs": None, "finish_reason": finish_reason,
+                     "message": {"role": "assistant", "content": text}}],
+        "usage": {"prompt_tokens": prompt_tokens, "completion_tokens": completion_tokens,
+                  "total_tokens": prompt_tokens + completion_tokens},
+        "stats": {"tokens_per_second": round(tps, 3), "time_to_first_token": round(ttft, 6),
+                  "generation_time": round(gen_time, 6), "stop_reason": stop_reason},
+        "model_info": {"arch": arch or (entry.arch if entry else ""),
+                       "quant": quant or (entry.quantization if entry else ""),
+                       "format": "gguf", "context_length": ctx},
+        "runtime": {"name": "nats-llm-studio-amd", "version": __version__, "supported_formats": ["gguf"]},
+    }
+
+
+def _messages(req: dict):
+    msgs = req.get("messages")
+    if not isinstance(msgs, list) or not msgs:
+        raise ValueError("'messages' must be a non-empty array")
+    for m in msgs:
+        if not isinstance(m, dict) or "role" not in m:
+            raise ValueError("each message needs a 'role'")
+    return msgs
+
+
+class StubBackend:
+    """Echo backend: returns the last user message (token counts = whitespace words)."""
+
+    name = "stub"
+
+    def __init__(self, default_model: str = "granite-3.0-2b-instruct"):
+        self.default_model = default_model
+        self.requests = 0
+
+    def loaded_ids(self):
+        return [self.default_model]
+
+    def chat(self, model_id: str, entry: Optional[ModelEntry], req: dict, done: Done, deadline: float = None,
+             stream_cb=None):
+        self.requests += 1
+        try:
+            msgs = _messages(req)
+        except ValueError as e:
+            done(400, _error_body(str(e)))
+            return
+        t0 = time.perf_counter()
+        last = next((m.get("content", "") for m in reversed(msgs) if m.get("role") == "user"), "")
+        if isinstance(last, list):
+            last = "".join(p.get("text", "") for p in last if isinstance(p, dict))
+        prompt_tokens = sum(len(str(m.get("content", "")).split()) for m in msgs)
+        mt = req.get("max_tokens")
+        words = str(last).split()
+        if isinstance(mt, int) and mt >= 0:
+            words = words[:mt]
+        text = " ".join(words)
+        if stream_cb:
+            stream_cb(text)
+        dt = time.perf_counter() - t0
+        done(200, chat_response(model_id, entry, text, prompt_tokens, len(words), "stop", "eosFound", dt, dt, 4096,
+                                arch="granite", quant="stub"))
+
+    def unload(self, model_id: str) -> bool:
+        return False
+
+    def stats(self):
+        return {"backend": "stub", "requests": self.requests}
+
+
+class EngineBackend:
+    """GGUF models served by the HIP engine; JIT-loaded, LRU-evicted."""
+
+    name = "engine"
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self._lock = threading.RLock()
+        self._loaded: "collections.OrderedDict[str, dict]" = collections.OrderedDict()
+        self._device = None
+
+    def device(self):
+        import torch
+        if self._device is None:
+            d = self.cfg.device
+            if d == "auto":
+                d = "cuda:0" if torch.cuda.is_available() else "cpu"
+            self._device = torch.device(d)
+        return self._device
+
+    def loaded_ids(self):
+        with self._lock:
+            return list(self._loaded)
+
+    def load(self, entry: ModelEntry) -> dict:
+        from ..engine.engine import Engine
+        from ..gguf.reader import GGUFReader
+        from ..models.llama import LlamaModel
+        from ..tokenizer.bpe import tokenizer_from_metadata
+        from ..tokenizer.chat_template import ChatTemplate, default_template
+        with self._lock:
+            if entry.id in self._loaded:
+                self._loaded.move_to_end(entry.id)
+                return self._loaded[entry.id]
+            while len(self._loaded) >= max(1, self.cfg.max_loaded_models):
+                old, st = self._loaded.popitem(last=False)
+                st["engine"].unload()
+            t0 = time.time()
+            reader = GGUFReader(entry.path)
+            md = reader.metadata
+            model = LlamaModel(reader, self.device())
+            tok = tokenizer_from_metadata(md)
+            tmpl = md.get("tokenizer.chat_template") or default_template(model.cfg.arch,
+                                                                         md.get("tokenizer.ggml.model", "gpt2"))
+            bos = tok.tokens[tok.bos_id] if tok.bos_id is not None else ""
+            eos = tok.tokens[tok.eos_id] if tok.eos_id is not None else ""
+            eng = Engine(model, tok, max_batch=self.cfg.max_batch, ctx=self.cfg.max_ctx or None,
+                         kv_mem_fraction=self.cfg.kv_mem_fraction, max_prefill_tokens=self.cfg.max_prefill_tokens)
+            eng.start()
+            st = {"engine": eng, "tok": tok, "tmpl": ChatTemplate(tmpl, bos, eos), "entry": entry,
+                  "load_s": time.time() - t0}
+            self._loaded[entry.id] = st
+            return st
+
+    def unload(self, model_id: str) -> bool:
+        with self._lock:
+            st = self._loaded.pop(model_id, None)
+        if st is None:
+            return False
+        st["engine"].unload()
+        return True
+
+    def chat(self, model_id: str, entry: Optional[ModelEntry], req: dict, done: Done, deadline: float = None,
+             stream_cb=None):
+        from ..engine.engine import GenRequest
+        from ..engine.sampling import SamplingParams
+        if entry is None:
+            done(404, _error_body(f"Model '{model_id}' not found"))
+            return
+        try:
+            msgs = _messages(req)
+        except ValueError as e:
+            done(400, _error_body(str(e)))
+            return
+        try:
+            st = self.load(entry)
+        except Exception as e:
+            done(500, _error_body(f"failed to load model '{model_id}': {e}"))
+            return
+        eng, tok, tmpl = st["engine"], st["tok"], st["tmpl"]
+        try:
+            prompt = tmpl.render(msgs, add_generation_prompt=True)
+        except Exception as e:
+            done(400, _error_body(f"chat template error: {e}"))
+            return
+        ids = tok.encode(prompt, add_bos=False)
+        params = SamplingParams.from_request(req, default_max=self.cfg.default_max_tokens)
+        on_token = None
+        if stream_cb is not None:
+            def on_token(t, _tok=tok):
+                stream_cb(_tok.decode([t]))
+        fut = eng.submit(GenRequest(ids, params, on_token=on_token, deadline=deadline))
+        ctx = eng.ctx
+
+        def finished(f):
+            try:
+                r = f.result()
+            except Exception as e:
+                done(400, _error_body(str(e)))
+                return
+            if r.finish_reason == "error":
+                done(500, _error_body(r.error or "generation failed"))
+                return
+            if r.finish_reason == "timeout":       # handler context expired (reference: 2 min, `:328`)
+                done(0, _error_body("context deadline exceeded"))
+                return
+            done(200, chat_response(model_id, entry, r.text, r.prompt_tokens, r.completion_tokens,
+                                    "length" if r.finish_reason == "length" else "stop", r.stop_reason,
+                                    r.time_to_first_token, r.generation_time, ctx))
+        fut.add_done_callback(finished)
+
+    def stats(self):
+        with self._lock:
+            return {"backend": "engine", "device": str(self._device),
+                    "models": {k: dict(v["engine"].stats(), load_s=round(v["load_s"], 3))
+                               for k, v in self._loaded.items()}}

@@ -1,0 +1,105 @@
+"""Worker configuration: environment (the README's variable names, `README.md:488-502`),
+`.env` files (written by the reference's setup scripts, `scripts/setup_unix.sh:109-118`)
+and CLI flags. The reference documents these but never reads them
+(`nats_llm_studio.go:34` takes constructor args only); here they are live.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+SUBJECT_PREFIX = "lmstudio"
+
+
+def load_dotenv(path: str = ".env", override: bool = False) -> Dict[str, str]:
+    vals = {}
+    if not os.path.exists(path):
+        return vals
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#") or "=" not in line:
+                continue
+            k, _, v = line.partition("=")
+            k = k.strip()
+            if k.startswith("export "):
+                k = k[7:].strip()
+            v = v.strip().strip('"').strip("'")
+            vals[k] = v
+            if override or k not in os.environ:
+                os.environ[k] = v
+    return vals
+
+
+@dataclass
+class WorkerConfig:
+    nats_url: str = "nats://127.0.0.1:4222"
+    models_dir: str = field(default_factory=lambda: os.path.expanduser("~/.lmstudio/models"))
+    queue_group: str = "lmstudio-workers"
+    subject_prefix: str = SUBJECT_PREFIX
+    bucket: str = "llm-models"
+    backend: str = "engine"            # engine | stub
+    device: str = "auto"               # auto | cuda:N | cpu
+    tp: int = 1
+    max_batch: int = 64
+    max_ctx: int = 0                   # 0 = model context length
+    kv_mem_fraction: float = 0.5
+    max_prefill_tokens: int = 2048
+    max_loaded_models: int = 1
+    default_max_tokens: int = 512
+    embedded_server: bool = False      # start an in-process NATS server at nats_url's port
+    store_dir: str = ""                # JetStream persistence for the embedded server
+    # per-subject handler timeouts (reference: list 30 s, pull 10 min, delete 2 min, chat 2 min)
+    timeout_list: float = 30.0
+    timeout_pull: float = 600.0
+    timeout_delete: float = 120.0
+    timeout_chat: float = 120.0
+    handler_workers: int = 4
+    lmstudio_base_url: str = "http://127.0.0.1:1234"   # accepted for .env parity; unused (no HTTP hop)
+
+    def subject(self, name: str) -> str:
+        return f"{self.subject_prefix}.{name}"
+
+    @classmethod
+    def from_env(cls, env: Optional[Dict[str, str]] = None) -> "WorkerConfig":
+        e = dict(os.environ if env is None else env)
+        c = cls()
+        c.nats_url = e.get("NATS_URL", c.nats_url)
+        c.models_dir = os.path.expanduser(e.get("MODELS_DIR", e.get("LMSTUDIO_MODELS_DIR", c.models_dir)))
+        c.queue_group = e.get("NATS_QUEUE_GROUP", c.queue_group)
+        c.bucket = e.get("BUCKET", e.get("NATS_OBJECT_BUCKET", c.bucket))
+        c.backend = e.get("BACKEND", c.backend)
+        c.device = e.get("DEVICE", c.device)
+        c.tp = int(e.get("TP", c.tp))
+        c.max_batch = int(e.get("MAX_BATCH", c.max_batch))
+        c.max_ctx = int(e.get("MAX_CTX", c.max_ctx))
+        c.kv_mem_fraction = float(e.get("KV_MEM_FRACTION", c.kv_mem_fraction))
+        c.lmstudio_base_url = e.get("LMSTUDIO_BASE_URL", c.lmstudio_base_url)
+        c.subject_prefix = e.get("SUBJECT_PREFIX", c.subject_prefix)
+        c.embedded_server = e.get("EMBEDDED_NATS", "0") in ("1", "true", "yes")
+        c.store_dir = e.get("NATS_STORE_DIR", c.store_dir)
+        return c
+
+    @classmethod
+    def from_args(cls, argv=None) -> "WorkerConfig":
+        load_dotenv(os.environ.get("DOTENV", ".env"))
+        c = cls.from_env()
+        ap = argparse.ArgumentParser("nats-llm-studio-amd worker")
+        ap.add_argument("--nats-url", default=c.nats_url)
+        ap.add_argument("--models-dir", default=c.models_dir)
+        ap.add_argument("--queue-group", default=c.queue_group)
+        ap.add_argument("--bucket", default=c.bucket)
+        ap.add_argument("--backend", default=c.backend, choices=["engine", "stub"])
+        ap.add_argument("--device", default=c.device)
+        ap.add_argument("--tp", type=int, default=c.tp)
+        ap.add_argument("--max-batch", type=int, default=c.max_batch)
+        ap.add_argument("--max-ctx", type=int, default=c.max_ctx)
+        ap.add_argument("--embedded-server", action="store_true", default=c.embedded_server)
+        ap.add_argument("--store-dir", default=c.store_dir)
+        ap.add_argument("--subject-prefix", default=c.subject_prefix)
+        a = ap.parse_args(argv)
+        for k, v in vars(a).items():
+            setattr(c, k, v)
+        return c

@@ -1,0 +1,253 @@
+"""The NATS service: the reference's four subjects (+ the README's bucket sync, metrics, health).
+
+Subjects (prefix `lmstudio`, `README.md:17-21`), each joined with queue group
+NATS_QUEUE_GROUP (`README.md:475-484` -- documented but never coded in the reference,
+whose `Server` never subscribes, `nats_llm_studio.go:181-205`):
+
+  lmstudio.list_models            -> onListModels   (`nats_llm_studio.go:228-248`)
+  lmstudio.pull_model             -> OnPullModel    (`:250-286`)
+  lmstudio.delete_model           -> OnDeleteModel  (`:288-324`)
+  lmstudio.chat_model             -> OnChatModel    (`:327-364`)
+  lmstudio.sync_model_from_bucket -> README.md:284-318 (design only in the reference)
+  lmstudio.metrics / lmstudio.health (observability; new)
+
+Validation order, error strings and envelope shapes are the reference's. Chat requests
+do not block a handler thread: they are handed to the continuous-batching engine and the
+reply is published from the completion callback, so one worker serves many concurrent chats
+(the reference serialises one generation per subscription).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from collections import defaultdict
+from typing import Optional
+
+from . import envelope
+from .backends import EngineBackend, StubBackend
+from .config import WorkerConfig
+from .registry import Registry
+from .store import ModelStore, PullError
+from ..natsio import Client
+from ..utils.metrics import LatencyHistogram
+
+
+class Service:
+    def __init__(self, cfg: WorkerConfig, client: Optional[Client] = None, backend=None):
+        self.cfg = cfg
+        self.client = client
+        self.registry = Registry(cfg.models_dir)
+        self.backend = backend or (StubBackend() if cfg.backend == "stub" else EngineBackend(cfg))
+        self.store: Optional[ModelStore] = None
+        self.subs = []
+        self.t_start = time.time()
+        self.counters = defaultdict(int)
+        self.latency = defaultdict(LatencyHistogram)
+        self._lock = threading.Lock()
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> "Service":
+        if self.client is None:
+            self.client = Client().connect(self.cfg.nats_url, name=f"nats-llm-studio-amd-{os.getpid()}")
+        self.store = ModelStore(self.client, self.cfg.models_dir, self.cfg.bucket)
+        self.registry.scan()
+        q = self.cfg.queue_group
+        w = self.cfg.handler_workers
+        routes = [
+            ("list_models", self.on_list_models, w),
+            ("pull_model", self.on_pull_model, 2),
+            ("delete_model", self.on_delete_model, 2),
+            ("chat_model", self.on_chat_model, w),
+            ("sync_model_from_bucket", self.on_sync_model_from_bucket, 2),
+            ("metrics", self.on_metrics, 1),
+            ("health", self.on_health, 1),
+        ]
+        for name, fn, workers in routes:
+            self.subs.append(self.client.subscribe(self.cfg.subject(name), q, self._wrap(name, fn), workers))
+        self.client.flush()
+        return self
+
+    def stop(self):
+        for s in self.subs:
+            s.unsubscribe()
+        self.subs.clear()
+        if hasattr(self.backend, "loaded_ids"):
+            for mid in list(self.backend.loaded_ids()):
+                try:
+                    self.backend.unload(mid)
+                except Exception:
+                    pass
+
+    def _wrap(self, name, fn):
+        def handler(msg):
+            t0 = time.perf_counter()
+            with self._lock:
+                self.counters[name] += 1
+            try:
+                fn(msg)
+            finally:
+                self.latency[name].add(time.perf_counter() - t0)
+        return handler
+
+    def respond(self, msg, body: bytes):
+        """respondJSON (`nats_llm_studio.go:207-217`): log (not raise) when there is no reply subject."""
+        if not msg.reply:
+            print(f"error responding to NATS message: nats: message does not have a reply", flush=True)
+            return
+        try:
+            self.client.publish(msg.reply, body)
+        except Exception as e:
+            print(f"error responding to NATS message: {e}", flush=True)
+
+    # ------------------------------------------------------------------ handlers
+    def on_list_models(self, msg):
+        try:
+            models = self.registry.list_api(self.backend.loaded_ids())
+        except Exception as e:
+            self.respond(msg, envelope.error(f"error reading model registry: {e}", {"http_status": 0}))
+            return
+        self.respond(msg, envelope.ok({"http_status": 200, "models": models}))
+
+    def on_pull_model(self, msg):
+        err = envelope.go_json_error(msg.data, "PullModelRequest", {"identifier": "Identifier"})
+        if err:
+            self.respond(msg, envelope.error(f"invalid JSON in PullModel: {err}"))
+            return
+        ident = envelope.get_field(msg.data, "identifier")
+        if not ident:
+            self.respond(msg, envelope.error("'identifier' is required"))
+            return
+        req = json.loads(msg.data)
+        try:
+            res = self.store.pull(ident)
+        except PullError as e:
+            self.respond(msg, envelope.failure(str(e), {"model": ident, "output": e.output}))
+            return
+        except Exception as e:
+            self.respond(msg, envelope.failure(f"failed to pull '{ident}': {e}", {"model": ident, "output": ""}))
+            return
+        self.registry.scan()
+        data = {"model": ident, "output": res["output"], "local_paths": res["paths"],
+                "bytes": res["bytes"], "seconds": round(res["seconds"], 3)}
+        if req.get("load") and isinstance(self.backend, EngineBackend):
+            ent = self.registry.resolve(ident) or (self.registry.resolve(os.path.basename(os.path.dirname(res["paths"][0])))
+                                                   if res["paths"] else None)
+            if ent is not None:
+                t0 = time.time()
+                try:
+                    self.backend.load(ent)
+                    data["loaded"] = ent.id
+                    data["load_seconds"] = round(time.time() - t0, 3)
+                except Exception as e:
+                    data["load_error"] = str(e)
+        self.respond(msg, envelope.ok(data))
+
+    def on_delete_model(self, msg):
+        err = envelope.go_json_error(msg.data, "DeleteModelRequest", {"model_id": "ModelID"})
+        if err:
+            self.respond(msg, envelope.error(f"invalid JSON in DeleteModel: {err}"))
+            return
+        mid = envelope.get_field(msg.data, "model_id")
+        if not mid:
+            self.respond(msg, envelope.error("'model_id' is required"))
+            return
+        self.registry.scan()
+        ent = self.registry.resolve(mid)
+        if ent is None:
+            self.respond(msg, envelope.failure(f"model not found: {mid}", {"model_id": mid, "dir": ""}))
+            return
+        self.backend.unload(ent.id)                       # best effort, like `lms unload` (`:87-97`)
+        d = ent.dir
+        if not self.registry.safe_dir(d):
+            self.respond(msg, envelope.failure(f"refusing to delete outside MODELS_DIR: {d}",
+                                               {"model_id": mid, "dir": d}))
+            return
+        if not os.path.isdir(d):
+            self.respond(msg, envelope.failure(f"model directory not found: {d}", {"model_id": mid, "dir": d}))
+            return
+        try:
+            ModelStore.remove_dir(d)
+        except OSError as e:
+            self.respond(msg, envelope.failure(f"error removing model directory {d}: {e}", {"model_id": mid, "dir": d}))
+            return
+        self.registry.scan()
+        self.respond(msg, envelope.ok({"model_id": mid, "deleted_dir": d}))
+
+    def on_chat_model(self, msg):
+        if len(msg.data) == 0:
+            self.respond(msg, envelope.error("payload vazio em ChatModel"))
+            return
+        err = envelope.go_json_error(msg.data, "", {"model": "Model"})
+        if err:
+            self.respond(msg, envelope.error(f"invalid JSON in ChatModel: {err}"))
+            return
+        model = envelope.get_field(msg.data, "model")
+        if not model:
+            self.respond(msg, envelope.error("'model' is required in ChatModel"))
+            return
+        req = json.loads(msg.data)
+        entry = self.registry.resolve(model)
+        if entry is None and isinstance(self.backend, EngineBackend):
+            self.registry.scan()
+            entry = self.registry.resolve(model)
+        deadline = time.monotonic() + self.cfg.timeout_chat
+        stream_cb = None
+        ssubj = req.get("stream_subject")
+        if req.get("stream") and isinstance(ssubj, str) and ssubj:
+            def stream_cb(delta, _s=ssubj):
+                try:
+                    self.client.publish(_s, json.dumps({"object": "chat.completion.chunk", "model": model,
+                                                        "choices": [{"index": 0, "delta": {"content": delta}}]}).encode())
+                except Exception:
+                    pass
+
+        def done(status: int, body: dict):
+            if status <= 0:
+                self.respond(msg, envelope.error(body.get("error", "chat failed"), {"http_status": 0}))
+            else:
+                self.respond(msg, envelope.ok({"http_status": status, "response": body}))
+        try:
+            self.backend.chat(entry.id if entry else model, entry, req, done, deadline, stream_cb)
+        except Exception as e:
+            self.respond(msg, envelope.error(f"chat backend error: {e}", {"http_status": 0}))
+
+    def on_sync_model_from_bucket(self, msg):
+        try:
+            req = json.loads(msg.data or b"{}")
+            if not isinstance(req, dict):
+                raise ValueError("request must be a JSON object")
+        except Exception as e:
+            self.respond(msg, envelope.error(f"invalid JSON in SyncModelFromBucket: {e}"))
+            return
+        missing = [k for k in ("object_name", "publisher", "model_dir") if not req.get(k)]
+        if missing:
+            self.respond(msg, envelope.error(f"'{missing[0]}' is required"))
+            return
+        bucket = req.get("bucket") or self.cfg.bucket
+        try:
+            res = self.store.sync(bucket, req["object_name"], req["publisher"], req["model_dir"],
+                                  req.get("filename", "model.gguf"))
+        except Exception as e:
+            self.respond(msg, envelope.failure(str(e), {"bucket": bucket, "object_name": req["object_name"]}))
+            return
+        self.registry.scan()          # the `lms import` step of README.md:305-308
+        self.respond(msg, envelope.ok(res))
+
+    def on_metrics(self, msg):
+        data = {
+            "uptime_s": round(time.time() - self.t_start, 3),
+            "requests": dict(self.counters),
+            "latency_ms": {k: v.summary_ms() for k, v in self.latency.items()},
+            "backend": self.backend.stats(),
+            "nats": self.client.stats(),
+            "models_dir": self.cfg.models_dir,
+            "queue_group": self.cfg.queue_group,
+        }
+        self.respond(msg, envelope.ok(data))
+
+    def on_health(self, msg):
+        self.respond(msg, envelope.ok({"status": "ok", "pid": os.getpid(), "backend": self.backend.name,
+                                       "models_loaded": self.backend.loaded_ids(),
+                                       "uptime_s": round(time.time() - self.t_start, 3)}))

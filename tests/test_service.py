@@ -1,0 +1,194 @@
+"""End-to-end service tests over the embedded NATS server (BASELINE config 1 + the model
+lifecycle). Error strings are the reference's (nats_llm_studio.go:256-344)."""
+import json
+import os
+import shutil
+import threading
+import time
+
+import pytest
+
+from nats_llm_studio_amd.natsio import Client, EmbeddedServer, NoRespondersError, ObjectStore
+from nats_llm_studio_amd.service.config import WorkerConfig
+from nats_llm_studio_amd.service.service import Service
+
+
+@pytest.fixture()
+def env(tmp_path):
+    srv = EmbeddedServer().start()
+    cfg = WorkerConfig(nats_url=srv.url, models_dir=str(tmp_path / "models"), backend="stub")
+    os.makedirs(cfg.models_dir)
+    svc = Service(cfg).start()
+    cli = Client().connect(srv.url)
+    yield srv, cfg, svc, cli
+    cli.close()
+    svc.stop()
+    svc.client.close()
+    srv.stop()
+
+
+def req(cli, name, payload, timeout=10):
+    data = payload if isinstance(payload, bytes) else json.dumps(payload).encode()
+    return json.loads(cli.request(f"lmstudio.{name}", data, timeout).data)
+
+
+def test_list_models_empty(env):
+    _, _, _, cli = env
+    r = req(cli, "list_models", {})
+    assert r == {"ok": True, "data": {"http_status": 200, "models": {"object": "list", "data": []}}}
+
+
+@pytest.mark.parametrize("subject,payload,err", [
+    ("pull_model", b"{bad", "invalid JSON in PullModel: invalid character 'b' looking for beginning of object key string"),
+    ("pull_model", b"{}", "'identifier' is required"),
+    ("pull_model", b'{"identifier": 5}',
+     "invalid JSON in PullModel: json: cannot unmarshal number into Go struct field PullModelRequest.identifier of type string"),
+    ("delete_model", b"nope", "invalid JSON in DeleteModel: invalid character 'o' in literal null (expecting 'u')"),
+    ("delete_model", b'{"model_id": ""}', "'model_id' is required"),
+    ("chat_model", b"", "payload vazio em ChatModel"),
+    ("chat_model", b"[", "invalid JSON in ChatModel: unexpected end of JSON input"),
+    ("chat_model", b'{"messages": []}', "'model' is required in ChatModel"),
+])
+def test_validation_errors(env, subject, payload, err):
+    _, _, _, cli = env
+    r = req(cli, subject, payload)
+    if subject == "delete_model" and payload == b"nope":
+        assert r["ok"] is False and r["error"].startswith("invalid JSON in DeleteModel: invalid character")
+    else:
+        assert r == {"ok": False, "error": err, "data": None}
+
+
+def test_chat_stub_echo(env):
+    _, _, _, cli = env
+    r = req(cli, "chat_model", {"model": "granite-3.0-2b-instruct",
+                                "messages": [{"role": "system", "content": "x"},
+                                             {"role": "user", "content": "hello over nats"}]})
+    assert r["ok"] is True and r["data"]["http_status"] == 200
+    resp = r["data"]["response"]
+    assert resp["object"] == "chat.completion" and resp["choices"][0]["message"]["content"] == "hello over nats"
+    assert resp["usage"]["completion_tokens"] == 3 and "stats" in resp and "model_info" in resp
+    bad = req(cli, "chat_model", {"model": "m", "messages": "notalist"})
+    assert bad["ok"] is True and bad["data"]["http_status"] == 400     # backend status, not bridge status
+
+
+def test_metrics_health(env):
+    _, _, _, cli = env
+    req(cli, "list_models", {})
+    m = req(cli, "metrics", {})
+    assert m["ok"] and m["data"]["requests"]["list_models"] >= 1 and "p50" in m["data"]["latency_ms"]["list_models"]
+    h = req(cli, "health", {})
+    assert h["data"]["status"] == "ok" and h["data"]["backend"] == "stub"
+
+
+def _push_tiny(srv_url, tiny_path, name):
+    c = Client().connect(srv_url)
+    o = ObjectStore(c, "llm-models")
+    o.create()
+    info = o.put_file(name, tiny_path)
+    c.close()
+    return info
+
+
+def test_pull_list_delete_lifecycle(env, tiny_models):
+    srv, cfg, svc, cli = env
+    name = "synthetic/tiny-llama-GGUF/tiny-llama-Q4_K_M.gguf"
+    info = _push_tiny(srv.url, tiny_models["tiny-llama"], name)
+    r = req(cli, "pull_model", {"identifier": "synthetic/tiny-llama"}, timeout=60)
+    assert r["ok"] is True and r["data"]["model"] == "synthetic/tiny-llama", r
+    local = os.path.join(cfg.models_dir, "synthetic", "tiny-llama-GGUF", "tiny-llama-Q4_K_M.gguf")
+    assert os.path.getsize(local) == info["size"]
+    lst = req(cli, "list_models", {})["data"]["models"]["data"]
+    assert [m["id"] for m in lst] == ["tiny-llama"]
+    m = lst[0]
+    assert m["publisher"] == "synthetic" and m["arch"] == "llama" and m["quantization"] == "Q4_K_M"
+    assert m["state"] == "not-loaded" and m["max_context_length"] == 512
+    # unknown model
+    r = req(cli, "pull_model", {"identifier": "nobody/nothing"})
+    assert r["ok"] is False and r["data"]["model"] == "nobody/nothing" and "not found" in r["error"]
+    # delete
+    r = req(cli, "delete_model", {"model_id": "tiny-llama"})
+    assert r["ok"] is True and r["data"] == {"model_id": "tiny-llama",
+                                            "deleted_dir": os.path.join(cfg.models_dir, "synthetic", "tiny-llama-GGUF")}
+    assert not os.path.exists(local)
+    r = req(cli, "delete_model", {"model_id": "tiny-llama"})
+    assert r["ok"] is False and r["data"] == {"model_id": "tiny-llama", "dir": ""}
+
+
+def test_sync_model_from_bucket(env, tiny_models):
+    srv, cfg, svc, cli = env
+    _push_tiny(srv.url, tiny_models["tiny-granite"], "ibm/granite/granite.gguf")
+    r = req(cli, "sync_model_from_bucket", {"bucket": "llm-models", "object_name": "ibm/granite/granite.gguf",
+                                            "publisher": "ibm", "model_dir": "granite-3.0-2b"}, timeout=60)
+    assert r["ok"] and r["data"]["local_path"].endswith("ibm/granite-3.0-2b/model.gguf")
+    ids = [m["id"] for m in req(cli, "list_models", {})["data"]["models"]["data"]]
+    assert ids == ["granite-3.0-2b"]
+    r = req(cli, "sync_model_from_bucket", {"object_name": "x"})
+    assert r == {"ok": False, "error": "'publisher' is required", "data": None}
+
+
+def test_delete_refuses_escape(env):
+    _, cfg, svc, cli = env
+    assert not svc.registry.safe_dir(cfg.models_dir)
+    assert not svc.registry.safe_dir("/etc")
+    assert svc.registry.safe_dir(os.path.join(cfg.models_dir, "a", "b"))
+
+
+def test_queue_group_scale_out(env):
+    srv, cfg, svc, cli = env
+    svc2 = Service(cfg).start()          # second worker, same queue group
+    try:
+        for _ in range(200):
+            assert req(cli, "list_models", {})["ok"]
+        assert svc.counters["list_models"] > 20 and svc2.counters["list_models"] > 20
+        assert svc.counters["list_models"] + svc2.counters["list_models"] == 200
+    finally:
+        svc2.stop()
+        svc2.client.close()
+
+
+def test_no_responders_when_down(tmp_path):
+    srv = EmbeddedServer().start()
+    cli = Client().connect(srv.url)
+    with pytest.raises(NoRespondersError):
+        cli.request("lmstudio.list_models", b"{}", 1)
+    cli.close()
+    srv.stop()
+
+
+def test_engine_backend_chat_cpu(tmp_path, tiny_models):
+    srv = EmbeddedServer().start()
+    md = tmp_path / "models" / "synthetic" / "tiny-llama-GGUF"
+    md.mkdir(parents=True)
+    shutil.copy(tiny_models["tiny-llama"], md / "tiny-llama-Q4_K_M.gguf")
+    cfg = WorkerConfig(nats_url=srv.url, models_dir=str(tmp_path / "models"), backend="engine", device="cpu",
+                       max_batch=8, max_ctx=256)
+    svc = Service(cfg).start()
+    cli = Client().connect(srv.url)
+    try:
+        body = {"model": "tiny-llama", "messages": [{"role": "user", "content": "Hello!"}], "max_tokens": 5,
+                "temperature": 0}
+        out = {}
+
+        def go(i):
+            out[i] = req(cli, "chat_model", dict(body, seed=i), timeout=120)
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(4)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        for i in range(4):
+            r = out[i]
+            assert r["ok"] and r["data"]["http_status"] == 200, r
+            resp = r["data"]["response"]
+            assert resp["usage"]["completion_tokens"] <= 5 and resp["model_info"]["quant"] == "Q4_K_M"
+        texts = {out[i]["data"]["response"]["choices"][0]["message"]["content"] for i in range(4)}
+        assert len(texts) == 1                         # greedy: identical answers for identical prompts
+        lst = req(cli, "list_models", {})["data"]["models"]["data"]
+        assert lst[0]["state"] == "loaded"
+        r = req(cli, "chat_model", {"model": "missing-model", "messages": [{"role": "user", "content": "x"}]})
+        assert r["ok"] and r["data"]["http_status"] == 404
+        r = req(cli, "delete_model", {"model_id": "tiny-llama"})       # unloads then deletes
+        assert r["ok"] and svc.backend.loaded_ids() == []
+    finally:
+        cli.close()
+        svc.stop()
+        svc.client.close()
+        srv.stop()
