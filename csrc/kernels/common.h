@@ -1,13 +1,19 @@
 // Shared device helpers for the gfx950 (CDNA4) kernels of nats_llm_studio_amd.
 //
-// Weight formats live on the device in GGUF block layout (never pre-dequantised:
-// decode is HBM-bound). Q4_K / Q5_K keep ggml's native 144/176-byte blocks (both
-// are multiples of 16 B, so every block is 16-B aligned). Q6_K (210 B) and Q8_0
-// (34 B) are not 16-B aligned, so the loader splits them into planes at load time
-// (same total bytes):
-//   Q6_K planes: ql[R*nb][128] | qh[R*nb][64] | sc[R*nb][16] | d[R*nb] (f16)
-//   Q8_0 planes: qs[R][K] (i8)  | d[R][K/32] (f16)
-// where R = rows, nb = K/256.
+// Weight formats live on the device in GGUF block encodings (never pre-dequantised:
+// decode is HBM-bound), re-tiled at load time ("tiled" layout, same bytes):
+//   rows are padded to 16 and grouped into 16-row tiles; for every (tile, 256-value
+//   super-block) the 16 rows' blocks form ONE contiguous "tile-block" of TB bytes,
+//   arranged so that each wave-wide 16-B load instruction of the GEMV reads 1 KiB
+//   contiguous (lane l = 16*g + r -> byte 16*l of a 1 KiB piece). Tile-blocks are
+//   ordered [tile][super-block], so a wave walking K streams sequential memory.
+//     Q4_K  TB=2304: hdr[r] (16) | P0[g][r] (16) | P1[g][r] (16)       (P = qs pieces g, g+4)
+//     Q5_K  TB=2816: hdr[r] | qh[h][r] (16, h=g&1) | P0[g][r] | P1[g][r]
+//     Q6_K  TB=3360: qa[l] | qb[l] | qh[l] (16 each) | sc[r] (16) | d[r] (2)
+//     Q8_0  TB=4352: qs[i][l] (4 x 16) | d[r][8] (f16)
+//     F16/BF16 TB=8192: v[t][l] (8 x 16);  F32 TB=16384: v[t][l] (16 x 16)
+// Embedding tables keep a row-major "rows" layout (gathered, not streamed):
+//   Q4_K/Q5_K native blocks; Q6_K planes ql|qh|sc|d; Q8_0 planes qs|d.
 //
 // MFMA operand mapping (v_mfma_f32_16x16x32_bf16): lane l = 16*g + r holds
 // A[row r][k = 8g + j] and B[k = 8g + j][col r], j = 0..7. The contraction order
@@ -93,9 +99,24 @@ template <> struct RawOf<QT_F32> { typedef RawF32 type; };
 // Geometry of a weight matrix on the device.
 struct WDesc {
   const uint8_t* w;  // base pointer (format-specific layout, see top of file)
-  int rows;          // R
+  int rows;          // R (padded to 16 in the tiled layout)
   int K;             // columns (multiple of 256)
 };
+
+template <int T> struct TileBytes;
+template <> struct TileBytes<QT_Q4_K> { static constexpr int v = 2304; };
+template <> struct TileBytes<QT_Q5_K> { static constexpr int v = 2816; };
+template <> struct TileBytes<QT_Q6_K> { static constexpr int v = 3360; };
+template <> struct TileBytes<QT_Q8_0> { static constexpr int v = 4352; };
+template <> struct TileBytes<QT_F16> { static constexpr int v = 8192; };
+template <> struct TileBytes<QT_BF16> { static constexpr int v = 8192; };
+template <> struct TileBytes<QT_F32> { static constexpr int v = 16384; };
+
+// base of the tile-block holding `row` (any row of the tile) at super-block sb
+template <int T>
+DEVI const uint8_t* tile_block(const WDesc& W, int row, int sb) {
+  return W.w + ((size_t)(row >> 4) * (W.K >> 8) + sb) * TileBytes<T>::v;
+}
 
 // k offset (within the 256 super-block) of K-step t for lane group g
 template <int T> DEVI int xoff(int t, int g);
@@ -115,13 +136,13 @@ template <> DEVI int xoff<QT_F32>(int t, int g) { return 64 * g + 8 * t; }
 // ---- Q4_K -----------------------------------------------------------------
 template <bool NT>
 DEVI RawQ4K load_raw_q4k(const WDesc& W, int row, int sb, int g) {
-  const int nb = W.K >> 8;
-  const uint8_t* b = W.w + ((size_t)row * nb + sb) * 144;
-  RawQ4K r;
-  r.hdr = NT ? ld16_nt(b) : ld16(b);
-  r.p0 = NT ? ld16_nt(b + 16 + 16 * g) : ld16(b + 16 + 16 * g);
-  r.p1 = NT ? ld16_nt(b + 16 + 16 * (g + 4)) : ld16(b + 16 + 16 * (g + 4));
-  return r;
+  const uint8_t* b = tile_block<QT_Q4_K>(W, row, sb);
+  const int r = row & 15, l = 16 * g + r;
+  RawQ4K x;
+  x.hdr = NT ? ld16_nt(b + 16 * r) : ld16(b + 16 * r);
+  x.p0 = NT ? ld16_nt(b + 256 + 16 * l) : ld16(b + 256 + 16 * l);
+  x.p1 = NT ? ld16_nt(b + 1280 + 16 * l) : ld16(b + 1280 + 16 * l);
+  return x;
 }
 
 // 16 bytes of nibbles -> 4 K-steps (low 0-7, low 8-15, high 0-7, high 8-15)
@@ -167,14 +188,14 @@ DEVI void deq_q4k(const RawQ4K& r, int g, bf16x8* wf) {
 // ---- Q5_K -----------------------------------------------------------------
 template <bool NT>
 DEVI RawQ5K load_raw_q5k(const WDesc& W, int row, int sb, int g) {
-  const int nb = W.K >> 8;
-  const uint8_t* b = W.w + ((size_t)row * nb + sb) * 176;
-  RawQ5K r;
-  r.hdr = NT ? ld16_nt(b) : ld16(b);
-  r.qh = NT ? ld16_nt(b + 16 + 16 * (g & 1)) : ld16(b + 16 + 16 * (g & 1));
-  r.p0 = NT ? ld16_nt(b + 48 + 16 * g) : ld16(b + 48 + 16 * g);
-  r.p1 = NT ? ld16_nt(b + 48 + 16 * (g + 4)) : ld16(b + 48 + 16 * (g + 4));
-  return r;
+  const uint8_t* b = tile_block<QT_Q5_K>(W, row, sb);
+  const int r = row & 15, l = 16 * g + r;
+  RawQ5K x;
+  x.hdr = NT ? ld16_nt(b + 16 * r) : ld16(b + 16 * r);
+  x.qh = NT ? ld16_nt(b + 256 + 16 * (16 * (g & 1) + r)) : ld16(b + 256 + 16 * (16 * (g & 1) + r));
+  x.p0 = NT ? ld16_nt(b + 768 + 16 * l) : ld16(b + 768 + 16 * l);
+  x.p1 = NT ? ld16_nt(b + 1792 + 16 * l) : ld16(b + 1792 + 16 * l);
+  return x;
 }
 
 DEVI void nib16h_to_frags(u32x4 p, u32x4 qh, int c, float a_lo, float m_lo, float a_hi, float m_hi,
@@ -223,24 +244,18 @@ DEVI void deq_q5k(const RawQ5K& r, int g, bf16x8* wf) {
   nib16h_to_frags(r.p1, r.qh, c1, a[2], mm[2], a[3], mm[3], wf + 4);
 }
 
-// ---- Q6_K (planes) ----------------------------------------------------------
+// ---- Q6_K ------------------------------------------------------------------
 template <bool NT>
 DEVI RawQ6K load_raw_q6k(const WDesc& W, int row, int sb, int g) {
-  const int nb = W.K >> 8;
-  const size_t nblk = (size_t)W.rows * nb;
-  const size_t bi = (size_t)row * nb + sb;
-  const int n = g >> 1, L0 = 16 * (g & 1);
-  const uint8_t* ql = W.w + bi * 128;
-  const uint8_t* qh = W.w + nblk * 128 + bi * 64;
-  const uint8_t* sc = W.w + nblk * 192 + bi * 16;
-  const uint16_t* dp = reinterpret_cast<const uint16_t*>(W.w + nblk * 208) + bi;
-  RawQ6K r;
-  r.qa = NT ? ld16_nt(ql + 64 * n + L0) : ld16(ql + 64 * n + L0);
-  r.qb = NT ? ld16_nt(ql + 64 * n + 32 + L0) : ld16(ql + 64 * n + 32 + L0);
-  r.qh = NT ? ld16_nt(qh + 32 * n + L0) : ld16(qh + 32 * n + L0);
-  r.sc = ld16(sc);
-  r.d = *dp;
-  return r;
+  const uint8_t* b = tile_block<QT_Q6_K>(W, row, sb);
+  const int r = row & 15, l = 16 * g + r;
+  RawQ6K x;
+  x.qa = NT ? ld16_nt(b + 16 * l) : ld16(b + 16 * l);
+  x.qb = NT ? ld16_nt(b + 1024 + 16 * l) : ld16(b + 1024 + 16 * l);
+  x.qh = NT ? ld16_nt(b + 2048 + 16 * l) : ld16(b + 2048 + 16 * l);
+  x.sc = ld16(b + 3072 + 16 * r);
+  x.d = *reinterpret_cast<const uint16_t*>(b + 3328 + 2 * r);
+  return x;
 }
 
 DEVI void deq_q6k(const RawQ6K& r, int g, bf16x8* wf) {
@@ -276,19 +291,18 @@ DEVI void deq_q6k(const RawQ6K& r, int g, bf16x8* wf) {
   }
 }
 
-// ---- Q8_0 (planes) ----------------------------------------------------------
+// ---- Q8_0 ------------------------------------------------------------------
 template <bool NT>
 DEVI RawQ8 load_raw_q8(const WDesc& W, int row, int sb, int g) {
-  const uint8_t* qs = W.w + (size_t)row * W.K + sb * 256 + 64 * g;
-  const uint16_t* dp = reinterpret_cast<const uint16_t*>(W.w + (size_t)W.rows * W.K) +
-                       (size_t)row * (W.K >> 5) + sb * 8 + 2 * g;
-  RawQ8 r;
-  r.q0 = NT ? ld16_nt(qs) : ld16(qs);
-  r.q1 = NT ? ld16_nt(qs + 16) : ld16(qs + 16);
-  r.q2 = NT ? ld16_nt(qs + 32) : ld16(qs + 32);
-  r.q3 = NT ? ld16_nt(qs + 48) : ld16(qs + 48);
-  r.d = *reinterpret_cast<const uint32_t*>(dp);
-  return r;
+  const uint8_t* b = tile_block<QT_Q8_0>(W, row, sb);
+  const int r = row & 15, l = 16 * g + r;
+  RawQ8 x;
+  x.q0 = NT ? ld16_nt(b + 16 * l) : ld16(b + 16 * l);
+  x.q1 = NT ? ld16_nt(b + 1024 + 16 * l) : ld16(b + 1024 + 16 * l);
+  x.q2 = NT ? ld16_nt(b + 2048 + 16 * l) : ld16(b + 2048 + 16 * l);
+  x.q3 = NT ? ld16_nt(b + 3072 + 16 * l) : ld16(b + 3072 + 16 * l);
+  x.d = *reinterpret_cast<const uint32_t*>(b + 4096 + 16 * r + 4 * g);
+  return x;
 }
 
 DEVI void deq_q8(const RawQ8& r, int g, bf16x8* wf) {
@@ -311,11 +325,12 @@ DEVI void deq_q8(const RawQ8& r, int g, bf16x8* wf) {
 // ---- plain F16 / BF16 / F32 ---------------------------------------------------
 template <bool NT>
 DEVI RawF16 load_raw_f16(const WDesc& W, int row, int sb, int g) {
-  const uint8_t* p = W.w + ((size_t)row * W.K + sb * 256 + 64 * g) * 2;
-  RawF16 r;
+  const uint8_t* b = tile_block<QT_F16>(W, row, sb);
+  const int l = 16 * g + (row & 15);
+  RawF16 x;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) r.v[t] = NT ? ld16_nt(p + 16 * t) : ld16(p + 16 * t);
-  return r;
+  for (int t = 0; t < 8; ++t) x.v[t] = NT ? ld16_nt(b + 1024 * t + 16 * l) : ld16(b + 1024 * t + 16 * l);
+  return x;
 }
 DEVI void deq_bf16(const RawF16& r, int g, bf16x8* wf) {
 #pragma unroll
@@ -335,11 +350,12 @@ DEVI void deq_f16(const RawF16& r, int g, bf16x8* wf) {
 }
 template <bool NT>
 DEVI RawF32 load_raw_f32(const WDesc& W, int row, int sb, int g) {
-  const uint8_t* p = W.w + ((size_t)row * W.K + sb * 256 + 64 * g) * 4;
-  RawF32 r;
+  const uint8_t* b = tile_block<QT_F32>(W, row, sb);
+  const int l = 16 * g + (row & 15);
+  RawF32 x;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) r.v[t] = NT ? ld16_nt(p + 16 * t) : ld16(p + 16 * t);
-  return r;
+  for (int t = 0; t < 16; ++t) x.v[t] = NT ? ld16_nt(b + 1024 * t + 16 * l) : ld16(b + 1024 * t + 16 * l);
+  return x;
 }
 DEVI void deq_f32(const RawF32& r, int g, bf16x8* wf) {
   float v[8];

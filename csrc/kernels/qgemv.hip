@@ -50,7 +50,8 @@ DEVI float silu(float g) { return g / (1.f + __expf(-g)); }
 
 template <int T, int WAVES, int RT, int MT>
 DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int r = lane & 15, g = lane >> 4;
   const WDesc W{S.w, S.rows, S.K};
   const int nb = S.K >> 8;
@@ -59,14 +60,17 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   int mcount = a.M;
   if (S.mcount) mcount = min(*S.mcount, a.M);
 
-  // activation row pointers for this lane (A operand row = batch row r of tile mt)
+  // Activation rows (A operand row = batch row r of tile mt). Padded / unmapped rows load a
+  // valid row (row 0: broadcast, cache-resident) and are zeroed with a select after the load:
+  // a lane-conditional load would compile to a branch + vmcnt(0) per K-step that drains the
+  // whole weight prefetch (cdna_hip_programming.md §5 "Three .s-level traps" (c)).
   const __bf16* xr[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    int m = mt * 16 + r;
-    int src = m < mcount ? m : -1;           // padded batch rows: no loads, zero fragment
+    const int m = mt * 16 + r;
+    int src = m < mcount ? m : -1;
     if (S.xmap) src = (m < mcount) ? S.xmap[m] : -1;
-    xr[mt] = src >= 0 ? a.x + (size_t)src * a.ldx : nullptr;
+    xr[mt] = a.x + (size_t)(src >= 0 ? src : 0) * a.ldx;
   }
   int rowc[RT];
 #pragma unroll
@@ -78,44 +82,59 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // weight stream: two super-blocks in flight ahead of the one being computed
+  // Weight stream: two register buffers with FIXED roles (A: even, B: odd super-blocks), the
+  // loop unrolled by two, so a buffer is reloaded (sb + 2) right after its dequant and no
+  // register holding an in-flight load is ever copied (a copy would force vmcnt(0)).
   typedef typename RawOf<T>::type Raw;
-  Raw cur[RT], nx1[RT];
+  Raw wA[RT], wB[RT];
+  // All weight loads are unconditional (super-block index clamped into [sb0, sb1)): a
+  // conditional load breaks hipcc's vmcnt bookkeeping at the join and it falls back to
+  // vmcnt(0). The clamped tail reloads hit L2 and are never consumed.
+  const int sbl = max(sb1 - 1, sb0);
   if (sb0 < sb1) {
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) cur[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
-  }
-  if (sb0 + 1 < sb1) {
+    for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) nx1[rt] = load_raw<T, true>(W, rowc[rt], sb0 + 1, g);
+    for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
   }
-  const bf16x8 zero8 = {};
-  for (int sb = sb0; sb < sb1; ++sb) {
-    Raw nx2[RT];
-    if (sb + 2 < sb1) {
+  auto step = [&](Raw (&w)[RT], int sb) {
+    // 1) activation fragments of this super-block (issued before this step's weight reload)
+    bf16x8 xa[8][MT];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) nx2[rt] = load_raw<T, true>(W, rowc[rt], sb + 2, g);
-    }
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        xa[t][mt] = *reinterpret_cast<const bf16x8*>(xr[mt] + sb * 256 + xoff<T>(t, g));
+    // the scheduler must not sink these loads below the weight reload (the in-order vmcnt
+    // wait for a late x load would then also wait for the reload)
+    __builtin_amdgcn_sched_barrier(0);
+    // 2) dequant (waits only for this buffer's loads, issued two steps ago)
     bf16x8 wf[RT][8];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) dequant<T>(cur[rt], g, wf[rt]);
+    for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
+    __builtin_amdgcn_sched_barrier(0);
+    // 3) reload the buffer two super-blocks ahead
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+    __builtin_amdgcn_sched_barrier(0);
+    // 4) MFMA
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const int ko = sb * 256 + xoff<T>(t, g);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 xa = xr[mt] ? *reinterpret_cast<const bf16x8*>(xr[mt] + ko) : zero8;
+        const bf16x8 x8 = xa[t][mt];   // rows >= mcount only reach output rows that are never stored
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
-          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
+          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x8, wf[rt][t], acc[rt][mt], 0, 0, 0);
       }
     }
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      cur[rt] = nx1[rt];
-      nx1[rt] = nx2[rt];
-    }
+  };
+  int sb = sb0;
+  for (; sb + 1 < sb1; sb += 2) {
+    step(wA, sb);
+    step(wB, sb + 1);
   }
+  if (sb < sb1) step(wA, sb);
 
   // ---- cross-wave reduction through LDS -------------------------------------
   // red: [WAVES][RT][MT][4][64] ; tile: [RT*16 rows][MT*16 batch]
@@ -234,7 +253,8 @@ DEVI int lds_off(int row, int k) {            // element offset in a [rows][256]
 
 template <int T, int WAVES, int RT, int MT>
 DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, __bf16* lds) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const WDesc W{S.w, S.rows, S.K};
   const int nb = S.K >> 8;
@@ -246,24 +266,24 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(base + rt * 16 + r, S.rows - 1);
 
   constexpr int NT = WAVES * 64;
-  constexpr int NCH = (MT * 16 * 32 + NT - 1) / NT;     // 16-B chunks staged per thread
+  constexpr int NCH = (MT * 16 * 32) / NT;               // 16-B chunks staged per thread
+  static_assert((MT * 16 * 32) % NT == 0, "staging must divide evenly");
   u32x4 xst[NCH];
   auto load_x = [&](int sb) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int idx = threadIdx.x + c * NT;
       const int row = idx >> 5, ch = idx & 31;
-      xst[c] = (row < M && idx < MT * 512) ? ld16(a.x + (size_t)row * a.ldx + sb * 256 + ch * 8) : u32x4{0, 0, 0, 0};
+      // rows >= M only feed output rows that are never stored: clamp, never branch
+      xst[c] = ld16(a.x + (size_t)min(row, M - 1) * a.ldx + sb * 256 + ch * 8);
     }
   };
   auto store_x = [&](int buf) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int idx = threadIdx.x + c * NT;
-      if (idx < MT * 512) {
-        const int row = idx >> 5, ch = idx & 31;
-        *reinterpret_cast<u32x4*>(lds + buf * (MT * 16 * 256) + lds_off(row, ch * 8)) = xst[c];
-      }
+      const int row = idx >> 5, ch = idx & 31;
+      *reinterpret_cast<u32x4*>(lds + buf * (MT * 16 * 256) + lds_off(row, ch * 8)) = xst[c];
     }
   };
 
@@ -274,30 +294,30 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   typedef typename RawOf<T>::type Raw;
-  Raw cur[RT], nx1[RT];
+  Raw wA[RT], wB[RT];
+  const int sbl = max(sb1 - 1, sb0);
   if (sb0 < sb1) {
     load_x(sb0);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) cur[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
+    for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
     store_x(0);
   }
-  if (sb0 + 1 < sb1) {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) nx1[rt] = load_raw<T, true>(W, rowc[rt], sb0 + 1, g);
-  }
   __syncthreads();
-  for (int sb = sb0; sb < sb1; ++sb) {
+  // fixed buffer roles, unrolled by two (see path A); x for sb+1 is staged through the other
+  // LDS buffer while sb is computed
+  auto step = [&](Raw (&w)[RT], int sb) {
     const int buf = (sb - sb0) & 1;
-    const bool more = sb + 1 < sb1;
-    Raw nx2[RT];
-    if (more) load_x(sb + 1);
-    if (sb + 2 < sb1) {
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) nx2[rt] = load_raw<T, true>(W, rowc[rt], sb + 2, g);
-    }
+    load_x(min(sb + 1, sbl));          // unconditional (clamped): see path A
+    __builtin_amdgcn_sched_barrier(0);
     bf16x8 wf[RT][8];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) dequant<T>(cur[rt], g, wf[rt]);
+    for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+    __builtin_amdgcn_sched_barrier(0);
     const __bf16* xb = lds + buf * (MT * 16 * 256);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -310,14 +330,15 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
       }
     }
-    if (more) store_x(buf ^ 1);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      cur[rt] = nx1[rt];
-      nx1[rt] = nx2[rt];
-    }
+    store_x(buf ^ 1);
     __syncthreads();
+  };
+  int sb = sb0;
+  for (; sb + 1 < sb1; sb += 2) {
+    step(wA, sb);
+    step(wB, sb + 1);
   }
+  if (sb < sb1) step(wA, sb);
 
   // ---- epilogue straight from the accumulators ---------------------------------
   // lane holds rows (base + rt*16 + r), batch rows mt*16 + 4g + i

@@ -115,12 +115,12 @@ class LlamaModel:
     def _t(self, name):
         return self.reader.tensor(name)
 
-    def _qw(self, raw, gt, rows, K, name) -> QWeight:
-        w = QWeight(raw, gt, rows, K, self.device, name)
+    def _qw(self, raw, gt, rows, K, name, layout="tiled") -> QWeight:
+        w = QWeight(raw, gt, rows, K, self.device, name, layout)
         self.weight_bytes += w.nbytes
         return w
 
-    def _matrix(self, name, rows_sl=None, cols_sl=None, expert=None) -> QWeight:
+    def _matrix(self, name, rows_sl=None, cols_sl=None, expert=None, layout="tiled") -> QWeight:
         ti = self._t(name)
         shape = ti.np_shape
         raw = ti.data
@@ -136,7 +136,7 @@ class LlamaModel:
         if cols_sl is not None:
             raw = _raw_cols(raw, ti.ggml_type, rows, K, *cols_sl)
             K = cols_sl[1] - cols_sl[0]
-        return self._qw(raw, ti.ggml_type, rows, K, name)
+        return self._qw(raw, ti.ggml_type, rows, K, name, layout)
 
     def _vec(self, name) -> torch.Tensor:
         return torch.from_numpy(self.reader.dequantized(name).astype(np.float32).copy()).to(self.device)
@@ -164,7 +164,7 @@ class LlamaModel:
     def _load(self):
         cfg, r = self.cfg, self.shard.rank
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
-        self.tok_embd = self._matrix("token_embd.weight")
+        self.tok_embd = self._matrix("token_embd.weight", layout="rows")      # gathered, not streamed
         self.layers: List[LayerWeights] = []
         for i in range(cfg.n_layer):
             p = f"blk.{i}."

@@ -35,7 +35,7 @@ def _p(t: Optional[torch.Tensor]) -> Optional[int]:
 # ---------------------------------------------------------------------------
 
 def to_device_layout(raw: np.ndarray, ggml_type: int, rows: int, K: int) -> np.ndarray:
-    """ggml block bytes -> the kernel's device layout (see csrc/kernels/common.h)."""
+    """ggml block bytes -> the "rows" layout (embedding tables; see csrc/kernels/common.h)."""
     t = GGMLType(ggml_type)
     raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)
     if t == GGMLType.Q6_K:
@@ -48,27 +48,86 @@ def to_device_layout(raw: np.ndarray, ggml_type: int, rows: int, K: int) -> np.n
     return raw
 
 
+TILE_BYTES = {GGMLType.Q4_K: 2304, GGMLType.Q5_K: 2816, GGMLType.Q6_K: 3360, GGMLType.Q8_0: 4352,
+              GGMLType.F16: 8192, GGMLType.BF16: 8192, GGMLType.F32: 16384}
+
+
+def tile_layout(raw: torch.Tensor, ggml_type: int, rows: int, K: int) -> torch.Tensor:
+    """ggml block bytes (uint8 tensor, any device) -> the GEMV "tiled" layout: rows padded to
+    16, one contiguous tile-block per (16-row tile, 256-value super-block), arranged so every
+    wave-wide 16-B load reads 1 KiB contiguous (csrc/kernels/common.h)."""
+    t = GGMLType(ggml_type)
+    nb = K // 256
+    rp = (rows + 15) // 16 * 16
+    T = rp // 16
+    rb = row_bytes(t, K)
+    b = raw.reshape(rows, rb)
+    if rp != rows:
+        b = torch.cat([b, torch.zeros(rp - rows, rb, dtype=torch.uint8, device=b.device)])
+    if t in (GGMLType.Q4_K, GGMLType.Q5_K):
+        bs = 144 if t == GGMLType.Q4_K else 176
+        q0 = 16 if t == GGMLType.Q4_K else 48
+        B = b.reshape(T, 16, nb, bs)
+        parts = [B[..., 0:16].permute(0, 2, 1, 3).reshape(T, nb, 256)]
+        if t == GGMLType.Q5_K:
+            parts.append(B[..., 16:48].reshape(T, 16, nb, 2, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 512))
+        qs = B[..., q0:q0 + 128].reshape(T, 16, nb, 8, 16)
+        parts.append(qs[:, :, :, 0:4].permute(0, 2, 3, 1, 4).reshape(T, nb, 1024))
+        parts.append(qs[:, :, :, 4:8].permute(0, 2, 3, 1, 4).reshape(T, nb, 1024))
+    elif t == GGMLType.Q6_K:
+        B = b.reshape(T, 16, nb, 210)
+        ql = B[..., 0:128].reshape(T, 16, nb, 2, 4, 16)
+        qa = ql[:, :, :, :, 0:2].reshape(T, 16, nb, 4, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 1024)
+        qb = ql[:, :, :, :, 2:4].reshape(T, 16, nb, 4, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 1024)
+        qh = B[..., 128:192].reshape(T, 16, nb, 4, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 1024)
+        sc = B[..., 192:208].permute(0, 2, 1, 3).reshape(T, nb, 256)
+        d = B[..., 208:210].permute(0, 2, 1, 3).reshape(T, nb, 32)
+        parts = [qa, qb, qh, sc, d]
+    elif t == GGMLType.Q8_0:
+        B = b.reshape(T, 16, nb, 8, 34)
+        d = B[..., 0:2].permute(0, 2, 1, 3, 4).reshape(T, nb, 256)
+        qs = B[..., 2:34].reshape(T, 16, nb, 4, 4, 16).permute(0, 2, 4, 3, 1, 5).reshape(T, nb, 4096)
+        parts = [qs, d]
+    elif t in (GGMLType.F16, GGMLType.BF16):
+        parts = [b.reshape(T, 16, nb, 4, 8, 16).permute(0, 2, 4, 3, 1, 5).reshape(T, nb, 8192)]
+    elif t == GGMLType.F32:
+        parts = [b.reshape(T, 16, nb, 4, 16, 16).permute(0, 2, 4, 3, 1, 5).reshape(T, nb, 16384)]
+    else:
+        raise NotImplementedError(f"tiled layout for {t.name}")
+    out = torch.cat(parts, dim=2) if len(parts) > 1 else parts[0]
+    assert out.shape[2] == TILE_BYTES[t]
+    return out.reshape(-1).contiguous()
+
+
 def row_bytes(ggml_type: int, K: int) -> int:
     blk, nb = GGML_BLOCK[GGMLType(ggml_type)]
     return K // blk * nb
 
 
 class QWeight:
-    """A [rows, K] weight matrix resident on `device` in its quantised form."""
+    """A [rows, K] weight matrix resident on `device` in its quantised form.
 
-    def __init__(self, raw: np.ndarray, ggml_type: int, rows: int, K: int, device, name: str = ""):
+    layout="tiled" (GEMV/GEMM operands) or "rows" (embedding tables, row gathers)."""
+
+    def __init__(self, raw: np.ndarray, ggml_type: int, rows: int, K: int, device, name: str = "",
+                 layout: str = "tiled"):
         self.type = int(ggml_type)
         self.rows = int(rows)
         self.K = int(K)
         self.name = name
+        self.layout = layout
         self.device = torch.device(device)
         if K % 256:
             raise ValueError(f"{name}: K={K} is not a multiple of 256")
-        dev = np.ascontiguousarray(to_device_layout(raw, ggml_type, rows, K))
-        with warnings.catch_warnings():     # read-only mmap views: .to(device) copies anyway
+        with warnings.catch_warnings():     # read-only mmap views: copied below
             warnings.simplefilter("ignore", UserWarning)
-            t = torch.from_numpy(dev)
-        self.data = t.to(self.device) if self.device.type != "cpu" else t.clone()
+            if layout == "rows":
+                t = torch.from_numpy(np.ascontiguousarray(to_device_layout(raw, ggml_type, rows, K)))
+                self.data = t.to(self.device) if self.device.type != "cpu" else t.clone()
+            else:
+                t = torch.from_numpy(np.ascontiguousarray(np.asarray(raw).view(np.uint8).reshape(-1)))
+                t = t.to(self.device) if self.device.type != "cpu" else t
+                self.data = tile_layout(t, ggml_type, rows, K)
         self._raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1) if self.device.type == "cpu" else None
         self._dense = None
 

@@ -80,3 +80,17 @@ def test_synthetic_model_plan(tiny_models):
     assert r.tensor("output.weight").type_name == "Q6_K"
     assert r.tensor("blk.0.attn_q.weight").type_name == "Q4_K"
     assert r.get("tokenizer.ggml.model") == "gpt2"
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16,
+                               GGMLType.F32])
+def test_tiled_layout_is_a_permutation(t):
+    """The tiled device layout keeps every byte (rows padded to 16 with zeros)."""
+    import torch
+    from nats_llm_studio_amd import ops
+    rows, K = 37, 512
+    raw = Q.random_blocks(t, rows * K, 0.05, np.random.default_rng(0))
+    tl = ops.tile_layout(torch.from_numpy(raw.copy()), t, rows, K).numpy()
+    rp = 48
+    assert tl.size == rp // 16 * (K // 256) * ops.TILE_BYTES[t]
+    assert sorted(tl.tolist()) == sorted(raw.tolist() + [0] * (tl.size - raw.size))

@@ -130,7 +130,9 @@ def test_rmsnorm_embed(gpu):
     ref = x * torch.rsqrt(x.pow(2).mean(1, keepdim=True) + 1e-5) * w
     _close(out[:5], ref, 1e-2)
     for t in TYPES:
-        qw, Wd = _qw(50, 512, t, gpu, 11)
+        raw = Q.random_blocks(t, 50 * 512, 0.05, np.random.default_rng(11))
+        qw = ops.QWeight(raw, t, 50, 512, gpu, layout="rows")
+        Wd = ops.QWeight(raw, t, 50, 512, "cpu").dense()
         ids = torch.tensor([0, 49, 7], dtype=torch.int32, device=gpu)
         e = torch.zeros(3, 512, device=gpu)
         ops.embed(ids, qw, e, 3, 2.0)
