@@ -31,6 +31,10 @@ from .sampling import SamplingParams, sample_rows
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64)
 
+# tensor-parallel control messages (rank 0 -> followers), see Engine.follow()
+_OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE = 0, 1, 2, 3
+_HDR = 8
+
 
 @dataclass
 class GenRequest:
@@ -118,6 +122,10 @@ class Engine:
                 per_block = 2 * self.cfg.n_layer * block_size * model.Hkv * model.D * 2
                 free, _ = torch.cuda.mem_get_info(self.dev)
                 num_blocks = int(min(num_blocks, kv_mem_fraction * free // per_block))
+        self.tp = model.comm if model.shard.size > 1 else None
+        self.rank = model.shard.rank
+        if self.tp is not None:                # every shard must hold the same KV block pool
+            num_blocks = self.tp.min_int(num_blocks)
         self.num_blocks = num_blocks
         self.kc, self.vc = model.kv_cache(num_blocks, block_size)
         self.alloc = BlockAllocator(num_blocks)
@@ -145,6 +153,8 @@ class Engine:
         self.stop_flag = False
         self._ids = itertools.count()
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0)
+        self.full_logits: Optional[torch.Tensor] = None
+        self._ctrl_hdr = torch.zeros(_HDR + self.max_batch, dtype=torch.int32)
 
     # ------------------------------------------------------------------ API
     def submit(self, req: GenRequest) -> Future:
@@ -188,6 +198,7 @@ class Engine:
         if self.thread is not None:
             self.thread.join()
             self.thread = None
+        self.stop_followers()
         for s in list(self.running) + list(self.waiting):
             self._finish(s, "cancelled", "engineShutdown")
         self.running.clear()
@@ -289,11 +300,10 @@ class Engine:
             if s.n_prefilled >= s.n_prompt:
                 rows.append(T - 1)
                 finishing.append(s)
-        b.meta.copy_(self.h_meta_p, non_blocking=self.dev.type == "cuda")
         nrows = max(1, len(rows))
-        lr = torch.tensor(rows + [0] * (nrows - len(rows)), dtype=torch.int32, device=self.dev)
-        self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
-                           logit_rows=lr, n_logits=nrows)
+        need = any(not s.req.params.greedy for s in finishing)
+        self._ctrl(_OP_PREFILL, T, nrows, need, rows + [0] * (nrows - len(rows)), len(batch), self.h_meta_p, pad)
+        self._exec_prefill(T, rows + [0] * (nrows - len(rows)), need)
         self.counters["prefill_tokens"] += T
         if finishing:
             toks = self._pick(finishing, b, list(range(len(finishing))))
@@ -301,6 +311,65 @@ class Engine:
             for s, t in zip(finishing, toks):
                 s.t_first = now
                 self._append(s, t)
+
+    def _exec_prefill(self, T: int, rows: List[int], need_logits: bool):
+        b = self.pb
+        b.meta.copy_(self.h_meta_p, non_blocking=self.dev.type == "cuda" and self.rank == 0)
+        lr = torch.tensor(rows, dtype=torch.int32, device=self.dev)
+        n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
+                               logit_rows=lr, n_logits=len(rows))
+        self._gather(b, n, need_logits)
+
+    def _gather(self, b, n: int, need_logits: bool):
+        if self.tp is not None and need_logits:
+            m = self.model
+            self.full_logits = self.tp.gather_logits(b.logits, n, m.cfg.vocab, m.vocab_per)
+        else:
+            self.full_logits = None
+
+    # ------------------------------------------------------------------ tensor parallel control
+    def _ctrl(self, op: int, T: int, nrows: int, need: bool, rows: List[int], nseq: int, hmeta: torch.Tensor,
+              pad: int):
+        """Rank 0: broadcast the step (header + used part of the packed metadata) to followers."""
+        if self.tp is None:
+            return
+        nb = self.max_blocks
+        hdr = self._ctrl_hdr
+        hdr.zero_()
+        hdr[:_HDR] = torch.tensor([op, T, nrows, int(need), nseq, pad, 0, 0], dtype=torch.int32)
+        if rows:
+            hdr[_HDR:_HDR + len(rows)] = torch.tensor(rows, dtype=torch.int32)
+        self.tp.bcast_ctrl(hdr)
+        if op in (_OP_PREFILL, _OP_DECODE):
+            self.tp.bcast_ctrl(hmeta[:5 * pad + nseq * nb].clone() if nseq else hmeta[:5 * pad].clone())
+
+    def stop_followers(self):
+        if self.tp is not None and self.rank == 0 and not getattr(self, "_followers_stopped", False):
+            self._followers_stopped = True
+            self._ctrl(_OP_STOP, 0, 0, False, [], 0, None, 0)
+
+    def follow(self):
+        """Follower rank main loop: replay every step rank 0 schedules until it sends STOP."""
+        assert self.tp is not None and self.rank != 0
+        nb = self.max_blocks
+        while True:
+            hdr = self.tp.bcast_ctrl(self._ctrl_hdr)
+            op, T, nrows, need, nseq, pad = (int(v) for v in hdr[:6])
+            if op == _OP_STOP:
+                return
+            if op == _OP_CAPTURE:
+                self._capture(T, LlamaModel.attn_splits(T, self.model.Hkv))
+                continue
+            hm = self.h_meta_p if op == _OP_PREFILL else self.h_meta_d
+            buf = torch.zeros(5 * pad + nseq * nb, dtype=torch.int32)
+            self.tp.bcast_ctrl(buf)
+            hm[:buf.numel()] = buf
+            if op == _OP_PREFILL:
+                self._exec_prefill(T, [int(v) for v in hdr[_HDR:_HDR + nrows]], bool(need))
+            else:
+                self.db.meta.copy_(hm)
+                self._run_decode(T)
+                self._gather(self.db, T, bool(need))
 
     def _pick(self, seqs: List[_Seq], b, rows: List[int]) -> List[int]:
         greedy = b.next_ids[:len(rows)].cpu().tolist() if self.dev.type != "cuda" else None
@@ -310,7 +379,8 @@ class Engine:
         out = list(greedy)
         sampled = [i for i, s in enumerate(seqs) if not s.req.params.greedy]
         if sampled:
-            toks = sample_rows(b.logits[[rows[i] for i in sampled]], [seqs[i].req.params for i in sampled],
+            lg = self.full_logits if self.full_logits is not None else b.logits
+            toks = sample_rows(lg[[rows[i] for i in sampled]], [seqs[i].req.params for i in sampled],
                                [seqs[i].tokens for i in sampled], [seqs[i].gen for i in sampled])
             for i, t in zip(sampled, toks):
                 out[i] = t
@@ -342,11 +412,14 @@ class Engine:
         slot[B:Bp] = -1
         tseq[B:Bp] = 0
         ctxl[B:Bp] = 0
+        need = any(not s.req.params.greedy for s in seqs)
+        self._ctrl(_OP_DECODE, Bp, 0, need, [], B, self.h_meta_d, pad)
         if self.dev.type == "cuda":
             b.meta.copy_(self.h_meta_d, non_blocking=True)
         else:
             b.meta.copy_(self.h_meta_d)
         self._run_decode(Bp)
+        self._gather(b, Bp, need)
         toks = self._pick(seqs, b, list(range(B)))
         self.counters["decode_tokens"] += B
         for s, t in zip(seqs, toks):
@@ -358,7 +431,7 @@ class Engine:
             self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
             return
         g = self.graphs.get(Bp)
-        if g is None:
+        if g is None:                          # TP followers capture lazily in the same step
             g = self._capture(Bp, ns)
         g.replay()
         self.counters["graph_replays"] += 1
@@ -385,6 +458,7 @@ class Engine:
         self.db.meta.copy_(self.h_meta_d)
         for Bp in buckets or [k for k in BUCKETS if k <= self.max_batch]:
             if Bp not in self.graphs:
+                self._ctrl(_OP_CAPTURE, Bp, 0, False, [], 0, None, 0)
                 self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv))
 
     # ------------------------------------------------------------------ completion

@@ -27,9 +27,14 @@ from .config import ModelConfig
 
 @dataclass
 class ShardSpec:
-    """Tensor-parallel shard of this process (rank of size); size 1 = whole model."""
+    """Model shard of this process (rank of size); size 1 = whole model.
+
+    Attention and dense FFNs are tensor-parallel (QKV / gate|up column-split, O / down
+    row-split, lm_head vocab-split). MoE experts are TP-sharded along their FFN dim by
+    default; with `ep=True` each rank instead owns E/size whole experts (expert parallel)."""
     rank: int = 0
     size: int = 1
+    ep: bool = False
 
 
 def _raw_rows(raw: np.ndarray, ggml_type: int, rows: int, K: int, r0: int, r1: int) -> np.ndarray:
@@ -98,6 +103,12 @@ class LlamaModel:
         self.Hkv = cfg.n_kv_head // n
         self.D = cfg.head_dim
         self.ffn = cfg.d_ff // n
+        self.ep = bool(shard.ep and cfg.n_expert and n > 1)
+        if self.ep and cfg.n_expert % n:
+            raise ValueError(f"EP={n} must divide the expert count ({cfg.n_expert})")
+        self.exp_ffn = cfg.d_ff if self.ep else self.ffn
+        per = cfg.n_expert // n if self.ep else cfg.n_expert
+        self.experts = list(range(shard.rank * per, (shard.rank + 1) * per)) if self.ep else list(range(cfg.n_expert))
         if (self.Hq * self.D) % 256 or self.ffn % 256:
             raise ValueError("TP shard widths must be multiples of 256 (K-quant super-blocks)")
         self.vocab_lo, self.vocab_hi = self._vocab_range()
@@ -110,6 +121,7 @@ class LlamaModel:
         n, r, V = self.shard.size, self.shard.rank, self.cfg.vocab
         per = (V + n - 1) // n
         per = (per + 15) // 16 * 16
+        self.vocab_per = per
         return min(V, r * per), min(V, (r + 1) * per)
 
     def _t(self, name):
@@ -141,15 +153,16 @@ class LlamaModel:
     def _vec(self, name) -> torch.Tensor:
         return torch.from_numpy(self.reader.dequantized(name).astype(np.float32).copy()).to(self.device)
 
-    def _gateup(self, gname, uname, expert=None) -> QWeight:
+    def _gateup(self, gname, uname, expert=None, ffn=None) -> QWeight:
         cfg, r = self.cfg, self.shard.rank
-        sl = (r * self.ffn, (r + 1) * self.ffn)
+        ffn = ffn or self.ffn
+        sl = (0, ffn) if ffn == cfg.d_ff else (r * ffn, (r + 1) * ffn)
         gt, ut = self._t(gname).ggml_type, self._t(uname).ggml_type
         if gt != ut:
             raise NotImplementedError("gate/up with different quant types")
         raw = ops.interleave_gate_up(self._raw_of(gname, sl, expert), self._raw_of(uname, sl, expert), gt,
-                                     self.ffn, cfg.d_model)
-        return self._qw(raw, gt, 2 * self.ffn, cfg.d_model, gname + "|up")
+                                     ffn, cfg.d_model)
+        return self._qw(raw, gt, 2 * ffn, cfg.d_model, gname + "|up")
 
     def _raw_of(self, name, rows_sl, expert=None):
         ti = self._t(name)
@@ -176,10 +189,11 @@ class LlamaModel:
             lw = LayerWeights(self._vec(p + "attn_norm.weight"), self._vec(p + "ffn_norm.weight"), qkv, wo)
             if cfg.n_expert:
                 lw.router = self._matrix(p + "ffn_gate_inp.weight")
-                for e in range(cfg.n_expert):
-                    lw.exp_gateup.append(self._gateup(p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", e))
-                    lw.exp_down.append(self._matrix(p + "ffn_down_exps.weight", None,
-                                                    (r * self.ffn, (r + 1) * self.ffn), expert=e))
+                F = self.exp_ffn
+                ksl = None if self.ep else (r * F, (r + 1) * F)
+                for e in self.experts:          # local experts (all of them unless EP)
+                    lw.exp_gateup.append(self._gateup(p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", e, F))
+                    lw.exp_down.append(self._matrix(p + "ffn_down_exps.weight", None, ksl, expert=e))
             else:
                 lw.gateup = self._gateup(p + "ffn_gate.weight", p + "ffn_up.weight")
                 lw.down = self._matrix(p + "ffn_down.weight", None, (r * self.ffn, (r + 1) * self.ffn))
@@ -216,7 +230,7 @@ class LlamaModel:
             qkv=torch.zeros(pad, (self.Hq + 2 * self.Hkv) * self.D, **f),
             q=torch.zeros(pad, nq, **bf),
             ao=torch.zeros(pad, nq, **bf),
-            act=torch.zeros(pad * (k if cfg.n_expert else 1), self.ffn, **bf),
+            act=torch.zeros(pad * (k if cfg.n_expert else 1), self.exp_ffn if cfg.n_expert else self.ffn, **bf),
             logits=torch.zeros(min(pad, max(64, max_seqs)), Vs, **f),
             keys=torch.zeros(pad, dtype=torch.int64, device=dev),
             next_ids=torch.zeros(pad, dtype=torch.int32, device=dev),
@@ -276,12 +290,11 @@ class LlamaModel:
             h = b.h.index_select(0, logit_rows[:n].long())
             h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
         ops.argmax_reset(b.keys)
-        ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale,
-                  argmax=b.keys if self.shard.size == 1 else None)
+        ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys)
         if self.shard.size == 1:
             ops.argmax_unpack(b.keys, n, b.next_ids)
         else:
-            self.comm.vocab_parallel_argmax(b.logits, n, self.vocab_lo, b.next_ids)
+            self.comm.vocab_parallel_argmax(b.keys, n, self.vocab_lo, b.next_ids)
         return n
 
     def _row_parallel(self, w: QWeight, xin: torch.Tensor, resid: torch.Tensor, T: int, alpha: float):
@@ -302,13 +315,14 @@ class LlamaModel:
         for c0 in range(0, T, 64):
             n = min(64, T - c0)
             ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap)
-            segs = [Seg(lw.exp_gateup[e], 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1])
-                    for e in range(E)]
-            for s0 in range(0, E, 8):
+            loc = list(zip(self.experts, lw.exp_gateup, lw.exp_down))
+            segs = [Seg(gu, 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, gu, _ in loc]
+            for s0 in range(0, len(segs), 8):
                 ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu")
-            segs = [Seg(lw.exp_down[e], 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1])
-                    for e in range(E)]
-            for s0 in range(0, E, 8):
+            if self.ep:                        # rows routed to other ranks' experts stay zero
+                m["yexp"][:n * k].zero_()
+            segs = [Seg(dn, 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, _, dn in loc]
+            for s0 in range(0, len(segs), 8):
                 ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32")
             if self.shard.size > 1:
                 self.comm.all_reduce(m["yexp"][:n * k])

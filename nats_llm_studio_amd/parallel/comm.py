@@ -1,0 +1,114 @@
+"""Tensor/expert-parallel communicator.
+
+The reference has no collectives at all (its only communication is NATS
+request-reply, `/root/reference/nats_llm_studio.go:207-217`); multi-GPU execution was LM
+Studio's concern. Here one process drives one GPU and the ranks of a model shard talk over
+`torch.distributed` (backend "nccl" = RCCL over xGMI on MI355X, gloo on CPU for tests):
+
+  * data plane (`group`): the row-parallel all-reduce after O-proj / down-proj (fused with
+    the residual: rank 0's GEMV adds into the residual, the other ranks overwrite it with
+    their partial, then ONE in-place sum), the MoE expert all-reduce, the vocab-parallel
+    greedy argmax (an int64 MAX all-reduce of packed (value, index) keys -- 8 bytes per
+    row instead of gathering [B, V] logits), and a logits all-gather only when a request
+    samples. Small all-reduces can be routed to the IPC one-shot kernel
+    (`parallel/oneshot.py`) instead of RCCL.
+  * control plane (`ctrl`, always gloo/TCP on the host): rank 0 (the scheduler) broadcasts
+    each step's header + packed int32 metadata so follower ranks launch the same step.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..ops import Seg
+
+_SIGN = -(1 << 63)
+
+
+class Comm:
+    def __init__(self, group=None, ctrl_group=None, device=None):
+        self.group = group
+        self.ctrl = ctrl_group if ctrl_group is not None else group
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+        self.src = dist.get_global_rank(group, 0) if group is not None else 0
+        self.device = torch.device(device) if device is not None else None
+        self.oneshot = None          # optional small-message all-reduce (parallel/oneshot.py)
+        self.stats = dict(all_reduce=0, all_reduce_bytes=0, ctrl=0)
+
+    # ------------------------------------------------------------------ data plane
+    def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
+        self.stats["all_reduce"] += 1
+        self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+        if op == dist.ReduceOp.SUM and self.oneshot is not None and self.oneshot.eligible(t):
+            self.oneshot.all_reduce(t)
+            return t
+        dist.all_reduce(t, op=op, group=self.group)
+        return t
+
+    def row_parallel_add(self, w, xin: torch.Tensor, resid: torch.Tensor, T: int, alpha: float):
+        """resid[:T] += alpha * sum_r x_r @ W_r^T  (W row-parallel: K split across ranks)."""
+        ops.qgemv([Seg(w)], xin, resid, T, alpha=alpha, epi="add" if self.rank == 0 else "f32")
+        self.all_reduce(resid[:T])
+
+    def vocab_parallel_argmax(self, keys: torch.Tensor, n: int, vocab_lo: int, next_ids: torch.Tensor):
+        """Per-rank fused-argmax keys (value<<32 | ~local_idx) -> global greedy ids on every rank."""
+        k = keys[:n]
+        if keys.is_cuda:                       # device keys are unsigned: make signed order match
+            k.bitwise_xor_(_SIGN)
+        k.sub_(vocab_lo)                       # ~local_idx - lo == ~(local_idx + lo): global index
+        self.all_reduce(k, op=dist.ReduceOp.MAX)
+        if keys.is_cuda:
+            k.bitwise_xor_(_SIGN)
+        ops.argmax_unpack(keys, n, next_ids)
+
+    def gather_logits(self, logits: torch.Tensor, n: int, vocab: int, per: int) -> torch.Tensor:
+        """Vocab-sharded logits [n, Vs] -> full [n, vocab] on every rank (only when sampling)."""
+        loc = torch.zeros(n, per, dtype=logits.dtype, device=logits.device)
+        vs = min(per, logits.shape[1])
+        loc[:, :vs] = logits[:n, :vs]
+        out = torch.empty(self.size * n, per, dtype=logits.dtype, device=logits.device)
+        dist.all_gather_into_tensor(out, loc, group=self.group)
+        return out.view(self.size, n, per).permute(1, 0, 2).reshape(n, self.size * per)[:, :vocab]
+
+    # ------------------------------------------------------------------ control plane
+    def bcast_ctrl(self, t: torch.Tensor):
+        """Host int32 tensor from rank 0 to all ranks (gloo)."""
+        self.stats["ctrl"] += 1
+        dist.broadcast(t, src=self.src, group=self.ctrl)
+        return t
+
+    def min_int(self, v: int) -> int:
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.ctrl)
+        return int(t.item())
+
+    def barrier(self):
+        dist.barrier(group=self.ctrl)
+
+
+def init_distributed(device_type: Optional[str] = None, timeout_s: float = 600.0) -> Comm:
+    """One process per GPU: reads RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT."""
+    import datetime
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dev = torch.device(f"cuda:{local}") if device_type == "cuda" else torch.device("cpu")
+    if device_type == "cuda":
+        torch.cuda.set_device(dev)
+    if not dist.is_initialized():
+        kw = dict(backend="nccl" if device_type == "cuda" else "gloo",
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if device_type == "cuda":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    ctrl = dist.new_group(backend="gloo") if device_type == "cuda" else None
+    comm = Comm(dist.group.WORLD, ctrl, dev)
+    if device_type == "cuda" and comm.size > 1 and os.environ.get("NLS_ONESHOT_AR", "0") == "1":
+        from .oneshot import OneShotAllReduce
+        comm.oneshot = OneShotAllReduce(comm)
+    return comm

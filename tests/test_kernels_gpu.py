@@ -208,3 +208,28 @@ def test_moe_route(gpu):
     for ex in range(E):
         toks = sorted(xr[ex * 64:ex * 64 + c[ex]].cpu().tolist())
         assert toks == sorted([t for t in range(T) if ex in e[t].tolist()])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_oneshot_allreduce_simulated(gpu, world):
+    """The one-shot IPC all-reduce protocol with W ranks as W concurrent streams on one GPU:
+    every rank must get the rank-ordered fp32 sum, bit-identical across ranks, over several
+    calls of varying size (epoch parity / slot reuse)."""
+    from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
+    cap = 1 << 16
+    g = SimulatedGroup(world, cap, gpu)
+    try:
+        for it, n in enumerate([4096, 100, 65536, 7, 4096 * 3, 4096]):
+            xs = [torch.randn(n, device=gpu) for _ in range(world)]
+            ref = xs[0].clone()
+            for r in range(1, world):
+                ref = ref + xs[r]
+            g.all_reduce(xs)
+            torch.cuda.synchronize()
+            assert int(g.err.item()) == 0, f"timeout at call {it}"
+            for r in range(world):
+                assert torch.equal(xs[r], xs[0])
+            torch.testing.assert_close(xs[0], ref, rtol=1e-6, atol=1e-5)
+    finally:
+        g.close()
