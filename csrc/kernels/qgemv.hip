@@ -1,515 +1,9 @@
-// Quantised GEMV / skinny GEMM for decode (M <= 64 activation rows), gfx950.
-//
-//   y[m, n] = alpha * sum_k x[m, k] * W[n, k]      (W in GGUF block formats)
-//
-// Design (SURVEY.md §2F "gemv_q*"): decode is HBM-bound on the weight stream,
-// so every weight byte is read exactly once, straight into VGPRs (no LDS round
-// trip, non-temporal loads), dequantised in registers to bf16 and fed to
-// v_mfma_f32_16x16x32_bf16 as the B operand (16 weight rows per tile). The
-// activation rows (batch, padded to 16) are the A operand, so batch 1..16 costs
-// the same MFMA issue as batch 1 and the weight dequant is amortised over the
-// whole batch. A workgroup owns RT*16 output rows; its WAVES waves split K and
-// reduce through LDS, so no atomics and bit-reproducible results.
-//
-// One launch may cover several weight matrices ("segments": fused Q|K|V with
-// per-matrix quant types, or the experts of an MoE layer) and applies a fused
-// epilogue: plain store, residual add (y += alpha*acc), SwiGLU on interleaved
-// gate/up rows, and a fused greedy arg-max (packed u64 atomicMax per row).
-#include "common.h"
+// Dispatcher of the quantised GEMV / GEMM (kernels: qgemv_impl.h, instantiated per type-set in
+// qgemv_k{0,1,2}.hip).
+#include "qgemv_impl.h"
 
-namespace {
+using namespace nls_gemv;
 
-enum Epi : int { EPI_F32 = 0, EPI_BF16 = 1, EPI_ADD_F32 = 2, EPI_SWIGLU_BF16 = 3 };
-
-struct Seg {
-  const uint8_t* w;
-  const int* xmap;     // optional: segment-local batch row -> x row (-1: none)
-  const int* ymap;     // optional: segment-local batch row -> y row
-  const int* mcount;   // optional: device count of valid rows (tiles skip when 0)
-  int type, rows, K, tile_begin, ycol, tile_begin_col;
-};
-struct SegList { Seg s[8]; int nseg; int pad[3]; };
-
-struct GemvArgs {
-  const __bf16* x; long ldx;
-  void* y; long ldy;
-  int M;               // rows of x / y (or max rows per segment when mapped)
-  int epi;
-  float alpha;
-  int pad;            // path B split-K: total raw output columns
-  unsigned long long* argmax;   // optional [M] packed (ordered value << 32 | ~idx)
-};
-
-DEVI unsigned long long argmax_key(float v, int idx) {
-  uint32_t u = __builtin_bit_cast(uint32_t, v);
-  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  return ((unsigned long long)u << 32) | (0xFFFFFFFFu - (uint32_t)idx);
-}
-
-DEVI float silu(float g) { return g / (1.f + __expf(-g)); }
-
-template <int T, int WAVES, int RT, int MT>
-DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
-  const int r = lane & 15, g = lane >> 4;
-  const WDesc W{S.w, S.rows, S.K};
-  const int nb = S.K >> 8;
-  const int sb0 = (nb * wave) / WAVES, sb1 = (nb * (wave + 1)) / WAVES;
-
-  int mcount = a.M;
-  if (S.mcount) mcount = min(*S.mcount, a.M);
-
-  // Activation rows (A operand row = batch row r of tile mt). Padded / unmapped rows load a
-  // valid row (row 0: broadcast, cache-resident) and are zeroed with a select after the load:
-  // a lane-conditional load would compile to a branch + vmcnt(0) per K-step that drains the
-  // whole weight prefetch (cdna_hip_programming.md §5 "Three .s-level traps" (c)).
-  const __bf16* xr[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = mt * 16 + r;
-    int src = m < mcount ? m : -1;
-    if (S.xmap) src = (m < mcount) ? S.xmap[m] : -1;
-    xr[mt] = a.x + (size_t)(src >= 0 ? src : 0) * a.ldx;
-  }
-  int rowc[RT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(row0 + rt * 16 + r, S.rows - 1);
-
-  f32x4 acc[RT][MT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // Weight stream: two register buffers with FIXED roles (A: even, B: odd super-blocks), the
-  // loop unrolled by two, so a buffer is reloaded (sb + 2) right after its dequant and no
-  // register holding an in-flight load is ever copied (a copy would force vmcnt(0)).
-  typedef typename RawOf<T>::type Raw;
-  Raw wA[RT], wB[RT];
-  // All weight loads are unconditional (super-block index clamped into [sb0, sb1)): a
-  // conditional load breaks hipcc's vmcnt bookkeeping at the join and it falls back to
-  // vmcnt(0). The clamped tail reloads hit L2 and are never consumed.
-  const int sbl = max(sb1 - 1, sb0);
-  if (sb0 < sb1) {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
-  }
-  auto step = [&](Raw (&w)[RT], int sb) {
-    // 1) activation fragments of this super-block (issued before this step's weight reload)
-    bf16x8 xa[8][MT];
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        xa[t][mt] = *reinterpret_cast<const bf16x8*>(xr[mt] + sb * 256 + xoff<T>(t, g));
-    // the scheduler must not sink these loads below the weight reload (the in-order vmcnt
-    // wait for a late x load would then also wait for the reload)
-    __builtin_amdgcn_sched_barrier(0);
-    // 2) dequant (waits only for this buffer's loads, issued two steps ago)
-    bf16x8 wf[RT][8];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
-    __builtin_amdgcn_sched_barrier(0);
-    // 3) reload the buffer two super-blocks ahead
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
-    __builtin_amdgcn_sched_barrier(0);
-    // 4) MFMA
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 x8 = xa[t][mt];   // rows >= mcount only reach output rows that are never stored
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x8, wf[rt][t], acc[rt][mt], 0, 0, 0);
-      }
-    }
-  };
-  int sb = sb0;
-  for (; sb + 1 < sb1; sb += 2) {
-    step(wA, sb);
-    step(wB, sb + 1);
-  }
-  if (sb < sb1) step(wA, sb);
-
-  // ---- cross-wave reduction through LDS -------------------------------------
-  // red: [WAVES][RT][MT][4][64] ; tile: [RT*16 rows][MT*16 batch]
-  float* red = lds;
-  float* tile = lds + WAVES * RT * MT * 256;
-  constexpr int NE = RT * MT * 256;
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        red[(((wave * RT + rt) * MT + mt) * 4 + c) * 64 + lane] = acc[rt][mt][c];
-  __syncthreads();
-  for (int e = threadIdx.x; e < NE; e += WAVES * 64) {
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) s += red[w * NE + e];
-    const int ln = e & 63, c = (e >> 6) & 3, mt = (e >> 8) % MT, rt = (e >> 8) / MT;
-    const int rr = rt * 16 + (ln & 15);
-    const int bb = mt * 16 + 4 * (ln >> 4) + c;
-    tile[rr * (MT * 16) + bb] = s * a.alpha;
-  }
-  __syncthreads();
-
-  // ---- epilogue ----------------------------------------------------------------
-  const int ncols = MT * 16;
-  if (a.epi == EPI_SWIGLU_BF16) {
-    // tile rows [16i, 16i+8) = gate, [16i+8, 16i+16) = up of outputs (row0/2 + 8i + j)
-    for (int e = threadIdx.x; e < RT * 8 * ncols; e += WAVES * 64) {
-      const int bb = e % ncols, j = e / ncols, rt = j >> 3, jj = j & 7;
-      if (bb >= mcount) continue;
-      const int grow = row0 + rt * 16 + jj;
-      if (grow >= S.rows) continue;
-      const float gv = tile[(rt * 16 + jj) * ncols + bb];
-      const float uv = tile[(rt * 16 + 8 + jj) * ncols + bb];
-      const int yrow = S.ymap ? S.ymap[bb] : bb;
-      const int n = S.ycol + (row0 >> 1) + rt * 8 + jj;
-      reinterpret_cast<__bf16*>(a.y)[(size_t)yrow * a.ldy + n] = (__bf16)(silu(gv) * uv);
-    }
-    return;
-  }
-  for (int e = threadIdx.x; e < RT * 16 * ncols; e += WAVES * 64) {
-    const int bb = e % ncols, rr = e / ncols;
-    const int row = row0 + rr;
-    if (bb >= mcount || row >= S.rows) continue;
-    const float v = tile[rr * ncols + bb];
-    const int yrow = S.ymap ? S.ymap[bb] : bb;
-    const size_t off = (size_t)yrow * a.ldy + S.ycol + row;
-    if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
-    else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
-  }
-  if (a.argmax) {
-    for (int bb = threadIdx.x; bb < min(mcount, ncols); bb += WAVES * 64) {
-      unsigned long long best = 0;
-      for (int rr = 0; rr < RT * 16; ++rr) {
-        const int row = row0 + rr;
-        if (row >= S.rows) break;
-        unsigned long long k = argmax_key(tile[rr * ncols + bb], S.ycol + row);
-        best = k > best ? k : best;
-      }
-      atomicMax(a.argmax + bb, best);
-    }
-  }
-}
-
-// KSET 0: Q4_K/Q6_K (the Q4_K_M mix); KSET 1: Q5_K/Q6_K/Q8_0; KSET 2: plain F16/BF16/F32. Splitting the format
-// switch keeps the register budget of the quantised kernels small (a switch case's
-// VGPR demand is paid by every case).
-template <int WAVES, int RT, int MT, int KSET>
-__global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tile = blockIdx.x;
-  Seg S = segs.s[0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i)
-    if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
-  if (S.mcount && *S.mcount <= 0) return;     // MoE expert with no routed tokens
-  const int row0 = (tile - S.tile_begin) * RT * 16;
-  if constexpr (KSET == 0) {
-    switch (S.type) {
-      case QT_Q4_K: gemv_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      default: break;
-    }
-  } else if constexpr (KSET == 1) {
-    switch (S.type) {
-      case QT_Q5_K: gemv_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, a, lds); break;
-      default: break;
-    }
-  } else {
-    switch (S.type) {
-      case QT_F16: gemv_tile<QT_F16, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_BF16: gemv_tile<QT_BF16, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_F32: gemv_tile<QT_F32, WAVES, RT, MT>(S, row0, a, lds); break;
-      default: break;
-    }
-  }
-}
-
-// ===========================================================================
-// Path B (batch >= ~16): waves split ROWS, not K. The activation tile of the current
-// 256-wide super-block (M x 256 bf16, XOR-swizzled 16-B chunks) is staged once per
-// workgroup in LDS (double-buffered) and read by every wave with ds_read_b128, so x is
-// fetched from L2 once per WAVES*RT*16 weight rows instead of once per 16. Optional
-// split-K over workgroups (KS > 1) writes fp32 partial slabs; splitk_reduce applies
-// the epilogue in a fixed order (deterministic, no float atomics).
-// ===========================================================================
-DEVI int lds_off(int row, int k) {            // element offset in a [rows][256] bf16 tile
-  const int ch = (k >> 3) ^ (row & 15);
-  return row * 256 + ch * 8 + (k & 7);
-}
-
-template <int T, int WAVES, int RT, int MT>
-DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, __bf16* lds) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const WDesc W{S.w, S.rows, S.K};
-  const int nb = S.K >> 8;
-  const int sb0 = (nb * kslice) / ks, sb1 = (nb * (kslice + 1)) / ks;
-  const int M = a.M;
-  const int base = row0 + wave * RT * 16;
-  int rowc[RT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(base + rt * 16 + r, S.rows - 1);
-
-  constexpr int NT = WAVES * 64;
-  constexpr int NCH = (MT * 16 * 32) / NT;               // 16-B chunks staged per thread
-  static_assert((MT * 16 * 32) % NT == 0, "staging must divide evenly");
-  u32x4 xst[NCH];
-  auto load_x = [&](int sb) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int idx = threadIdx.x + c * NT;
-      const int row = idx >> 5, ch = idx & 31;
-      // rows >= M only feed output rows that are never stored: clamp, never branch
-      xst[c] = ld16(a.x + (size_t)min(row, M - 1) * a.ldx + sb * 256 + ch * 8);
-    }
-  };
-  auto store_x = [&](int buf) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int idx = threadIdx.x + c * NT;
-      const int row = idx >> 5, ch = idx & 31;
-      *reinterpret_cast<u32x4*>(lds + buf * (MT * 16 * 256) + lds_off(row, ch * 8)) = xst[c];
-    }
-  };
-
-  f32x4 acc[RT][MT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  typedef typename RawOf<T>::type Raw;
-  Raw wA[RT], wB[RT];
-  const int sbl = max(sb1 - 1, sb0);
-  if (sb0 < sb1) {
-    load_x(sb0);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
-    store_x(0);
-  }
-  __syncthreads();
-  // fixed buffer roles, unrolled by two (see path A); x for sb+1 is staged through the other
-  // LDS buffer while sb is computed
-  auto step = [&](Raw (&w)[RT], int sb) {
-    const int buf = (sb - sb0) & 1;
-    load_x(min(sb + 1, sbl));          // unconditional (clamped): see path A
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 wf[RT][8];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
-    __builtin_amdgcn_sched_barrier(0);
-    const __bf16* xb = lds + buf * (MT * 16 * 256);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int ko = xoff<T>(t, g);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
-      }
-    }
-    store_x(buf ^ 1);
-    __syncthreads();
-  };
-  int sb = sb0;
-  for (; sb + 1 < sb1; sb += 2) {
-    step(wA, sb);
-    step(wB, sb + 1);
-  }
-  if (sb < sb1) step(wA, sb);
-
-  // ---- epilogue straight from the accumulators ---------------------------------
-  // lane holds rows (base + rt*16 + r), batch rows mt*16 + 4g + i
-  if (ks > 1) {
-    const int ntot = a.pad;      // total output columns (all segments, raw rows)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int row = base + rt * 16 + r;
-      if (row >= S.rows) continue;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int b = mt * 16 + 4 * g + i;
-          if (b < M) ws[((size_t)kslice * M + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][i];
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    const int row = base + rt * 16 + r;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = mt * 16 + 4 * g + i;
-        const float v = acc[rt][mt][i] * a.alpha;
-        if (a.epi == EPI_SWIGLU_BF16) {
-          const float u = __shfl_xor(v, 8, 64);
-          if (r < 8 && b < M && row < S.rows) {
-            const int n = S.ycol + ((base + rt * 16) >> 1) + r;
-            reinterpret_cast<__bf16*>(a.y)[(size_t)b * a.ldy + n] = (__bf16)(silu(v) * u);
-          }
-          continue;
-        }
-        if (b < M && row < S.rows) {
-          const size_t off = (size_t)b * a.ldy + S.ycol + row;
-          if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
-          else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-          else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
-        }
-        if (a.argmax) {
-          unsigned long long k = (row < S.rows) ? argmax_key(v, S.ycol + row) : 0ull;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            const unsigned long long ok = __shfl_xor(k, o, 64);
-            k = ok > k ? ok : k;
-          }
-          if (r == 0 && b < M) atomicMax(a.argmax + b, k);
-        }
-      }
-    }
-  }
-}
-
-template <int WAVES, int RT, int MT, int KSET>
-__global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs a, int ks, float* ws) {
-  extern __shared__ __attribute__((aligned(16))) __bf16 xlds[];
-  const int tile = blockIdx.x / ks, kslice = blockIdx.x % ks;
-  Seg S = segs.s[0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i)
-    if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
-  const int row0 = (tile - S.tile_begin) * WAVES * RT * 16;
-  if constexpr (KSET == 0) {
-    switch (S.type) {
-      case QT_Q4_K: mm_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      default: break;
-    }
-  } else if constexpr (KSET == 1) {
-    switch (S.type) {
-      case QT_Q5_K: mm_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q8_0: mm_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      default: break;
-    }
-  } else {
-    switch (S.type) {
-      case QT_F16: mm_tile<QT_F16, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_BF16: mm_tile<QT_BF16, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_F32: mm_tile<QT_F32, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      default: break;
-    }
-  }
-}
-
-// Split-K reduction + epilogue. ws: [ks][M][ntot] fp32 (ntot = raw output rows over all segments)
-struct RedSeg { int col0, rows, ycol, pad; };
-struct RedList { RedSeg s[8]; int nseg, pad[3]; };
-
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks, int M, int ntot, RedList rl,
-                                     GemvArgs a) {
-  const int b = blockIdx.y;
-  const bool swiglu = a.epi == EPI_SWIGLU_BF16;
-  const int nout = swiglu ? ntot / 2 : ntot;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nout; j += gridDim.x * blockDim.x) {
-    int col = swiglu ? (j >> 3) * 16 + (j & 7) : j;
-    RedSeg S = rl.s[0];
-    for (int i = 1; i < rl.nseg; ++i)
-      if (col >= rl.s[i].col0) S = rl.s[i];
-    float v = 0.f, u = 0.f;
-    for (int k = 0; k < ks; ++k) {
-      v += ws[((size_t)k * M + b) * ntot + col];
-      if (swiglu) u += ws[((size_t)k * M + b) * ntot + col + 8];
-    }
-    v *= a.alpha;
-    u *= a.alpha;
-    const int row = col - S.col0;
-    if (swiglu) {
-      const int n = S.ycol + (row >> 4) * 8 + (row & 7);
-      reinterpret_cast<__bf16*>(a.y)[(size_t)b * a.ldy + n] = (__bf16)(silu(v) * u);
-      continue;
-    }
-    const size_t off = (size_t)b * a.ldy + S.ycol + row;
-    if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
-    else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
-    if (a.argmax) atomicMax(a.argmax + b, argmax_key(v, S.ycol + row));
-  }
-}
-
-template <int WAVES, int RT, int MT>
-int launch_t(const SegList& sl, int ntiles, const GemvArgs& a, hipStream_t st, int kset) {
-  const size_t lds = (size_t)(WAVES + 1) * RT * MT * 256 * sizeof(float);
-  if (kset == 0)
-    hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, 0>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
-  else if (kset == 1)
-    hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, 1>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
-  else
-    hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, 2>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
-  return (int)hipGetLastError();
-}
-
-template <int WAVES, int RT>
-int launch_mt(int mt, const SegList& sl, int nt, const GemvArgs& a, hipStream_t st, int kset) {
-  switch (mt) {
-    case 1: return launch_t<WAVES, RT, 1>(sl, nt, a, st, kset);
-    case 2: return launch_t<WAVES, RT, 2>(sl, nt, a, st, kset);
-    case 3: return launch_t<WAVES, RT, 3>(sl, nt, a, st, kset);
-    case 4: return launch_t<WAVES, RT, 4>(sl, nt, a, st, kset);
-  }
-  return -1;
-}
-
-template <int WAVES, int RT, int MT>
-int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st, int kset) {
-  const size_t lds = (size_t)2 * MT * 16 * 256 * sizeof(__bf16);
-  if (kset == 0)
-    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, 0>), dim3(ntiles * ks), dim3(WAVES * 64), lds, st, sl, a, ks, ws);
-  else if (kset == 1)
-    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, 1>), dim3(ntiles * ks), dim3(WAVES * 64), lds, st, sl, a, ks, ws);
-  else
-    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, 2>), dim3(ntiles * ks), dim3(WAVES * 64), lds, st, sl, a, ks, ws);
-  return (int)hipGetLastError();
-}
-
-template <int WAVES, int RT>
-int launch_b_mt(int mt, const SegList& sl, int nt, int ks, float* ws, const GemvArgs& a, hipStream_t st,
-                int kset) {
-  switch (mt) {
-    case 1: return launch_b<WAVES, RT, 1>(sl, nt, ks, ws, a, st, kset);
-    case 2: return launch_b<WAVES, RT, 2>(sl, nt, ks, ws, a, st, kset);
-    case 3: return launch_b<WAVES, RT, 3>(sl, nt, ks, ws, a, st, kset);
-    case 4: return launch_b<WAVES, RT, 4>(sl, nt, ks, ws, a, st, kset);
-  }
-  return -1;
-}
-
-}  // namespace
 
 extern "C" {
 
@@ -528,9 +22,9 @@ struct NlsSeg {
 int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
               float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
               void* stream) {
-  if (nseg < 1 || nseg > 8 || M < 1 || M > 64 || (rt != 1 && rt != 2) || (waves != 4 && waves != 8))
-    return -1;
-  if (mode == 1 && ks > 1 && !ws) return -1;
+  if (nseg < 1 || nseg > 8 || M < 1 || (rt != 1 && rt != 2) || (waves != 4 && waves != 8)) return -1;
+  if (M > 64 && mode != 1) return -1;   // large M: path B in blocks of 128 activation rows
+  if (mode == 1 && ks > 1 && (!ws || M > 64)) return -1;
   SegList sl{};
   int tiles = 0, cols = 0;
   const int tile_rows = (mode == 1 ? waves : 1) * rt * 16;
@@ -564,15 +58,13 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
   const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
   GemvArgs a{(const __bf16*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax};
-  const int mt = (M + 15) / 16;
+  const int mt = M > 64 ? 8 : (M + 15) / 16;
+  const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
+  auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : launch_k2);
   if (mode == 1) {
     if (ks < 1) ks = 1;
-    int rc;
-    if (waves == 8) rc = rt == 1 ? launch_b_mt<8, 1>(mt, sl, tiles, ks, (float*)ws, a, st, kset)
-                                 : launch_b_mt<8, 2>(mt, sl, tiles, ks, (float*)ws, a, st, kset);
-    else rc = rt == 1 ? launch_b_mt<4, 1>(mt, sl, tiles, ks, (float*)ws, a, st, kset)
-                      : launch_b_mt<4, 2>(mt, sl, tiles, ks, (float*)ws, a, st, kset);
+    const int rc = launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
     if (rc || ks == 1) return rc;
     RedList rl{};
     for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};
@@ -582,9 +74,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, ks, M, cols, rl, a);
     return (int)hipGetLastError();
   }
-  if (waves == 8)
-    return rt == 1 ? launch_mt<8, 1>(mt, sl, tiles, a, st, kset) : launch_mt<8, 2>(mt, sl, tiles, a, st, kset);
-  return rt == 1 ? launch_mt<4, 1>(mt, sl, tiles, a, st, kset) : launch_mt<4, 2>(mt, sl, tiles, a, st, kset);
+  return launch(0, waves, rt, mt, sl, tiles, 1, nullptr, a, st, 1);
 }
 
 }  // extern "C"

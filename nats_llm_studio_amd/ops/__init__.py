@@ -193,14 +193,17 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
     if x.is_cuda:
         L = _lib.lib()
         mapped = any(s.xmap is not None for s in segs)
-        if M > 64 and not mapped:
+        if mode < 0 or waves == 0:
+            mode, waves, rt, ks = gemv_config(segs, M) if not mapped else (0, 8, 1, 1)
+        if M > 64 and (mapped or mode != 1):
+            # mapped (MoE) rows / path A: chunks of 64 rows
             for m0 in range(0, M, 64):
                 mm = min(64, M - m0)
                 qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt,
                       mode, ks)
             return y
-        if mode < 0 or waves == 0:
-            mode, waves, rt, ks = gemv_config(segs, M) if not mapped else (0, 8, 1, 1)
+        if M > 64:
+            ks = 1                    # large M: MFMA GEMM over 128-row activation blocks
         arr = (_lib.NlsSeg * len(segs))()
         for i, s in enumerate(segs):
             arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,

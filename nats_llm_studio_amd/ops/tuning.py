@@ -11,14 +11,14 @@ import os
 
 _TABLE = None
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemv_tuning.json")
-MBUCKETS = (1, 2, 4, 8, 16, 32, 48, 64)
+MBUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 128, 256, 512, 1024, 2048)
 
 
 def _mb(M: int) -> int:
     for b in MBUCKETS:
         if M <= b:
             return b
-    return 64
+    return MBUCKETS[-1]
 
 
 def key(segs, M: int) -> str:
@@ -42,6 +42,8 @@ def heuristic(segs, M: int):
     K = segs[0].w.K
     if M <= 8:
         return (0, 8, 1, 1)
+    if M > 64:                   # MFMA GEMM: 128 weight rows x 128 activation rows per workgroup
+        return (1, 8, 1, 1)
     waves, rt = 8, 1
     tiles = sum((s.w.rows + waves * rt * 16 - 1) // (waves * rt * 16) for s in segs)
     ks = 1

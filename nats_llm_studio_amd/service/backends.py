@@ -111,6 +111,7 @@ class EngineBackend:
         self._lock = threading.RLock()
         self._loaded: "collections.OrderedDict[str, dict]" = collections.OrderedDict()
         self._device = None
+        self.pinned = False          # tensor-parallel worker: serves only its preloaded model
 
     def device(self):
         import torch
@@ -125,38 +126,53 @@ class EngineBackend:
         with self._lock:
             return list(self._loaded)
 
-    def load(self, entry: ModelEntry) -> dict:
+    def build_state(self, entry: ModelEntry, shard=None, comm=None, start: bool = True) -> dict:
+        """GGUF -> device model + tokenizer + chat template + engine (one TP shard if `shard`)."""
         from ..engine.engine import Engine
         from ..gguf.reader import GGUFReader
-        from ..models.llama import LlamaModel
+        from ..models.llama import LlamaModel, ShardSpec
         from ..tokenizer.bpe import tokenizer_from_metadata
         from ..tokenizer.chat_template import ChatTemplate, default_template
+        t0 = time.time()
+        reader = GGUFReader(entry.path)
+        md = reader.metadata
+        model = LlamaModel(reader, self.device(), shard or ShardSpec(), comm)
+        tok = tokenizer_from_metadata(md)
+        tmpl = md.get("tokenizer.chat_template") or default_template(model.cfg.arch,
+                                                                     md.get("tokenizer.ggml.model", "gpt2"))
+        bos = tok.tokens[tok.bos_id] if tok.bos_id is not None else ""
+        eos = tok.tokens[tok.eos_id] if tok.eos_id is not None else ""
+        eng = Engine(model, tok, max_batch=self.cfg.max_batch, ctx=self.cfg.max_ctx or None,
+                     kv_mem_fraction=self.cfg.kv_mem_fraction, max_prefill_tokens=self.cfg.max_prefill_tokens)
+        if start:
+            eng.start()
+        return {"engine": eng, "tok": tok, "tmpl": ChatTemplate(tmpl, bos, eos), "entry": entry,
+                "load_s": time.time() - t0}
+
+    def adopt(self, st: dict, pinned: bool = True):
+        """Serve an already-built state (tensor-parallel rank 0); other models are refused."""
+        with self._lock:
+            self._loaded[st["entry"].id] = st
+            self.pinned = pinned
+
+    def load(self, entry: ModelEntry) -> dict:
         with self._lock:
             if entry.id in self._loaded:
                 self._loaded.move_to_end(entry.id)
                 return self._loaded[entry.id]
+            if self.pinned:
+                raise RuntimeError(f"this tensor-parallel worker serves only {list(self._loaded)}")
             while len(self._loaded) >= max(1, self.cfg.max_loaded_models):
                 old, st = self._loaded.popitem(last=False)
                 st["engine"].unload()
-            t0 = time.time()
-            reader = GGUFReader(entry.path)
-            md = reader.metadata
-            model = LlamaModel(reader, self.device())
-            tok = tokenizer_from_metadata(md)
-            tmpl = md.get("tokenizer.chat_template") or default_template(model.cfg.arch,
-                                                                         md.get("tokenizer.ggml.model", "gpt2"))
-            bos = tok.tokens[tok.bos_id] if tok.bos_id is not None else ""
-            eos = tok.tokens[tok.eos_id] if tok.eos_id is not None else ""
-            eng = Engine(model, tok, max_batch=self.cfg.max_batch, ctx=self.cfg.max_ctx or None,
-                         kv_mem_fraction=self.cfg.kv_mem_fraction, max_prefill_tokens=self.cfg.max_prefill_tokens)
-            eng.start()
-            st = {"engine": eng, "tok": tok, "tmpl": ChatTemplate(tmpl, bos, eos), "entry": entry,
-                  "load_s": time.time() - t0}
+            st = self.build_state(entry)
             self._loaded[entry.id] = st
             return st
 
     def unload(self, model_id: str) -> bool:
         with self._lock:
+            if self.pinned:
+                return False
             st = self._loaded.pop(model_id, None)
         if st is None:
             return False
@@ -217,3 +233,47 @@ class EngineBackend:
             return {"backend": "engine", "device": str(self._device),
                     "models": {k: dict(v["engine"].stats(), load_s=round(v["load_s"], 3))
                                for k, v in self._loaded.items()}}
+
+
+class HttpBackend:
+    """The reference's own mode: forward to an LM Studio server (`LMSTUDIO_BASE_URL`).
+
+    ListModels / Chat semantics of `/root/reference/nats_llm_studio.go:136-179`: the raw
+    body and the HTTP status are returned WITHOUT checking the status (a non-200 still
+    yields ok:true with http_status); the chat payload is forwarded verbatim with
+    Content-Type application/json; a 2-minute client timeout (`:36`)."""
+
+    name = "http"
+
+    def __init__(self, base_url: str, timeout: float = 120.0):
+        self.base = base_url.rstrip("/")
+        self.timeout = timeout
+        self.requests = 0
+
+    def _do(self, method: str, path: str, body: Optional[bytes] = None):
+        import urllib.error
+        import urllib.request
+        req = urllib.request.Request(self.base + path, data=body, method=method)
+        if body is not None:
+            req.add_header("Content-Type", "application/json")
+        try:
+            with urllib.request.urlopen(req, timeout=self.timeout) as r:
+                return r.status, r.read()
+        except urllib.error.HTTPError as e:       # non-2xx: body + status, not an error
+            return e.code, e.read()
+
+    def list_models_raw(self):
+        return self._do("GET", "/api/v0/models")
+
+    def chat_raw(self, payload: bytes):
+        self.requests += 1
+        return self._do("POST", "/api/v0/chat/completions", payload)
+
+    def loaded_ids(self):
+        return []
+
+    def unload(self, model_id: str) -> bool:
+        return False
+
+    def stats(self):
+        return {"backend": "http", "base_url": self.base, "requests": self.requests}

@@ -40,9 +40,11 @@ class WorkerConfig:
     queue_group: str = "lmstudio-workers"
     subject_prefix: str = SUBJECT_PREFIX
     bucket: str = "llm-models"
-    backend: str = "engine"            # engine | stub
+    backend: str = "engine"            # engine | stub | http (proxy to an LM Studio server, the reference's mode)
     device: str = "auto"               # auto | cuda:N | cpu
-    tp: int = 1
+    tp: int = 1                        # tensor-parallel ranks (launch with torchrun, one process per GPU)
+    ep: bool = False                   # MoE: expert-parallel instead of TP-sharded experts
+    model: str = ""                    # model to preload (registry id or .gguf path; required when tp > 1)
     max_batch: int = 64
     max_ctx: int = 0                   # 0 = model context length
     kv_mem_fraction: float = 0.5
@@ -57,7 +59,7 @@ class WorkerConfig:
     timeout_delete: float = 120.0
     timeout_chat: float = 120.0
     handler_workers: int = 4
-    lmstudio_base_url: str = "http://127.0.0.1:1234"   # accepted for .env parity; unused (no HTTP hop)
+    lmstudio_base_url: str = "http://127.0.0.1:1234"   # used by the `http` backend only
 
     def subject(self, name: str) -> str:
         return f"{self.subject_prefix}.{name}"
@@ -73,6 +75,8 @@ class WorkerConfig:
         c.backend = e.get("BACKEND", c.backend)
         c.device = e.get("DEVICE", c.device)
         c.tp = int(e.get("TP", c.tp))
+        c.ep = e.get("EP", "0") in ("1", "true", "yes")
+        c.model = e.get("MODEL", c.model)
         c.max_batch = int(e.get("MAX_BATCH", c.max_batch))
         c.max_ctx = int(e.get("MAX_CTX", c.max_ctx))
         c.kv_mem_fraction = float(e.get("KV_MEM_FRACTION", c.kv_mem_fraction))
@@ -91,7 +95,10 @@ class WorkerConfig:
         ap.add_argument("--models-dir", default=c.models_dir)
         ap.add_argument("--queue-group", default=c.queue_group)
         ap.add_argument("--bucket", default=c.bucket)
-        ap.add_argument("--backend", default=c.backend, choices=["engine", "stub"])
+        ap.add_argument("--backend", default=c.backend, choices=["engine", "stub", "http"])
+        ap.add_argument("--lmstudio-base-url", default=c.lmstudio_base_url)
+        ap.add_argument("--model", default=c.model)
+        ap.add_argument("--ep", action="store_true", default=c.ep)
         ap.add_argument("--device", default=c.device)
         ap.add_argument("--tp", type=int, default=c.tp)
         ap.add_argument("--max-batch", type=int, default=c.max_batch)

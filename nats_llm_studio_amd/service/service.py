@@ -26,7 +26,7 @@ from collections import defaultdict
 from typing import Optional
 
 from . import envelope
-from .backends import EngineBackend, StubBackend
+from .backends import EngineBackend, HttpBackend, StubBackend
 from .config import WorkerConfig
 from .registry import Registry
 from .store import ModelStore, PullError
@@ -39,7 +39,14 @@ class Service:
         self.cfg = cfg
         self.client = client
         self.registry = Registry(cfg.models_dir)
-        self.backend = backend or (StubBackend() if cfg.backend == "stub" else EngineBackend(cfg))
+        if backend is None:
+            if cfg.backend == "stub":
+                backend = StubBackend()
+            elif cfg.backend == "http":
+                backend = HttpBackend(cfg.lmstudio_base_url, cfg.timeout_chat)
+            else:
+                backend = EngineBackend(cfg)
+        self.backend = backend
         self.store: Optional[ModelStore] = None
         self.subs = []
         self.t_start = time.time()
@@ -102,7 +109,24 @@ class Service:
             print(f"error responding to NATS message: {e}", flush=True)
 
     # ------------------------------------------------------------------ handlers
+    def _raw_json(self, body: bytes):
+        """json.RawMessage: a non-JSON backend body makes marshalling fail -> literal fallback."""
+        try:
+            return json.loads(body.decode("utf-8") if body else "")
+        except (UnicodeDecodeError, ValueError):
+            return None
+
     def on_list_models(self, msg):
+        if isinstance(self.backend, HttpBackend):           # `nats_llm_studio.go:228-248`
+            try:
+                status, body = self.backend.list_models_raw()
+            except Exception as e:
+                self.respond(msg, envelope.error(f"error calling LM Studio: {e}", {"http_status": 0}))
+                return
+            raw = self._raw_json(body)
+            self.respond(msg, envelope.FALLBACK if raw is None else
+                         envelope.ok({"http_status": status, "models": raw}))
+            return
         try:
             models = self.registry.list_api(self.backend.loaded_ids())
         except Exception as e:
@@ -188,6 +212,16 @@ class Service:
             self.respond(msg, envelope.error("'model' is required in ChatModel"))
             return
         req = json.loads(msg.data)
+        if isinstance(self.backend, HttpBackend):           # forwards the ORIGINAL bytes (`:348`)
+            try:
+                status, body = self.backend.chat_raw(bytes(msg.data))
+            except Exception as e:
+                self.respond(msg, envelope.error(f"error calling LM Studio: {e}", {"http_status": 0}))
+                return
+            raw = self._raw_json(body)
+            self.respond(msg, envelope.FALLBACK if raw is None else
+                         envelope.ok({"http_status": status, "response": raw}))
+            return
         entry = self.registry.resolve(model)
         if entry is None and isinstance(self.backend, EngineBackend):
             self.registry.scan()

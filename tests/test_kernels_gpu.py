@@ -233,3 +233,45 @@ def test_oneshot_allreduce_simulated(gpu, world):
             torch.testing.assert_close(xs[0], ref, rtol=1e-6, atol=1e-5)
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q8_0, GGMLType.BF16])
+@pytest.mark.parametrize("M", [65, 128, 200, 300])
+@pytest.mark.parametrize("wr", [(8, 1), (4, 2)])
+def test_qgemm_large_m(gpu, t, M, wr):
+    """Large-M MFMA GEMM (prefill / big decode batches): 128-row activation blocks, XCD-grouped
+    weight tiles, partial last block; plain store, residual add and fused argmax."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    waves, rt = wr
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=1, waves=waves, rt=rt, ks=1, argmax=keys)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    assert float(y[M:].abs().max().cpu()) == 0.0 if M < pad else True
+    ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+    ops.argmax_unpack(keys, M, ids)
+    assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=1, waves=waves, rt=rt, ks=1)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+
+
+def test_qgemm_large_m_swiglu(gpu):
+    K, F = 512, 256
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 333
+    x = _x(M, K, gpu)
+    y = torch.zeros(x.shape[0], F, dtype=torch.bfloat16, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=1, waves=8, rt=1, ks=1)
+    xf = x[:M].float().cpu()
+    _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)

@@ -110,3 +110,61 @@ def test_tp2_matches_tp1(tmp_path, fam, ep):
     assert lg.shape[1] == spec.vocab
     err = abs(lg - ref).max() / (abs(ref).max() + 1e-6)
     assert err < 1e-3, err
+
+
+def _tp_worker_main(rank, world, port, argv):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from nats_llm_studio_amd import worker
+    raise SystemExit(worker.main(argv))
+
+
+def test_tp_worker_serves_chat_over_nats(tmp_path):
+    """torchrun-style TP=2 worker: both ranks load shards, rank 0 answers lmstudio.chat_model
+    over NATS, the follower executes every step; SIGTERM releases both."""
+    import json
+    import signal
+    import time
+    from nats_llm_studio_amd.natsio import Client, EmbeddedServer
+    spec = _TP_SPECS["llama"]
+    d = tmp_path / "models" / "synthetic" / "tp-llama-GGUF"
+    d.mkdir(parents=True)
+    write_synthetic_gguf(str(d / "tp-llama-Q4_K_M.gguf"), spec.name, "Q4_K_M", seed=2, spec=spec)
+    srv = EmbeddedServer().start()
+    argv = ["--nats-url", srv.url, "--models-dir", str(tmp_path / "models"), "--tp", "2", "--model", "tp-llama",
+            "--max-batch", "4", "--max-ctx", "256", "--device", "cpu"]
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker_main, args=(r, 2, port, argv)) for r in range(2)]
+    for p in procs:
+        p.start()
+    cli = Client().connect(srv.url)
+    try:
+        deadline = time.time() + 120
+        r = None
+        while time.time() < deadline:
+            try:
+                r = json.loads(cli.request("lmstudio.health", b"{}", 2).data)
+                break
+            except Exception:
+                assert all(p.exitcode in (None, 0) for p in procs), [p.exitcode for p in procs]
+                time.sleep(0.5)
+        assert r and r["ok"] and r["data"]["models_loaded"] == ["tp-llama"]
+        body = {"model": "tp-llama", "messages": [{"role": "user", "content": "hello there"}], "max_tokens": 5,
+                "temperature": 0}
+        r = json.loads(cli.request("lmstudio.chat_model", json.dumps(body).encode(), 120).data)
+        assert r["ok"] is True and r["data"]["http_status"] == 200, r
+        assert r["data"]["response"]["usage"]["completion_tokens"] >= 1
+        r2 = json.loads(cli.request("lmstudio.chat_model", json.dumps(body).encode(), 120).data)
+        assert r2["data"]["response"]["choices"][0]["message"]["content"] == \
+            r["data"]["response"]["choices"][0]["message"]["content"]
+    finally:
+        cli.close()
+        os.kill(procs[0].pid, signal.SIGTERM)
+        for p in procs:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+        srv.stop()
+    assert [p.exitcode for p in procs] == [0, 0]

@@ -192,3 +192,83 @@ def test_engine_backend_chat_cpu(tmp_path, tiny_models):
         svc.stop()
         svc.client.close()
         srv.stop()
+
+
+class _FakeLMStudio:
+    """Minimal LM Studio REST v0 stand-in for the `http` backend (the reference's own mode)."""
+
+    def __init__(self):
+        import http.server
+
+        outer = self
+        self.bodies = []
+
+        class H(http.server.BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def _send(self, code, body: bytes):
+                self.send_response(code)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def do_GET(self):
+                if self.path == "/api/v0/models":
+                    self._send(200, b'{"object":"list","data":[{"id":"m1","object":"model","state":"loaded"}]}')
+                else:
+                    self._send(404, b'{"error":"nope"}')
+
+            def do_POST(self):
+                n = int(self.headers.get("Content-Length", 0))
+                body = self.rfile.read(n)
+                outer.bodies.append((self.headers.get("Content-Type"), body))
+                req = json.loads(body)
+                if req.get("model") == "missing":
+                    self._send(404, b'{"error":"Model not found"}')
+                elif req.get("model") == "garbage":
+                    self._send(200, b"data: not json")
+                else:
+                    self._send(200, json.dumps({"object": "chat.completion", "model": req["model"],
+                                                "choices": [{"message": {"role": "assistant", "content": "hi"}}]}).encode())
+
+        self.srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self.url = f"http://127.0.0.1:{self.srv.server_address[1]}"
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    def close(self):
+        self.srv.shutdown()
+
+
+def test_http_backend_proxy_semantics(tmp_path):
+    """backend=http reproduces nats_llm_studio.go:136-179/228-364: raw bodies embedded, status
+    NOT checked (404 -> ok:true + http_status 404), payload forwarded verbatim as JSON, a
+    non-JSON body -> the literal marshal-failure fallback, transport failure -> http_status 0."""
+    lm = _FakeLMStudio()
+    srv = EmbeddedServer().start()
+    cfg = WorkerConfig(nats_url=srv.url, models_dir=str(tmp_path), backend="http", lmstudio_base_url=lm.url)
+    svc = Service(cfg).start()
+    cli = Client().connect(srv.url)
+    try:
+        r = req(cli, "list_models", {})
+        assert r == {"ok": True, "data": {"http_status": 200, "models": {
+            "object": "list", "data": [{"id": "m1", "object": "model", "state": "loaded"}]}}}
+        raw = b'{"model": "m1",   "messages": [{"role": "user", "content": "x"}], "extra": 1}'
+        r = req(cli, "chat_model", raw)
+        assert r["ok"] is True and r["data"]["http_status"] == 200
+        assert r["data"]["response"]["choices"][0]["message"]["content"] == "hi"
+        assert lm.bodies[-1] == ("application/json", raw)
+        r = req(cli, "chat_model", {"model": "missing"})
+        assert r == {"ok": True, "data": {"http_status": 404, "response": {"error": "Model not found"}}}
+        r = cli.request("lmstudio.chat_model", b'{"model": "garbage"}', 10).data
+        assert bytes(r) == b'{"ok":false,"error":"internal error serializing response"}'
+        lm.close()
+        svc.backend.base = "http://127.0.0.1:1"           # nothing listens: transport error
+        r = req(cli, "chat_model", {"model": "m1"})
+        assert r["ok"] is False and r["error"].startswith("error calling LM Studio:")
+        assert r["data"] == {"http_status": 0}
+    finally:
+        cli.close()
+        svc.stop()
+        svc.client.close()
+        srv.stop()

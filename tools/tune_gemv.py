@@ -41,8 +41,10 @@ def shapes(spec, base=GGMLType.Q4_K, more=GGMLType.Q6_K):
     return out
 
 
-def configs(K):
+def configs(K, M=1):
     nb = K // 256
+    if M > 64:
+        return [(1, 8, 1, 1), (1, 4, 1, 1), (1, 4, 2, 1), (1, 8, 2, 1)]
     c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
     for waves in (4, 8):
         for rt in (1, 2):
@@ -106,12 +108,13 @@ def main():
             segs.append(ops.Seg(w, col))
             col += rows
         ncol = col // 2 if epi == "swiglu" else col
-        x = torch.randn(64, K, device=dev).to(torch.bfloat16)
-        y = torch.zeros(64, ncol, dtype=torch.bfloat16 if epi == "swiglu" else torch.float32, device=dev)
-        keys = torch.zeros(64, dtype=torch.int64, device=dev)
+        mmax = max(64, max(Ms))
+        x = torch.randn(mmax, K, device=dev).to(torch.bfloat16)
+        y = torch.zeros(mmax, ncol, dtype=torch.bfloat16 if epi == "swiglu" else torch.float32, device=dev)
+        keys = torch.zeros(mmax, dtype=torch.int64, device=dev)
         for M in Ms:
             res = []
-            for cfg in configs(K):
+            for cfg in configs(K, M):
                 us = time_cfg(segs, x, y, M, epi, keys, cfg)
                 if us is not None:
                     res.append((us, cfg))
@@ -119,7 +122,9 @@ def main():
             best_us, best = res[0]
             k = tuning.key(segs, M)
             table[k] = list(best)
-            line = (f"{name:8s} M={M:3d} best={best} {best_us:8.2f}us {nbytes / best_us / 1e3:7.1f} GB/s | "
+            tf = 2.0 * M * col * K / best_us / 1e6
+            line = (f"{name:8s} M={M:3d} best={best} {best_us:8.2f}us {nbytes / best_us / 1e3:7.1f} GB/s "
+                    f"{tf:7.1f} TFLOP/s | "
                     + " ".join(f"{c}:{u:.1f}" for u, c in res[:4]))
             print(line, flush=True)
             log.write(line + "\n")
