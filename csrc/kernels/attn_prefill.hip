@@ -1,0 +1,197 @@
+// Causal flash attention for prefill over the paged KV cache, on MFMA (gfx950).
+// SURVEY.md §2F attn_prefill.
+//
+// Work item = one "query block": up to 16 consecutive prompt tokens of ONE sequence
+// (t0, ntok, seq, pos0) -- the engine cuts each sequence's prefill chunk into such blocks.
+// Workgroup = (query block, kv head, quad of query heads): its 4 waves are 4 query heads of
+// the same GQA group, so every K/V tile is staged in LDS once and used by 4 heads.
+//
+// Per 64-key tile and wave (16 tokens x 1 head):
+//   S^T = K Q^T    v_mfma_f32_16x16x32_bf16, A = K rows from LDS, B = Q^T from registers.
+//                  The transposed product puts one TOKEN per lane column, so each lane holds
+//                  4 consecutive keys of its token per 16-key n-tile: the row max / sum of the
+//                  online softmax need only 2 cross-lane shuffles.
+//   O += P V       A = P straight from the S^T accumulators (no LDS round trip): lane (g, r)
+//                  holds token r's keys {4g..4g+3, 16+4g..16+4g+3} of a 32-key group, and the
+//                  MFMA's K order is free, so B = V rows in that same key order, read from a
+//                  TRANSPOSED V tile in LDS (Vt[d][key], two 8-byte reads per fragment).
+// Softmax in base 2 with the scale folded in; rows past ntok are computed but never stored.
+#include "common.h"
+
+namespace {
+
+constexpr float LOG2E_P = 1.4426950408889634f;
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restrict__ q, long ldq,
+                                                           const __bf16* __restrict__ kc,
+                                                           const __bf16* __restrict__ vc,
+                                                           const int* __restrict__ block_tables, int bt_stride,
+                                                           const int* __restrict__ qblocks, int Hkv, int G, int bs,
+                                                           float scale, __bf16* __restrict__ out, long ldo) {
+  constexpr int KT = 64;           // keys per tile
+  constexpr int KSTR = D + 8;      // K tile row stride (elements): conflict-free ds_read_b128
+  constexpr int VSTR = KT + 8;     // Vt row stride (keys): conflict-free ds_read_b64
+  constexpr int NKK = D / 32;      // k-steps of S^T over the head dim
+  constexpr int NDT = D / 16;      // n-tiles of O over the head dim
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[KT * KSTR];
+  __shared__ __attribute__((aligned(16))) __bf16 Vt[D * VSTR];
+
+  const int qb = blockIdx.x, hk = blockIdx.y, hq = blockIdx.z;
+  const int t0 = qblocks[qb * 4], ntok = qblocks[qb * 4 + 1], seq = qblocks[qb * 4 + 2],
+            pos0 = qblocks[qb * 4 + 3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int head = hk * G + hq * 4 + wave;
+  const int* bt = block_tables + (size_t)seq * bt_stride;
+  const float sl2 = scale * LOG2E_P;
+
+  bf16x8 qf[NKK];
+  {
+    const __bf16* qrow = q + (size_t)(t0 + min(r, ntok - 1)) * ldq + (size_t)head * D;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + kk * 32 + 8 * g);
+  }
+  const int qpos = pos0 + r;                  // this lane's token (column of S^T)
+  const bool qvalid = r < ntok;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkeys = pos0 + ntok;
+  for (int k0 = 0; k0 < nkeys; k0 += KT) {
+    __syncthreads();                           // previous tile fully consumed
+    // ---- stage K [64][D] and V^T [D][64] of keys k0..k0+63 (zero past the end)
+    for (int c = threadIdx.x; c < KT * (D / 8); c += 256) {
+      const int key = c / (D / 8), ch = c % (D / 8);
+      const int p = k0 + key;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (p < nkeys) {
+        const long slot = (long)bt[p / bs] * bs + p % bs;
+        v = ld16(kc + ((size_t)slot * Hkv + hk) * D + ch * 8);
+      }
+      *reinterpret_cast<u32x4*>(Ks + key * KSTR + ch * 8) = v;
+    }
+    for (int c = threadIdx.x; c < (KT / 2) * (D / 8); c += 256) {
+      const int kp = c / (D / 8), ch = c % (D / 8);
+      const int p = k0 + 2 * kp;
+      u32x4 va = u32x4{0u, 0u, 0u, 0u}, vb = u32x4{0u, 0u, 0u, 0u};
+      if (p < nkeys) {
+        const long slot = (long)bt[p / bs] * bs + p % bs;
+        va = ld16(vc + ((size_t)slot * Hkv + hk) * D + ch * 8);
+      }
+      if (p + 1 < nkeys) {
+        const long slot = (long)bt[(p + 1) / bs] * bs + (p + 1) % bs;
+        vb = ld16(vc + ((size_t)slot * Hkv + hk) * D + ch * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // dims ch*8+2j and ch*8+2j+1: pair the two keys per dim into one 4-byte store
+        const uint32_t lo = (va[j] & 0xFFFFu) | (vb[j] << 16);
+        const uint32_t hi = (va[j] >> 16) | (vb[j] & 0xFFFF0000u);
+        *reinterpret_cast<uint32_t*>(Vt + (ch * 8 + 2 * j) * VSTR + 2 * kp) = lo;
+        *reinterpret_cast<uint32_t*>(Vt + (ch * 8 + 2 * j + 1) * VSTR + 2 * kp) = hi;
+      }
+    }
+    __syncthreads();
+
+    // ---- S^T = K Q^T : s[nt][i] = S[token r][key k0 + nt*16 + 4g + i]
+    f32x4 s[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (nt * 16 + r) * KSTR + kk * 32 + 8 * g);
+        s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[kk], s[nt], 0, 0, 0);
+      }
+    }
+    // ---- causal mask + online softmax (base 2)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = k0 + nt * 16 + 4 * g + i;
+        const float v = (qvalid && key <= qpos) ? s[nt][i] * sl2 : -INFINITY;
+        s[nt][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = (mn == -INFINITY) ? 0.f : exp2f(s[nt][i] - mn);
+        s[nt][i] = p;
+        ps += p;
+      }
+    l = l * alpha + ps;
+    m = mn;
+    // O rows are tokens 4g+i: their alpha lives in lane column 4g+i
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float ai = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt][i] *= ai;
+    }
+    // ---- O += P V over two 32-key groups
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      bf16x8 pa;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pa[i] = (__bf16)s[2 * kg][i];
+        pa[4 + i] = (__bf16)s[2 * kg + 1][i];
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const __bf16* vrow = Vt + (dt * 16 + r) * VSTR + kg * 32 + 4 * g;
+        const uint2 lo = *reinterpret_cast<const uint2*>(vrow);
+        const uint2 hi = *reinterpret_cast<const uint2*>(vrow + 16);
+        u32x4 bw = u32x4{lo.x, lo.y, hi.x, hi.y};
+        const bf16x8 b = __builtin_bit_cast(bf16x8, bw);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, b, o[dt], 0, 0, 0);
+      }
+    }
+  }
+  // ---- normalise and store: lane holds O[token 4g+i][dt*16 + r]
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tok = 4 * g + i;
+    const float li = __shfl(l, tok, 64);
+    if (tok < ntok) {
+      const float inv = li > 0.f ? 1.f / li : 0.f;
+      __bf16* orow = out + (size_t)(t0 + tok) * ldo + (size_t)head * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) orow[dt * 16 + r] = (__bf16)(o[dt][i] * inv);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int nls_attn_prefill(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                                int bt_stride, const int* qblocks, int nqb, int Hq, int Hkv, int D, int block_size,
+                                float scale, void* out, long ldo, void* stream) {
+  if (Hq % Hkv || (Hq / Hkv) % 4 || (D != 64 && D != 128) || nqb < 1) return -1;
+  const int G = Hq / Hkv;
+  dim3 grid(nqb, Hkv, G / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 128)
+    hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const __bf16*)kc,
+                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (__bf16*)out,
+                       ldo);
+  else
+    hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const __bf16*)kc,
+                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (__bf16*)out,
+                       ldo);
+  return (int)hipGetLastError();
+}

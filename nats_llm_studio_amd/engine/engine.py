@@ -107,7 +107,8 @@ class _Seq:
 class Engine:
     def __init__(self, model: LlamaModel, tokenizer=None, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, max_prefill_tokens: int = 2048, use_graphs: bool = True,
-                 ctx: Optional[int] = None, kv_mem_fraction: float = 0.5, eos_ids: Seq[int] = ()):
+                 ctx: Optional[int] = None, kv_mem_fraction: float = 0.5, eos_ids: Seq[int] = (),
+                 prefill_attn: bool = True):
         self.model = model
         self.tok = tokenizer
         self.cfg = model.cfg
@@ -130,6 +131,7 @@ class Engine:
         self.kc, self.vc = model.kv_cache(num_blocks, block_size)
         self.alloc = BlockAllocator(num_blocks)
         self.max_prefill = max_prefill_tokens
+        self.prefill_attn = prefill_attn      # MFMA flash-prefill attention (else per-token decode kernel)
         self.db = model.step_buffers(self.max_batch, self.max_batch, self.max_blocks)
         self.pb = model.step_buffers(max_prefill_tokens, self.max_batch, self.max_blocks)
         pin = self.dev.type == "cuda"
@@ -316,8 +318,12 @@ class Engine:
         b = self.pb
         b.meta.copy_(self.h_meta_p, non_blocking=self.dev.type == "cuda" and self.rank == 0)
         lr = torch.tensor(rows, dtype=torch.int32, device=self.dev)
+        pad = b.pad
+        h = self.h_meta_p.numpy()
+        qb = ops.prefill_blocks(h[3 * pad:4 * pad], h[pad:2 * pad], T) if self.prefill_attn else None
+        qbt = torch.from_numpy(qb).to(self.dev) if qb is not None and len(qb) else None
         n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
-                               logit_rows=lr, n_logits=len(rows))
+                               logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb))
         self._gather(b, n, need_logits)
 
     def _gather(self, b, n: int, need_logits: bool):

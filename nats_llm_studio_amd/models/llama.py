@@ -260,8 +260,10 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ forward
     def forward(self, b: StepBuffers, kc: torch.Tensor, vc: torch.Tensor, T: int, block_size: int,
-                n_split: int = 1, logit_rows: Optional[torch.Tensor] = None, n_logits: Optional[int] = None):
-        """Runs T tokens through the model; leaves greedy ids in b.next_ids[:n] and logits in b.logits[:n]."""
+                n_split: int = 1, logit_rows: Optional[torch.Tensor] = None, n_logits: Optional[int] = None,
+                qblocks: Optional[torch.Tensor] = None, nqb: int = 0):
+        """Runs T tokens through the model; leaves greedy ids in b.next_ids[:n] and logits in b.logits[:n].
+        With `qblocks` (prompt chunks, ops.prefill_blocks) attention runs the MFMA flash-prefill kernel."""
         cfg = self.cfg
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         x = b.x
@@ -273,8 +275,12 @@ class LlamaModel:
             ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
             ops.qgemv(lw.qkv, b.h, b.qkv, T)
             ops.rope_kv(b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D, cfg.rope_neox)
-            ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
-                          block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws)
+            if qblocks is not None and nqb > 0 and ops.attention_prefill_ok(Hq, Hkv, D):
+                ops.attention_prefill(b.q, kc[L], vc[L], b.block_tables, qblocks, nqb, b.tok_seq, b.ctx_len, b.ao,
+                                      T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)
+            else:
+                ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
+                              block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws)
             self._row_parallel(lw.wo, b.ao, x, T, cfg.residual_scale)
             ops.rmsnorm(x, lw.ffn_norm, b.h, T, cfg.eps)
             if cfg.n_expert:

@@ -368,6 +368,40 @@ def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables:
     return out
 
 
+def prefill_blocks(tok_seq, pos, T: int):
+    """Query blocks for attention_prefill: (t0, ntok<=16, seq, pos0) over runs of consecutive
+    tokens of one sequence (numpy int arrays in, int32 [nqb, 4] out)."""
+    ts = np.asarray(tok_seq[:T])
+    ps = np.asarray(pos[:T])
+    if T == 0:
+        return np.zeros((0, 4), np.int32)
+    cut = np.flatnonzero((ts[1:] != ts[:-1]) | (ps[1:] != ps[:-1] + 1)) + 1
+    starts = np.concatenate([[0], cut])
+    ends = np.concatenate([cut, [T]])
+    out = []
+    for a, b in zip(starts, ends):
+        for t in range(a, b, 16):
+            out.append((t, min(16, b - t), ts[a], ps[t]))
+    return np.asarray(out, dtype=np.int32).reshape(-1, 4)
+
+
+def attention_prefill_ok(Hq: int, Hkv: int, D: int) -> bool:
+    return Hq % Hkv == 0 and (Hq // Hkv) % 4 == 0 and D in (64, 128)
+
+
+def attention_prefill(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables: torch.Tensor,
+                      qblocks: torch.Tensor, nqb: int, tok_seq: torch.Tensor, ctx_len: torch.Tensor,
+                      out: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, block_size: int, scale: float):
+    """Causal MFMA flash attention over the paged cache for prompt chunks (query blocks of 16)."""
+    if q.is_cuda:
+        _lib.check(_lib.lib().nls_attn_prefill(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
+                                               block_tables.data_ptr(), block_tables.stride(0), qblocks.data_ptr(),
+                                               nqb, Hq, Hkv, D, block_size, float(scale), out.data_ptr(),
+                                               out.stride(0), _stream_ptr(q)), "nls_attn_prefill")
+        return out
+    return attention(q, kc, vc, block_tables, tok_seq, ctx_len, out, T, Hq, Hkv, D, block_size, scale)
+
+
 def argmax(logits: torch.Tensor, M: int, out: torch.Tensor):
     V = logits.shape[1]
     if logits.is_cuda:

@@ -35,6 +35,8 @@ _SIGS = {
     "nls_attn_decode": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                         c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p,
                         c_void_p],
+    "nls_attn_prefill": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                         c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_ar_alloc": [c_long, c_int, c_void_p, c_void_p],
     "nls_ar_open": [c_void_p, c_void_p],
     "nls_ar_close": [c_void_p],

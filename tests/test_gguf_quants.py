@@ -94,3 +94,11 @@ def test_tiled_layout_is_a_permutation(t):
     rp = 48
     assert tl.size == rp // 16 * (K // 256) * ops.TILE_BYTES[t]
     assert sorted(tl.tolist()) == sorted(raw.tolist() + [0] * (tl.size - raw.size))
+
+
+def test_prefill_blocks():
+    from nats_llm_studio_amd.ops import prefill_blocks
+    tseq = np.array([0] * 20 + [1] * 3 + [2] * 16)
+    pos = np.concatenate([np.arange(20), np.arange(50, 53), np.arange(16)])
+    qb = prefill_blocks(tseq, pos, len(tseq))
+    assert qb.tolist() == [[0, 16, 0, 0], [16, 4, 0, 16], [20, 3, 1, 50], [23, 16, 2, 0]]

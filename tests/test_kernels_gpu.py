@@ -275,3 +275,35 @@ def test_qgemm_large_m_swiglu(gpu):
     ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=1, waves=8, rt=1, ks=1)
     xf = x[:M].float().cpu()
     _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
+
+
+@pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8)])
+def test_attention_prefill_paged(gpu, D, G):
+    """MFMA flash-prefill vs the fp32 reference: 3 sequences, chunks that start mid-context
+    (chunked prefill), partial 16-token blocks, scattered KV pages."""
+    torch.manual_seed(0)
+    Hkv, bs = 2, 16
+    Hq = Hkv * G
+    # (seq, pos0, n): seq 0 fresh 37 tokens, seq 1 continues at 100 for 20, seq 2 at 5 for 16
+    chunks = [(0, 0, 37), (1, 100, 20), (2, 5, 16)]
+    nblk = 16
+    perm = torch.randperm(3 * nblk).view(3, nblk).int()
+    slots = 3 * nblk * bs
+    kc = (torch.randn(slots, Hkv, D) * 0.5).to(torch.bfloat16)
+    vc = torch.randn(slots, Hkv, D).to(torch.bfloat16)
+    T = sum(n for _, _, n in chunks)
+    pos, tseq = [], []
+    for s, p0, n in chunks:
+        pos += list(range(p0, p0 + n))
+        tseq += [s] * n
+    pos = np.array(pos, np.int32)
+    tseq = np.array(tseq, np.int32)
+    q = (torch.randn(T, Hq * D)).to(torch.bfloat16)
+    ctx = torch.from_numpy(pos + 1)
+    ref = torch.zeros(T, Hq * D, dtype=torch.bfloat16)
+    ops.attention(q, kc, vc, perm, torch.from_numpy(tseq), ctx, ref, T, Hq, Hkv, D, bs, D ** -0.5)
+    qb = ops.prefill_blocks(tseq, pos, T)
+    out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=gpu)
+    ops.attention_prefill(q.to(gpu), kc.to(gpu), vc.to(gpu), perm.to(gpu), torch.from_numpy(qb).to(gpu), len(qb),
+                          None, None, out, T, Hq, Hkv, D, bs, D ** -0.5)
+    _close(out.cpu(), ref, 2e-2)
