@@ -27,7 +27,7 @@ import torch
 
 from .. import ops
 from ..models.llama import LlamaModel
-from .sampling import SamplingParams, sample_rows
+from .sampling import SamplingParams, sample_rows, sample_rows_gpu
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
 
@@ -386,7 +386,8 @@ class Engine:
         sampled = [i for i, s in enumerate(seqs) if not s.req.params.greedy]
         if sampled:
             lg = self.full_logits if self.full_logits is not None else b.logits
-            toks = sample_rows(lg[[rows[i] for i in sampled]], [seqs[i].req.params for i in sampled],
+            fn = sample_rows_gpu if lg.is_cuda else sample_rows
+            toks = fn(lg[[rows[i] for i in sampled]], [seqs[i].req.params for i in sampled],
                                [seqs[i].tokens for i in sampled], [seqs[i].gen for i in sampled])
             for i, t in zip(sampled, toks):
                 out[i] = t

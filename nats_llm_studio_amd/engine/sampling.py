@@ -98,3 +98,39 @@ def sample_rows(logits: torch.Tensor, params: Sequence[SamplingParams], historie
             tok = int(torch.multinomial(probs, 1, generator=g))
         out.append(tok)
     return out
+
+
+HIST = 64      # penalty window (last tokens)
+
+
+def uniform(gen: Optional[torch.Generator]) -> float:
+    if gen is not None:
+        return float(torch.rand(1, generator=gen).item())
+    import random
+    return random.random()
+
+
+def sample_rows_gpu(logits: torch.Tensor, params: Sequence[SamplingParams], histories: Sequence[Sequence[int]],
+                    generators: Sequence[Optional[torch.Generator]]) -> List[int]:
+    """All sampled rows of a step in ONE kernel launch (csrc/kernels/sample.hip).
+    `logits` [n, V] fp32 on the GPU is used as scratch (penalties are applied in place)."""
+    import ctypes
+    import numpy as np
+    from ..ops import _lib
+    n, V = logits.shape
+    lg = logits if logits.is_contiguous() and logits.dtype == torch.float32 else logits.float().contiguous()
+    P = (_lib.SampleParams * n)()
+    hist = np.full((n, HIST), -1, dtype=np.int32)
+    for i, p in enumerate(params):
+        h = list(histories[i])[-HIST:]
+        hist[i, :len(h)] = h
+        P[i] = _lib.SampleParams(p.temperature, p.top_p, p.min_p, p.repeat_penalty, p.presence_penalty,
+                                 p.frequency_penalty, uniform(generators[i]), int(p.top_k or 0), len(h), 0)
+    dev = lg.device
+    pbytes = torch.frombuffer(bytearray(bytes(P)), dtype=torch.uint8).to(dev)
+    hd = torch.from_numpy(hist).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.lib().nls_sample(lg.data_ptr(), lg.stride(0), n, V, pbytes.data_ptr(), hd.data_ptr(), HIST,
+                                     out.data_ptr(), stream), "nls_sample")
+    return out.cpu().tolist()

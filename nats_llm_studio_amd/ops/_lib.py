@@ -14,6 +14,12 @@ _lib = None
 c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
 
 
+class SampleParams(ctypes.Structure):
+    _fields_ = [("temperature", c_float), ("top_p", c_float), ("min_p", c_float), ("repeat_penalty", c_float),
+                ("presence_penalty", c_float), ("frequency_penalty", c_float), ("u", c_float),
+                ("top_k", c_int), ("n_hist", c_int), ("pad", c_int)]
+
+
 class NlsSeg(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("xmap", c_void_p), ("ymap", c_void_p), ("mcount", c_void_p),
                 ("type", c_int), ("rows", c_int), ("K", c_int), ("ycol", c_int)]
@@ -37,6 +43,8 @@ _SIGS = {
                         c_void_p],
     "nls_attn_prefill": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_void_p, c_long, c_void_p],
+    "nls_sample": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "nls_sample_params_size": [],
     "nls_ar_alloc": [c_long, c_int, c_void_p, c_void_p],
     "nls_ar_open": [c_void_p, c_void_p],
     "nls_ar_close": [c_void_p],

