@@ -73,9 +73,29 @@ def build_natscore(force: bool = False) -> str:
     return out
 
 
+def _natscore_lib_srcs():
+    return [s for s in sorted(glob.glob(os.path.join(CSRC, "natscore", "*.cpp"))) if not s.endswith("bindings.cpp")]
+
+
+def build_tool(name: str = "nls-nats", src: str = "nls_nats.cpp", extra=(), out_dir: str = None,
+               force: bool = False, cxx: str = "g++") -> str:
+    """Native executables over natscore (no Python): the `nls-nats` CLI (server / req / obj ...)."""
+    out = os.path.join(out_dir or os.path.join(ROOT, "bin"), name)
+    srcs = [os.path.join(CSRC, "tools", src)] + _natscore_lib_srcs()
+    deps = srcs + glob.glob(os.path.join(CSRC, "natscore", "*.h"))
+    if force or _stale(out, deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        tmp = out + ".tmp"
+        _run([cxx, "-O2", "-std=c++17", "-pthread", f"-I{os.path.join(CSRC, 'natscore')}", *extra, *srcs,
+              "-o", tmp])
+        os.replace(tmp, out)
+    return out
+
+
 def build_all(force: bool = False):
     k = build_kernels(force)
     n = build_natscore(force)
+    build_tool(force=force)
     return k, n
 
 

@@ -117,7 +117,10 @@ def sample_rows_gpu(logits: torch.Tensor, params: Sequence[SamplingParams], hist
     import ctypes
     import numpy as np
     from ..ops import _lib
-    n, V = logits.shape
+    n, V = len(params), logits.shape[1]
+    if logits.shape[0] < n:
+        raise ValueError(f"{logits.shape[0]} logit rows for {n} sampling requests")
+    logits = logits[:n]
     lg = logits if logits.is_contiguous() and logits.dtype == torch.float32 else logits.float().contiguous()
     P = (_lib.SampleParams * n)()
     hist = np.full((n, HIST), -1, dtype=np.int32)

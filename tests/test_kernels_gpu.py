@@ -324,7 +324,7 @@ def test_sample_kernel(gpu):
     base[0, 789] = 8.0
     n = 2000
     lg = base.repeat(n, 1).to(gpu)
-    greedy = sample_rows_gpu(lg.clone(), [SamplingParams()] * 4, [[]] * 4, [None] * 4)
+    greedy = sample_rows_gpu(lg[:4].clone(), [SamplingParams()] * 4, [[]] * 4, [None] * 4)
     assert greedy == [123] * 4
     k1 = sample_rows_gpu(lg[:4].clone(), [SamplingParams(temperature=1.0, top_k=1)] * 4, [[]] * 4, [None] * 4)
     assert k1 == [123] * 4
