@@ -57,6 +57,10 @@ class GenResult:
     time_to_first_token: float
     generation_time: float
     error: Optional[str] = None
+    t_submit: float = 0.0                  # monotonic marks for request tracing
+    t_admit: float = 0.0
+    t_first: float = 0.0
+    t_done: float = 0.0
 
     @property
     def tokens_per_second(self) -> float:
@@ -82,8 +86,8 @@ class BlockAllocator:
 
 
 class _Seq:
-    __slots__ = ("req", "fut", "tokens", "n_prompt", "n_prefilled", "blocks", "t_submit", "t_first", "t_done",
-                 "gen", "max_new", "done", "text_cache")
+    __slots__ = ("req", "fut", "tokens", "n_prompt", "n_prefilled", "blocks", "t_submit", "t_admit", "t_first",
+                 "t_done", "gen", "max_new", "done", "text_cache")
 
     def __init__(self, req: GenRequest, fut: Future):
         self.req = req
@@ -93,6 +97,7 @@ class _Seq:
         self.n_prefilled = 0
         self.blocks: List[int] = []
         self.t_submit = time.monotonic()
+        self.t_admit = None
         self.t_first = None
         self.t_done = None
         self.gen = None
@@ -268,6 +273,7 @@ class Engine:
                 if blocks is None:
                     break
                 s.blocks = blocks
+                s.t_admit = time.monotonic()
                 self.waiting.popleft()
                 self.running.append(s)
 
@@ -515,7 +521,8 @@ class Engine:
         gen_ids = gen
         t_first = s.t_first or s.t_done
         res = GenResult(s.req.request_id, gen_ids, text, s.n_prompt, len(gen), finish, reason,
-                        t_first - s.t_submit, max(s.t_done - t_first, 1e-9), error)
+                        t_first - s.t_submit, max(s.t_done - t_first, 1e-9), error,
+                        s.t_submit, s.t_admit or s.t_done, t_first, s.t_done)
         if not s.fut.done():
             s.fut.set_result(res)
 

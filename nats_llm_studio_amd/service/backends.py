@@ -19,7 +19,7 @@ from typing import Callable, Dict, Optional
 from .. import __version__
 from .registry import ModelEntry
 
-Done = Callable[[int, dict], None]      # (http_status, body)
+Done = Callable[..., None]      # (http_status, body[, trace marks])
 
 
 def _error_body(msg: str) -> dict:
@@ -225,7 +225,9 @@ class EngineBackend:
                 return
             done(200, chat_response(model_id, entry, r.text, r.prompt_tokens, r.completion_tokens,
                                     "length" if r.finish_reason == "length" else "stop", r.stop_reason,
-                                    r.time_to_first_token, r.generation_time, ctx))
+                                    r.time_to_first_token, r.generation_time, ctx),
+                 {"queued": r.t_submit, "admitted": r.t_admit, "first_token": r.t_first, "done": r.t_done,
+                  "request_id": r.request_id})
         fut.add_done_callback(finished)
 
     def stats(self):

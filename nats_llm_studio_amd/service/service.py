@@ -32,6 +32,7 @@ from .registry import Registry
 from .store import ModelStore, PullError
 from ..natsio import Client
 from ..utils.metrics import LatencyHistogram
+from ..utils.tracing import Tracer
 
 
 class Service:
@@ -52,6 +53,7 @@ class Service:
         self.t_start = time.time()
         self.counters = defaultdict(int)
         self.latency = defaultdict(LatencyHistogram)
+        self.tracer = Tracer()
         self._lock = threading.Lock()
 
     # ------------------------------------------------------------------ lifecycle
@@ -200,6 +202,7 @@ class Service:
         self.respond(msg, envelope.ok({"model_id": mid, "deleted_dir": d}))
 
     def on_chat_model(self, msg):
+        t_recv = time.monotonic()
         if len(msg.data) == 0:
             self.respond(msg, envelope.error("payload vazio em ChatModel"))
             return
@@ -237,11 +240,22 @@ class Service:
                 except Exception:
                     pass
 
-        def done(status: int, body: dict):
+        t_valid = time.monotonic()
+
+        def done(status: int, body: dict, marks: dict = None):
             if status <= 0:
                 self.respond(msg, envelope.error(body.get("error", "chat failed"), {"http_status": 0}))
             else:
                 self.respond(msg, envelope.ok({"http_status": status, "response": body}))
+            mk = {"recv": t_recv, "validated": t_valid, "responded": time.monotonic()}
+            rid = ""
+            for k, v in (marks or {}).items():
+                if k == "request_id":
+                    rid = v
+                elif v:
+                    mk[k] = v
+            self.tracer.record("chat_model", rid or body.get("id", ""), mk,
+                               {"model": model, "http_status": status})
         try:
             self.backend.chat(entry.id if entry else model, entry, req, done, deadline, stream_cb)
         except Exception as e:
@@ -274,6 +288,7 @@ class Service:
             "uptime_s": round(time.time() - self.t_start, 3),
             "requests": dict(self.counters),
             "latency_ms": {k: v.summary_ms() for k, v in self.latency.items()},
+            "trace": self.tracer.summary(),
             "backend": self.backend.stats(),
             "nats": self.client.stats(),
             "models_dir": self.cfg.models_dir,

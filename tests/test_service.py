@@ -183,6 +183,9 @@ def test_engine_backend_chat_cpu(tmp_path, tiny_models):
         assert len(texts) == 1                         # greedy: identical answers for identical prompts
         lst = req(cli, "list_models", {})["data"]["models"]["data"]
         assert lst[0]["state"] == "loaded"
+        tr = req(cli, "metrics", {})["data"]["trace"]      # recv->validate->queue->prefill->decode->respond
+        assert {"validate", "queue", "prefill", "decode", "respond", "total"} <= set(tr["phases_ms"])
+        assert tr["phases_ms"]["total"]["count"] == 4 and tr["recent"][-1]["request_id"].startswith("req-")
         r = req(cli, "chat_model", {"model": "missing-model", "messages": [{"role": "user", "content": "x"}]})
         assert r["ok"] and r["data"]["http_status"] == 404
         r = req(cli, "delete_model", {"model_id": "tiny-llama"})       # unloads then deletes
