@@ -34,6 +34,7 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
 # tensor-parallel control messages (rank 0 -> followers), see Engine.follow()
 _OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE = 0, 1, 2, 3
 _HDR = 8
+_NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
 
 
 @dataclass
@@ -87,7 +88,7 @@ class BlockAllocator:
 
 class _Seq:
     __slots__ = ("req", "fut", "tokens", "n_prompt", "n_prefilled", "blocks", "t_submit", "t_admit", "t_first",
-                 "t_done", "gen", "max_new", "done", "text_cache")
+                 "t_done", "gen", "max_new", "done", "text_cache", "row", "n_fed")
 
     def __init__(self, req: GenRequest, fut: Future):
         self.req = req
@@ -103,6 +104,8 @@ class _Seq:
         self.gen = None
         self.max_new = req.params.max_tokens
         self.done = False
+        self.row = -1          # decode-batch row (stable for the sequence's life)
+        self.n_fed = 0         # positions whose KV is written or being written
 
     @property
     def generated(self) -> List[int]:
@@ -113,7 +116,7 @@ class Engine:
     def __init__(self, model: LlamaModel, tokenizer=None, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, max_prefill_tokens: int = 2048, use_graphs: bool = True,
                  ctx: Optional[int] = None, kv_mem_fraction: float = 0.5, eos_ids: Seq[int] = (),
-                 prefill_attn: bool = True):
+                 prefill_attn: bool = True, async_decode: bool = True):
         self.model = model
         self.tok = tokenizer
         self.cfg = model.cfg
@@ -140,9 +143,18 @@ class Engine:
         self.db = model.step_buffers(self.max_batch, self.max_batch, self.max_blocks)
         self.pb = model.step_buffers(max_prefill_tokens, self.max_batch, self.max_blocks)
         pin = self.dev.type == "cuda"
-        self.h_meta_d = torch.zeros(self.db.meta.numel(), dtype=torch.int32, pin_memory=pin)
+        # decode metadata / next-token host buffers are double-buffered (async decode: step N+1 is
+        # prepared and launched while step N's copies may still be in flight)
+        self.h_meta_d2 = [torch.zeros(self.db.meta.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.h_meta_d = self.h_meta_d2[0]
         self.h_meta_p = torch.zeros(self.pb.meta.numel(), dtype=torch.int32, pin_memory=pin)
         self.h_next = torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin)
+        self.h_next2 = [torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._ev = [torch.cuda.Event() for _ in range(2)] if pin else [None, None]
+        self._kbuf = 1
+        self._inflight = None
+        self.rows: List[Optional[_Seq]] = [None] * self.max_batch
+        self.async_decode = async_decode
         self.use_graphs = use_graphs and self.dev.type == "cuda"
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.eos = set(int(e) for e in eos_ids)
@@ -205,6 +217,10 @@ class Engine:
         if self.thread is not None:
             self.thread.join()
             self.thread = None
+        try:
+            self._drain()
+        except Exception:
+            pass
         self.stop_followers()
         for s in list(self.running) + list(self.waiting):
             self._finish(s, "cancelled", "engineShutdown")
@@ -242,10 +258,13 @@ class Engine:
         self._expire()
         self._admit()
         if any(s.n_prefilled < s.n_prompt for s in self.running):
+            self._drain()
             self._prefill()
         dec = [s for s in self.running if s.n_prefilled >= s.n_prompt and not s.done]
         if dec:
             self._decode(dec)
+        else:
+            self._drain()
         self.running = [s for s in self.running if not s.done]
         self.counters["steps"] += 1
 
@@ -284,7 +303,8 @@ class Engine:
         b, pad = self.pb, self.pb.pad
         h = self.h_meta_p.numpy()
         ids, pos, slot, tseq, ctxl = (h[i * pad:(i + 1) * pad] for i in range(5))
-        bt = h[5 * pad:].reshape(self.max_batch, self.max_blocks)
+        h[5 * pad:6 * pad] = 0                              # use_prev: prefill feeds host ids
+        bt = h[_NSEG * pad:].reshape(self.max_batch, self.max_blocks)
         budget = self.max_prefill
         T = 0
         rows, finishing = [], []
@@ -353,7 +373,7 @@ class Engine:
             hdr[_HDR:_HDR + len(rows)] = torch.tensor(rows, dtype=torch.int32)
         self.tp.bcast_ctrl(hdr)
         if op in (_OP_PREFILL, _OP_DECODE):
-            self.tp.bcast_ctrl(hmeta[:5 * pad + nseq * nb].clone() if nseq else hmeta[:5 * pad].clone())
+            self.tp.bcast_ctrl(hmeta[:_NSEG * pad + nseq * nb].clone())
 
     def stop_followers(self):
         if self.tp is not None and self.rank == 0 and not getattr(self, "_followers_stopped", False):
@@ -373,7 +393,7 @@ class Engine:
                 self._capture(T, LlamaModel.attn_splits(T, self.model.Hkv))
                 continue
             hm = self.h_meta_p if op == _OP_PREFILL else self.h_meta_d
-            buf = torch.zeros(5 * pad + nseq * nb, dtype=torch.int32)
+            buf = torch.zeros(_NSEG * pad + nseq * nb, dtype=torch.int32)
             self.tp.bcast_ctrl(buf)
             hm[:buf.numel()] = buf
             if op == _OP_PREFILL:
@@ -381,7 +401,8 @@ class Engine:
             else:
                 self.db.meta.copy_(hm)
                 self._run_decode(T)
-                self._gather(self.db, T, bool(need))
+                if need:
+                    self._gather(self.db, T, True)
 
     def _pick(self, seqs: List[_Seq], b, rows: List[int]) -> List[int]:
         greedy = b.next_ids[:len(rows)].cpu().tolist() if self.dev.type != "cuda" else None
@@ -405,43 +426,167 @@ class Engine:
                 return k
         return self.max_batch
 
-    def _decode(self, seqs: List[_Seq]):
-        b, pad = self.db, self.db.pad
-        B = len(seqs)
-        Bp = self._bucket(B)
-        h = self.h_meta_d.numpy()
-        ids, pos, slot, tseq, ctxl = (h[i * pad:(i + 1) * pad] for i in range(5))
-        bt = h[5 * pad:].reshape(self.max_batch, self.max_blocks)
-        for i, s in enumerate(seqs):
-            p = len(s.tokens) - 1
-            ids[i] = s.tokens[-1]
-            pos[i] = p
-            slot[i] = self._slot(s, p)
-            tseq[i] = i
-            ctxl[i] = p + 1
-            bt[i, :len(s.blocks)] = s.blocks
-        ids[B:Bp] = 0
-        pos[B:Bp] = 0
-        slot[B:Bp] = -1
-        tseq[B:Bp] = 0
-        ctxl[B:Bp] = 0
-        need = any(not s.req.params.greedy for s in seqs)
-        self._ctrl(_OP_DECODE, Bp, 0, need, [], B, self.h_meta_d, pad)
+    # ------------------------------------------------------------------ decode
+    # Rows: a decoding sequence keeps one row of the decode batch (and its block-table row) for
+    # its whole life, so consecutive steps can chain on the device: with `use_prev` set, a row's
+    # input token is the previous step's next_ids entry (written by the previous graph replay),
+    # and the host can launch step N+1 before it has read step N's tokens (async decode). The
+    # host then digests step N (stop checks, callbacks) while the GPU runs step N+1. A sequence
+    # that stops on EOS / stop strings at step N runs one discarded step inside its own KV
+    # reservation; sequences that will hit max_tokens are never launched past their budget.
+    def _free_row(self) -> int:
+        for i, s in enumerate(self.rows):
+            if s is None:
+                return i
+        raise RuntimeError("no free decode row")
+
+    def _assign_row(self, s: _Seq):
+        r = self._free_row()
+        self.rows[r] = s
+        s.row = r
+        s.n_fed = len(s.tokens) - 1
+        nb = len(s.blocks)
+        for hm in self.h_meta_d2:
+            bt = hm.numpy()[_NSEG * self.db.pad:].reshape(self.max_batch, self.max_blocks)
+            bt[r, :nb] = s.blocks
+            bt[r, nb:] = 0
+
+    def _release_rows(self, keep=()):
+        keep = set(id(x) for x in keep)
+        for i, s in enumerate(self.rows):
+            if s is not None and s.done and id(s) not in keep:
+                self.rows[i] = None
+                s.row = -1
+
+    def _compact(self, seqs: List[_Seq]):
+        """Re-pack rows 0..n-1 (only with no step in flight: moved rows get host-side ids)."""
+        for i in range(len(self.rows)):
+            self.rows[i] = None
+        for s in seqs:
+            s.row = -1
+        for s in sorted(seqs, key=lambda x: x.t_submit):
+            self._assign_row(s)
+
+    def _build_meta(self, k: int, launch: List[_Seq], prev: set) -> int:
+        """Fill pinned meta buffer k for the rows of `launch`; returns the padded bucket."""
+        pad = self.db.pad
+        h = self.h_meta_d2[k].numpy()
+        ids, pos, slot, tseq, ctxl, usep = (h[i * pad:(i + 1) * pad] for i in range(_NSEG))
+        bt = h[_NSEG * pad:].reshape(self.max_batch, self.max_blocks)
+        top = max(s.row for s in launch) + 1
+        Bp = self._bucket(top)
+        ids[:Bp] = 0
+        pos[:Bp] = 0
+        slot[:Bp] = -1
+        ctxl[:Bp] = 0
+        usep[:Bp] = 0
+        tseq[:Bp] = np.arange(Bp)
+        rows = np.fromiter((s.row for s in launch), dtype=np.int64, count=len(launch))
+        p = np.fromiter((s.n_fed for s in launch), dtype=np.int64, count=len(launch))
+        up = np.fromiter((id(s) in prev for s in launch), dtype=bool, count=len(launch))
+        ids[rows] = [0 if u else s.tokens[-1] for s, u in zip(launch, up)]
+        usep[rows] = up
+        pos[rows] = p
+        ctxl[rows] = p + 1
+        slot[rows] = bt[rows, p // self.bs] * self.bs + p % self.bs
+        return Bp
+
+    def _launch(self, launch: List[_Seq], prev: set, need: bool = False):
+        k = self._kbuf = self._kbuf ^ 1
+        Bp = self._build_meta(k, launch, prev)
+        pad = self.db.pad
+        self._ctrl(_OP_DECODE, Bp, 0, need, [], Bp, self.h_meta_d2[k], pad)
+        b = self.db
         if self.dev.type == "cuda":
-            b.meta.copy_(self.h_meta_d, non_blocking=True)
+            b.meta.copy_(self.h_meta_d2[k], non_blocking=True)
         else:
-            b.meta.copy_(self.h_meta_d)
+            b.meta.copy_(self.h_meta_d2[k])
         self._run_decode(Bp)
-        self._gather(b, Bp, need)
-        toks = self._pick(seqs, b, list(range(B)))
-        self.counters["decode_tokens"] += B
-        for s, t in zip(seqs, toks):
-            self._append(s, t)
+        for s in launch:
+            s.n_fed += 1
+        if self.dev.type == "cuda":
+            self.h_next2[k][:Bp].copy_(b.next_ids[:Bp], non_blocking=True)
+            self._ev[k].record()
+        else:
+            self.h_next2[k][:Bp].copy_(b.next_ids[:Bp])
+        self.counters["decode_tokens"] += len(launch)
+        return ([(s.row, s) for s in launch], k)
+
+    def _process(self, infl):
+        snap, k = infl
+        if self.dev.type == "cuda":
+            self._ev[k].synchronize()
+        toks = self.h_next2[k].numpy()
+        for row, s in snap:
+            if not s.done:
+                self._append(s, int(toks[row]))
+
+    def _drain(self):
+        if self._inflight is not None:
+            infl, self._inflight = self._inflight, None
+            self._process(infl)
+            self._release_rows()
+
+    def _decode(self, seqs: List[_Seq]):
+        for s in seqs:
+            if s.row < 0:
+                self._assign_row(s)
+        greedy = all(s.req.params.greedy for s in seqs)
+        chain = self.async_decode and greedy
+        if not chain:
+            self._drain()
+        n_rows = max(s.row for s in seqs) + 1
+        if self._bucket(n_rows) > self._bucket(len(seqs)) and self._inflight is None:
+            self._compact(seqs)
+        infl = self._inflight
+        prev = set(id(s) for _, s in infl[0]) if infl is not None else set()
+        launch = []
+        for s in seqs:
+            ahead = 1 if id(s) in prev else 0
+            if len(s.tokens) - s.n_prompt + ahead >= s.max_new or s.n_fed >= self.ctx:
+                continue                       # finishes (length) with the step in flight
+            launch.append(s)
+        if not chain:
+            # synchronous step (sampling / penalties need the host between steps)
+            need = any(not s.req.params.greedy for s in launch)
+            new = self._launch(launch, prev, need) if launch else None
+            if new is not None:
+                self._process_sync(new, launch, need)
+            self._release_rows()
+            return
+        new = self._launch(launch, prev) if launch else None
+        self._inflight = None
+        if infl is not None:
+            self._process(infl)
+        self._inflight = new
+        self._release_rows(keep=[s for _, s in new[0]] if new is not None else ())
+
+    def _process_sync(self, new, launch: List[_Seq], need: bool):
+        snap, k = new
+        b = self.db
+        rows = [r for r, _ in snap]
+        if self.dev.type == "cuda":
+            self._ev[k].synchronize()
+        greedy = self.h_next2[k].numpy()
+        out = [int(greedy[r]) for r in rows]
+        sampled = [i for i, s in enumerate(launch) if not s.req.params.greedy]
+        if need:                               # (TP: followers gather in the same step)
+            self._gather(b, self._bucket(max(rows) + 1), True)
+        if sampled:
+            lg = self.full_logits if self.full_logits is not None else b.logits
+            fn = sample_rows_gpu if lg.is_cuda else sample_rows
+            toks = fn(lg[[rows[i] for i in sampled]], [launch[i].req.params for i in sampled],
+                      [launch[i].tokens for i in sampled], [launch[i].gen for i in sampled])
+            for i, t in zip(sampled, toks):
+                out[i] = t
+        for s, t in zip(launch, out):
+            if not s.done:
+                self._append(s, t)
 
     def _run_decode(self, Bp: int):
         ns = LlamaModel.attn_splits(Bp, self.model.Hkv)
         if not self.use_graphs:
-            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
+            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True)
             return
         g = self.graphs.get(Bp)
         if g is None:                          # TP followers capture lazily in the same step
@@ -451,11 +596,11 @@ class Engine:
 
     def _capture(self, Bp: int, ns: int):
         # eager warm-up allocates every lazily sized workspace before capture
-        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
+        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns)
+            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True)
         torch.cuda.synchronize(self.dev)
         self.graphs[Bp] = g
         return g
@@ -464,11 +609,12 @@ class Engine:
         """Pre-capture decode graphs (padded rows have ctx 0 / slot -1: no KV writes)."""
         if not self.use_graphs:
             return
+        self._drain()
         pad = self.db.pad
-        h = self.h_meta_d.numpy()
-        h[:] = 0
+        h = self.h_meta_d2[0].numpy()
+        h[:_NSEG * pad] = 0
         h[2 * pad:3 * pad] = -1
-        self.db.meta.copy_(self.h_meta_d)
+        self.db.meta.copy_(self.h_meta_d2[0])
         for Bp in buckets or [k for k in BUCKETS if k <= self.max_batch]:
             if Bp not in self.graphs:
                 self._ctrl(_OP_CAPTURE, Bp, 0, False, [], 0, None, 0)

@@ -74,6 +74,7 @@ class StepBuffers:
     tok_seq: torch.Tensor
     ctx_len: torch.Tensor
     block_tables: torch.Tensor
+    use_prev: torch.Tensor
     x: torch.Tensor
     h: torch.Tensor
     qkv: torch.Tensor
@@ -211,20 +212,21 @@ class LlamaModel:
 
     def step_buffers(self, cap: int, max_seqs: int, max_blocks: int) -> StepBuffers:
         """All int32 step metadata lives in ONE tensor (`meta`) so the engine refreshes it
-        with a single host->device copy per step: [ids|pos|slot|tok_seq|ctx_len|block_tables]."""
+        with a single host->device copy per step: [ids|pos|slot|tok_seq|ctx_len|use_prev|block_tables].
+        use_prev[i] != 0: row i's input token is next_ids[i] of the previous step (chained decode)."""
         cfg, dev = self.cfg, self.device
         pad = (cap + 63) // 64 * 64
         Vs = self.vocab_hi - self.vocab_lo
         nq = self.Hq * self.D
         k = max(1, cfg.n_expert_used)
-        meta = torch.zeros(5 * pad + max_seqs * max_blocks, dtype=torch.int32, device=dev)
+        meta = torch.zeros(6 * pad + max_seqs * max_blocks, dtype=torch.int32, device=dev)
         f = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
         b = StepBuffers(
             cap=cap,
             ids=meta[0:pad], pos=meta[pad:2 * pad], slot=meta[2 * pad:3 * pad],
-            tok_seq=meta[3 * pad:4 * pad], ctx_len=meta[4 * pad:5 * pad],
-            block_tables=meta[5 * pad:].view(max_seqs, max_blocks),
+            tok_seq=meta[3 * pad:4 * pad], ctx_len=meta[4 * pad:5 * pad], use_prev=meta[5 * pad:6 * pad],
+            block_tables=meta[6 * pad:].view(max_seqs, max_blocks),
             x=torch.zeros(pad, cfg.d_model, **f),
             h=torch.zeros(pad, cfg.d_model, **bf),
             qkv=torch.zeros(pad, (self.Hq + 2 * self.Hkv) * self.D, **f),
@@ -261,12 +263,14 @@ class LlamaModel:
     # ------------------------------------------------------------------ forward
     def forward(self, b: StepBuffers, kc: torch.Tensor, vc: torch.Tensor, T: int, block_size: int,
                 n_split: int = 1, logit_rows: Optional[torch.Tensor] = None, n_logits: Optional[int] = None,
-                qblocks: Optional[torch.Tensor] = None, nqb: int = 0):
+                qblocks: Optional[torch.Tensor] = None, nqb: int = 0, feed_prev: bool = False):
         """Runs T tokens through the model; leaves greedy ids in b.next_ids[:n] and logits in b.logits[:n].
         With `qblocks` (prompt chunks, ops.prefill_blocks) attention runs the MFMA flash-prefill kernel."""
         cfg = self.cfg
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         x = b.x
+        if feed_prev:                          # chained decode: previous step's tokens, on device
+            torch.where(b.use_prev[:T] != 0, b.next_ids[:T], b.ids[:T], out=b.ids[:T])
         ops.embed(b.ids, self.tok_embd, x, T, cfg.embedding_scale)
         need = T * Hq * n_split * (D + 2)
         if n_split > 1 and b.attn_ws.numel() < need:
