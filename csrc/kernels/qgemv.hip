@@ -24,7 +24,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
               void* stream) {
   if (nseg < 1 || nseg > 8 || M < 1 || (rt != 1 && rt != 2) || (waves != 4 && waves != 8)) return -1;
   if (M > 64 && mode != 1) return -1;   // large M: path B in blocks of 128 activation rows
-  if (mode == 1 && ks > 1 && (!ws || M > 64)) return -1;
+  if (mode == 1 && ks > 1 && !ws) return -1;
   SegList sl{};
   int tiles = 0, cols = 0;
   const int tile_rows = (mode == 1 ? waves : 1) * rt * 16;
@@ -57,7 +57,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   }
   if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
   const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
-  GemvArgs a{(const __bf16*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax};
+  GemvArgs a{(const __bf16*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax, 0, M};
   const int mt = M > 64 ? 8 : (M + 15) / 16;
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;

@@ -40,6 +40,7 @@ struct GemvArgs {
   float alpha;
   int pad;            // path B split-K: total raw output columns
   unsigned long long* argmax;   // optional [M] packed (ordered value << 32 | ~idx)
+  int m0, mtot;       // large-M split-K: first activation row of this block, total rows (slab index)
 };
 
 DEVI unsigned long long argmax_key(float v, int idx) {
@@ -355,7 +356,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int b = mt * 16 + 4 * g + i;
-          if (b < M) ws[((size_t)kslice * M + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][i];
+          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][i];
         }
     }
     return;
@@ -406,11 +407,14 @@ __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs 
     // Large M (prefill / big decode batches): blocks of MT*16 activation rows. The workgroups
     // sharing one weight tile are placed on ONE XCD (dispatch assigns workgroup i to XCD i % 8),
     // so each weight tile is fetched from HBM once per XCD L2 instead of once per m-block.
+    // With split-K (ks > 1) the K slices of a tile are also kept on its XCD.
     const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
-    const int mb = j % nmb;
-    tile = (j / nmb) * 8 + xcd;
+    kslice = j % ks;
+    const int mb = (j / ks) % nmb;
+    tile = (j / ks / nmb) * 8 + xcd;
     if (tile >= ntiles) return;
     const int m0 = mb * MT * 16;
+    a.m0 = m0;
     a.x += (size_t)m0 * a.ldx;
     const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32) ? 4 : 2;
     a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
@@ -506,7 +510,7 @@ int launch_mt(int mt, const SegList& sl, int nt, const GemvArgs& a, hipStream_t 
 template <int WAVES, int RT, int MT, int KSET>
 int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st, int nmb) {
   const size_t lds = (size_t)2 * MT * 16 * 256 * sizeof(__bf16);
-  const int grid = nmb > 1 ? ((ntiles + 7) / 8) * 8 * nmb : ntiles * ks;
+  const int grid = nmb > 1 ? ((ntiles + 7) / 8) * 8 * nmb * ks : ntiles * ks;
   hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, KSET>), dim3(grid), dim3(WAVES * 64), lds, st, sl, a, ks, ws,
                      ntiles, nmb);
   return (int)hipGetLastError();

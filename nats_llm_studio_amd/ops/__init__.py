@@ -202,8 +202,6 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
                 qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt,
                       mode, ks)
             return y
-        if M > 64:
-            ks = 1                    # large M: MFMA GEMM over 128-row activation blocks
         arr = (_lib.NlsSeg * len(segs))()
         for i, s in enumerate(segs):
             arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,

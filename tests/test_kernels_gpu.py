@@ -239,7 +239,7 @@ def test_oneshot_allreduce_simulated(gpu, world):
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q8_0, GGMLType.BF16])
 @pytest.mark.parametrize("M", [65, 128, 200, 300])
-@pytest.mark.parametrize("wr", [(8, 1), (4, 2)])
+@pytest.mark.parametrize("wr", [(8, 1, 1), (4, 2, 1), (8, 1, 3)])
 def test_qgemm_large_m(gpu, t, M, wr):
     """Large-M MFMA GEMM (prefill / big decode batches): 128-row activation blocks, XCD-grouped
     weight tiles, partial last block; plain store, residual add and fused argmax."""
@@ -248,9 +248,9 @@ def test_qgemm_large_m(gpu, t, M, wr):
     x = _x(M, K, gpu)
     pad = x.shape[0]
     y = torch.zeros(pad, rows, device=gpu)
-    waves, rt = wr
+    waves, rt, ks = wr
     keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, mode=1, waves=waves, rt=rt, ks=1, argmax=keys)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=1, waves=waves, rt=rt, ks=ks, argmax=keys)
     ref = x[:M].float().cpu() @ Wd.t()
     _close(y[:M], ref)
     assert float(y[M:].abs().max().cpu()) == 0.0 if M < pad else True
@@ -259,7 +259,7 @@ def test_qgemm_large_m(gpu, t, M, wr):
     assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
     base = torch.randn(pad, rows, device=gpu)
     y2 = base.clone()
-    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=1, waves=waves, rt=rt, ks=1)
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=1, waves=waves, rt=rt, ks=ks)
     _close(y2[:M], base[:M].cpu() + 0.5 * ref)
 
 
@@ -276,6 +276,9 @@ def test_qgemm_large_m_swiglu(gpu):
     y = torch.zeros(x.shape[0], F, dtype=torch.bfloat16, device=gpu)
     ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=1, waves=8, rt=1, ks=1)
     xf = x[:M].float().cpu()
+    y3 = torch.zeros_like(y)
+    ops.qgemv([ops.Seg(w)], x, y3, M, epi="swiglu", mode=1, waves=8, rt=1, ks=2)
+    _close(y3[:M], y[:M].cpu(), 1e-2)
     _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
 
 
