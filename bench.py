@@ -131,12 +131,18 @@ def main():
         extra["single_stream_ttft_ms"] = round(r.time_to_first_token * 1e3, 2)
 
     rtt = None
+    chat_rtt = None
     if not args.no_rtt and rank == 0:
         try:
             from nats_llm_studio_amd.service.bench_rtt import measure_rtt
             rtt = measure_rtt(n=500)
         except Exception as e:  # natscore missing -> report null, never fake
             extra["rtt_error"] = str(e)[:200]
+        try:   # chat_model on the real 8B engine (after the timed region; engine idle)
+            from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_rtt
+            chat_rtt = measure_engine_chat_rtt(eng, reader.metadata, n=30)
+        except Exception as e:
+            extra["chat_rtt_error"] = str(e)[:300]
 
     if rank == 0:
         value = tok_sum / t_max
@@ -161,7 +167,8 @@ def main():
                 "concurrency_per_gpu": B,
                 "hipgraph": not args.no_graphs,
             },
-            "p50_rtt_ms": None if rtt is None else rtt.get("p50_ms"),
+            "p50_rtt_ms": (chat_rtt or {}).get("p50_ms", None if rtt is None else rtt.get("p50_ms")),
+            "rtt_chat_model_engine": chat_rtt,
             "rtt": rtt,
             "weights_gb": round(model.weight_bytes / 1e9, 3),
             "timings_s": {"gguf_write": round(t_gen, 1), "load": round(t_load, 1), "prefill_all": round(t_prefill, 3)},

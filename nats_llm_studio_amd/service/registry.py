@@ -87,6 +87,10 @@ class Registry:
                         entries[e.id] = e
                         for a in e.aliases:
                             alias.setdefault(a.lower(), e.id)
+        for e in getattr(self, "_extra", {}).values():       # added entries survive re-scans
+            entries.setdefault(e.id, e)
+            for a in [e.id] + list(e.aliases):
+                alias.setdefault(a.lower(), e.id)
         with self._lock:
             self._entries = entries
             self._alias = alias
@@ -119,6 +123,15 @@ class Registry:
             aliases=[mid, f"{pub}/{mdir}", f"{pub}/{mid}", mdir, stem, f"{pub}/{mdir}/{fname}", f"{pub}/{stem}"],
         )
         return e
+
+    def add(self, e: ModelEntry):
+        """Register an entry that does not live under models_dir (e.g. a preloaded model)."""
+        with self._lock:
+            self._entries[e.id] = e
+            for a in [e.id] + list(e.aliases):
+                self._alias.setdefault(a.lower(), e.id)
+        self._extra = getattr(self, "_extra", {})
+        self._extra[e.id] = e
 
     def resolve(self, ident: str) -> Optional[ModelEntry]:
         with self._lock:

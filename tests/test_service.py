@@ -275,3 +275,16 @@ def test_http_backend_proxy_semantics(tmp_path):
         svc.stop()
         svc.client.close()
         srv.stop()
+
+
+def test_engine_chat_rtt_helper(tiny_models):
+    """bench.py's chat_model RTT against a real engine (CPU here, the 8B GPU engine in the bench)."""
+    from nats_llm_studio_amd.engine.engine import Engine
+    from nats_llm_studio_amd.gguf.reader import GGUFReader
+    from nats_llm_studio_amd.models.llama import LlamaModel
+    from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_rtt
+    r = GGUFReader(tiny_models["tiny-llama"])
+    eng = Engine(LlamaModel(r, "cpu"), None, max_batch=4, ctx=256, num_blocks=64, use_graphs=False)
+    out = measure_engine_chat_rtt(eng, r.metadata, model_id="tiny-llama", n=3, warmup=1)
+    assert out["n"] == 3 and 0 < out["p50_ms"] <= out["p99_ms"] and out["prompt_tokens"] > 0
+    assert eng.thread is None
