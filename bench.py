@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--concurrency", type=int, default=64, help="in-flight chat requests per GPU")
+    ap.add_argument("--concurrency", type=int, default=256, help="in-flight chat requests per GPU")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--ftype", default="Q4_K_M")
@@ -77,14 +77,18 @@ def main():
     t_load = time.time() - t0
 
     B = args.concurrency
-    need_tokens = args.prompt_len + args.warmup + args.steps + 8
-    eng = Engine(model, None, max_batch=B, max_prefill_tokens=2048, use_graphs=not args.no_graphs,
+    max_prefill = 2048
+    # sequences prefilled early already decode while later ones prefill: budget those steps too
+    prefill_steps = (B * args.prompt_len + max_prefill - 1) // max_prefill
+    gen_tokens = args.warmup + args.steps + prefill_steps + 8
+    need_tokens = args.prompt_len + gen_tokens
+    eng = Engine(model, None, max_batch=B, max_prefill_tokens=max_prefill, use_graphs=not args.no_graphs,
                  ctx=max(need_tokens + 16, 512), num_blocks=B * ((need_tokens + 15) // 16 + 1))
     eng.capture_all()
     rng = np.random.default_rng(rank)
     vocab = model.cfg.vocab
     futs = [eng.submit(GenRequest(list(rng.integers(0, min(vocab, 100000), args.prompt_len)),
-                                  SamplingParams(max_tokens=args.warmup + args.steps + 4, ignore_eos=True)))
+                                  SamplingParams(max_tokens=gen_tokens, ignore_eos=True)))
             for _ in range(B)]
     # prefill every request (not timed), then warm up the decode loop
     t0 = time.time()
