@@ -291,6 +291,87 @@ DEVI void deq_q6k(const RawQ6K& r, int g, bf16x8* wf) {
   }
 }
 
+// ---- per-K-step dequant (Q4_K / Q6_K): scales once per super-block, then one 8-value
+// fragment per MFMA K-step, so a tile's 64 bf16 values never sit in registers at once
+// (the large-M GEMM keeps RT weight tiles x MT activation tiles of accumulators live).
+struct ScQ4K { float a[4], m[4]; };
+struct ScQ6K { float a[4]; };
+
+DEVI void prep_q4k(const RawQ4K& r, int g, ScQ4K& s) {
+  const float d = h2f(r.hdr[0] & 0xFFFF), dmin = h2f(r.hdr[0] >> 16);
+  const int c0 = g >> 1;
+  const int js[4] = {2 * c0, 2 * c0 + 1, 4 + 2 * c0, 5 + 2 * c0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int sc, m;
+    if (i < 2) k4_scale_min_t<false>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
+    else k4_scale_min_t<true>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
+    s.a[i] = d * (float)sc;
+    s.m[i] = dmin * (float)m;
+  }
+}
+
+// fragment t of deq_q4k's output (t = 4*(p1) + 2*(high nibble) + half)
+DEVI bf16x8 frag_q4k(const RawQ4K& r, const ScQ4K& s, int t) {
+  const u32x4 p = t < 4 ? r.p0 : r.p1;
+  const int half = t & 1, hi = (t >> 1) & 1, si = (t < 4 ? 0 : 2) + hi;
+  const uint32_t w0 = p[2 * half], w1 = p[2 * half + 1];
+  const int sh = 4 * hi;
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = s.a[si] * (float)((w0 >> (8 * i + sh)) & 0xF) - s.m[si];
+    v[4 + i] = s.a[si] * (float)((w1 >> (8 * i + sh)) & 0xF) - s.m[si];
+  }
+  return pack8(v);
+}
+
+DEVI void prep_q6k(const RawQ6K& r, int g, ScQ6K& s) {
+  const float d = h2f((uint16_t)r.d);
+  const int n = g >> 1, par = g & 1;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = 8 * n + par + 2 * u;
+    const int8_t sc = (int8_t)((r.sc[idx >> 2] >> (8 * (idx & 3))) & 0xFF);
+    s.a[u] = d * (float)sc;
+  }
+}
+
+// fragment t of deq_q6k's output (t = 2*u + s)
+DEVI bf16x8 frag_q6k(const RawQ6K& r, const ScQ6K& sc, int t) {
+  const int u = t >> 1, sidx = t & 1;
+  const u32x4 ql = (u & 1) ? r.qb : r.qa;
+  const int nshift = (u >> 1) ? 4 : 0, hshift = 2 * u;
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t wl = ql[2 * sidx + q], wh = r.qh[2 * sidx + q];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lo = (wl >> (8 * i + nshift)) & 0xF;
+      const int hi = (wh >> (8 * i + hshift)) & 3;
+      v[4 * q + i] = sc.a[u] * (float)((lo | (hi << 4)) - 32);
+    }
+  }
+  return pack8(v);
+}
+
+template <int T> struct ScOf { typedef int type; };
+template <> struct ScOf<QT_Q4_K> { typedef ScQ4K type; };
+template <> struct ScOf<QT_Q6_K> { typedef ScQ6K type; };
+template <int T> constexpr bool kPerStep = (T == QT_Q4_K || T == QT_Q6_K);
+
+template <int T>
+DEVI void prep_sc(const typename RawOf<T>::type& r, int g, typename ScOf<T>::type& s) {
+  if constexpr (T == QT_Q4_K) prep_q4k(r, g, s);
+  else if constexpr (T == QT_Q6_K) prep_q6k(r, g, s);
+}
+template <int T>
+DEVI bf16x8 frag_t(const typename RawOf<T>::type& r, const typename ScOf<T>::type& s, int t) {
+  if constexpr (T == QT_Q4_K) return frag_q4k(r, s, t);
+  else return frag_q6k(r, s, t);
+}
+
 // ---- Q8_0 ------------------------------------------------------------------
 template <bool NT>
 DEVI RawQ8 load_raw_q8(const WDesc& W, int row, int sb, int g) {

@@ -271,22 +271,33 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   constexpr int NT = WAVES * 64;
   constexpr int NCH = (MT * 16 * 32) / NT;               // 16-B chunks staged per thread
   static_assert((MT * 16 * 32) % NT == 0, "staging must divide evenly");
-  u32x4 xst[NCH];
-  auto load_x = [&](int sb) {
+  // large tiles stage x in two halves (half the staging registers)
+  constexpr bool SPLITX = kPerStep<T> && MT >= 4 && NCH % 2 == 0;
+  constexpr int NCHR = SPLITX ? NCH / 2 : NCH;
+  u32x4 xst[NCHR];
+  auto load_xh = [&](int sb, int h) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int idx = threadIdx.x + c * NT;
+    for (int c = 0; c < NCHR; ++c) {
+      const int idx = threadIdx.x + (c + h * NCHR) * NT;
       const int row = idx >> 5, ch = idx & 31;
       // rows >= M only feed output rows that are never stored: clamp, never branch
       xst[c] = ld16(a.x + (size_t)min(row, M - 1) * a.ldx + sb * 256 + ch * 8);
     }
   };
-  auto store_x = [&](int buf) {
+  auto store_xh = [&](int buf, int h) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int idx = threadIdx.x + c * NT;
+    for (int c = 0; c < NCHR; ++c) {
+      const int idx = threadIdx.x + (c + h * NCHR) * NT;
       const int row = idx >> 5, ch = idx & 31;
       *reinterpret_cast<u32x4*>(lds + buf * (MT * 16 * 256) + lds_off(row, ch * 8)) = xst[c];
+    }
+  };
+  auto stage_full = [&](int sb, int buf) {      // prologue: both halves
+    load_xh(sb, 0);
+    store_xh(buf, 0);
+    if constexpr (SPLITX) {
+      load_xh(sb, 1);
+      store_xh(buf, 1);
     }
   };
 
@@ -300,40 +311,70 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   Raw wA[RT], wB[RT];
   const int sbl = max(sb1 - 1, sb0);
   if (sb0 < sb1) {
-    load_x(sb0);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
-    store_x(0);
+    stage_full(sb0, 0);
   }
   __syncthreads();
   // fixed buffer roles, unrolled by two (see path A); x for sb+1 is staged through the other
   // LDS buffer while sb is computed
   auto step = [&](Raw (&w)[RT], int sb) {
     const int buf = (sb - sb0) & 1;
-    load_x(min(sb + 1, sbl));          // unconditional (clamped): see path A
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 wf[RT][8];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+    const int nxt = min(sb + 1, sbl);  // unconditional (clamped): see path A
+    load_xh(nxt, 0);
     __builtin_amdgcn_sched_barrier(0);
     const __bf16* xb = lds + buf * (MT * 16 * 256);
+    if constexpr (kPerStep<T> && MT >= 4) {
+      // large tiles: per-K-step fragments (scales once per super-block), weight buffer reloaded
+      // after its last use; x half 0 written after K-steps 0-3, half 1 loaded then, written last
+      typename ScOf<T>::type sc[RT];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int ko = xoff<T>(t, g);
+      for (int rt = 0; rt < RT; ++rt) prep_sc<T>(w[rt], g, sc[rt]);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
+      for (int t = 0; t < 8; ++t) {
+        if (SPLITX && t == 4) {
+          store_xh(buf ^ 1, 0);
+          load_xh(nxt, 1);
+        }
+        bf16x8 wt[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
+        for (int rt = 0; rt < RT; ++rt) wt[rt] = frag_t<T>(w[rt], sc[rt], t);
+        const int ko = xoff<T>(t, g);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+            acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wt[rt], acc[rt][mt], 0, 0, 0);
+        }
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+      store_xh(buf ^ 1, SPLITX ? 1 : 0);
+    } else {
+      bf16x8 wf[RT][8];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int ko = xoff<T>(t, g);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+            acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
+        }
+      }
+      store_xh(buf ^ 1, 0);
     }
-    store_x(buf ^ 1);
     __syncthreads();
   };
   int sb = sb0;
