@@ -60,6 +60,53 @@ __global__ __launch_bounds__(512) void rmsnorm_kernel(const float* __restrict__ 
   }
 }
 
+// Fused split-K reduce + residual add + RMSNorm (row-parallel projections): the GEMM left
+// ks fp32 partial slabs ws[k][M][D]; x[m] += alpha * sum_k ws[k][m] (fixed order: deterministic),
+// then out[m] = bf16(rmsnorm(x[m]) * w). One launch instead of reduce + norm, and x is read once.
+__global__ __launch_bounds__(512) void splitk_add_rmsnorm_kernel(const float* __restrict__ ws, int ks, int M,
+                                                                 float alpha, float* __restrict__ x, long ldx,
+                                                                 const float* __restrict__ w,
+                                                                 __bf16* __restrict__ out, long ldo, int D,
+                                                                 float eps) {
+  __shared__ float sh[8];
+  const int m = blockIdx.x;
+  float* xr = x + (size_t)m * ldx;
+  float4 v[4];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = (threadIdx.x + j * 512) * 4;
+    if (i < D) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < ks; ++k) {
+        const float4 p = *reinterpret_cast<const float4*>(ws + ((size_t)k * M + m) * D + i);
+        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+      }
+      float4 r = *reinterpret_cast<const float4*>(xr + i);
+      r.x += alpha * acc.x; r.y += alpha * acc.y; r.z += alpha * acc.z; r.w += alpha * acc.w;
+      *reinterpret_cast<float4*>(xr + i) = r;
+      v[j] = r;
+    } else {
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    ss += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+  }
+  ss = block_sum<512>(ss, sh);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  __bf16* o = out + (size_t)m * ldo;
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = (threadIdx.x + j * 512) * 4;
+    if (i < D) {
+      const float4 ww = *reinterpret_cast<const float4*>(w + i);
+      bf16x4 r = {(__bf16)(v[j].x * inv * ww.x), (__bf16)(v[j].y * inv * ww.y), (__bf16)(v[j].z * inv * ww.z),
+                  (__bf16)(v[j].w * inv * ww.w)};
+      *reinterpret_cast<bf16x4*>(o + i) = r;
+    }
+  }
+}
+
 // f32 -> f32 variant (final norm feeding an fp32 reference / lm-head in f32)
 __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restrict__ x, long ldx,
                                                           const float* __restrict__ w,
@@ -250,6 +297,14 @@ int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, i
   else
     hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, x, ldx, w,
                        (__bf16*)out, ldo, D, eps);
+  return (int)hipGetLastError();
+}
+
+int nls_splitk_add_rmsnorm(const float* ws, int ks, int M, float alpha, float* x, long ldx, const float* w,
+                           void* out, long ldo, int D, float eps, void* stream) {
+  if (D % 4 || D > 8192 || ks < 1) return -1;
+  hipLaunchKernelGGL(splitk_add_rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, ws, ks, M, alpha, x, ldx,
+                     w, (__bf16*)out, ldo, D, eps);
   return (int)hipGetLastError();
 }
 

@@ -25,6 +25,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   if (nseg < 1 || nseg > 8 || M < 1 || (rt != 1 && rt != 2) || (waves != 4 && waves != 8)) return -1;
   if (M > 64 && mode != 1) return -1;   // large M: path B in blocks of 128 activation rows
   if (mode == 1 && ks > 1 && !ws) return -1;
+  if (epi == EPI_SLABS && (mode != 1 || ks < 2)) return -1;   // slabs exist only with split-K
   SegList sl{};
   int tiles = 0, cols = 0;
   const int tile_rows = (mode == 1 ? waves : 1) * rt * 16;
@@ -65,7 +66,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   if (mode == 1) {
     if (ks < 1) ks = 1;
     const int rc = launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
-    if (rc || ks == 1) return rc;
+    if (rc || ks == 1 || epi == EPI_SLABS) return rc;
     RedList rl{};
     for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};
     rl.nseg = nseg;

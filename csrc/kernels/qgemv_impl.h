@@ -21,7 +21,9 @@
 namespace nls_gemv {
 
 
-enum Epi : int { EPI_F32 = 0, EPI_BF16 = 1, EPI_ADD_F32 = 2, EPI_SWIGLU_BF16 = 3 };
+// EPI_SLABS: split-K partial slabs only (the caller fuses the reduce, e.g. with RMSNorm);
+// EPI_ARGMAX: fused arg-max keys only, no logits stored (greedy decode)
+enum Epi : int { EPI_F32 = 0, EPI_BF16 = 1, EPI_ADD_F32 = 2, EPI_SWIGLU_BF16 = 3, EPI_SLABS = 4, EPI_ARGMAX = 5 };
 
 struct Seg {
   const uint8_t* w;
@@ -189,7 +191,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     const size_t off = (size_t)yrow * a.ldy + S.ycol + row;
     if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
     else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+    else if (a.epi == EPI_BF16) reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
   }
   if (a.argmax) {
     for (int bb = threadIdx.x; bb < min(mcount, ncols); bb += WAVES * 64) {
@@ -423,7 +425,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           const size_t off = (size_t)b * a.ldy + S.ycol + row;
           if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
           else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-          else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+          else if (a.epi == EPI_BF16) reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
         }
         if (a.argmax) {
           unsigned long long k = (row < S.rows) ? argmax_key(v, S.ycol + row) : 0ull;
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs 
     const int m0 = mb * MT * 16;
     a.m0 = m0;
     a.x += (size_t)m0 * a.ldx;
-    const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32) ? 4 : 2;
+    const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
     a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
     if (a.argmax) a.argmax += m0;
     a.M = min(MT * 16, a.M - m0);
@@ -523,7 +525,7 @@ static __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks
     const size_t off = (size_t)b * a.ldy + S.ycol + row;
     if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
     else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+    else if (a.epi == EPI_BF16) reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
     if (a.argmax) atomicMax(a.argmax + b, argmax_key(v, S.ycol + row));
   }
 }

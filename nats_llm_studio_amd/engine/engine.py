@@ -156,7 +156,7 @@ class Engine:
         self.rows: List[Optional[_Seq]] = [None] * self.max_batch
         self.async_decode = async_decode
         self.use_graphs = use_graphs and self.dev.type == "cuda"
-        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}     # (bucket, logits needed) -> graph
         self.eos = set(int(e) for e in eos_ids)
         if tokenizer is not None and getattr(tokenizer, "eos_id", None) is not None:
             self.eos.add(int(tokenizer.eos_id))
@@ -349,7 +349,8 @@ class Engine:
         qb = ops.prefill_blocks(h[3 * pad:4 * pad], h[pad:2 * pad], T) if self.prefill_attn else None
         qbt = torch.from_numpy(qb).to(self.dev) if qb is not None and len(qb) else None
         n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
-                               logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb))
+                               logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb),
+                               need_logits=need_logits)
         self._gather(b, n, need_logits)
 
     def _gather(self, b, n: int, need_logits: bool):
@@ -400,7 +401,7 @@ class Engine:
                 self._exec_prefill(T, [int(v) for v in hdr[_HDR:_HDR + nrows]], bool(need))
             else:
                 self.db.meta.copy_(hm)
-                self._run_decode(T)
+                self._run_decode(T, bool(need))
                 if need:
                     self._gather(self.db, T, True)
 
@@ -501,7 +502,7 @@ class Engine:
             b.meta.copy_(self.h_meta_d2[k], non_blocking=True)
         else:
             b.meta.copy_(self.h_meta_d2[k])
-        self._run_decode(Bp)
+        self._run_decode(Bp, need)
         for s in launch:
             s.n_fed += 1
         if self.dev.type == "cuda":
@@ -583,26 +584,26 @@ class Engine:
             if not s.done:
                 self._append(s, t)
 
-    def _run_decode(self, Bp: int):
+    def _run_decode(self, Bp: int, need_logits: bool = False):
         ns = LlamaModel.attn_splits(Bp, self.model.Hkv)
         if not self.use_graphs:
-            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True)
+            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True, need_logits=need_logits)
             return
-        g = self.graphs.get(Bp)
+        g = self.graphs.get((Bp, need_logits))
         if g is None:                          # TP followers capture lazily in the same step
-            g = self._capture(Bp, ns)
+            g = self._capture(Bp, ns, need_logits)
         g.replay()
         self.counters["graph_replays"] += 1
 
-    def _capture(self, Bp: int, ns: int):
+    def _capture(self, Bp: int, ns: int, need_logits: bool = False):
         # eager warm-up allocates every lazily sized workspace before capture
-        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True)
+        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True, need_logits=need_logits)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True)
+            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True, need_logits=need_logits)
         torch.cuda.synchronize(self.dev)
-        self.graphs[Bp] = g
+        self.graphs[(Bp, need_logits)] = g
         return g
 
     def capture_all(self, buckets: Seq[int] = None):
@@ -616,7 +617,7 @@ class Engine:
         h[2 * pad:3 * pad] = -1
         self.db.meta.copy_(self.h_meta_d2[0])
         for Bp in buckets or [k for k in BUCKETS if k <= self.max_batch]:
-            if Bp not in self.graphs:
+            if (Bp, False) not in self.graphs:
                 self._ctrl(_OP_CAPTURE, Bp, 0, False, [], 0, None, 0)
                 self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv))
 

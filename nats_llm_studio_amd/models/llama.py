@@ -263,7 +263,8 @@ class LlamaModel:
     # ------------------------------------------------------------------ forward
     def forward(self, b: StepBuffers, kc: torch.Tensor, vc: torch.Tensor, T: int, block_size: int,
                 n_split: int = 1, logit_rows: Optional[torch.Tensor] = None, n_logits: Optional[int] = None,
-                qblocks: Optional[torch.Tensor] = None, nqb: int = 0, feed_prev: bool = False):
+                qblocks: Optional[torch.Tensor] = None, nqb: int = 0, feed_prev: bool = False,
+                need_logits: bool = True):
         """Runs T tokens through the model; leaves greedy ids in b.next_ids[:n] and logits in b.logits[:n].
         With `qblocks` (prompt chunks, ops.prefill_blocks) attention runs the MFMA flash-prefill kernel."""
         cfg = self.cfg
@@ -275,8 +276,12 @@ class LlamaModel:
         need = T * Hq * n_split * (D + 2)
         if n_split > 1 and b.attn_ws.numel() < need:
             b.attn_ws = torch.zeros(need, dtype=torch.float32, device=self.device)
+        fused = self.shard.size == 1            # row-parallel GEMM + residual + next RMSNorm in one pass
+        fused_prev = True                       # layer 0's input norm is applied just below
+        ops.rmsnorm(x, self.layers[0].attn_norm, b.h, T, cfg.eps)
         for L, lw in enumerate(self.layers):
-            ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
+            if L > 0 and not fused_prev:
+                ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
             ops.qgemv(lw.qkv, b.h, b.qkv, T)
             ops.rope_kv(b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D, cfg.rope_neox)
             if qblocks is not None and nqb > 0 and ops.attention_prefill_ok(Hq, Hkv, D):
@@ -285,14 +290,24 @@ class LlamaModel:
             else:
                 ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
                               block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws)
-            self._row_parallel(lw.wo, b.ao, x, T, cfg.residual_scale)
-            ops.rmsnorm(x, lw.ffn_norm, b.h, T, cfg.eps)
+            if fused:
+                ops.qgemv_add_rmsnorm(Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps)
+            else:
+                self._row_parallel(lw.wo, b.ao, x, T, cfg.residual_scale)
+                ops.rmsnorm(x, lw.ffn_norm, b.h, T, cfg.eps)
+            nxt = self.layers[L + 1].attn_norm if L + 1 < len(self.layers) else self.out_norm
+            fused_prev = False
             if cfg.n_expert:
                 self._moe(lw, b, T)
             else:
                 ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
-                self._row_parallel(lw.down, b.act, x, T, cfg.residual_scale)
-        ops.rmsnorm(x, self.out_norm, b.h, T, cfg.eps)
+                if fused:
+                    ops.qgemv_add_rmsnorm(Seg(lw.down), b.act, x, nxt, b.h, T, cfg.residual_scale, cfg.eps)
+                    fused_prev = True
+                else:
+                    self._row_parallel(lw.down, b.act, x, T, cfg.residual_scale)
+        if not fused_prev:
+            ops.rmsnorm(x, self.out_norm, b.h, T, cfg.eps)
         h = b.h
         n = T
         if logit_rows is not None:
@@ -300,7 +315,9 @@ class LlamaModel:
             h = b.h.index_select(0, logit_rows[:n].long())
             h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
         ops.argmax_reset(b.keys)
-        ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys)
+        # greedy-only steps keep just the fused arg-max keys (no [n, V] logits written)
+        ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
+                  epi="f32" if need_logits else "argmax")
         if self.shard.size == 1:
             ops.argmax_unpack(b.keys, n, b.next_ids)
         else:

@@ -19,7 +19,7 @@ from ..gguf.constants import GGMLType, GGML_BLOCK
 from ..gguf.quants import dequantize
 from . import _lib
 
-EPI = {"f32": 0, "bf16": 1, "add": 2, "swiglu": 3}
+EPI = {"f32": 0, "bf16": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5}
 
 
 def _stream_ptr(t: torch.Tensor) -> int:
@@ -237,13 +237,35 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
             y[yi, s.ycol:s.ycol + n // 2] = out.to(y.dtype)
         elif epi == "add":
             y[yi, s.ycol:s.ycol + n] += acc.to(y.dtype)
-        else:
+        elif epi != "argmax":
             y[yi, s.ycol:s.ycol + n] = acc.to(y.dtype)
         if argmax is not None:
             v, idx = acc.max(dim=1)
             key = _argmax_keys(v, idx + s.ycol)
             argmax[yi] = torch.maximum(argmax[yi], key)
     return y
+
+
+def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torch.Tensor, h: torch.Tensor, M: int,
+                      alpha: float, eps: float, cfg=None):
+    """x[:M] += alpha * xin @ W^T, then h[:M] = rmsnorm(x[:M]) * norm_w (bf16). With a split-K
+    launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel."""
+    if x.is_cuda and seg.xmap is None:
+        mode, waves, rt, ks = cfg or gemv_config([seg], M)
+        if mode == 1 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
+            L = _lib.lib()
+            ws = _workspace(x.device, ks * M * seg.w.rows)
+            arr = (_lib.NlsSeg * 1)()
+            arr[0] = _lib.NlsSeg(seg.w.data.data_ptr(), None, None, None, seg.w.type, seg.w.rows, seg.w.K, 0)
+            st = _stream_ptr(x)
+            _lib.check(L.nls_qgemv(arr, 1, xin.data_ptr(), xin.stride(0), x.data_ptr(), x.stride(0), M, float(alpha),
+                                   EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
+            _lib.check(L.nls_splitk_add_rmsnorm(ws.data_ptr(), ks, M, float(alpha), x.data_ptr(), x.stride(0),
+                                                norm_w.data_ptr(), h.data_ptr(), h.stride(0), x.shape[1], float(eps),
+                                                st), "nls_splitk_add_rmsnorm")
+            return h
+    qgemv([seg], xin, x, M, alpha=alpha, epi="add")
+    return rmsnorm(x, norm_w, h, M, eps)
 
 
 def _argmax_keys(v: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:

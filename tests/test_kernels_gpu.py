@@ -346,3 +346,39 @@ def test_sample_kernel(gpu):
     g2 = [torch.Generator().manual_seed(7) for _ in range(8)]
     pp = [SamplingParams(temperature=1.5)] * 8
     assert sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g1) == sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g2)
+
+
+@pytest.mark.parametrize("M,cfg", [(5, (1, 8, 1, 4)), (64, (1, 4, 1, 2)), (200, (1, 8, 1, 3)), (200, (1, 8, 1, 1)),
+                                   (7, (0, 4, 1, 1))])
+def test_qgemv_add_rmsnorm_fused(gpu, M, cfg):
+    """Row-parallel projection + residual + next RMSNorm (split-K slabs reduced by the fused kernel)."""
+    D, K = 512, 768
+    w, Wd = _qw(D, K, GGMLType.Q4_K, gpu, 11)
+    xin = _x(M, K, gpu)
+    pad = xin.shape[0]
+    base = torch.randn(pad, D, device=gpu)
+    x = base.clone()
+    nw = (1 + 0.1 * torch.randn(D)).to(gpu)
+    h = torch.zeros(pad, D, dtype=torch.bfloat16, device=gpu)
+    ops.qgemv_add_rmsnorm(ops.Seg(w), xin, x, nw, h, M, 0.7, 1e-5, cfg=cfg)
+    xr = base[:M].cpu() + 0.7 * (xin[:M].float().cpu() @ Wd.t())
+    _close(x[:M], xr)
+    hr = xr * torch.rsqrt(xr.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu()
+    _close(h[:M], hr, 3e-2)
+
+
+def test_lm_head_argmax_only_epilogue(gpu):
+    """Greedy decode: arg-max keys without writing logits."""
+    K, V = 512, 1000
+    w, Wd = _qw(V, K, GGMLType.Q6_K, gpu, 12)
+    for M, cfg in ((3, (0, 4, 1, 1)), (40, (1, 8, 1, 2)), (150, (1, 8, 1, 1))):
+        x = _x(M, K, gpu)
+        y = torch.full((x.shape[0], V), 7.0, device=gpu)
+        keys = torch.zeros(x.shape[0], dtype=torch.int64, device=gpu)
+        mode, waves, rt, ks = cfg
+        ops.qgemv([ops.Seg(w)], x, y, M, epi="argmax", argmax=keys, mode=mode, waves=waves, rt=rt, ks=ks)
+        ids = torch.zeros(x.shape[0], dtype=torch.int32, device=gpu)
+        ops.argmax_unpack(keys, M, ids)
+        ref = (x[:M].float().cpu() @ Wd.t()).argmax(1)
+        assert (ids[:M].cpu().long() == ref).float().mean() > 0.98
+        assert bool((y == 7.0).all())
