@@ -126,7 +126,9 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
 // qkv row: [Hq*D | Hkv*D | Hkv*D] f32. cs: [max_pos][D/2][2] (cos, sin) f32.
 // neox=0: adjacent pairs (2i, 2i+1) -- GGUF llama "NORM" rope; neox=1: (i, i+D/2).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, long ldqkv,
+// `ks` > 1: the QKV projection left split-K partial slabs (qkv = ks slabs of [T][ldqkv], stride
+// `slab` floats) and this kernel sums them in fixed order while rotating (fused reduce + RoPE).
+__global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, long ldqkv, int ks, long slab,
                                                       const int* __restrict__ pos,
                                                       const int* __restrict__ slot,
                                                       const float* __restrict__ cs,
@@ -135,6 +137,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
                                                       int Hq, int Hkv, int D, int neox) {
   const int t = blockIdx.x;
   const float* row = qkv + (size_t)t * ldqkv;
+  auto ld = [&](int col) {
+    float v = row[col];
+    for (int k = 1; k < ks; ++k) v += row[(size_t)k * slab + col];
+    return v;
+  };
   const int p = pos[t];
   const long s = slot[t];  // int32 slot index, widened
   const int half = D >> 1;
@@ -142,7 +149,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
   for (int idx = threadIdx.x; idx < (Hq + Hkv) * half; idx += blockDim.x) {
     const int h = idx / half, i = idx - h * half;
     const int i0 = neox ? i : 2 * i, i1 = neox ? i + half : 2 * i + 1;
-    const float x0 = row[h * D + i0], x1 = row[h * D + i1];
+    const float x0 = ld(h * D + i0), x1 = ld(h * D + i1);
     const float cc = c[2 * i], ss = c[2 * i + 1];
     const float y0 = x0 * cc - x1 * ss, y1 = x0 * ss + x1 * cc;
     if (h < Hq) {
@@ -155,9 +162,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
     }
   }
   if (s >= 0) {
-    const float* vr = row + (size_t)(Hq + Hkv) * D;
+    const int v0 = (Hq + Hkv) * D;
     __bf16* vd = vc + (size_t)s * Hkv * D;
-    for (int i = threadIdx.x; i < Hkv * D; i += blockDim.x) vd[i] = (__bf16)vr[i];
+    for (int i = threadIdx.x; i < Hkv * D; i += blockDim.x) vd[i] = (__bf16)ld(v0 + i);
   }
 }
 
@@ -308,9 +315,10 @@ int nls_splitk_add_rmsnorm(const float* ws, int ks, int M, float alpha, float* x
   return (int)hipGetLastError();
 }
 
-int nls_rope_kv(const float* qkv, long ldqkv, const int* pos, const int* slot, const float* cs, void* q_out,
-                long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox, void* stream) {
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, pos, slot, cs,
+int nls_rope_kv(const float* qkv, long ldqkv, int ks, long slab, const int* pos, const int* slot, const float* cs,
+                void* q_out, long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox, void* stream) {
+  if (ks < 1) return -1;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, pos, slot, cs,
                      (__bf16*)q_out, ldq, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, D, neox);
   return (int)hipGetLastError();
 }

@@ -282,8 +282,8 @@ class LlamaModel:
         for L, lw in enumerate(self.layers):
             if L > 0 and not fused_prev:
                 ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
-            ops.qgemv(lw.qkv, b.h, b.qkv, T)
-            ops.rope_kv(b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D, cfg.rope_neox)
+            ops.qkv_rope_kv(lw.qkv, b.h, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
+                            cfg.rope_neox)
             if qblocks is not None and nqb > 0 and ops.attention_prefill_ok(Hq, Hkv, D):
                 ops.attention_prefill(b.q, kc[L], vc[L], b.block_tables, qblocks, nqb, b.tok_seq, b.ctx_len, b.ao,
                                       T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)

@@ -312,7 +312,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.
             kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, neox: bool = False):
     """kc/vc: [slots, Hkv, D] bf16 for one layer. slot (int32) < 0 skips the cache write."""
     if qkv.is_cuda:
-        _lib.check(_lib.lib().nls_rope_kv(qkv.data_ptr(), qkv.stride(0), pos.data_ptr(), slot.data_ptr(),
+        _lib.check(_lib.lib().nls_rope_kv(qkv.data_ptr(), qkv.stride(0), 1, 0, pos.data_ptr(), slot.data_ptr(),
                                           cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(),
                                           vc.data_ptr(), T, Hq, Hkv, D, int(neox), _stream_ptr(qkv)), "nls_rope_kv")
         return
@@ -339,6 +339,32 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.
     ok = sl >= 0
     kc[sl[ok]] = k[ok].to(kc.dtype)
     vc[sl[ok]] = v[ok].to(vc.dtype)
+
+
+def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
+                cs: torch.Tensor, q_out: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int,
+                D: int, neox: bool = False, cfg=None):
+    """QKV projection + RoPE + paged KV append. With a split-K launch config the partial slabs
+    are summed inside the RoPE kernel (no separate reduce pass, no fp32 qkv round trip)."""
+    if h.is_cuda and all(s.xmap is None for s in segs):
+        mode, waves, rt, ks = cfg or gemv_config(segs, T)
+        ncol = sum(s.w.rows for s in segs)
+        contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
+        if mode == 1 and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
+            L = _lib.lib()
+            ws = _workspace(h.device, ks * T * ncol)
+            arr = (_lib.NlsSeg * len(segs))()
+            for i, s in enumerate(segs):
+                arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), None, None, None, s.w.type, s.w.rows, s.w.K, s.ycol)
+            st = _stream_ptr(h)
+            _lib.check(L.nls_qgemv(arr, len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
+                                   EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
+            _lib.check(L.nls_rope_kv(ws.data_ptr(), ncol, ks, T * ncol, pos.data_ptr(), slot.data_ptr(),
+                                     cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(), vc.data_ptr(),
+                                     T, Hq, Hkv, D, int(neox), st), "nls_rope_kv")
+            return
+    qgemv(segs, h, qkv, T)
+    rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox)
 
 
 def embed(ids: torch.Tensor, w: QWeight, out: torch.Tensor, T: int, scale: float = 1.0):

@@ -382,3 +382,35 @@ def test_lm_head_argmax_only_epilogue(gpu):
         ref = (x[:M].float().cpu() @ Wd.t()).argmax(1)
         assert (ids[:M].cpu().long() == ref).float().mean() > 0.98
         assert bool((y == 7.0).all())
+
+
+@pytest.mark.parametrize("cfg", [(1, 8, 1, 2), (1, 8, 1, 3), (0, 4, 1, 1)])
+@pytest.mark.parametrize("M", [3, 70])
+def test_qkv_rope_kv_fused(gpu, cfg, M):
+    """QKV projection (3 segments) + RoPE + KV append, split-K slabs summed inside the RoPE kernel."""
+    Hq, Hkv, D, K = 4, 2, 128, 512
+    wq, Wq = _qw(Hq * D, K, GGMLType.Q4_K, gpu, 21)
+    wk, Wk = _qw(Hkv * D, K, GGMLType.Q4_K, gpu, 22)
+    wv, Wv = _qw(Hkv * D, K, GGMLType.Q6_K, gpu, 23)
+    segs = [ops.Seg(wq, 0), ops.Seg(wk, Hq * D), ops.Seg(wv, (Hq + Hkv) * D)]
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    cs = ops.rope_table(512, D, 10000.0, gpu)
+    pos = torch.arange(pad, dtype=torch.int32, device=gpu) * 3
+    slot = torch.arange(pad, dtype=torch.int32, device=gpu)
+    qkv = torch.zeros(pad, (Hq + 2 * Hkv) * D, device=gpu)
+    outs = []
+    for c in (cfg, None):
+        q = torch.zeros(pad, Hq * D, dtype=torch.bfloat16, device=gpu)
+        kc = torch.zeros(pad, Hkv, D, dtype=torch.bfloat16, device=gpu)
+        vc = torch.zeros_like(kc)
+        if c is None:       # reference: plain GEMM then the rope kernel on the CPU path
+            qkv_ref = x[:M].float().cpu() @ torch.cat([Wq, Wk, Wv]).t()
+            qc, kcc, vcc = q.cpu(), kc.cpu(), vc.cpu()
+            ops.rope_kv(qkv_ref, pos.cpu(), slot.cpu(), cs.cpu(), qc, kcc, vcc, M, Hq, Hkv, D)
+            outs.append((qc, kcc, vcc))
+        else:
+            ops.qkv_rope_kv(segs, x, qkv, pos, slot, cs, q, kc, vc, M, Hq, Hkv, D, cfg=c)
+            outs.append((q.cpu(), kc.cpu(), vc.cpu()))
+    for a, b in zip(outs[0], outs[1]):
+        _close(a[:M], b[:M], 3e-2)

@@ -44,10 +44,10 @@ def shapes(spec, base=GGMLType.Q4_K, more=GGMLType.Q6_K):
 def configs(K, M=1):
     nb = K // 256
     if M > 64:   # large-M GEMM (128-row activation blocks), optionally split-K over workgroups
-        c = [(1, 4, 2, 1), (1, 8, 2, 1)]
+        c = [(1, 4, 2, 1)]
         for ks in (1, 2, 4, 8):
             if ks <= max(1, nb // 2):
-                c += [(1, 8, 1, ks), (1, 4, 1, ks)]
+                c += [(1, 8, 1, ks), (1, 4, 1, ks), (1, 8, 2, ks)]
         return c
     c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
     for waves in (4, 8):
