@@ -161,7 +161,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp16",   # f16 activations + f16 MFMA on Q4_K_M weights, fp32 accumulate and residual
             "data": "synthetic prompts, random-init GGUF weights (Q4_K_M mix: Q4_K + Q6_K), no network",
             "config": {
                 "model": f"{args.model} {args.ftype}",

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     const __bf16* __restrict__ q, long ldq, const __bf16* __restrict__ kc, const __bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
     const int* __restrict__ ctx_len, int Hkv, int bs, float scale, int chunk, int n_split,
-    __bf16* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml) {
+    act_t* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml) {
   constexpr int LPT = D / 8;          // lanes per key
   constexpr int TPW = 64 / LPT;       // keys per wave per step
   constexpr int NSTREAM = 4 * TPW;    // independent softmax streams per workgroup
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
     const int qh = kh * G + h;
     if (n_split == 1) {
-      out[(size_t)t * ldo + (size_t)qh * D + d] = (__bf16)(L > 0.f ? O / L : 0.f);
+      out[(size_t)t * ldo + (size_t)qh * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
     } else {
       const size_t pi = ((size_t)t * Hq + qh) * n_split + split;
       part_o[pi * D + d] = O;
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 template <int D>
 __global__ void attn_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
                                     const int* __restrict__ ctx_len, int Hq, int n_split, int chunk, int bs,
-                                    __bf16* __restrict__ out, long ldo) {
+                                    act_t* __restrict__ out, long ldo) {
   const int t = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
   const int ctx = ctx_len[t];
   if (chunk <= 0) {
@@ -200,13 +200,13 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
       O += part_o[(pb + s) * D + d] * f;
     }
   }
-  out[(size_t)t * ldo + (size_t)h * D + d] = (__bf16)(L > 0.f ? O / L : 0.f);
+  out[(size_t)t * ldo + (size_t)h * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
 }
 
 template <int D, int G>
 void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const __bf16* kc, const __bf16* vc,
                  const int* bt, int bts, const int* ts, const int* cl, int Hkv, int bs, float scale, int chunk,
-                 int ns, __bf16* out, long ldo, float* po, float* pml) {
+                 int ns, act_t* out, long ldo, float* po, float* pml) {
   hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, q, ldq, kc, vc, bt, bts, ts, cl, Hkv, bs,
                      scale, chunk, ns, out, ldo, po, pml);
 }
@@ -229,7 +229,7 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
   const __bf16* qq = (const __bf16*)q;
   const __bf16* k = (const __bf16*)kc;
   const __bf16* v = (const __bf16*)vc;
-  __bf16* o = (__bf16*)out;
+  act_t* o = (act_t*)out;
 #define NLS_ATTN_CASE(DD, GG)                                                                                 \
   if (D == DD && G == GG) {                                                                                  \
     launch_attn<DD, GG>(grid, st, qq, ldq, k, v, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
                                                            const __bf16* __restrict__ vc,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ qblocks, int Hkv, int G, int bs,
-                                                           float scale, __bf16* __restrict__ out, long ldo) {
+                                                           float scale, act_t* __restrict__ out, long ldo) {
   constexpr int KT = 64;           // keys per tile
   constexpr int KSTR = D + 8;      // K tile row stride (elements): conflict-free ds_read_b128
   constexpr int VSTR = KT + 8;     // Vt row stride (keys): conflict-free ds_read_b64
@@ -169,9 +169,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
     const float li = __shfl(l, tok, 64);
     if (tok < ntok) {
       const float inv = li > 0.f ? 1.f / li : 0.f;
-      __bf16* orow = out + (size_t)(t0 + tok) * ldo + (size_t)head * D;
+      act_t* orow = out + (size_t)(t0 + tok) * ldo + (size_t)head * D;
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) orow[dt * 16 + r] = (__bf16)(o[dt][i] * inv);
+      for (int dt = 0; dt < NDT; ++dt) orow[dt * 16 + r] = (act_t)(o[dt][i] * inv);
     }
   }
 }
@@ -187,11 +187,11 @@ extern "C" int nls_attn_prefill(const void* q, long ldq, const void* kc, const v
   hipStream_t st = (hipStream_t)stream;
   if (D == 128)
     hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const __bf16*)kc,
-                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (__bf16*)out,
+                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (act_t*)out,
                        ldo);
   else
     hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const __bf16*)kc,
-                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (__bf16*)out,
+                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (act_t*)out,
                        ldo);
   return (int)hipGetLastError();
 }

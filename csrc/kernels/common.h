@@ -4,31 +4,41 @@
 // decode is HBM-bound), re-tiled at load time ("tiled" layout, same bytes):
 //   rows are padded to 16 and grouped into 16-row tiles; for every (tile, 256-value
 //   super-block) the 16 rows' blocks form ONE contiguous "tile-block" of TB bytes,
-//   arranged so that each wave-wide 16-B load instruction of the GEMV reads 1 KiB
-//   contiguous (lane l = 16*g + r -> byte 16*l of a 1 KiB piece). Tile-blocks are
-//   ordered [tile][super-block], so a wave walking K streams sequential memory.
-//     Q4_K  TB=2304: hdr[r] (16) | P0[g][r] (16) | P1[g][r] (16)       (P = qs pieces g, g+4)
-//     Q5_K  TB=2816: hdr[r] | qh[h][r] (16, h=g&1) | P0[g][r] | P1[g][r]
-//     Q6_K  TB=3360: qa[l] | qb[l] | qh[l] (16 each) | sc[r] (16) | d[r] (2)
-//     Q8_0  TB=4352: qs[i][l] (4 x 16) | d[r][8] (f16)
-//     F16/BF16 TB=8192: v[t][l] (8 x 16);  F32 TB=16384: v[t][l] (16 x 16)
+//   arranged so that each wave-wide 16-B load instruction reads 1 KiB contiguous
+//   (lane l = 16*g + r -> byte 16*l of a 1 KiB piece). Tile-blocks are ordered
+//   [tile][super-block], so a wave walking K streams sequential memory.
+//
+// Every format uses the SAME lane -> k map: K-step t (0..7) of lane group g covers
+// k = 32*t + 8*g .. +8 of the super-block (so a K-step is one 32-wide MFMA K slice and
+// each 64-wide quarter of a super-block is spread evenly over all 64 lanes: the LDS-W
+// GEMM dequantises quarter q with every lane busy). Per (g, r) the pieces hold:
+//     Q4_K  TB=2304: hdr[r] (16) | P_h[g][r] (16) h=0,1: qs bytes 8g..8g+7 of chunks 2h, 2h+1
+//     Q5_K  TB=2816: hdr[r] | QH[g][r] (8): qh bytes 8g..8g+7 | P_0 | P_1
+//     Q6_K  TB=3360: QL_n[g][r] (16) n=0,1: ql[64n+8g..+8] | ql[64n+32+8g..+8]
+//                    | QH[g][r] (16): qh[8g..+8] | qh[32+8g..+8] | sc[r] (16) | d[r] (2)
+//     Q8_0  TB=4352: Q_p[g][r] (16) p=0..3: blocks 2p, 2p+1, bytes 8g..8g+7 | d[r][8] (f16)
+//     F16/BF16 TB=8192: v[t][g][r] (16);  F32 TB=16384: v[t][half][g][r] (16)
 // Embedding tables keep a row-major "rows" layout (gathered, not streamed):
 //   Q4_K/Q5_K native blocks; Q6_K planes ql|qh|sc|d; Q8_0 planes qs|d.
 //
-// MFMA operand mapping (v_mfma_f32_16x16x32_bf16): lane l = 16*g + r holds
-// A[row r][k = 8g + j] and B[k = 8g + j][col r], j = 0..7. The contraction order
-// inside K is free, so each format picks, per 256-value super-block, a lane->k
-// assignment where (a) a lane's weight bytes are contiguous 16-B loads and (b)
-// each K-step's 8 values are 8 *consecutive* k (so the activation fragment is one
-// 16-B load). xoff(t, g) below is the first k of K-step t for lane group g.
+// Activations (every GEMM/GEMV input) are f16 (`act_t`) and the matrix cores run
+// v_mfma_f32_16x16x32_f16: lane l = 16*g + r holds A[row r][k = 8g + j] and
+// B[k = 8g + j][col r], j = 0..7. K-quant values are integers < 256, so they are
+// dequantised with the f16 "magic number" trick: v_perm_b32 places byte b under the
+// exponent byte 0x64 -> f16 (1024 + b) exactly, then one packed subtract (exact) and one
+// packed FMA with the sub-block scale (single rounding) give d*sc*q - dmin*m, two values
+// per instruction. The residual stream and all accumulators stay fp32.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 act_t;   // activation dtype of GEMM operands (torch.float16 on the host)
 
 enum QType : int {
   QT_F32 = 0, QT_F16 = 1, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14, QT_BF16 = 30
@@ -44,46 +54,48 @@ DEVI u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
 DEVI u32x4 ld16_nt(const void* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
-
-// ggml get_scale_min_k4 over the 12 packed scale bytes held as 3 dwords.
-// HI selects the j >= 4 branch at compile time (the sub-block index itself may be
-// lane-dependent, the branch never is for the lane->k maps used here).
-DEVI int byte_of(uint32_t s0, uint32_t s1, uint32_t s2, int i) {
-  uint32_t w = i < 4 ? s0 : (i < 8 ? s1 : s2);
-  return (w >> (8 * (i & 3))) & 0xFF;
-}
-template <bool HI>
-DEVI void k4_scale_min_t(int j, uint32_t s0, uint32_t s1, uint32_t s2, int& sc, int& m) {
-  if constexpr (!HI) {
-    sc = byte_of(s0, s1, s2, j) & 63;
-    m = byte_of(s0, s1, s2, j + 4) & 63;
-  } else {
-    const int b4 = byte_of(s0, s1, s2, j + 4);
-    sc = (b4 & 0xF) | ((byte_of(s0, s1, s2, j - 4) >> 6) << 4);
-    m = (b4 >> 4) | ((byte_of(s0, s1, s2, j) >> 6) << 4);
-  }
-}
-DEVI void k4_scale_min(int j, uint32_t s0, uint32_t s1, uint32_t s2, int& sc, int& m) {
-  if (j < 4) k4_scale_min_t<false>(j, s0, s1, s2, sc, m);
-  else k4_scale_min_t<true>(j, s0, s1, s2, sc, m);
+DEVI u32x2 ld8(const void* p) { return *reinterpret_cast<const u32x2*>(p); }
+DEVI u32x2 ld8_nt(const void* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
 }
 
-DEVI bf16x8 pack8(const float* v) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
-  return r;
+DEVI f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// ---- f16 magic-number helpers -------------------------------------------------------
+DEVI f16x2 as_h2(uint32_t u) { return __builtin_bit_cast(f16x2, u); }
+DEVI uint32_t as_u32(f16x2 h) { return __builtin_bit_cast(uint32_t, h); }
+DEVI f16x2 h2(_Float16 v) { return f16x2{v, v}; }
+// bytes 0,1 (mag_lo) / 2,3 (mag_hi) of w -> f16 pair (1024 + b_i), exact for b_i < 1024
+DEVI f16x2 mag_lo(uint32_t w) { return as_h2(__builtin_amdgcn_perm(0x64646464u, w, 0x04010400u)); }
+DEVI f16x2 mag_hi(uint32_t w) { return as_h2(__builtin_amdgcn_perm(0x64646464u, w, 0x04030402u)); }
+
+// 8 small unsigned ints (bytes of n0, n1) -> f16x8 of a*(b - off0) + c.  `off` = 1024 + the
+// format's zero point (exact), then one FMA: a single rounding per value.
+DEVI f16x8 frag8(uint32_t n0, uint32_t n1, f16x2 off, f16x2 a, f16x2 c) {
+  u32x4 u;
+  u[0] = as_u32(__builtin_elementwise_fma(mag_lo(n0) - off, a, c));
+  u[1] = as_u32(__builtin_elementwise_fma(mag_hi(n0) - off, a, c));
+  u[2] = as_u32(__builtin_elementwise_fma(mag_lo(n1) - off, a, c));
+  u[3] = as_u32(__builtin_elementwise_fma(mag_hi(n1) - off, a, c));
+  return __builtin_bit_cast(f16x8, u);
+}
+// 4 bytes -> two f16 pairs (b - off) (exact small integers), e.g. 6-bit scales
+DEVI void bytes_to_h(uint32_t w, f16x2 off, f16x2& lo, f16x2& hi) {
+  lo = mag_lo(w) - off;
+  hi = mag_hi(w) - off;
 }
 
 // ---------------------------------------------------------------------------
-// Per-format raw loads (one super-block of 256 values, one row, one lane group g)
-// and register dequantisation into 8 bf16x8 B-fragments.
+// Per-format raw loads (one super-block of 256 values, one row, one lane group g),
+// per-super-block scale preparation, and per-K-step fragments.
 // ---------------------------------------------------------------------------
 
 struct RawQ4K { u32x4 hdr, p0, p1; };
-struct RawQ5K { u32x4 hdr, p0, p1, qh; };
+struct RawQ5K { u32x4 hdr, p0, p1; u32x2 qh; };
 struct RawQ6K { u32x4 qa, qb, qh; u32x4 sc; uint32_t d; };
-struct RawQ8 { u32x4 q0, q1, q2, q3; uint32_t d; };
+struct RawQ8 { u32x4 q[4]; u32x4 d; };
 struct RawF16 { u32x4 v[8]; };
 struct RawF32 { u32x4 v[16]; };
 
@@ -95,6 +107,18 @@ template <> struct RawOf<QT_Q8_0> { typedef RawQ8 type; };
 template <> struct RawOf<QT_F16> { typedef RawF16 type; };
 template <> struct RawOf<QT_BF16> { typedef RawF16 type; };
 template <> struct RawOf<QT_F32> { typedef RawF32 type; };
+
+// Per-super-block scales of one row, as f16: value = a[s] * q + c[s] for sub-scale s.
+struct ScK { _Float16 a[8], c[8]; };          // Q4_K / Q5_K: s = K-step t (32-value sub-blocks)
+struct ScQ6K { _Float16 a[8]; };               // Q6_K: 16-value sub-blocks, lane-dependent index
+struct ScQ8 { _Float16 a[8]; };                // Q8_0: block t
+struct ScNone { };
+
+template <int T> struct ScOf { typedef ScNone type; };
+template <> struct ScOf<QT_Q4_K> { typedef ScK type; };
+template <> struct ScOf<QT_Q5_K> { typedef ScK type; };
+template <> struct ScOf<QT_Q6_K> { typedef ScQ6K type; };
+template <> struct ScOf<QT_Q8_0> { typedef ScQ8 type; };
 
 // Geometry of a weight matrix on the device.
 struct WDesc {
@@ -118,22 +142,10 @@ DEVI const uint8_t* tile_block(const WDesc& W, int row, int sb) {
   return W.w + ((size_t)(row >> 4) * (W.K >> 8) + sb) * TileBytes<T>::v;
 }
 
-// k offset (within the 256 super-block) of K-step t for lane group g
-template <int T> DEVI int xoff(int t, int g);
-template <> DEVI int xoff<QT_Q4_K>(int t, int g) {
-  int c = (t < 4 ? 0 : 2) + (g >> 1);
-  return 64 * c + 32 * ((t >> 1) & 1) + 16 * (g & 1) + 8 * (t & 1);
-}
-template <> DEVI int xoff<QT_Q5_K>(int t, int g) { return xoff<QT_Q4_K>(t, g); }
-template <> DEVI int xoff<QT_Q6_K>(int t, int g) {
-  return 128 * (g >> 1) + 32 * (t >> 1) + 16 * (g & 1) + 8 * (t & 1);
-}
-template <> DEVI int xoff<QT_Q8_0>(int t, int g) { return 64 * g + 8 * t; }
-template <> DEVI int xoff<QT_F16>(int t, int g) { return 64 * g + 8 * t; }
-template <> DEVI int xoff<QT_BF16>(int t, int g) { return 64 * g + 8 * t; }
-template <> DEVI int xoff<QT_F32>(int t, int g) { return 64 * g + 8 * t; }
+// k offset (within the 256 super-block) of K-step t for lane group g: the same for all formats
+template <int T> DEVI int xoff(int t, int g) { return 32 * t + 8 * g; }
 
-// ---- Q4_K -----------------------------------------------------------------
+// ---- Q4_K / Q5_K ---------------------------------------------------------------
 template <bool NT>
 DEVI RawQ4K load_raw_q4k(const WDesc& W, int row, int sb, int g) {
   const uint8_t* b = tile_block<QT_Q4_K>(W, row, sb);
@@ -144,104 +156,61 @@ DEVI RawQ4K load_raw_q4k(const WDesc& W, int row, int sb, int g) {
   x.p1 = NT ? ld16_nt(b + 1280 + 16 * l) : ld16(b + 1280 + 16 * l);
   return x;
 }
-
-// 16 bytes of nibbles -> 4 K-steps (low 0-7, low 8-15, high 0-7, high 8-15)
-DEVI void nib16_to_frags(u32x4 p, float a_lo, float m_lo, float a_hi, float m_hi, bf16x8* out) {
-  float v[8];
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {        // bytes 0-7 / 8-15
-    uint32_t w0 = p[2 * half], w1 = p[2 * half + 1];
-    uint32_t l0 = w0 & 0x0F0F0F0Fu, l1 = w1 & 0x0F0F0F0Fu;
-    uint32_t h0 = (w0 >> 4) & 0x0F0F0F0Fu, h1 = (w1 >> 4) & 0x0F0F0F0Fu;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[i] = a_lo * (float)((l0 >> (8 * i)) & 0xFF) - m_lo;
-      v[4 + i] = a_lo * (float)((l1 >> (8 * i)) & 0xFF) - m_lo;
-    }
-    out[half] = pack8(v);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[i] = a_hi * (float)((h0 >> (8 * i)) & 0xFF) - m_hi;
-      v[4 + i] = a_hi * (float)((h1 >> (8 * i)) & 0xFF) - m_hi;
-    }
-    out[2 + half] = pack8(v);
-  }
-}
-
-DEVI void deq_q4k(const RawQ4K& r, int g, bf16x8* wf) {
-  const float d = h2f(r.hdr[0] & 0xFFFF), dmin = h2f(r.hdr[0] >> 16);
-  const int c0 = g >> 1;
-  int sc, m;
-  float a[4], mm[4];
-  const int js[4] = {2 * c0, 2 * c0 + 1, 4 + 2 * c0, 5 + 2 * c0};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i < 2) k4_scale_min_t<false>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
-    else k4_scale_min_t<true>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
-    a[i] = d * (float)sc;
-    mm[i] = dmin * (float)m;
-  }
-  nib16_to_frags(r.p0, a[0], mm[0], a[1], mm[1], wf);
-  nib16_to_frags(r.p1, a[2], mm[2], a[3], mm[3], wf + 4);
-}
-
-// ---- Q5_K -----------------------------------------------------------------
 template <bool NT>
 DEVI RawQ5K load_raw_q5k(const WDesc& W, int row, int sb, int g) {
   const uint8_t* b = tile_block<QT_Q5_K>(W, row, sb);
   const int r = row & 15, l = 16 * g + r;
   RawQ5K x;
   x.hdr = NT ? ld16_nt(b + 16 * r) : ld16(b + 16 * r);
-  x.qh = NT ? ld16_nt(b + 256 + 16 * (16 * (g & 1) + r)) : ld16(b + 256 + 16 * (16 * (g & 1) + r));
+  x.qh = NT ? ld8_nt(b + 256 + 8 * l) : ld8(b + 256 + 8 * l);
   x.p0 = NT ? ld16_nt(b + 768 + 16 * l) : ld16(b + 768 + 16 * l);
   x.p1 = NT ? ld16_nt(b + 1792 + 16 * l) : ld16(b + 1792 + 16 * l);
   return x;
 }
 
-DEVI void nib16h_to_frags(u32x4 p, u32x4 qh, int c, float a_lo, float m_lo, float a_hi, float m_hi,
-                          bf16x8* out) {
-  float v[8];
-  const int slo = 2 * c, shi = 2 * c + 1;
+// ggml get_scale_min_k4 for all 8 sub-blocks at once (bytes of 3 dwords), then f16:
+// a[s] = d * sc[s], c[s] = -dmin * m[s]
+DEVI void prep_kquant(const u32x4& hdr, ScK& s) {
+  const uint32_t s0 = hdr[1], s1 = hdr[2], s2 = hdr[3];
+  const uint32_t sc_lo = s0 & 0x3F3F3F3Fu, m_lo = s1 & 0x3F3F3F3Fu;
+  const uint32_t sc_hi = (s2 & 0x0F0F0F0Fu) | ((s0 >> 2) & 0x30303030u);
+  const uint32_t m_hi = ((s2 >> 4) & 0x0F0F0F0Fu) | ((s1 >> 2) & 0x30303030u);
+  const f16x2 d = h2(__builtin_bit_cast(_Float16, (uint16_t)(hdr[0] & 0xFFFF)));
+  const f16x2 nd = -h2(__builtin_bit_cast(_Float16, (uint16_t)(hdr[0] >> 16)));
+  const f16x2 k1024 = h2((_Float16)1024.f);
+  f16x2 v[4];
+  bytes_to_h(sc_lo, k1024, v[0], v[1]);
+  bytes_to_h(sc_hi, k1024, v[2], v[3]);
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    uint32_t w[2] = {p[2 * half], p[2 * half + 1]};
-    uint32_t h[2] = {qh[2 * half], qh[2 * half + 1]};
+  for (int i = 0; i < 4; ++i) {
+    const f16x2 p = v[i] * d;
+    s.a[2 * i] = p[0];
+    s.a[2 * i + 1] = p[1];
+  }
+  bytes_to_h(m_lo, k1024, v[0], v[1]);
+  bytes_to_h(m_hi, k1024, v[2], v[3]);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t byte = (w[q] >> (8 * i)) & 0xFF;
-        uint32_t hb = (h[q] >> (8 * i)) & 0xFF;
-        v[4 * q + i] = a_lo * (float)((byte & 0xF) | (((hb >> slo) & 1) << 4)) - m_lo;
-      }
-    out[half] = pack8(v);
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t byte = (w[q] >> (8 * i)) & 0xFF;
-        uint32_t hb = (h[q] >> (8 * i)) & 0xFF;
-        v[4 * q + i] = a_hi * (float)((byte >> 4) | (((hb >> shi) & 1) << 4)) - m_hi;
-      }
-    out[2 + half] = pack8(v);
+  for (int i = 0; i < 4; ++i) {
+    const f16x2 p = v[i] * nd;
+    s.c[2 * i] = p[0];
+    s.c[2 * i + 1] = p[1];
   }
 }
 
-DEVI void deq_q5k(const RawQ5K& r, int g, bf16x8* wf) {
-  const float d = h2f(r.hdr[0] & 0xFFFF), dmin = h2f(r.hdr[0] >> 16);
-  const int c0 = g >> 1, c1 = 2 + (g >> 1);
-  int sc, m;
-  float a[4], mm[4];
-  const int js[4] = {2 * c0, 2 * c0 + 1, 2 * c1, 2 * c1 + 1};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i < 2) k4_scale_min_t<false>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
-    else k4_scale_min_t<true>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
-    a[i] = d * (float)sc;
-    mm[i] = dmin * (float)m;
-  }
-  nib16h_to_frags(r.p0, r.qh, c0, a[0], mm[0], a[1], mm[1], wf);
-  nib16h_to_frags(r.p1, r.qh, c1, a[2], mm[2], a[3], mm[3], wf + 4);
+// K-step t of Q4_K: chunk c = t >> 1 (in piece h = t >> 2, words 2*((t>>1)&1) +{0,1}), nibble t & 1
+DEVI f16x8 frag_q4k(const RawQ4K& r, const ScK& s, int t) {
+  const u32x4 p = t < 4 ? r.p0 : r.p1;
+  const int wi = 2 * ((t >> 1) & 1), sh = 4 * (t & 1);
+  const uint32_t n0 = (p[wi] >> sh) & 0x0F0F0F0Fu, n1 = (p[wi + 1] >> sh) & 0x0F0F0F0Fu;
+  return frag8(n0, n1, h2((_Float16)1024.f), h2(s.a[t]), h2(s.c[t]));
+}
+// Q5_K: plus the 5th bit = bit t of the lane's 8 qh bytes
+DEVI f16x8 frag_q5k(const RawQ5K& r, const ScK& s, int t) {
+  const u32x4 p = t < 4 ? r.p0 : r.p1;
+  const int wi = 2 * ((t >> 1) & 1), sh = 4 * (t & 1);
+  const uint32_t n0 = ((p[wi] >> sh) & 0x0F0F0F0Fu) | (((r.qh[0] >> t) & 0x01010101u) << 4);
+  const uint32_t n1 = ((p[wi + 1] >> sh) & 0x0F0F0F0Fu) | (((r.qh[1] >> t) & 0x01010101u) << 4);
+  return frag8(n0, n1, h2((_Float16)1024.f), h2(s.a[t]), h2(s.c[t]));
 }
 
 // ---- Q6_K ------------------------------------------------------------------
@@ -257,119 +226,30 @@ DEVI RawQ6K load_raw_q6k(const WDesc& W, int row, int sb, int g) {
   x.d = *reinterpret_cast<const uint16_t*>(b + 3328 + 2 * r);
   return x;
 }
-
-DEVI void deq_q6k(const RawQ6K& r, int g, bf16x8* wf) {
-  const float d = h2f((uint16_t)r.d);
-  const int n = g >> 1, par = g & 1;
-  float a[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    int idx = 8 * n + par + 2 * u;   // scale index
-    int8_t s = (int8_t)((r.sc[idx >> 2] >> (8 * (idx & 3))) & 0xFF);
-    a[u] = d * (float)s;
-  }
-  float v[8];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const u32x4 ql = (u & 1) ? r.qb : r.qa;
-    const int nshift = (u >> 1) ? 4 : 0;     // q1,q2 low nibble; q3,q4 high nibble
-    const int hshift = 2 * u;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {            // bytes 8s .. 8s+7 of the 16-byte range
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        uint32_t wl = ql[2 * s + q], wh = r.qh[2 * s + q];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          int lo = (wl >> (8 * i + nshift)) & 0xF;
-          int hi = (wh >> (8 * i + hshift)) & 3;
-          v[4 * q + i] = a[u] * (float)((lo | (hi << 4)) - 32);
-        }
-      }
-      wf[2 * u + s] = pack8(v);
-    }
-  }
-}
-
-// ---- per-K-step dequant (Q4_K / Q6_K): scales once per super-block, then one 8-value
-// fragment per MFMA K-step, so a tile's 64 bf16 values never sit in registers at once
-// (the large-M GEMM keeps RT weight tiles x MT activation tiles of accumulators live).
-struct ScQ4K { float a[4], m[4]; };
-struct ScQ6K { float a[4]; };
-
-DEVI void prep_q4k(const RawQ4K& r, int g, ScQ4K& s) {
-  const float d = h2f(r.hdr[0] & 0xFFFF), dmin = h2f(r.hdr[0] >> 16);
-  const int c0 = g >> 1;
-  const int js[4] = {2 * c0, 2 * c0 + 1, 4 + 2 * c0, 5 + 2 * c0};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int sc, m;
-    if (i < 2) k4_scale_min_t<false>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
-    else k4_scale_min_t<true>(js[i], r.hdr[1], r.hdr[2], r.hdr[3], sc, m);
-    s.a[i] = d * (float)sc;
-    s.m[i] = dmin * (float)m;
-  }
-}
-
-// fragment t of deq_q4k's output (t = 4*(p1) + 2*(high nibble) + half)
-DEVI bf16x8 frag_q4k(const RawQ4K& r, const ScQ4K& s, int t) {
-  const u32x4 p = t < 4 ? r.p0 : r.p1;
-  const int half = t & 1, hi = (t >> 1) & 1, si = (t < 4 ? 0 : 2) + hi;
-  const uint32_t w0 = p[2 * half], w1 = p[2 * half + 1];
-  const int sh = 4 * hi;
-  float v[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[i] = s.a[si] * (float)((w0 >> (8 * i + sh)) & 0xF) - s.m[si];
-    v[4 + i] = s.a[si] * (float)((w1 >> (8 * i + sh)) & 0xF) - s.m[si];
-  }
-  return pack8(v);
-}
-
+// scale of K-step t for lane group g: int8 sc[2t + (g >> 1)] * d
 DEVI void prep_q6k(const RawQ6K& r, int g, ScQ6K& s) {
-  const float d = h2f((uint16_t)r.d);
-  const int n = g >> 1, par = g & 1;
+  const uint32_t sel = (g >> 1) ? 0x07050301u : 0x06040200u;   // odd / even bytes of two dwords
+  const uint32_t e0 = __builtin_amdgcn_perm(r.sc[1], r.sc[0], sel) ^ 0x80808080u;   // t = 0..3
+  const uint32_t e1 = __builtin_amdgcn_perm(r.sc[3], r.sc[2], sel) ^ 0x80808080u;   // t = 4..7
+  const f16x2 d = h2(__builtin_bit_cast(_Float16, (uint16_t)(r.d & 0xFFFF)));
+  const f16x2 off = h2((_Float16)1152.f);     // 1024 + 128 (int8 via xor 0x80)
+  f16x2 v[4];
+  bytes_to_h(e0, off, v[0], v[1]);
+  bytes_to_h(e1, off, v[2], v[3]);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int idx = 8 * n + par + 2 * u;
-    const int8_t sc = (int8_t)((r.sc[idx >> 2] >> (8 * (idx & 3))) & 0xFF);
-    s.a[u] = d * (float)sc;
+  for (int i = 0; i < 4; ++i) {
+    const f16x2 p = v[i] * d;
+    s.a[2 * i] = p[0];
+    s.a[2 * i + 1] = p[1];
   }
 }
-
-// fragment t of deq_q6k's output (t = 2*u + s)
-DEVI bf16x8 frag_q6k(const RawQ6K& r, const ScQ6K& sc, int t) {
-  const int u = t >> 1, sidx = t & 1;
-  const u32x4 ql = (u & 1) ? r.qb : r.qa;
-  const int nshift = (u >> 1) ? 4 : 0, hshift = 2 * u;
-  float v[8];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t wl = ql[2 * sidx + q], wh = r.qh[2 * sidx + q];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int lo = (wl >> (8 * i + nshift)) & 0xF;
-      const int hi = (wh >> (8 * i + hshift)) & 3;
-      v[4 * q + i] = sc.a[u] * (float)((lo | (hi << 4)) - 32);
-    }
-  }
-  return pack8(v);
-}
-
-template <int T> struct ScOf { typedef int type; };
-template <> struct ScOf<QT_Q4_K> { typedef ScQ4K type; };
-template <> struct ScOf<QT_Q6_K> { typedef ScQ6K type; };
-template <int T> constexpr bool kPerStep = (T == QT_Q4_K || T == QT_Q6_K);
-
-template <int T>
-DEVI void prep_sc(const typename RawOf<T>::type& r, int g, typename ScOf<T>::type& s) {
-  if constexpr (T == QT_Q4_K) prep_q4k(r, g, s);
-  else if constexpr (T == QT_Q6_K) prep_q6k(r, g, s);
-}
-template <int T>
-DEVI bf16x8 frag_t(const typename RawOf<T>::type& r, const typename ScOf<T>::type& s, int t) {
-  if constexpr (T == QT_Q4_K) return frag_q4k(r, s, t);
-  else return frag_q6k(r, s, t);
+// K-step t: n = t >> 2 (ql piece), low/high nibble (t >> 1) & 1, ql run t & 1, qh bits 2*(t & 3)
+DEVI f16x8 frag_q6k(const RawQ6K& r, const ScQ6K& s, int t) {
+  const u32x4 ql = t < 4 ? r.qa : r.qb;
+  const int wi = 2 * (t & 1), sh = 4 * ((t >> 1) & 1), hs = 2 * (t & 3), hw = 2 * (t >> 2);
+  const uint32_t n0 = ((ql[wi] >> sh) & 0x0F0F0F0Fu) | (((r.qh[hw] >> hs) & 0x03030303u) << 4);
+  const uint32_t n1 = ((ql[wi + 1] >> sh) & 0x0F0F0F0Fu) | (((r.qh[hw + 1] >> hs) & 0x03030303u) << 4);
+  return frag8(n0, n1, h2((_Float16)1056.f), h2(s.a[t]), h2((_Float16)0.f));
 }
 
 // ---- Q8_0 ------------------------------------------------------------------
@@ -378,29 +258,24 @@ DEVI RawQ8 load_raw_q8(const WDesc& W, int row, int sb, int g) {
   const uint8_t* b = tile_block<QT_Q8_0>(W, row, sb);
   const int r = row & 15, l = 16 * g + r;
   RawQ8 x;
-  x.q0 = NT ? ld16_nt(b + 16 * l) : ld16(b + 16 * l);
-  x.q1 = NT ? ld16_nt(b + 1024 + 16 * l) : ld16(b + 1024 + 16 * l);
-  x.q2 = NT ? ld16_nt(b + 2048 + 16 * l) : ld16(b + 2048 + 16 * l);
-  x.q3 = NT ? ld16_nt(b + 3072 + 16 * l) : ld16(b + 3072 + 16 * l);
-  x.d = *reinterpret_cast<const uint32_t*>(b + 4096 + 16 * r + 4 * g);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) x.q[p] = NT ? ld16_nt(b + 1024 * p + 16 * l) : ld16(b + 1024 * p + 16 * l);
+  x.d = ld16(b + 4096 + 16 * r);
   return x;
 }
-
-DEVI void deq_q8(const RawQ8& r, int g, bf16x8* wf) {
-  const float d0 = h2f(r.d & 0xFFFF), d1 = h2f(r.d >> 16);
-  const u32x4 q[4] = {r.q0, r.q1, r.q2, r.q3};
-  float v[8];
+DEVI void prep_q8(const RawQ8& r, ScQ8& s) {
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const float d = t < 4 ? d0 : d1;
-    uint32_t w0 = q[t >> 1][2 * (t & 1)], w1 = q[t >> 1][2 * (t & 1) + 1];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[i] = d * (float)(int8_t)((w0 >> (8 * i)) & 0xFF);
-      v[4 + i] = d * (float)(int8_t)((w1 >> (8 * i)) & 0xFF);
-    }
-    wf[t] = pack8(v);
+  for (int i = 0; i < 4; ++i) {
+    const f16x2 d = as_h2(r.d[i]);
+    s.a[2 * i] = d[0];
+    s.a[2 * i + 1] = d[1];
   }
+}
+DEVI f16x8 frag_q8(const RawQ8& r, const ScQ8& s, int t) {
+  const u32x4 p = r.q[t >> 1];
+  const int wi = 2 * (t & 1);
+  return frag8(p[wi] ^ 0x80808080u, p[wi + 1] ^ 0x80808080u, h2((_Float16)1152.f), h2(s.a[t]),
+               h2((_Float16)0.f));
 }
 
 // ---- plain F16 / BF16 / F32 ---------------------------------------------------
@@ -413,22 +288,6 @@ DEVI RawF16 load_raw_f16(const WDesc& W, int row, int sb, int g) {
   for (int t = 0; t < 8; ++t) x.v[t] = NT ? ld16_nt(b + 1024 * t + 16 * l) : ld16(b + 1024 * t + 16 * l);
   return x;
 }
-DEVI void deq_bf16(const RawF16& r, int g, bf16x8* wf) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) wf[t] = __builtin_bit_cast(bf16x8, r.v[t]);
-}
-DEVI void deq_f16(const RawF16& r, int g, bf16x8* wf) {
-  float v[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = h2f(r.v[t][i] & 0xFFFF);
-      v[2 * i + 1] = h2f(r.v[t][i] >> 16);
-    }
-    wf[t] = pack8(v);
-  }
-}
 template <bool NT>
 DEVI RawF32 load_raw_f32(const WDesc& W, int row, int sb, int g) {
   const uint8_t* b = tile_block<QT_F32>(W, row, sb);
@@ -438,20 +297,28 @@ DEVI RawF32 load_raw_f32(const WDesc& W, int row, int sb, int g) {
   for (int t = 0; t < 16; ++t) x.v[t] = NT ? ld16_nt(b + 1024 * t + 16 * l) : ld16(b + 1024 * t + 16 * l);
   return x;
 }
-DEVI void deq_f32(const RawF32& r, int g, bf16x8* wf) {
-  float v[8];
+DEVI f16x8 frag_f16(const RawF16& r, int t) { return __builtin_bit_cast(f16x8, r.v[t]); }
+DEVI f16x8 frag_bf16(const RawF16& r, int t) {
+  f16x8 o;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // NB: copy the vector element out first; __builtin_bit_cast on an ext_vector
-      // element lvalue returns element 0 with hipcc (ROCm 7.2).
-      const uint32_t u0 = r.v[2 * t][i], u1 = r.v[2 * t + 1][i];
-      v[i] = __uint_as_float(u0);
-      v[4 + i] = __uint_as_float(u1);
-    }
-    wf[t] = pack8(v);
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t u = r.v[t][i];
+    o[2 * i] = (_Float16)__uint_as_float(u << 16);
+    o[2 * i + 1] = (_Float16)__uint_as_float(u & 0xFFFF0000u);
   }
+  return o;
+}
+DEVI f16x8 frag_f32(const RawF32& r, int t) {
+  f16x8 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    // NB: copy the vector element out first; __builtin_bit_cast on an ext_vector
+    // element lvalue returns element 0 with hipcc (ROCm 7.2).
+    const uint32_t u0 = r.v[2 * t][i], u1 = r.v[2 * t + 1][i];
+    o[i] = (_Float16)__uint_as_float(u0);
+    o[4 + i] = (_Float16)__uint_as_float(u1);
+  }
+  return o;
 }
 
 // ---- uniform dispatch ---------------------------------------------------------
@@ -465,16 +332,48 @@ DEVI typename RawOf<T>::type load_raw(const WDesc& W, int row, int sb, int g) {
   else return load_raw_f32<NT>(W, row, sb, g);
 }
 
+// scales of one super-block (once), then frag_t(t) per K-step
 template <int T>
-DEVI void dequant(const typename RawOf<T>::type& r, int g, bf16x8* wf) {
-  if constexpr (T == QT_Q4_K) deq_q4k(r, g, wf);
-  else if constexpr (T == QT_Q5_K) deq_q5k(r, g, wf);
-  else if constexpr (T == QT_Q6_K) deq_q6k(r, g, wf);
-  else if constexpr (T == QT_Q8_0) deq_q8(r, g, wf);
-  else if constexpr (T == QT_F16) deq_f16(r, g, wf);
-  else if constexpr (T == QT_BF16) deq_bf16(r, g, wf);
-  else deq_f32(r, g, wf);
+DEVI void prep_sc(const typename RawOf<T>::type& r, int g, typename ScOf<T>::type& s) {
+  if constexpr (T == QT_Q4_K || T == QT_Q5_K) prep_kquant(r.hdr, s);
+  else if constexpr (T == QT_Q6_K) prep_q6k(r, g, s);
+  else if constexpr (T == QT_Q8_0) prep_q8(r, s);
 }
+template <int T>
+DEVI f16x8 frag_t(const typename RawOf<T>::type& r, const typename ScOf<T>::type& s, int t) {
+  if constexpr (T == QT_Q4_K) return frag_q4k(r, s, t);
+  else if constexpr (T == QT_Q5_K) return frag_q5k(r, s, t);
+  else if constexpr (T == QT_Q6_K) return frag_q6k(r, s, t);
+  else if constexpr (T == QT_Q8_0) return frag_q8(r, s, t);
+  else if constexpr (T == QT_F16) return frag_f16(r, t);
+  else if constexpr (T == QT_BF16) return frag_bf16(r, t);
+  else return frag_f32(r, t);
+}
+// all 8 K-step fragments of a super-block
+template <int T>
+DEVI void dequant(const typename RawOf<T>::type& r, int g, f16x8* wf) {
+  typename ScOf<T>::type s;
+  prep_sc<T>(r, g, s);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) wf[t] = frag_t<T>(r, s, t);
+}
+
+// ggml get_scale_min_k4 (scalar; embedding gather only)
+DEVI int byte_of(uint32_t s0, uint32_t s1, uint32_t s2, int i) {
+  uint32_t w = i < 4 ? s0 : (i < 8 ? s1 : s2);
+  return (w >> (8 * (i & 3))) & 0xFF;
+}
+DEVI void k4_scale_min(int j, uint32_t s0, uint32_t s1, uint32_t s2, int& sc, int& m) {
+  if (j < 4) {
+    sc = byte_of(s0, s1, s2, j) & 63;
+    m = byte_of(s0, s1, s2, j + 4) & 63;
+  } else {
+    const int b4 = byte_of(s0, s1, s2, j + 4);
+    sc = (b4 & 0xF) | ((byte_of(s0, s1, s2, j - 4) >> 6) << 4);
+    m = (b4 >> 4) | ((byte_of(s0, s1, s2, j) >> 6) << 4);
+  }
+}
+
 
 // Scalar dequant of element k of a row (embedding gather; not a hot path).
 DEVI float dequant_elem(const WDesc& W, int type, int row, int k) {

@@ -1,6 +1,6 @@
 // Elementwise / normalisation / positional / gather kernels (gfx950), SURVEY.md §2F:
 // embed_gather_q, rmsnorm, rope (+ paged KV append), dequant_* (prefill + tests),
-// logits argmax. All bf16/f32 traffic is 16-B vectorised where rows allow it
+// logits argmax. All f16/bf16/f32 traffic is 16-B vectorised where rows allow it
 // (cdna_hip_programming.md Guideline 13).
 #include "common.h"
 
@@ -26,13 +26,13 @@ DEVI float block_sum(float v, float* sh) {
 }
 
 // ---------------------------------------------------------------------------
-// RMSNorm: out_bf16[m] = x[m] * rsqrt(mean(x^2) + eps) * w      (x f32, fp32 accumulate)
+// RMSNorm: out_f16[m] = x[m] * rsqrt(mean(x^2) + eps) * w      (x f32, fp32 accumulate)
 // Single pass: each of the 512 threads keeps its <= 4 float4 of the row in registers
 // (D <= 8192), so the row is read once and the kernel is one reduction deep.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(512) void rmsnorm_kernel(const float* __restrict__ x, long ldx,
                                                       const float* __restrict__ w,
-                                                      __bf16* __restrict__ out, long ldo, int D,
+                                                      act_t* __restrict__ out, long ldo, int D,
                                                       float eps) {
   __shared__ float sh[8];
   const float* xr = x + (size_t)blockIdx.x * ldx;
@@ -46,27 +46,27 @@ __global__ __launch_bounds__(512) void rmsnorm_kernel(const float* __restrict__ 
   }
   ss = block_sum<512>(ss, sh);
   const float inv = rsqrtf(ss / (float)D + eps);
-  __bf16* o = out + (size_t)blockIdx.x * ldo;
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  act_t* o = out + (size_t)blockIdx.x * ldo;
+  typedef act_t act4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = (threadIdx.x + j * 512) * 4;
     if (i < D) {
       const float4 ww = *reinterpret_cast<const float4*>(w + i);
-      bf16x4 r = {(__bf16)(v[j].x * inv * ww.x), (__bf16)(v[j].y * inv * ww.y), (__bf16)(v[j].z * inv * ww.z),
-                  (__bf16)(v[j].w * inv * ww.w)};
-      *reinterpret_cast<bf16x4*>(o + i) = r;
+      act4 r = {(act_t)(v[j].x * inv * ww.x), (act_t)(v[j].y * inv * ww.y), (act_t)(v[j].z * inv * ww.z),
+                (act_t)(v[j].w * inv * ww.w)};
+      *reinterpret_cast<act4*>(o + i) = r;
     }
   }
 }
 
 // Fused split-K reduce + residual add + RMSNorm (row-parallel projections): the GEMM left
 // ks fp32 partial slabs ws[k][M][D]; x[m] += alpha * sum_k ws[k][m] (fixed order: deterministic),
-// then out[m] = bf16(rmsnorm(x[m]) * w). One launch instead of reduce + norm, and x is read once.
+// then out[m] = f16(rmsnorm(x[m]) * w). One launch instead of reduce + norm, and x is read once.
 __global__ __launch_bounds__(512) void splitk_add_rmsnorm_kernel(const float* __restrict__ ws, int ks, int M,
                                                                  float alpha, float* __restrict__ x, long ldx,
                                                                  const float* __restrict__ w,
-                                                                 __bf16* __restrict__ out, long ldo, int D,
+                                                                 act_t* __restrict__ out, long ldo, int D,
                                                                  float eps) {
   __shared__ float sh[8];
   const int m = blockIdx.x;
@@ -93,16 +93,16 @@ __global__ __launch_bounds__(512) void splitk_add_rmsnorm_kernel(const float* __
   }
   ss = block_sum<512>(ss, sh);
   const float inv = rsqrtf(ss / (float)D + eps);
-  __bf16* o = out + (size_t)m * ldo;
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  act_t* o = out + (size_t)m * ldo;
+  typedef act_t act4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = (threadIdx.x + j * 512) * 4;
     if (i < D) {
       const float4 ww = *reinterpret_cast<const float4*>(w + i);
-      bf16x4 r = {(__bf16)(v[j].x * inv * ww.x), (__bf16)(v[j].y * inv * ww.y), (__bf16)(v[j].z * inv * ww.z),
-                  (__bf16)(v[j].w * inv * ww.w)};
-      *reinterpret_cast<bf16x4*>(o + i) = r;
+      act4 r = {(act_t)(v[j].x * inv * ww.x), (act_t)(v[j].y * inv * ww.y), (act_t)(v[j].z * inv * ww.z),
+                (act_t)(v[j].w * inv * ww.w)};
+      *reinterpret_cast<act4*>(o + i) = r;
     }
   }
 }
@@ -180,11 +180,11 @@ __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids,
 }
 
 // ---------------------------------------------------------------------------
-// Whole-tensor dequant to bf16 (prefill GEMM operand, tests). One wave = 16 rows
+// Whole-tensor dequant to f16 (tests / debugging). One wave = 16 rows
 // x one 256 super-block, using the same register dequant as the GEMV.
 // ---------------------------------------------------------------------------
 template <int T>
-__global__ __launch_bounds__(256) void dequant_kernel(WDesc W, __bf16* __restrict__ out, long ldo) {
+__global__ __launch_bounds__(256) void dequant_kernel(WDesc W, act_t* __restrict__ out, long ldo) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int row = blockIdx.x * 16 + r;
@@ -192,12 +192,12 @@ __global__ __launch_bounds__(256) void dequant_kernel(WDesc W, __bf16* __restric
   if (sb >= (W.K >> 8)) return;
   const int rowc = min(row, W.rows - 1);
   auto raw = load_raw<T, false>(W, rowc, sb, g);
-  bf16x8 wf[8];
+  f16x8 wf[8];
   dequant<T>(raw, g, wf);
   if (row >= W.rows) return;
 #pragma unroll
   for (int t = 0; t < 8; ++t)
-    *reinterpret_cast<bf16x8*>(out + (size_t)row * ldo + sb * 256 + xoff<T>(t, g)) = wf[t];
+    *reinterpret_cast<f16x8*>(out + (size_t)row * ldo + sb * 256 + xoff<T>(t, g)) = wf[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -303,7 +303,7 @@ int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, i
                        (float*)out, ldo, D, eps);
   else
     hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, x, ldx, w,
-                       (__bf16*)out, ldo, D, eps);
+                       (act_t*)out, ldo, D, eps);
   return (int)hipGetLastError();
 }
 
@@ -311,7 +311,7 @@ int nls_splitk_add_rmsnorm(const float* ws, int ks, int M, float alpha, float* x
                            void* out, long ldo, int D, float eps, void* stream) {
   if (D % 4 || D > 8192 || ks < 1) return -1;
   hipLaunchKernelGGL(splitk_add_rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, ws, ks, M, alpha, x, ldx,
-                     w, (__bf16*)out, ldo, D, eps);
+                     w, (act_t*)out, ldo, D, eps);
   return (int)hipGetLastError();
 }
 
@@ -335,7 +335,7 @@ int nls_dequant(const void* w, int type, int rows, int K, void* out, long ldo, v
   WDesc W{(const uint8_t*)w, rows, K};
   dim3 grid((rows + 15) / 16, ((K >> 8) + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
-  __bf16* o = (__bf16*)out;
+  act_t* o = (act_t*)out;
   switch (type) {
     case QT_Q4_K: hipLaunchKernelGGL(dequant_kernel<QT_Q4_K>, grid, dim3(256), 0, st, W, o, ldo); break;
     case QT_Q5_K: hipLaunchKernelGGL(dequant_kernel<QT_Q5_K>, grid, dim3(256), 0, st, W, o, ldo); break;

@@ -31,7 +31,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   const int tile_rows = (mode == 1 ? waves : 1) * rt * 16;
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
-    if (epi == EPI_SWIGLU_BF16 && segs[i].rows % 16) return -1;
+    if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
     if (mode == 1 && segs[i].xmap) return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;
@@ -58,7 +58,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   }
   if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
   const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
-  GemvArgs a{(const __bf16*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax, 0, M};
+  GemvArgs a{(const act_t*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax, 0, M};
   const int mt = M > 64 ? 8 : (M + 15) / 16;
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
@@ -70,7 +70,7 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
     RedList rl{};
     for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};
     rl.nseg = nseg;
-    const int nout = epi == EPI_SWIGLU_BF16 ? cols / 2 : cols;
+    const int nout = epi == EPI_SWIGLU ? cols / 2 : cols;
     dim3 grid((nout + 255) / 256, M);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, ks, M, cols, rl, a);
     return (int)hipGetLastError();

@@ -4,8 +4,8 @@
 //
 // Design (SURVEY.md §2F "gemv_q*"): decode is HBM-bound on the weight stream,
 // so every weight byte is read exactly once, straight into VGPRs (no LDS round
-// trip, non-temporal loads), dequantised in registers to bf16 and fed to
-// v_mfma_f32_16x16x32_bf16 as the B operand (16 weight rows per tile). The
+// trip, non-temporal loads), dequantised in registers to f16 (magic-number dequant,
+// common.h) and fed to v_mfma_f32_16x16x32_f16 as the B operand (16 weight rows per tile). The
 // activation rows (batch, padded to 16) are the A operand, so batch 1..16 costs
 // the same MFMA issue as batch 1 and the weight dequant is amortised over the
 // whole batch. A workgroup owns RT*16 output rows; its WAVES waves split K and
@@ -23,7 +23,7 @@ namespace nls_gemv {
 
 // EPI_SLABS: split-K partial slabs only (the caller fuses the reduce, e.g. with RMSNorm);
 // EPI_ARGMAX: fused arg-max keys only, no logits stored (greedy decode)
-enum Epi : int { EPI_F32 = 0, EPI_BF16 = 1, EPI_ADD_F32 = 2, EPI_SWIGLU_BF16 = 3, EPI_SLABS = 4, EPI_ARGMAX = 5 };
+enum Epi : int { EPI_F32 = 0, EPI_ACT = 1, EPI_ADD_F32 = 2, EPI_SWIGLU = 3, EPI_SLABS = 4, EPI_ARGMAX = 5 };
 
 struct Seg {
   const uint8_t* w;
@@ -35,7 +35,7 @@ struct Seg {
 struct SegList { Seg s[8]; int nseg; int pad[3]; };
 
 struct GemvArgs {
-  const __bf16* x; long ldx;
+  const act_t* x; long ldx;
   void* y; long ldy;
   int M;               // rows of x / y (or max rows per segment when mapped)
   int epi;
@@ -69,7 +69,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   // valid row (row 0: broadcast, cache-resident) and are zeroed with a select after the load:
   // a lane-conditional load would compile to a branch + vmcnt(0) per K-step that drains the
   // whole weight prefetch (cdna_hip_programming.md §5 "Three .s-level traps" (c)).
-  const __bf16* xr[MT];
+  const act_t* xr[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
@@ -104,17 +104,17 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   }
   auto step = [&](Raw (&w)[RT], int sb) {
     // 1) activation fragments of this super-block (issued before this step's weight reload)
-    bf16x8 xa[8][MT];
+    f16x8 xa[8][MT];
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        xa[t][mt] = *reinterpret_cast<const bf16x8*>(xr[mt] + sb * 256 + xoff<T>(t, g));
+        xa[t][mt] = *reinterpret_cast<const f16x8*>(xr[mt] + sb * 256 + xoff<T>(t, g));
     // the scheduler must not sink these loads below the weight reload (the in-order vmcnt
     // wait for a late x load would then also wait for the reload)
     __builtin_amdgcn_sched_barrier(0);
     // 2) dequant (waits only for this buffer's loads, issued two steps ago)
-    bf16x8 wf[RT][8];
+    f16x8 wf[RT][8];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
     __builtin_amdgcn_sched_barrier(0);
@@ -127,10 +127,10 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     for (int t = 0; t < 8; ++t) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 x8 = xa[t][mt];   // rows >= mcount only reach output rows that are never stored
+        const f16x8 x8 = xa[t][mt];   // rows >= mcount only reach output rows that are never stored
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
-          acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x8, wf[rt][t], acc[rt][mt], 0, 0, 0);
+          acc[rt][mt] = mfma16(x8, wf[rt][t], acc[rt][mt]);
       }
     }
   };
@@ -167,7 +167,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 
   // ---- epilogue ----------------------------------------------------------------
   const int ncols = MT * 16;
-  if (a.epi == EPI_SWIGLU_BF16) {
+  if (a.epi == EPI_SWIGLU) {
     // tile rows [16i, 16i+8) = gate, [16i+8, 16i+16) = up of outputs (row0/2 + 8i + j)
     for (int e = threadIdx.x; e < RT * 8 * ncols; e += WAVES * 64) {
       const int bb = e % ncols, j = e / ncols, rt = j >> 3, jj = j & 7;
@@ -178,7 +178,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
       const float uv = tile[(rt * 16 + 8 + jj) * ncols + bb];
       const int yrow = S.ymap ? S.ymap[bb] : bb;
       const int n = S.ycol + (row0 >> 1) + rt * 8 + jj;
-      reinterpret_cast<__bf16*>(a.y)[(size_t)yrow * a.ldy + n] = (__bf16)(silu(gv) * uv);
+      reinterpret_cast<act_t*>(a.y)[(size_t)yrow * a.ldy + n] = (act_t)(silu(gv) * uv);
     }
     return;
   }
@@ -191,7 +191,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     const size_t off = (size_t)yrow * a.ldy + S.ycol + row;
     if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
     else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else if (a.epi == EPI_BF16) reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+    else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
   }
   if (a.argmax) {
     for (int bb = threadIdx.x; bb < min(mcount, ncols); bb += WAVES * 64) {
@@ -245,19 +245,19 @@ __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArg
 
 // ===========================================================================
 // Path B (batch >= ~16): waves split ROWS, not K. The activation tile of the current
-// 256-wide super-block (M x 256 bf16, XOR-swizzled 16-B chunks) is staged once per
+// 256-wide super-block (M x 256 f16, XOR-swizzled 16-B chunks) is staged once per
 // workgroup in LDS (double-buffered) and read by every wave with ds_read_b128, so x is
 // fetched from L2 once per WAVES*RT*16 weight rows instead of once per 16. Optional
 // split-K over workgroups (KS > 1) writes fp32 partial slabs; splitk_reduce applies
 // the epilogue in a fixed order (deterministic, no float atomics).
 // ===========================================================================
-DEVI int lds_off(int row, int k) {            // element offset in a [rows][256] bf16 tile
+DEVI int lds_off(int row, int k) {            // element offset in a [rows][256] f16 tile
   const int ch = (k >> 3) ^ (row & 15);
   return row * 256 + ch * 8 + (k & 7);
 }
 
 template <int T, int WAVES, int RT, int MT>
-DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, __bf16* lds) {
+DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -274,7 +274,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   constexpr int NCH = (MT * 16 * 32) / NT;               // 16-B chunks staged per thread
   static_assert((MT * 16 * 32) % NT == 0, "staging must divide evenly");
   // large tiles stage x in two halves (half the staging registers)
-  constexpr bool SPLITX = kPerStep<T> && MT >= 4 && NCH % 2 == 0;
+  constexpr bool SPLITX = MT >= 4 && NCH % 2 == 0;
   constexpr int NCHR = SPLITX ? NCH / 2 : NCH;
   u32x4 xst[NCHR];
   auto load_xh = [&](int sb, int h) {
@@ -327,8 +327,8 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     const int nxt = min(sb + 1, sbl);  // unconditional (clamped): see path A
     load_xh(nxt, 0);
     __builtin_amdgcn_sched_barrier(0);
-    const __bf16* xb = lds + buf * (MT * 16 * 256);
-    if constexpr (kPerStep<T> && MT >= 4) {
+    const act_t* xb = lds + buf * (MT * 16 * 256);
+    if constexpr (MT >= 4) {
       // large tiles: per-K-step fragments (scales once per super-block), weight buffer reloaded
       // after its last use; x half 0 written after K-steps 0-3, half 1 loaded then, written last
       typename ScOf<T>::type sc[RT];
@@ -340,16 +340,16 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           store_xh(buf ^ 1, 0);
           load_xh(nxt, 1);
         }
-        bf16x8 wt[RT];
+        f16x8 wt[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) wt[rt] = frag_t<T>(w[rt], sc[rt], t);
         const int ko = xoff<T>(t, g);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
+          const f16x8 xa = *reinterpret_cast<const f16x8*>(xb + lds_off(mt * 16 + r, ko));
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
-            acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wt[rt], acc[rt][mt], 0, 0, 0);
+            acc[rt][mt] = mfma16(xa, wt[rt], acc[rt][mt]);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -357,7 +357,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
       store_xh(buf ^ 1, SPLITX ? 1 : 0);
     } else {
-      bf16x8 wf[RT][8];
+      f16x8 wf[RT][8];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
       __builtin_amdgcn_sched_barrier(0);
@@ -369,10 +369,10 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
         const int ko = xoff<T>(t, g);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 xa = *reinterpret_cast<const bf16x8*>(xb + lds_off(mt * 16 + r, ko));
+          const f16x8 xa = *reinterpret_cast<const f16x8*>(xb + lds_off(mt * 16 + r, ko));
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
-            acc[rt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[rt][t], acc[rt][mt], 0, 0, 0);
+            acc[rt][mt] = mfma16(xa, wf[rt][t], acc[rt][mt]);
         }
       }
       store_xh(buf ^ 1, 0);
@@ -413,11 +413,11 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       for (int i = 0; i < 4; ++i) {
         const int b = mt * 16 + 4 * g + i;
         const float v = acc[rt][mt][i] * a.alpha;
-        if (a.epi == EPI_SWIGLU_BF16) {
+        if (a.epi == EPI_SWIGLU) {
           const float u = __shfl_xor(v, 8, 64);
           if (r < 8 && b < M && row < S.rows) {
             const int n = S.ycol + ((base + rt * 16) >> 1) + r;
-            reinterpret_cast<__bf16*>(a.y)[(size_t)b * a.ldy + n] = (__bf16)(silu(v) * u);
+            reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
           }
           continue;
         }
@@ -425,7 +425,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           const size_t off = (size_t)b * a.ldy + S.ycol + row;
           if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
           else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-          else if (a.epi == EPI_BF16) reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+          else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
         }
         if (a.argmax) {
           unsigned long long k = (row < S.rows) ? argmax_key(v, S.ycol + row) : 0ull;
@@ -444,7 +444,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 template <int WAVES, int RT, int MT, int KSET>
 __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                          int nmb) {
-  extern __shared__ __attribute__((aligned(16))) __bf16 xlds[];
+  extern __shared__ __attribute__((aligned(16))) act_t xlds[];
   int tile, kslice = 0;
   if (nmb > 1) {
     // Large M (prefill / big decode batches): blocks of MT*16 activation rows. The workgroups
@@ -502,7 +502,7 @@ struct RedList { RedSeg s[8]; int nseg, pad[3]; };
 static __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks, int M, int ntot, RedList rl,
                                      GemvArgs a) {
   const int b = blockIdx.y;
-  const bool swiglu = a.epi == EPI_SWIGLU_BF16;
+  const bool swiglu = a.epi == EPI_SWIGLU;
   const int nout = swiglu ? ntot / 2 : ntot;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nout; j += gridDim.x * blockDim.x) {
     int col = swiglu ? (j >> 3) * 16 + (j & 7) : j;
@@ -519,13 +519,13 @@ static __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks
     const int row = col - S.col0;
     if (swiglu) {
       const int n = S.ycol + (row >> 4) * 8 + (row & 7);
-      reinterpret_cast<__bf16*>(a.y)[(size_t)b * a.ldy + n] = (__bf16)(silu(v) * u);
+      reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
       continue;
     }
     const size_t off = (size_t)b * a.ldy + S.ycol + row;
     if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
     else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else if (a.epi == EPI_BF16) reinterpret_cast<__bf16*>(a.y)[off] = (__bf16)v;
+    else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
     if (a.argmax) atomicMax(a.argmax + b, argmax_key(v, S.ycol + row));
   }
 }
@@ -552,7 +552,7 @@ int launch_mt(int mt, const SegList& sl, int nt, const GemvArgs& a, hipStream_t 
 
 template <int WAVES, int RT, int MT, int KSET>
 int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st, int nmb) {
-  const size_t lds = (size_t)2 * MT * 16 * 256 * sizeof(__bf16);
+  const size_t lds = (size_t)2 * MT * 16 * 256 * sizeof(act_t);
   const int grid = nmb > 1 ? ((ntiles + 7) / 8) * 8 * nmb * ks : ntiles * ks;
   hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, KSET>), dim3(grid), dim3(WAVES * 64), lds, st, sl, a, ks, ws,
                      ntiles, nmb);

@@ -221,18 +221,19 @@ class LlamaModel:
         k = max(1, cfg.n_expert_used)
         meta = torch.zeros(6 * pad + max_seqs * max_blocks, dtype=torch.int32, device=dev)
         f = dict(dtype=torch.float32, device=dev)
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)     # q (attention operand, like the KV cache)
+        act = dict(dtype=ops.ACT_DTYPE, device=dev)     # GEMM inputs: h, attention output, SwiGLU output
         b = StepBuffers(
             cap=cap,
             ids=meta[0:pad], pos=meta[pad:2 * pad], slot=meta[2 * pad:3 * pad],
             tok_seq=meta[3 * pad:4 * pad], ctx_len=meta[4 * pad:5 * pad], use_prev=meta[5 * pad:6 * pad],
             block_tables=meta[6 * pad:].view(max_seqs, max_blocks),
             x=torch.zeros(pad, cfg.d_model, **f),
-            h=torch.zeros(pad, cfg.d_model, **bf),
+            h=torch.zeros(pad, cfg.d_model, **act),
             qkv=torch.zeros(pad, (self.Hq + 2 * self.Hkv) * self.D, **f),
             q=torch.zeros(pad, nq, **bf),
-            ao=torch.zeros(pad, nq, **bf),
-            act=torch.zeros(pad * (k if cfg.n_expert else 1), self.exp_ffn if cfg.n_expert else self.ffn, **bf),
+            ao=torch.zeros(pad, nq, **act),
+            act=torch.zeros(pad * (k if cfg.n_expert else 1), self.exp_ffn if cfg.n_expert else self.ffn, **act),
             logits=torch.zeros(min(pad, max(64, max_seqs)), Vs, **f),
             keys=torch.zeros(pad, dtype=torch.int64, device=dev),
             next_ids=torch.zeros(pad, dtype=torch.int32, device=dev),

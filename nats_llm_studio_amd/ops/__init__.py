@@ -19,7 +19,8 @@ from ..gguf.constants import GGMLType, GGML_BLOCK
 from ..gguf.quants import dequantize
 from . import _lib
 
-EPI = {"f32": 0, "bf16": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5}
+EPI = {"f32": 0, "act": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5}
+ACT_DTYPE = torch.float16   # activation dtype of every GEMM/GEMV input and SwiGLU/RMSNorm/attention output
 
 
 def _stream_ptr(t: torch.Tensor) -> int:
@@ -69,29 +70,28 @@ def tile_layout(raw: torch.Tensor, ggml_type: int, rows: int, K: int) -> torch.T
         q0 = 16 if t == GGMLType.Q4_K else 48
         B = b.reshape(T, 16, nb, bs)
         parts = [B[..., 0:16].permute(0, 2, 1, 3).reshape(T, nb, 256)]
-        if t == GGMLType.Q5_K:
-            parts.append(B[..., 16:48].reshape(T, 16, nb, 2, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 512))
-        qs = B[..., q0:q0 + 128].reshape(T, 16, nb, 8, 16)
-        parts.append(qs[:, :, :, 0:4].permute(0, 2, 3, 1, 4).reshape(T, nb, 1024))
-        parts.append(qs[:, :, :, 4:8].permute(0, 2, 3, 1, 4).reshape(T, nb, 1024))
+        if t == GGMLType.Q5_K:        # QH[g][r][8]: qh bytes 8g..8g+7
+            parts.append(B[..., 16:48].reshape(T, 16, nb, 4, 8).permute(0, 2, 3, 1, 4).reshape(T, nb, 512))
+        # P_h[g][r] = chunk 2h bytes 8g..+8 | chunk 2h+1 bytes 8g..+8   (qs byte = 32c + 8g + i)
+        qs = B[..., q0:q0 + 128].reshape(T, 16, nb, 2, 2, 4, 8)
+        parts.append(qs.permute(0, 2, 3, 5, 1, 4, 6).reshape(T, nb, 2048))
     elif t == GGMLType.Q6_K:
         B = b.reshape(T, 16, nb, 210)
-        ql = B[..., 0:128].reshape(T, 16, nb, 2, 4, 16)
-        qa = ql[:, :, :, :, 0:2].reshape(T, 16, nb, 4, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 1024)
-        qb = ql[:, :, :, :, 2:4].reshape(T, 16, nb, 4, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 1024)
-        qh = B[..., 128:192].reshape(T, 16, nb, 4, 16).permute(0, 2, 3, 1, 4).reshape(T, nb, 1024)
-        sc = B[..., 192:208].permute(0, 2, 1, 3).reshape(T, nb, 256)
-        d = B[..., 208:210].permute(0, 2, 1, 3).reshape(T, nb, 32)
-        parts = [qa, qb, qh, sc, d]
+        ql = B[..., 0:128].reshape(T, 16, nb, 2, 2, 4, 8)          # ql byte = 64n + 32run + 8g + i
+        qh = B[..., 128:192].reshape(T, 16, nb, 2, 4, 8)           # qh byte = 32n + 8g + i
+        parts = [ql.permute(0, 2, 3, 5, 1, 4, 6).reshape(T, nb, 2048),     # QL_n[g][r][run][8]
+                 qh.permute(0, 2, 4, 1, 3, 5).reshape(T, nb, 1024),        # QH[g][r][n][8]
+                 B[..., 192:208].permute(0, 2, 1, 3).reshape(T, nb, 256),
+                 B[..., 208:210].permute(0, 2, 1, 3).reshape(T, nb, 32)]
     elif t == GGMLType.Q8_0:
         B = b.reshape(T, 16, nb, 8, 34)
         d = B[..., 0:2].permute(0, 2, 1, 3, 4).reshape(T, nb, 256)
-        qs = B[..., 2:34].reshape(T, 16, nb, 4, 4, 16).permute(0, 2, 4, 3, 1, 5).reshape(T, nb, 4096)
-        parts = [qs, d]
+        qs = B[..., 2:34].reshape(T, 16, nb, 4, 2, 4, 8)           # block 2p + bb, byte 8g + i
+        parts = [qs.permute(0, 2, 3, 5, 1, 4, 6).reshape(T, nb, 4096), d]
     elif t in (GGMLType.F16, GGMLType.BF16):
-        parts = [b.reshape(T, 16, nb, 4, 8, 16).permute(0, 2, 4, 3, 1, 5).reshape(T, nb, 8192)]
+        parts = [b.reshape(T, 16, nb, 8, 4, 16).permute(0, 2, 3, 4, 1, 5).reshape(T, nb, 8192)]
     elif t == GGMLType.F32:
-        parts = [b.reshape(T, 16, nb, 4, 16, 16).permute(0, 2, 4, 3, 1, 5).reshape(T, nb, 16384)]
+        parts = [b.reshape(T, 16, nb, 8, 4, 2, 16).permute(0, 2, 3, 5, 4, 1, 6).reshape(T, nb, 16384)]
     else:
         raise NotImplementedError(f"tiled layout for {t.name}")
     out = torch.cat(parts, dim=2) if len(parts) > 1 else parts[0]
@@ -136,12 +136,12 @@ class QWeight:
         return self.data.numel()
 
     def dense(self, dtype=torch.float32) -> torch.Tensor:
-        """Dequantised [rows, K] (CPU: numpy ggml codec; GPU: HIP dequant kernel, bf16)."""
+        """Dequantised [rows, K] (CPU: numpy ggml codec; GPU: HIP dequant kernel, f16)."""
         if self.device.type == "cpu":
             if self._dense is None:
                 self._dense = torch.from_numpy(dequantize(self._raw, self.type, (self.rows, self.K)).copy())
             return self._dense.to(dtype)
-        out = torch.empty(self.rows, self.K, dtype=torch.bfloat16, device=self.device)
+        out = torch.empty(self.rows, self.K, dtype=ACT_DTYPE, device=self.device)
         _lib.check(_lib.lib().nls_dequant(self.data.data_ptr(), self.type, self.rows, self.K, out.data_ptr(),
                                           self.K, _stream_ptr(out)), "nls_dequant")
         return out.to(dtype)
@@ -189,8 +189,10 @@ def gemv_config(segs: Sequence[Seg], M: int):
 
 def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
           argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1):
-    """y (epilogue) alpha * x[:M] @ W^T for each segment. x: bf16 [>=pad16(M), K]."""
+    """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K]."""
     if x.is_cuda:
+        if x.dtype != ACT_DTYPE:
+            raise TypeError(f"qgemv: activations must be {ACT_DTYPE}, got {x.dtype}")
         L = _lib.lib()
         mapped = any(s.xmap is not None for s in segs)
         if mode < 0 or waves == 0:
@@ -248,7 +250,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
 
 def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torch.Tensor, h: torch.Tensor, M: int,
                       alpha: float, eps: float, cfg=None):
-    """x[:M] += alpha * xin @ W^T, then h[:M] = rmsnorm(x[:M]) * norm_w (bf16). With a split-K
+    """x[:M] += alpha * xin @ W^T, then h[:M] = rmsnorm(x[:M]) * norm_w (f16). With a split-K
     launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel."""
     if x.is_cuda and seg.xmap is None:
         mode, waves, rt, ks = cfg or gemv_config([seg], M)

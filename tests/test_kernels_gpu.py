@@ -24,8 +24,8 @@ def _qw(rows, K, t, dev, seed=0):
 def _x(M, K, dev, seed=1):
     g = torch.Generator().manual_seed(seed)
     pad = (M + 63) // 64 * 64
-    x = torch.zeros(pad, K, dtype=torch.bfloat16)
-    x[:M] = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    x = torch.zeros(pad, K, dtype=ops.ACT_DTYPE)
+    x[:M] = torch.randn(M, K, generator=g).to(ops.ACT_DTYPE)
     return x.to(dev)
 
 
@@ -53,10 +53,12 @@ def test_qgemv_types(gpu, t, M, cfg):
 
 
 def test_dequant_kernel_exact(gpu):
+    """Register dequant (f16 magic-number path) vs the numpy ggml codec: f16 rounding only
+    (one rounding of d*sc*q - dmin*m; cancellation bounded by the row scale)."""
     for t in TYPES:
         w, Wd = _qw(48, 512, t, gpu, seed=3)
         d = w.dense().float().cpu()
-        torch.testing.assert_close(d, Wd.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-6)
+        torch.testing.assert_close(d, Wd, rtol=2e-3, atol=2e-3 * Wd.abs().max().item())
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -97,7 +99,7 @@ def test_qgemv_swiglu(gpu, cfg):
     U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
     for M in (1, 20):
         x = _x(M, K, gpu)
-        y = torch.zeros(64, F, dtype=torch.bfloat16, device=gpu)
+        y = torch.zeros(64, F, dtype=ops.ACT_DTYPE, device=gpu)
         ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=mode, waves=waves, rt=rt, ks=ks)
         xf = x[:M].float().cpu()
         ref = torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t())
@@ -125,7 +127,7 @@ def test_qgemv_mapped_rows(gpu):
 def test_rmsnorm_embed(gpu):
     x = torch.randn(5, 1024, device=gpu)
     w = torch.randn(1024, device=gpu)
-    out = torch.zeros(64, 1024, dtype=torch.bfloat16, device=gpu)
+    out = torch.zeros(64, 1024, dtype=ops.ACT_DTYPE, device=gpu)
     ops.rmsnorm(x, w, out, 5, 1e-5)
     ref = x * torch.rsqrt(x.pow(2).mean(1, keepdim=True) + 1e-5) * w
     _close(out[:5], ref, 1e-2)
@@ -175,9 +177,9 @@ def test_attention_paged(gpu, D, G, n_split, chunk):
     q = torch.randn(T, Hq * D, generator=g).to(torch.bfloat16)
     ts = torch.arange(T, dtype=torch.int32)
     cl = torch.tensor(ctx, dtype=torch.int32)
-    ref = torch.zeros(T, Hq * D, dtype=torch.bfloat16)
+    ref = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE)
     ops.attention(q, kc, vc, bt, ts, cl, ref, T, Hq, Hkv, D, bs, D ** -0.5)
-    out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=gpu)
+    out = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE, device=gpu)
     ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), ts.to(gpu), cl.to(gpu), out, T, Hq, Hkv, D, bs,
                   D ** -0.5, chunk=chunk, n_split=n_split)
     torch.testing.assert_close(out.cpu().float(), ref.float(), rtol=2e-2, atol=2e-2)
@@ -273,7 +275,7 @@ def test_qgemm_large_m_swiglu(gpu):
     U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
     M = 333
     x = _x(M, K, gpu)
-    y = torch.zeros(x.shape[0], F, dtype=torch.bfloat16, device=gpu)
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
     ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=1, waves=8, rt=1, ks=1)
     xf = x[:M].float().cpu()
     y3 = torch.zeros_like(y)
@@ -305,10 +307,10 @@ def test_attention_prefill_paged(gpu, D, G):
     tseq = np.array(tseq, np.int32)
     q = (torch.randn(T, Hq * D)).to(torch.bfloat16)
     ctx = torch.from_numpy(pos + 1)
-    ref = torch.zeros(T, Hq * D, dtype=torch.bfloat16)
+    ref = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE)
     ops.attention(q, kc, vc, perm, torch.from_numpy(tseq), ctx, ref, T, Hq, Hkv, D, bs, D ** -0.5)
     qb = ops.prefill_blocks(tseq, pos, T)
-    out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=gpu)
+    out = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE, device=gpu)
     ops.attention_prefill(q.to(gpu), kc.to(gpu), vc.to(gpu), perm.to(gpu), torch.from_numpy(qb).to(gpu), len(qb),
                           None, None, out, T, Hq, Hkv, D, bs, D ** -0.5)
     _close(out.cpu(), ref, 2e-2)
@@ -359,7 +361,7 @@ def test_qgemv_add_rmsnorm_fused(gpu, M, cfg):
     base = torch.randn(pad, D, device=gpu)
     x = base.clone()
     nw = (1 + 0.1 * torch.randn(D)).to(gpu)
-    h = torch.zeros(pad, D, dtype=torch.bfloat16, device=gpu)
+    h = torch.zeros(pad, D, dtype=ops.ACT_DTYPE, device=gpu)
     ops.qgemv_add_rmsnorm(ops.Seg(w), xin, x, nw, h, M, 0.7, 1e-5, cfg=cfg)
     xr = base[:M].cpu() + 0.7 * (xin[:M].float().cpu() @ Wd.t())
     _close(x[:M], xr)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-step breakdown of a rocprofv3 kernel trace of bench.py: decode steps are delimited by the
 argmax_unpack kernel that ends every forward; reports GPU busy vs wall per step and the kernel
-mix of the last N decode steps.  usage: analyze_trace.py run_kernel_trace.csv [--last 20]"""
+mix of the last N decode steps.  usage: analyze_trace.py run_kernel_trace.csv|run_results.db [--last 20]"""
 import csv
 import re
 import sys
@@ -14,10 +14,20 @@ def short(name):
     return name.strip()[:90]
 
 
+def load_rows(path):
+    """kernel_trace.csv (--output-format csv) or the rocpd sqlite .db (ROCm 7.2 default)."""
+    if path.endswith(".db"):
+        import sqlite3
+        c = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in c.execute("select name, start, end from kernels")]
+    return list(csv.DictReader(open(path)))
+
+
 def main():
     path = sys.argv[1]
     last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 20
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = sorted(load_rows(path), key=lambda r: int(r["Start_Timestamp"]))
     steps, cur = [], []
     for r in rows:
         cur.append(r)

@@ -113,8 +113,8 @@ def main():
             col += rows
         ncol = col // 2 if epi == "swiglu" else col
         mmax = max(64, max(Ms))
-        x = torch.randn(mmax, K, device=dev).to(torch.bfloat16)
-        y = torch.zeros(mmax, ncol, dtype=torch.bfloat16 if epi == "swiglu" else torch.float32, device=dev)
+        x = torch.randn(mmax, K, device=dev).to(ops.ACT_DTYPE)
+        y = torch.zeros(mmax, ncol, dtype=ops.ACT_DTYPE if epi == "swiglu" else torch.float32, device=dev)
         keys = torch.zeros(mmax, dtype=torch.int64, device=dev)
         for M in Ms:
             res = []
