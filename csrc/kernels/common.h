@@ -108,11 +108,17 @@ template <> struct RawOf<QT_F16> { typedef RawF16 type; };
 template <> struct RawOf<QT_BF16> { typedef RawF16 type; };
 template <> struct RawOf<QT_F32> { typedef RawF32 type; };
 
-// Per-super-block scales of one row, as f16: value = a[s] * q + c[s] for sub-scale s.
-struct ScK { _Float16 a[8], c[8]; };          // Q4_K / Q5_K: s = K-step t (32-value sub-blocks)
-struct ScQ6K { _Float16 a[8]; };               // Q6_K: 16-value sub-blocks, lane-dependent index
-struct ScQ8 { _Float16 a[8]; };                // Q8_0: block t
+// Per-super-block scales of one row, as f16 pairs (a2[i] = scales 2i, 2i+1; kept as packed
+// vectors: arrays of scalar halves end up in scratch): value = a[s] * q + c[s] for sub-scale s.
+struct ScK { f16x2 a2[4], c2[4]; };          // Q4_K / Q5_K: s = K-step t (32-value sub-blocks)
+struct ScQ6K { f16x2 a2[4]; };               // Q6_K: 16-value sub-blocks, lane-dependent index
+struct ScQ8 { f16x2 a2[4]; };                // Q8_0: block t
 struct ScNone { };
+// broadcast scale s (compile-time after unrolling) of a packed array
+DEVI f16x2 bcast(const f16x2* a2, int s) {
+  const f16x2 p = a2[s >> 1];
+  return (s & 1) ? __builtin_shufflevector(p, p, 1, 1) : __builtin_shufflevector(p, p, 0, 0);
+}
 
 template <int T> struct ScOf { typedef ScNone type; };
 template <> struct ScOf<QT_Q4_K> { typedef ScK type; };
@@ -182,19 +188,11 @@ DEVI void prep_kquant(const u32x4& hdr, ScK& s) {
   bytes_to_h(sc_lo, k1024, v[0], v[1]);
   bytes_to_h(sc_hi, k1024, v[2], v[3]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f16x2 p = v[i] * d;
-    s.a[2 * i] = p[0];
-    s.a[2 * i + 1] = p[1];
-  }
+  for (int i = 0; i < 4; ++i) s.a2[i] = v[i] * d;
   bytes_to_h(m_lo, k1024, v[0], v[1]);
   bytes_to_h(m_hi, k1024, v[2], v[3]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f16x2 p = v[i] * nd;
-    s.c[2 * i] = p[0];
-    s.c[2 * i + 1] = p[1];
-  }
+  for (int i = 0; i < 4; ++i) s.c2[i] = v[i] * nd;
 }
 
 // K-step t of Q4_K: chunk c = t >> 1 (in piece h = t >> 2, words 2*((t>>1)&1) +{0,1}), nibble t & 1
@@ -202,7 +200,7 @@ DEVI f16x8 frag_q4k(const RawQ4K& r, const ScK& s, int t) {
   const u32x4 p = t < 4 ? r.p0 : r.p1;
   const int wi = 2 * ((t >> 1) & 1), sh = 4 * (t & 1);
   const uint32_t n0 = (p[wi] >> sh) & 0x0F0F0F0Fu, n1 = (p[wi + 1] >> sh) & 0x0F0F0F0Fu;
-  return frag8(n0, n1, h2((_Float16)1024.f), h2(s.a[t]), h2(s.c[t]));
+  return frag8(n0, n1, h2((_Float16)1024.f), bcast(s.a2, t), bcast(s.c2, t));
 }
 // Q5_K: plus the 5th bit = bit t of the lane's 8 qh bytes
 DEVI f16x8 frag_q5k(const RawQ5K& r, const ScK& s, int t) {
@@ -210,7 +208,7 @@ DEVI f16x8 frag_q5k(const RawQ5K& r, const ScK& s, int t) {
   const int wi = 2 * ((t >> 1) & 1), sh = 4 * (t & 1);
   const uint32_t n0 = ((p[wi] >> sh) & 0x0F0F0F0Fu) | (((r.qh[0] >> t) & 0x01010101u) << 4);
   const uint32_t n1 = ((p[wi + 1] >> sh) & 0x0F0F0F0Fu) | (((r.qh[1] >> t) & 0x01010101u) << 4);
-  return frag8(n0, n1, h2((_Float16)1024.f), h2(s.a[t]), h2(s.c[t]));
+  return frag8(n0, n1, h2((_Float16)1024.f), bcast(s.a2, t), bcast(s.c2, t));
 }
 
 // ---- Q6_K ------------------------------------------------------------------
@@ -237,11 +235,7 @@ DEVI void prep_q6k(const RawQ6K& r, int g, ScQ6K& s) {
   bytes_to_h(e0, off, v[0], v[1]);
   bytes_to_h(e1, off, v[2], v[3]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f16x2 p = v[i] * d;
-    s.a[2 * i] = p[0];
-    s.a[2 * i + 1] = p[1];
-  }
+  for (int i = 0; i < 4; ++i) s.a2[i] = v[i] * d;
 }
 // K-step t: n = t >> 2 (ql piece), low/high nibble (t >> 1) & 1, ql run t & 1, qh bits 2*(t & 3)
 DEVI f16x8 frag_q6k(const RawQ6K& r, const ScQ6K& s, int t) {
@@ -249,7 +243,7 @@ DEVI f16x8 frag_q6k(const RawQ6K& r, const ScQ6K& s, int t) {
   const int wi = 2 * (t & 1), sh = 4 * ((t >> 1) & 1), hs = 2 * (t & 3), hw = 2 * (t >> 2);
   const uint32_t n0 = ((ql[wi] >> sh) & 0x0F0F0F0Fu) | (((r.qh[hw] >> hs) & 0x03030303u) << 4);
   const uint32_t n1 = ((ql[wi + 1] >> sh) & 0x0F0F0F0Fu) | (((r.qh[hw + 1] >> hs) & 0x03030303u) << 4);
-  return frag8(n0, n1, h2((_Float16)1056.f), h2(s.a[t]), h2((_Float16)0.f));
+  return frag8(n0, n1, h2((_Float16)1056.f), bcast(s.a2, t), h2((_Float16)0.f));
 }
 
 // ---- Q8_0 ------------------------------------------------------------------
@@ -265,16 +259,12 @@ DEVI RawQ8 load_raw_q8(const WDesc& W, int row, int sb, int g) {
 }
 DEVI void prep_q8(const RawQ8& r, ScQ8& s) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f16x2 d = as_h2(r.d[i]);
-    s.a[2 * i] = d[0];
-    s.a[2 * i + 1] = d[1];
-  }
+  for (int i = 0; i < 4; ++i) s.a2[i] = as_h2(r.d[i]);
 }
 DEVI f16x8 frag_q8(const RawQ8& r, const ScQ8& s, int t) {
   const u32x4 p = r.q[t >> 1];
   const int wi = 2 * (t & 1);
-  return frag8(p[wi] ^ 0x80808080u, p[wi + 1] ^ 0x80808080u, h2((_Float16)1152.f), h2(s.a[t]),
+  return frag8(p[wi] ^ 0x80808080u, p[wi + 1] ^ 0x80808080u, h2((_Float16)1152.f), bcast(s.a2, t),
                h2((_Float16)0.f));
 }
 

@@ -1,0 +1,308 @@
+// Large-M quantised GEMM (prefill chunks, decode batches >= 128), gfx950.
+//
+//   y[m, n] = alpha * sum_k x[m, k] * W[n, k]      (W in GGUF K-quant blocks, x f16)
+//
+// Why a second GEMM (vs path B of qgemv_impl.h, where every wave dequantises its own weight
+// rows into registers and re-reads the activation tile from LDS once per MFMA): at M >= 128
+// that design is VALU- and LDS-bound (PMC on gate/up M=256: 6.7 VALU instructions per MFMA,
+// 21 % MFMA busy). Here each workgroup DEQUANTISES ITS WEIGHT TILE ONCE INTO LDS and all
+// eight waves share it:
+//   * workgroup tile = 128 weight rows x BM activation rows (BM = 64*WM: 256 or 128),
+//     8 waves as WM (M) x 8/WM (N), each wave a 64 x (128*WM/8) output tile of
+//     v_mfma_f32_16x16x32_f16 accumulators (0.5-0.75 LDS reads per MFMA);
+//   * K advances in quarters of a super-block (64 values): x quarter [BM][64] and the
+//     dequantised W quarter [128][64] live in double-buffered, XOR-swizzled LDS
+//     (16-B chunk c of row r stored at c ^ (r & 7): conflict-free ds_read_b128);
+//   * wave w streams the raw blocks of tile-block w (16 rows) one super-block ahead and
+//     dequantises ONE quarter per step with every lane busy (the v2 tile layouts of
+//     common.h put each quarter's bytes in all 64 lanes) -- about one packed-f16 VALU
+//     instruction per MFMA;
+//   * one barrier per quarter: stage quarter j+1 (x registers -> LDS, dequant -> LDS) and
+//     issue the global loads of quarter j+2, then the 32 MFMAs of quarter j.
+// Grid: (tile, m-block, k-slice) with every m-block and k-slice of a weight tile on ONE XCD
+// (dispatch puts workgroup i on XCD i % 8), so a weight tile is fetched once per XCD L2.
+// Split-K (ks > 1) writes fp32 slabs reduced by the launcher's reduce kernels (fused with
+// RoPE / residual+RMSNorm where the model uses them).
+#pragma once
+#include "qgemv_impl.h"
+
+namespace nls_gemm {
+using namespace nls_gemv;
+
+template <int T, int WM>
+DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds) {
+  constexpr int MTW = 4;                 // 16-row activation tiles per wave
+  constexpr int WN = 8 / WM;
+  constexpr int NTW = 8 / WN;            // 16-row weight tiles per wave
+  constexpr int BM = WM * MTW * 16;
+  constexpr int XS = BM * 64, WSZ = 128 * 64;    // f16 elements per buffer
+  constexpr int NXU = BM * 8 / 512;              // 16-B x chunks staged per thread per quarter
+  act_t* Xs = lds;                       // [2][BM][64]
+  act_t* Ws = lds + 2 * XS;              // [2][128][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave / WN, wn = wave % WN;
+  const WDesc W{S.w, S.rows, S.K};
+  const int nb = S.K >> 8;
+  const int sb0 = (nb * kslice) / ks, sb1 = (nb * (kslice + 1)) / ks;
+  const int sbl = max(sb1 - 1, sb0);
+  const int M = a.M;
+  const int drow = min(row0 + wave * 16 + r, S.rows - 1);   // this wave's dequant rows (clamped)
+
+  f32x4 acc[MTW][NTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 xr[NXU];
+  auto load_x = [&](int sb, int q) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NXU; ++u) {
+      const int idx = threadIdx.x + 512 * u, row = idx >> 3, ch = idx & 7;
+      // rows >= M only feed outputs that are never stored: clamp, never branch
+      xr[u] = ld16(a.x + (size_t)min(row, M - 1) * a.ldx + sb * 256 + q * 64 + ch * 8);
+    }
+  };
+  auto store_x = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NXU; ++u) {
+      const int idx = threadIdx.x + 512 * u, row = idx >> 3, ch = idx & 7;
+      *reinterpret_cast<u32x4*>(Xs + buf * XS + row * 64 + ((ch ^ (row & 7)) << 3)) = xr[u];
+    }
+  };
+  typedef typename RawOf<T>::type Raw;
+  typedef typename ScOf<T>::type Sc;
+  // One quarter step: dequantise W quarter `qn` of `rw` into buffer buf^1 and run the 32 MFMAs
+  // of buffer buf. Program order = issue order wanted: both fragments' VALU first (independent
+  // of the MFMAs, so the scheduler interleaves them into the MFMA stream), the K-step's LDS
+  // reads before this step's W writes (the writes go to the other buffer).
+  auto step_mma = [&](const Raw& rw, const Sc& sc, int qn, int buf) __attribute__((always_inline)) {
+    const act_t* xb = Xs + buf * XS;
+    const act_t* wb = Ws + buf * WSZ;
+    act_t* wn_ = Ws + (buf ^ 1) * WSZ + (wave * 16 + r) * 64;
+    f16x8 f[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) f[s] = frag_t<T>(rw, sc, 2 * qn + s);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = ((4 * s + g) ^ (r & 7)) << 3;
+      f16x8 A[MTW], B[NTW];
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) A[i] = *reinterpret_cast<const f16x8*>(xb + (wm * MTW * 16 + 16 * i + r) * 64 + co);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) B[j] = *reinterpret_cast<const f16x8*>(wb + (wn * NTW * 16 + 16 * j + r) * 64 + co);
+      *reinterpret_cast<f16x8*>(wn_ + co) = f[s];
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(A[i], B[j], acc[i][j]);
+    }
+  };
+  auto deq_w = [&](const Raw& rw, const Sc& sc, int q, int buf) __attribute__((always_inline)) {
+    const int row = wave * 16 + r;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const f16x8 f = frag_t<T>(rw, sc, 2 * q + s);
+      *reinterpret_cast<f16x8*>(Ws + buf * WSZ + row * 64 + (((4 * s + g) ^ (r & 7)) << 3)) = f;
+    }
+  };
+
+  Raw rA, rB;
+  Sc sA, sB;
+  if (sb0 < sb1) {
+    rA = load_raw<T, true>(W, drow, sb0, g);
+    rB = load_raw<T, true>(W, drow, min(sb0 + 1, sbl), g);
+    load_x(sb0, 0);
+    prep_sc<T>(rA, g, sA);
+    store_x(0);
+    deq_w(rA, sA, 0, 0);
+    load_x(sb0, 1);
+  }
+  __syncthreads();
+  // one super-block = 4 quarter steps; buffer parity = quarter & 1. Every load is unconditional
+  // (indices clamped): a conditional load breaks hipcc's vmcnt bookkeeping (qgemv_impl.h).
+  auto sb_step = [&](Raw& rc, Sc& sc, Raw& rn, Sc& sn, int sb) __attribute__((always_inline)) {
+    const int nx = min(sb + 1, sbl);
+    // Each step: write the x registers loaded one step ago into LDS, re-issue the next x loads
+    // at once (sched_barrier: hipcc would otherwise sink them to the end of the step, right
+    // before their use after the barrier), then dequant of the next W quarter + the MFMAs.
+    // q = 0
+    store_x(1);
+    load_x(sb, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    step_mma(rc, sc, 1, 0);
+    __syncthreads();
+    // q = 1
+    store_x(0);
+    load_x(sb, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    step_mma(rc, sc, 2, 1);
+    __syncthreads();
+    // q = 2: last use of rc -> reload it two super-blocks ahead
+    store_x(1);
+    load_x(nx, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    step_mma(rc, sc, 3, 0);
+    rc = load_raw<T, true>(W, drow, min(sb + 2, sbl), g);
+    __syncthreads();
+    // q = 3: stage quarter 0 of the next super-block
+    store_x(0);
+    load_x(nx, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    prep_sc<T>(rn, g, sn);
+    step_mma(rn, sn, 0, 1);
+    __syncthreads();
+  };
+  int sb = sb0;
+  for (; sb + 1 < sb1; sb += 2) {
+    sb_step(rA, sA, rB, sB, sb);
+    sb_step(rB, sB, rA, sA, sb + 1);
+  }
+  if (sb < sb1) sb_step(rA, sA, rB, sB, sb);
+
+  // ---- epilogue from the accumulators: lane holds weight row rbase + 16j + r and
+  // activation rows mbase + 16i + 4g + e
+  const int rbase = row0 + wn * NTW * 16, mbase = wm * MTW * 16;
+  if (ks > 1) {
+    const int ntot = a.pad;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int row = rbase + 16 * j + r;
+      if (row >= S.rows) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int b = mbase + 16 * i + 4 * g + e;
+          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[i][j][e];
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int row = rbase + 16 * j + r;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int b = mbase + 16 * i + 4 * g + e;
+        const float v = acc[i][j][e] * a.alpha;
+        if (a.epi == EPI_SWIGLU) {
+          const float u = __shfl_xor(v, 8, 64);
+          if (r < 8 && b < M && row < S.rows) {
+            const int n = S.ycol + ((rbase + 16 * j) >> 1) + r;
+            reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
+          }
+          continue;
+        }
+        if (b < M && row < S.rows) {
+          const size_t off = (size_t)b * a.ldy + S.ycol + row;
+          if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
+          else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
+          else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
+        }
+      }
+    }
+  }
+  if (a.argmax) {
+    // greedy arg-max: max over the lane's NTW rows, then the 16 lanes of a row group, then the
+    // workgroup's waves through LDS (free after the main loop) -> ONE global atomic per
+    // activation row per workgroup (vs one per 16 rows: 1M contended 64-bit atomics on the
+    // 128K-row lm_head otherwise)
+    unsigned long long* red = reinterpret_cast<unsigned long long*>(lds);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < BM; idx += 512) red[idx] = 0ull;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned long long k = 0ull;
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int row = rbase + 16 * j + r;
+          const unsigned long long kj = (row < S.rows) ? argmax_key(acc[i][j][e] * a.alpha, S.ycol + row) : 0ull;
+          k = kj > k ? kj : k;
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const unsigned long long ok = __shfl_xor(k, o, 64);
+          k = ok > k ? ok : k;
+        }
+        if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
+      }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < M; idx += 512) atomicMax(a.argmax + idx, red[idx]);
+  }
+}
+
+template <int WM, int KSET>
+__global__ __launch_bounds__(512) void qmm_lds_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+                                                      int nmb) {
+  extern __shared__ __attribute__((aligned(16))) act_t lds[];
+  constexpr int BM = WM * 64;
+  // (tile, m-block, k-slice) with all m-blocks and k-slices of a tile on one XCD
+  const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
+  const int kslice = j % ks;
+  const int mb = (j / ks) % nmb;
+  const int tile = (j / ks / nmb) * 8 + xcd;
+  if (tile >= ntiles) return;
+  const int m0 = mb * BM;
+  a.m0 = m0;
+  a.x += (size_t)m0 * a.ldx;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+  a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (a.argmax) a.argmax += m0;
+  a.M = min(BM, a.M - m0);
+  Seg S = segs.s[0];
+#pragma unroll
+  for (int s = 1; s < 8; ++s)
+    if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
+  const int row0 = (tile - S.tile_begin) * 128;
+  if constexpr (KSET == 0) {
+    switch (S.type) {
+      case QT_Q4_K: lds_tile<QT_Q4_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      default: break;
+    }
+  } else {
+    switch (S.type) {
+      case QT_Q5_K: lds_tile<QT_Q5_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      case QT_Q8_0: lds_tile<QT_Q8_0, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      default: break;
+    }
+  }
+}
+
+template <int WM, int KSET>
+int launch_lds_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
+  constexpr int BM = WM * 64;
+  const int nmb = (a.M + BM - 1) / BM;
+  const size_t lds = (size_t)2 * (BM + 128) * 64 * sizeof(act_t);
+  const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
+  static bool attr = false;
+  if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
+    if (hipFuncSetAttribute((const void*)qmm_lds_kernel<WM, KSET>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return -1;
+    attr = true;
+  }
+  hipLaunchKernelGGL((qmm_lds_kernel<WM, KSET>), dim3(grid), dim3(512), lds, st, sl, a, ks, ws, ntiles, nmb);
+  return (int)hipGetLastError();
+}
+
+template <int KSET>
+int launch_lds_kset(int wm, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
+  if (wm == 4) return launch_lds_t<4, KSET>(sl, ntiles, ks, ws, a, st);
+  if (wm == 2) return launch_lds_t<2, KSET>(sl, ntiles, ks, ws, a, st);
+  return -1;
+}
+
+int launch_lds_k0(int wm, const SegList&, int, int, float*, const GemvArgs&, hipStream_t);
+int launch_lds_k1(int wm, const SegList&, int, int, float*, const GemvArgs&, hipStream_t);
+
+}  // namespace nls_gemm

@@ -1,6 +1,6 @@
 // Dispatcher of the quantised GEMV / GEMM (kernels: qgemv_impl.h, instantiated per type-set in
 // qgemv_k{0,1,2}.hip).
-#include "qgemv_impl.h"
+#include "qgemm_impl.h"
 
 using namespace nls_gemv;
 
@@ -18,21 +18,25 @@ struct NlsSeg {
 
 // mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
 // mode 1: path B (waves split rows, LDS-staged activations, optional split-K `ks` with workspace
-//         `ws` of ks*M*sum(rows) floats). Returns 0 on success, a hipError_t, or -1 on bad arguments.
+//         `ws` of ks*M*sum(rows) floats).
+// mode 2: large-M LDS-dequant GEMM (qgemm_impl.h; K-quant types only): 8 waves, `rt` = WM (4: 256-row
+//         activation blocks, 2: 128-row), optional split-K as mode 1.
+// Returns 0 on success, a hipError_t, or -1 on bad arguments.
 int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
               float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
               void* stream) {
-  if (nseg < 1 || nseg > 8 || M < 1 || (rt != 1 && rt != 2) || (waves != 4 && waves != 8)) return -1;
-  if (M > 64 && mode != 1) return -1;   // large M: path B in blocks of 128 activation rows
-  if (mode == 1 && ks > 1 && !ws) return -1;
-  if (epi == EPI_SLABS && (mode != 1 || ks < 2)) return -1;   // slabs exist only with split-K
+  if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
+  if (mode == 2 ? (waves != 8 || (rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) return -1;
+  if (M > 64 && mode == 0) return -1;   // large M: path B / LDS GEMM
+  if (mode != 0 && ks > 1 && !ws) return -1;
+  if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = (mode == 1 ? waves : 1) * rt * 16;
+  const int tile_rows = mode == 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16;
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
-    if (mode == 1 && segs[i].xmap) return -1;
+    if (mode != 0 && segs[i].xmap) return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;
     sl.s[i].ymap = segs[i].ymap;
@@ -63,9 +67,12 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
   auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : launch_k2);
-  if (mode == 1) {
+  if (mode == 2 && kset == 2) return -1;   // plain float weights: path B only
+  if (mode != 0) {
     if (ks < 1) ks = 1;
-    const int rc = launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
+    const int rc = mode == 2 ? (kset == 0 ? nls_gemm::launch_lds_k0 : nls_gemm::launch_lds_k1)(rt, sl, tiles, ks,
+                                                                                             (float*)ws, a, st)
+                             : launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
     if (rc || ks == 1 || epi == EPI_SLABS) return rc;
     RedList rl{};
     for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};

@@ -182,7 +182,8 @@ def _workspace(dev, n: int) -> torch.Tensor:
 
 def gemv_config(segs: Sequence[Seg], M: int):
     """(mode, waves, rt, ks) for a launch. mode 0 = waves split K (small batch, mapped rows);
-    mode 1 = waves split rows over an LDS-staged activation tile (+ split-K across workgroups)."""
+    mode 1 = waves split rows over an LDS-staged activation tile (+ split-K across workgroups);
+    mode 2 = large-M LDS-dequant GEMM (K-quants; rt = waves along M: 256- or 128-row blocks)."""
     from . import tuning
     return tuning.select(segs, M)
 
@@ -197,7 +198,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         mapped = any(s.xmap is not None for s in segs)
         if mode < 0 or waves == 0:
             mode, waves, rt, ks = gemv_config(segs, M) if not mapped else (0, 8, 1, 1)
-        if M > 64 and (mapped or mode != 1):
+        if M > 64 and (mapped or mode == 0):
             # mapped (MoE) rows / path A: chunks of 64 rows
             for m0 in range(0, M, 64):
                 mm = min(64, M - m0)
@@ -209,7 +210,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
             arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
                                  s.w.K, s.ycol)
         ws = None
-        if mode == 1 and ks > 1:
+        if mode != 0 and ks > 1:
             ws = _workspace(x.device, ks * M * sum(s.w.rows for s in segs)).data_ptr()
         rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
                          EPI[epi], _p(argmax), waves, rt, mode, ks, ws, _stream_ptr(x))
@@ -254,7 +255,7 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
     launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel."""
     if x.is_cuda and seg.xmap is None:
         mode, waves, rt, ks = cfg or gemv_config([seg], M)
-        if mode == 1 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
+        if mode != 0 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
             L = _lib.lib()
             ws = _workspace(x.device, ks * M * seg.w.rows)
             arr = (_lib.NlsSeg * 1)()
@@ -352,7 +353,7 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        if mode == 1 and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
+        if mode != 0 and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
             L = _lib.lib()
             ws = _workspace(h.device, ks * T * ncol)
             arr = (_lib.NlsSeg * len(segs))()

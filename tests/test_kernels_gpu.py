@@ -351,7 +351,7 @@ def test_sample_kernel(gpu):
 
 
 @pytest.mark.parametrize("M,cfg", [(5, (1, 8, 1, 4)), (64, (1, 4, 1, 2)), (200, (1, 8, 1, 3)), (200, (1, 8, 1, 1)),
-                                   (7, (0, 4, 1, 1))])
+                                   (7, (0, 4, 1, 1)), (256, (2, 8, 4, 4)), (130, (2, 8, 2, 2))])
 def test_qgemv_add_rmsnorm_fused(gpu, M, cfg):
     """Row-parallel projection + residual + next RMSNorm (split-K slabs reduced by the fused kernel)."""
     D, K = 512, 768
@@ -373,7 +373,7 @@ def test_lm_head_argmax_only_epilogue(gpu):
     """Greedy decode: arg-max keys without writing logits."""
     K, V = 512, 1000
     w, Wd = _qw(V, K, GGMLType.Q6_K, gpu, 12)
-    for M, cfg in ((3, (0, 4, 1, 1)), (40, (1, 8, 1, 2)), (150, (1, 8, 1, 1))):
+    for M, cfg in ((3, (0, 4, 1, 1)), (40, (1, 8, 1, 2)), (150, (1, 8, 1, 1)), (256, (2, 8, 4, 1))):
         x = _x(M, K, gpu)
         y = torch.full((x.shape[0], V), 7.0, device=gpu)
         keys = torch.zeros(x.shape[0], dtype=torch.int64, device=gpu)
@@ -386,8 +386,8 @@ def test_lm_head_argmax_only_epilogue(gpu):
         assert bool((y == 7.0).all())
 
 
-@pytest.mark.parametrize("cfg", [(1, 8, 1, 2), (1, 8, 1, 3), (0, 4, 1, 1)])
-@pytest.mark.parametrize("M", [3, 70])
+@pytest.mark.parametrize("cfg", [(1, 8, 1, 2), (1, 8, 1, 3), (0, 4, 1, 1), (2, 8, 4, 2), (2, 8, 2, 1)])
+@pytest.mark.parametrize("M", [3, 70, 256])
 def test_qkv_rope_kv_fused(gpu, cfg, M):
     """QKV projection (3 segments) + RoPE + KV append, split-K slabs summed inside the RoPE kernel."""
     Hq, Hkv, D, K = 4, 2, 128, 512
@@ -397,7 +397,7 @@ def test_qkv_rope_kv_fused(gpu, cfg, M):
     segs = [ops.Seg(wq, 0), ops.Seg(wk, Hq * D), ops.Seg(wv, (Hq + Hkv) * D)]
     x = _x(M, K, gpu)
     pad = x.shape[0]
-    cs = ops.rope_table(512, D, 10000.0, gpu)
+    cs = ops.rope_table(1024, D, 10000.0, gpu)
     pos = torch.arange(pad, dtype=torch.int32, device=gpu) * 3
     slot = torch.arange(pad, dtype=torch.int32, device=gpu)
     qkv = torch.zeros(pad, (Hq + 2 * Hkv) * D, device=gpu)
@@ -416,3 +416,52 @@ def test_qkv_rope_kv_fused(gpu, cfg, M):
             outs.append((q.cpu(), kc.cpu(), vc.cpu()))
     for a, b in zip(outs[0], outs[1]):
         _close(a[:M], b[:M], 3e-2)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("M", [65, 256, 300, 520])
+@pytest.mark.parametrize("wm,ks", [(4, 1), (2, 1), (4, 3)])
+def test_qgemm_lds(gpu, t, M, wm, ks):
+    """Large-M LDS-dequant GEMM (mode 2): weight tile dequantised once into LDS and shared by
+    8 waves; partial last 128-row weight tile and activation block; store, add, argmax."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=2, waves=8, rt=wm, ks=ks, argmax=keys)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    assert float(y[M:].abs().max().cpu()) == 0.0 if M < pad else True
+    ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+    ops.argmax_unpack(keys, M, ids)
+    assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=2, waves=8, rt=wm, ks=ks)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+
+
+@pytest.mark.parametrize("ks", [1, 2])
+def test_qgemm_lds_swiglu_multiseg(gpu, ks):
+    """Mode 2 with the SwiGLU epilogue, and a Q|K|V-style multi-segment (Q4_K, Q4_K, Q6_K) launch."""
+    K, F = 512, 256
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 333
+    x = _x(M, K, gpu)
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=2, waves=8, rt=4, ks=ks)
+    xf = x[:M].float().cpu()
+    _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(128, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(128, K, GGMLType.Q6_K, gpu, 3)
+    yq = torch.zeros(x.shape[0], 512, device=gpu)
+    ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)], x, yq, M, mode=2, waves=8, rt=4, ks=ks)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())

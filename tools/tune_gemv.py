@@ -41,13 +41,15 @@ def shapes(spec, base=GGMLType.Q4_K, more=GGMLType.Q6_K):
     return out
 
 
-def configs(K, M=1):
+def configs(K, M=1, quant=True):
     nb = K // 256
-    if M > 64:   # large-M GEMM (128-row activation blocks), optionally split-K over workgroups
+    if M > 64:   # large-M GEMM: path B (128-row activation blocks) or the LDS-dequant GEMM (mode 2)
         c = [(1, 4, 2, 1)]
         for ks in (1, 2, 4, 8):
             if ks <= max(1, nb // 2):
-                c += [(1, 8, 1, ks), (1, 4, 1, ks), (1, 8, 2, ks)]
+                c += [(1, 8, 1, ks), (1, 8, 2, ks)]
+                if quant:
+                    c += [(2, 8, 4, ks), (2, 8, 2, ks)]
         return c
     c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
     for waves in (4, 8):
@@ -118,7 +120,7 @@ def main():
         keys = torch.zeros(mmax, dtype=torch.int64, device=dev)
         for M in Ms:
             res = []
-            for cfg in configs(K, M):
+            for cfg in configs(K, M, all(int(t) in (8, 12, 13, 14) for t, _ in segdef)):
                 us = time_cfg(segs, x, y, M, epi, keys, cfg)
                 if us is not None:
                     res.append((us, cfg))
