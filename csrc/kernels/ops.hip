@@ -135,36 +135,64 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
                                                       __bf16* __restrict__ q_out, long ldq,
                                                       __bf16* __restrict__ kc, __bf16* __restrict__ vc,
                                                       int Hq, int Hkv, int D, int neox) {
+  // Vectorised: every thread owns 4 consecutive columns (16-B slab loads, 8-B bf16 stores).
   const int t = blockIdx.x;
   const float* row = qkv + (size_t)t * ldqkv;
-  auto ld = [&](int col) {
-    float v = row[col];
-    for (int k = 1; k < ks; ++k) v += row[(size_t)k * slab + col];
+  auto ld4 = [&](int col) {
+    float4 v = *reinterpret_cast<const float4*>(row + col);
+    for (int k = 1; k < ks; ++k) {
+      const float4 u = *reinterpret_cast<const float4*>(row + (size_t)k * slab + col);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
     return v;
+  };
+  typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+  auto st4 = [](__bf16* d, float a, float b, float c, float e) {
+    *reinterpret_cast<bf4*>(d) = bf4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)e};
   };
   const int p = pos[t];
   const long s = slot[t];  // int32 slot index, widened
   const int half = D >> 1;
-  const float* c = cs + (size_t)p * D;
-  for (int idx = threadIdx.x; idx < (Hq + Hkv) * half; idx += blockDim.x) {
-    const int h = idx / half, i = idx - h * half;
-    const int i0 = neox ? i : 2 * i, i1 = neox ? i + half : 2 * i + 1;
-    const float x0 = ld(h * D + i0), x1 = ld(h * D + i1);
-    const float cc = c[2 * i], ss = c[2 * i + 1];
-    const float y0 = x0 * cc - x1 * ss, y1 = x0 * ss + x1 * cc;
-    if (h < Hq) {
-      q_out[(size_t)t * ldq + h * D + i0] = (__bf16)y0;
-      q_out[(size_t)t * ldq + h * D + i1] = (__bf16)y1;
-    } else if (s >= 0) {
-      __bf16* kd = kc + ((size_t)s * Hkv + (h - Hq)) * D;
-      kd[i0] = (__bf16)y0;
-      kd[i1] = (__bf16)y1;
+  const float* c = cs + (size_t)p * D;   // [D/2][2] (cos, sin)
+  auto dst = [&](int h) -> __bf16* {
+    return h < Hq ? q_out + (size_t)t * ldq + h * D : kc + ((size_t)s * Hkv + (h - Hq)) * D;
+  };
+  const int nh = s >= 0 ? Hq + Hkv : Hq;         // padded rows (slot -1) write no K/V
+  if (!neox) {
+    // adjacent pairs: columns col..col+3 = pairs col/2, col/2+1
+    for (int idx = threadIdx.x; idx < nh * (D / 4); idx += blockDim.x) {
+      const int h = idx / (D / 4), col = 4 * (idx - h * (D / 4));
+      const float4 x = ld4(h * D + col);
+      const float4 cw = *reinterpret_cast<const float4*>(c + col);   // (cos, sin) of pairs col/2, col/2+1
+      st4(dst(h) + col, x.x * cw.x - x.y * cw.y, x.x * cw.y + x.y * cw.x, x.z * cw.z - x.w * cw.w,
+          x.z * cw.w + x.w * cw.z);
+    }
+  } else {
+    // NEOX halves: columns i..i+3 pair with i+half..i+half+3
+    for (int idx = threadIdx.x; idx < nh * (half / 4); idx += blockDim.x) {
+      const int h = idx / (half / 4), i = 4 * (idx - h * (half / 4));
+      const float4 a = ld4(h * D + i), b = ld4(h * D + half + i);
+      const float4 c0 = *reinterpret_cast<const float4*>(c + 2 * i), c1 = *reinterpret_cast<const float4*>(c + 2 * i + 4);
+      const float cc[4] = {c0.x, c0.z, c1.x, c1.z}, sn[4] = {c0.y, c0.w, c1.y, c1.w};
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+      float y0[4], y1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        y0[u] = av[u] * cc[u] - bv[u] * sn[u];
+        y1[u] = av[u] * sn[u] + bv[u] * cc[u];
+      }
+      __bf16* d = dst(h);
+      st4(d + i, y0[0], y0[1], y0[2], y0[3]);
+      st4(d + half + i, y1[0], y1[1], y1[2], y1[3]);
     }
   }
   if (s >= 0) {
     const int v0 = (Hq + Hkv) * D;
     __bf16* vd = vc + (size_t)s * Hkv * D;
-    for (int i = threadIdx.x; i < Hkv * D; i += blockDim.x) vd[i] = (__bf16)ld(v0 + i);
+    for (int i = 4 * threadIdx.x; i < Hkv * D; i += 4 * blockDim.x) {
+      const float4 v = ld4(v0 + i);
+      st4(vd + i, v.x, v.y, v.z, v.w);
+    }
   }
 }
 

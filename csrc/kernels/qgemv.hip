@@ -1,6 +1,7 @@
 // Dispatcher of the quantised GEMV / GEMM (kernels: qgemv_impl.h, instantiated per type-set in
 // qgemv_k{0,1,2}.hip).
 #include "qgemm_impl.h"
+#include "qgemm_dma.h"
 
 using namespace nls_gemv;
 
@@ -21,18 +22,24 @@ struct NlsSeg {
 //         `ws` of ks*M*sum(rows) floats).
 // mode 2: large-M LDS-dequant GEMM (qgemm_impl.h; K-quant types only): 8 waves, `rt` = WM (4: 256-row
 //         activation blocks, 2: 128-row), optional split-K as mode 1.
+// mode 3: large-M LDS-DMA GEMM (qgemm_dma.h; Q4_K/Q5_K/Q6_K only): 4 waves, `rt` = activation
+//         tiles per block (16: 256 rows, 8: 128 rows), optional split-K as mode 1.
 // Returns 0 on success, a hipError_t, or -1 on bad arguments.
 int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
               float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
               void* stream) {
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
-  if (mode == 2 ? (waves != 8 || (rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) return -1;
+  if (mode == 3) {
+    if (waves != 4 || (rt != 8 && rt != 16)) return -1;
+  } else if (mode == 2 ? (waves != 8 || (rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) {
+    return -1;
+  }
   if (M > 64 && mode == 0) return -1;   // large M: path B / LDS GEMM
   if (mode != 0 && ks > 1 && !ws) return -1;
   if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16;
+  const int tile_rows = mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16;
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -67,12 +74,19 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
   auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : launch_k2);
-  if (mode == 2 && kset == 2) return -1;   // plain float weights: path B only
+  if (mode >= 2 && kset == 2) return -1;   // plain float weights: path B only
+  if (mode == 3)
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].type == QT_Q8_0) return -1;   // raw Q8_0 tiles do not fit the DMA LDS budget
   if (mode != 0) {
     if (ks < 1) ks = 1;
-    const int rc = mode == 2 ? (kset == 0 ? nls_gemm::launch_lds_k0 : nls_gemm::launch_lds_k1)(rt, sl, tiles, ks,
-                                                                                             (float*)ws, a, st)
-                             : launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
+    int rc;
+    if (mode == 3)
+      rc = (kset == 0 ? nls_dma::launch_dma_k0 : nls_dma::launch_dma_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
+    else if (mode == 2)
+      rc = (kset == 0 ? nls_gemm::launch_lds_k0 : nls_gemm::launch_lds_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
+    else
+      rc = launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
     if (rc || ks == 1 || epi == EPI_SLABS) return rc;
     RedList rl{};
     for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};

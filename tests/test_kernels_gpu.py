@@ -465,3 +465,53 @@ def test_qgemm_lds_swiglu_multiseg(gpu, ks):
     yq = torch.zeros(x.shape[0], 512, device=gpu)
     ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)], x, yq, M, mode=2, waves=8, rt=4, ks=ks)
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K])
+@pytest.mark.parametrize("M", [65, 256, 300, 520])
+@pytest.mark.parametrize("mt,ks", [(16, 1), (8, 1), (16, 3), (8, 2)])
+def test_qgemm_dma(gpu, t, M, mt, ks):
+    """Large-M LDS-DMA GEMM (mode 3): activation quarters and raw weight tile-blocks arrive by
+    global_load_lds, weights dequantised per wave in registers; partial last 128-row weight tile and
+    activation block, K slices with 1..n super-blocks; store, add, argmax."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=3, waves=4, rt=mt, ks=ks, argmax=keys)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    assert float(y[M:].abs().max().cpu()) == 0.0 if M < pad else True
+    ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+    ops.argmax_unpack(keys, M, ids)
+    assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=3, waves=4, rt=mt, ks=ks)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+
+
+@pytest.mark.parametrize("ks", [1, 2])
+def test_qgemm_dma_swiglu_multiseg(gpu, ks):
+    """Mode 3 with the SwiGLU epilogue, and a Q|K|V-style multi-segment (Q4_K, Q4_K, Q6_K) launch."""
+    K, F = 1024, 384
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 256
+    x = _x(M, K, gpu)
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=3, waves=4, rt=16, ks=ks)
+    xf = x[:M].float().cpu()
+    _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(128, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(128, K, GGMLType.Q6_K, gpu, 3)
+    yq = torch.zeros(x.shape[0], 512, device=gpu)
+    ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)], x, yq, M, mode=3, waves=4, rt=16, ks=ks)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())

@@ -45,11 +45,11 @@ def configs(K, M=1, quant=True):
     nb = K // 256
     if M > 64:   # large-M GEMM: path B (128-row activation blocks) or the LDS-dequant GEMM (mode 2)
         c = [(1, 4, 2, 1)]
-        for ks in (1, 2, 4, 8):
+        for ks in (1, 2, 3, 4, 6, 8):
             if ks <= max(1, nb // 2):
                 c += [(1, 8, 1, ks), (1, 8, 2, ks)]
                 if quant:
-                    c += [(2, 8, 4, ks), (2, 8, 2, ks)]
+                    c += [(2, 8, 4, ks), (2, 8, 2, ks), (3, 4, 16, ks), (3, 4, 8, ks)]
         return c
     c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
     for waves in (4, 8):
