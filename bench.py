@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--concurrency", type=int, default=256, help="in-flight chat requests per GPU")
+    ap.add_argument("--concurrency", type=int, default=512, help="in-flight chat requests per GPU")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--ftype", default="Q4_K_M")

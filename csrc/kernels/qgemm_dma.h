@@ -140,23 +140,32 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   Raw raw[RT];
   Sc sc[RT];
 
-  // one quarter: 2 K-steps x (RT fragments, MT A reads, RT*MT MFMAs)
+  // one quarter: 2 K-steps x (RT fragments, MT A reads, RT*MT MFMAs). Every A fragment of the
+  // quarter is requested up front (2*MT ds_read_b128 in flight) and the weight fragments are
+  // dequantised while they land, so the LDS latency is exposed once per quarter, not per MFMA
+  // pair (hipcc otherwise issues one read, waits lgkmcnt(0), runs its RT MFMAs, and repeats).
   auto quarter = [&](int j, int q) __attribute__((always_inline)) {
     const uint8_t* xb = Xs + (j % 3) * XS;
+    f16x8 xa[2][MT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f16x8 wf[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) wf[rt] = frag_t<T>(raw[rt], sc[rt], 2 * q + t);
-      const int c = 4 * t + g;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int row = mt * 16 + r;
-        const f16x8 xa = *reinterpret_cast<const f16x8*>(xb + row * 128 + ((c ^ (row & 7)) << 4));
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt][mt] = mfma16(xa, wf[rt], acc[rt][mt]);
+        const int row = mt * 16 + r, c = 4 * t + g;
+        xa[t][mt] = *reinterpret_cast<const f16x8*>(xb + row * 128 + ((c ^ (row & 7)) << 4));
       }
-    }
+    f16x8 wf[2][RT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wf[t][rt] = frag_t<T>(raw[rt], sc[rt], 2 * q + t);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt][mt] = mfma16(xa[t][mt], wf[t][rt], acc[rt][mt]);
   };
 
   if (nq > 0) {

@@ -13,6 +13,7 @@ each decode step:
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import math
 import threading
@@ -69,26 +70,88 @@ class GenResult:
 
 
 class BlockAllocator:
-    def __init__(self, n: int):
+    """Paged-KV block pool with automatic prefix caching.
+
+    Full prompt blocks are content-addressed by a chained hash of their tokens (block i's key
+    covers tokens [0, (i+1)*bs)), so a request whose prompt starts like an earlier one (same
+    system prompt / chat history) maps those blocks read-only and prefills only the rest. Blocks
+    are reference-counted; a released cached block keeps its KV and sits in an LRU until the pool
+    needs it, uncached free blocks are handed out first."""
+
+    def __init__(self, n: int, cache: bool = True):
         self.n = n
-        self.free: Deque[int] = deque(range(n))
+        self.cache_enabled = cache
+        self.free: Deque[int] = deque(range(n))           # never-cached / invalidated blocks
+        self.lru: "collections.OrderedDict[int, None]" = collections.OrderedDict()   # cached, ref 0
+        self.ref = [0] * n
+        self.key_of: Dict[int, int] = {}                   # block -> chain hash
+        self.block_of: Dict[int, int] = {}                 # chain hash -> block
+        self.hits = 0                                      # prompt tokens served from the cache
+
+    @staticmethod
+    def chain_keys(tokens: Seq[int], bs: int, n_blocks: int) -> List[int]:
+        keys, h = [], 0
+        for i in range(n_blocks):
+            h = hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+            keys.append(h)
+        return keys
+
+    def match(self, keys: Seq[int]) -> List[int]:
+        """Longest cached prefix (blocks are pinned: ref += 1)."""
+        out = []
+        if not self.cache_enabled:
+            return out
+        for k in keys:
+            b = self.block_of.get(k)
+            if b is None:
+                break
+            out.append(b)
+        for b in out:
+            if self.ref[b] == 0:
+                self.lru.pop(b, None)
+            self.ref[b] += 1
+        return out
 
     def alloc(self, k: int) -> Optional[List[int]]:
-        if k > len(self.free):
+        if k > len(self.free) + len(self.lru):
             return None
-        return [self.free.popleft() for _ in range(k)]
+        out = []
+        for _ in range(k):
+            if self.free:
+                b = self.free.popleft()
+            else:                                           # evict the least recently used cached block
+                b, _ = self.lru.popitem(last=False)
+                del self.block_of[self.key_of.pop(b)]
+            self.ref[b] = 1
+            out.append(b)
+        return out
+
+    def register(self, blocks: Seq[int], keys: Seq[int]):
+        """Publish full prompt blocks (after their KV is written) for later requests."""
+        if not self.cache_enabled:
+            return
+        for b, k in zip(blocks, keys):
+            if k not in self.block_of and b not in self.key_of:
+                self.block_of[k] = b
+                self.key_of[b] = k
 
     def release(self, blocks: Seq[int]):
-        self.free.extend(blocks)
+        for b in blocks:
+            self.ref[b] -= 1
+            if self.ref[b] == 0:
+                if b in self.key_of:
+                    self.lru[b] = None
+                else:
+                    self.free.append(b)
 
     @property
     def n_free(self) -> int:
-        return len(self.free)
+        return len(self.free) + len(self.lru)
 
 
 class _Seq:
     __slots__ = ("req", "fut", "tokens", "n_prompt", "n_prefilled", "blocks", "t_submit", "t_admit", "t_first",
-                 "t_done", "gen", "max_new", "done", "text_cache", "row", "n_fed")
+                 "t_done", "gen", "max_new", "done", "text_cache", "row", "n_fed", "keys", "n_cached")
 
     def __init__(self, req: GenRequest, fut: Future):
         self.req = req
@@ -106,6 +169,8 @@ class _Seq:
         self.done = False
         self.row = -1          # decode-batch row (stable for the sequence's life)
         self.n_fed = 0         # positions whose KV is written or being written
+        self.keys: List[int] = []   # prefix-cache chain hashes of the full prompt blocks
+        self.n_cached = 0      # prompt tokens whose KV came from the prefix cache
 
     @property
     def generated(self) -> List[int]:
@@ -116,7 +181,7 @@ class Engine:
     def __init__(self, model: LlamaModel, tokenizer=None, max_batch: int = 64, block_size: int = 16,
                  num_blocks: Optional[int] = None, max_prefill_tokens: int = 2048, use_graphs: bool = True,
                  ctx: Optional[int] = None, kv_mem_fraction: float = 0.5, eos_ids: Seq[int] = (),
-                 prefill_attn: bool = True, async_decode: bool = True):
+                 prefill_attn: bool = True, async_decode: bool = True, prefix_cache: bool = True):
         self.model = model
         self.tok = tokenizer
         self.cfg = model.cfg
@@ -137,7 +202,7 @@ class Engine:
             num_blocks = self.tp.min_int(num_blocks)
         self.num_blocks = num_blocks
         self.kc, self.vc = model.kv_cache(num_blocks, block_size)
-        self.alloc = BlockAllocator(num_blocks)
+        self.alloc = BlockAllocator(num_blocks, cache=prefix_cache)
         self.max_prefill = max_prefill_tokens
         self.prefill_attn = prefill_attn      # MFMA flash-prefill attention (else per-token decode kernel)
         self.db = model.step_buffers(self.max_batch, self.max_batch, self.max_blocks)
@@ -288,10 +353,16 @@ class Engine:
             while self.waiting and len(self.running) < self.max_batch:
                 s = self.waiting[0]
                 need = math.ceil((s.n_prompt + s.max_new) / self.bs)
-                blocks = self.alloc.alloc(need)
+                # full prompt blocks, leaving >= 1 prompt token to prefill (its logits pick token 1)
+                s.keys = BlockAllocator.chain_keys(s.tokens, self.bs, (s.n_prompt - 1) // self.bs)
+                hit = self.alloc.match(s.keys)
+                blocks = self.alloc.alloc(need - len(hit))
                 if blocks is None:
+                    self.alloc.release(hit)
                     break
-                s.blocks = blocks
+                s.blocks = hit + blocks
+                s.n_prefilled = s.n_cached = len(hit) * self.bs
+                self.alloc.hits += s.n_cached
                 s.t_admit = time.monotonic()
                 self.waiting.popleft()
                 self.running.append(s)
@@ -328,6 +399,7 @@ class Engine:
             if s.n_prefilled >= s.n_prompt:
                 rows.append(T - 1)
                 finishing.append(s)
+                self.alloc.register(s.blocks[:len(s.keys)], s.keys)
         nrows = max(1, len(rows))
         need = any(not s.req.params.greedy for s in finishing)
         self._ctrl(_OP_PREFILL, T, nrows, need, rows + [0] * (nrows - len(rows)), len(batch), self.h_meta_p, pad)
@@ -676,4 +748,5 @@ class Engine:
     def stats(self) -> dict:
         return dict(self.counters, running=len(self.running), waiting=len(self.waiting),
                     kv_blocks_free=self.alloc.n_free, kv_blocks_total=self.num_blocks,
+                    prefix_cache_hit_tokens=self.alloc.hits, prefix_cache_blocks=len(self.alloc.block_of),
                     graphs=sorted(self.graphs))

@@ -42,6 +42,7 @@ class ModelSpec:
     attention_scale: float = 0.0  # 0 -> 1/sqrt(head_dim)
     logit_scale: float = 1.0
     publisher: str = "synthetic"
+    rope_freqs: bool = False      # Llama-3.1-style `rope_freqs.weight` frequency factors
 
     @property
     def head_dim(self) -> int:
@@ -60,6 +61,7 @@ SPECS: Dict[str, ModelSpec] = {
     "tiny-llama": ModelSpec("tiny-llama", "llama", 2, 512, 4, 2, 768, 1024, 512, 10000.0),
     "tiny-mixtral": ModelSpec("tiny-mixtral", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,
                               n_expert=4, n_expert_used=2, tokenizer="llama"),
+    "tiny-llama31": ModelSpec("tiny-llama31", "llama", 2, 512, 4, 2, 768, 1024, 512, 500000.0, rope_freqs=True),
     "tiny-granite": ModelSpec("tiny-granite", "granite", 2, 512, 8, 2, 768, 1000, 512, 10000.0,
                               tied_embeddings=True, embedding_scale=12.0, residual_scale=0.22,
                               attention_scale=0.015625, logit_scale=8.0),
@@ -87,6 +89,8 @@ def tensor_plan(spec: ModelSpec, ftype: str):
     nq, nkv = spec.n_head * hd, spec.n_kv_head * hd
     std = 0.02
     plan = [("token_embd.weight", (spec.vocab, d), emb_t, std * 2)]
+    if spec.rope_freqs:
+        plan.append(("rope_freqs.weight", (hd // 2,), GGMLType.F32, -2.0))
     for i in range(spec.n_layer):
         p = f"blk.{i}."
         mb = use_more_bits(i, spec.n_layer)
@@ -176,6 +180,16 @@ def _metadata(w: GGUFWriter, spec: ModelSpec, ftype: str, name: str):
         w.add("tokenizer.chat_template", tsyn.MISTRAL_TEMPLATE)
 
 
+def llama3_rope_factors(head_dim: int, base: float, factor: float = 8.0, low: float = 1.0, high: float = 4.0,
+                        orig_ctx: int = 8192) -> np.ndarray:
+    """Per-frequency divisors of Llama-3.1 RoPE scaling (what convert_hf_to_gguf stores in rope_freqs)."""
+    inv = 1.0 / (base ** (np.arange(0, head_dim, 2, dtype=np.float64) / head_dim))
+    wl = 2 * np.pi / inv
+    lo_wl, hi_wl = orig_ctx / low, orig_ctx / high
+    smooth = (orig_ctx / wl - low) / (high - low)
+    return np.where(wl < hi_wl, 1.0, np.where(wl > lo_wl, factor, 1.0 / ((1 - smooth) / factor + smooth)))
+
+
 def write_synthetic_gguf(path: str, spec_name: str, ftype: str = "Q4_K_M", seed: int = 0,
                          progress=None, spec: Optional[ModelSpec] = None) -> str:
     spec = spec or SPECS[spec_name]
@@ -184,7 +198,10 @@ def write_synthetic_gguf(path: str, spec_name: str, ftype: str = "Q4_K_M", seed:
     _metadata(w, spec, ftype, os.path.splitext(os.path.basename(path))[0])
     for name, shape, gt, std in tensor_plan(spec, ftype):
         n = int(np.prod(shape))
-        if std < 0:   # norm weights: ~1
+        if std == -2.0:   # rope frequency factors (llama.cpp llama3 recipe: factor 8, low/high 1/4)
+            def prod(n=n):
+                return llama3_rope_factors(2 * n, spec.rope_base).astype(np.float32).view(np.uint8)
+        elif std < 0:   # norm weights: ~1
             def prod(n=n):
                 return (1.0 + 0.1 * rng.standard_normal(n).astype(np.float32)).view(np.uint8)
         else:

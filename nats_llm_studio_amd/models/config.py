@@ -27,6 +27,7 @@ class ModelConfig:
     attention_scale: float = 0.0
     logit_scale: float = 1.0
     rope_neox: bool = False
+    rope_pos_scale: float = 1.0      # 1 / rope.scaling.factor for linear scaling
 
     @property
     def attn_softmax_scale(self) -> float:
@@ -64,4 +65,6 @@ class ModelConfig:
             tied_embeddings="output.weight" not in set(tensor_names) if tensor_names else False,
             embedding_scale=float(g("embedding_scale", 1.0)), residual_scale=float(g("residual_scale", 1.0)),
             attention_scale=float(g("attention.scale", 0.0)), logit_scale=float(g("logit_scale", 1.0)),
+            rope_pos_scale=(1.0 / float(g("rope.scaling.factor", 1.0) or 1.0)
+                            if str(g("rope.scaling.type", "none")) == "linear" else 1.0),
         )

@@ -115,7 +115,8 @@ class LlamaModel:
         self.vocab_lo, self.vocab_hi = self._vocab_range()
         self.weight_bytes = 0
         self._load()
-        self.cs = ops.rope_table(cfg.ctx, self.D, cfg.rope_base, self.device)
+        ff = reader.dequantized("rope_freqs.weight") if "rope_freqs.weight" in reader.tensors else None
+        self.cs = ops.rope_table(cfg.ctx, self.D, cfg.rope_base, self.device, ff, cfg.rope_pos_scale)
 
     # ------------------------------------------------------------------ loading
     def _vocab_range(self):

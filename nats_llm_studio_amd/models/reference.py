@@ -32,7 +32,9 @@ class ReferenceModel:
         cfg = self.cfg
         D = x.shape[-1]
         inv = 1.0 / (cfg.rope_base ** (torch.arange(0, D, 2, dtype=torch.float64) / D))
-        ang = (pos.double()[:, None] * inv[None, :]).float()
+        if "rope_freqs.weight" in self.r.tensors:         # Llama-3.1+ frequency factors
+            inv = inv / self.w("rope_freqs.weight").double().reshape(-1)[:D // 2]
+        ang = ((pos.double() * cfg.rope_pos_scale)[:, None] * inv[None, :]).float()
         c, s = torch.cos(ang)[:, None, :], torch.sin(ang)[:, None, :]
         x0, x1 = x[..., 0::2], x[..., 1::2]
         return torch.stack([x0 * c - x1 * s, x0 * s + x1 * c], dim=-1).flatten(-2)

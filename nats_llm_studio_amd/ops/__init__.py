@@ -304,9 +304,20 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, M: int, eps: fl
     return out
 
 
-def rope_table(max_pos: int, head_dim: int, base: float, device) -> torch.Tensor:
+def rope_inv_freq(head_dim: int, base: float, freq_factors=None) -> np.ndarray:
+    """theta_i = base^(-2i/D), divided by GGUF `rope_freqs.weight` when present (Llama-3.1+ long-context
+    frequency scaling, llama.cpp `rope_freq_factors`)."""
     inv = 1.0 / (base ** (np.arange(0, head_dim, 2, dtype=np.float64) / head_dim))
-    ang = np.arange(max_pos, dtype=np.float64)[:, None] * inv[None, :]
+    if freq_factors is not None:
+        inv = inv / np.asarray(freq_factors, dtype=np.float64).reshape(-1)[:head_dim // 2]
+    return inv
+
+
+def rope_table(max_pos: int, head_dim: int, base: float, device, freq_factors=None,
+               pos_scale: float = 1.0) -> torch.Tensor:
+    """[max_pos, D/2, 2] (cos, sin). `pos_scale` < 1: linear RoPE scaling (`rope.scaling.type=linear`)."""
+    inv = rope_inv_freq(head_dim, base, freq_factors)
+    ang = (np.arange(max_pos, dtype=np.float64) * pos_scale)[:, None] * inv[None, :]
     cs = np.stack([np.cos(ang), np.sin(ang)], axis=-1).astype(np.float32)   # [P, D/2, 2]
     return torch.from_numpy(cs).to(device)
 

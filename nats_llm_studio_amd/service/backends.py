@@ -206,8 +206,13 @@ class EngineBackend:
         params = SamplingParams.from_request(req, default_max=self.cfg.default_max_tokens)
         on_token = None
         if stream_cb is not None:
-            def on_token(t, _tok=tok):
-                stream_cb(_tok.decode([t]))
+            from ..tokenizer.bpe import StreamDecoder
+            sd = StreamDecoder(tok)
+
+            def on_token(t, _sd=sd):
+                d = _sd.push(t)
+                if d:
+                    stream_cb(d)
         fut = eng.submit(GenRequest(ids, params, on_token=on_token, deadline=deadline))
         ctx = eng.ctx
 

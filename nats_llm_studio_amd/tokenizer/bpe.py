@@ -252,3 +252,28 @@ def tokenizer_from_metadata(md: dict):
                                 None if eos is None else int(eos), add_bos,
                                 bool(md.get("tokenizer.ggml.add_space_prefix", True)))
     raise NotImplementedError(f"tokenizer model {model!r}")
+
+
+class StreamDecoder:
+    """Incremental detokenisation for streamed deltas (`stream: true`).
+
+    Decoding one token at a time splits multi-byte UTF-8 characters (a CJK character or an emoji
+    is often 2-4 byte-level tokens) and drops SentencePiece word-boundary spaces. This keeps a
+    short window: `prefix` = text of ids[p:r] already emitted, `full` = text of ids[p:]; the delta
+    is what `full` adds, held back while it still ends in an incomplete sequence (U+FFFD)."""
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.ids = []
+        self.p = 0      # window start
+        self.r = 0      # end of the already-emitted part of the window
+
+    def push(self, t: int) -> str:
+        self.ids.append(int(t))
+        prefix = self.tok.decode(self.ids[self.p:self.r]) if self.r > self.p else ""
+        full = self.tok.decode(self.ids[self.p:])
+        if full.endswith("�") or len(full) <= len(prefix):
+            return ""
+        delta = full[len(prefix):]
+        self.p, self.r = self.r, len(self.ids)
+        return delta

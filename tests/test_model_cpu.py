@@ -1,0 +1,41 @@
+"""Whole-model CPU path (torch reference ops behind the same LlamaModel/Engine code the GPU runs)
+vs the independent fp32 oracle (models/reference.py), incl. Llama-3.1 `rope_freqs` frequency factors."""
+import numpy as np
+import pytest
+import torch
+
+from nats_llm_studio_amd.gguf.reader import GGUFReader
+from nats_llm_studio_amd.models.llama import LlamaModel
+from nats_llm_studio_amd.models.reference import ReferenceModel
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama31", "tiny-granite"])
+def test_cpu_prefill_matches_reference(tiny_models, name):
+    r = GGUFReader(tiny_models[name])
+    m = LlamaModel(r, "cpu")
+    ref = ReferenceModel(r)
+    S = 24
+    ids = list(np.random.default_rng(0).integers(0, 900, S))
+    b = m.step_buffers(64, 4, 8)
+    kc, vc = m.kv_cache(8, 16)
+    b.ids[:S] = torch.tensor(ids, dtype=torch.int32)
+    b.pos[:S] = torch.arange(S)
+    b.slot[:S] = torch.arange(S)
+    b.tok_seq[:S] = 0
+    b.ctx_len[:S] = torch.arange(S) + 1
+    b.block_tables[0] = torch.arange(8)
+    m.forward(b, kc, vc, S, 16)
+    rl = ref.logits(ids)
+    err = (b.logits[:S] - rl).abs().max().item()
+    assert err < 0.02 * rl.abs().max().item(), err
+
+
+def test_rope_freqs_change_the_rotation(tiny_models):
+    """The Llama-3.1 factors are applied (a model that ignored them would differ from the oracle)."""
+    from nats_llm_studio_amd import ops
+    r = GGUFReader(tiny_models["tiny-llama31"])
+    ff = r.dequantized("rope_freqs.weight")
+    assert ff.max() > 1.0
+    m = LlamaModel(r, "cpu")
+    plain = ops.rope_table(m.cfg.ctx, m.D, m.cfg.rope_base, "cpu")
+    assert not torch.allclose(m.cs[100], plain[100])

@@ -43,3 +43,17 @@ def test_multipart_content(tiny_models):
     ct = ChatTemplate(md["tokenizer.chat_template"])
     s = ct.render([{"role": "user", "content": [{"type": "text", "text": "a"}, {"type": "text", "text": "b"}]}])
     assert "<|start_of_role|>user<|end_of_role|>ab" in s
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite"])
+def test_stream_decoder_reassembles_text(tiny_models, name):
+    """Streamed deltas concatenate to the full decode: multi-byte UTF-8 split over byte tokens is held
+    back until complete, SentencePiece word spaces survive token-by-token emission."""
+    from nats_llm_studio_amd.tokenizer.bpe import StreamDecoder
+    tok = tokenizer_from_metadata(GGUFReader(tiny_models[name]).metadata)
+    for t in TEXTS:
+        ids = tok.encode(t, add_bos=False)
+        sd = StreamDecoder(tok)
+        deltas = [sd.push(i) for i in ids]
+        assert "".join(deltas) == tok.decode(ids), (name, t, deltas)
+        assert all("�" not in d for d in deltas)
