@@ -129,6 +129,7 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
 // `ks` > 1: the QKV projection left split-K partial slabs (qkv = ks slabs of [T][ldqkv], stride
 // `slab` floats) and this kernel sums them in fixed order while rotating (fused reduce + RoPE).
 __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, long ldqkv, int ks, long slab,
+                                                      const float* __restrict__ bias,
                                                       const int* __restrict__ pos,
                                                       const int* __restrict__ slot,
                                                       const float* __restrict__ cs,
@@ -142,6 +143,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
     float4 v = *reinterpret_cast<const float4*>(row + col);
     for (int k = 1; k < ks; ++k) {
       const float4 u = *reinterpret_cast<const float4*>(row + (size_t)k * slab + col);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    if (bias) {     // QKV projection bias (Qwen2), added before the rotation
+      const float4 u = *reinterpret_cast<const float4*>(bias + col);
       v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
     }
     return v;
@@ -343,10 +348,11 @@ int nls_splitk_add_rmsnorm(const float* ws, int ks, int M, float alpha, float* x
   return (int)hipGetLastError();
 }
 
-int nls_rope_kv(const float* qkv, long ldqkv, int ks, long slab, const int* pos, const int* slot, const float* cs,
-                void* q_out, long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox, void* stream) {
-  if (ks < 1) return -1;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, pos, slot, cs,
+int nls_rope_kv(const float* qkv, long ldqkv, int ks, long slab, const float* bias, const int* pos, const int* slot,
+                const float* cs, void* q_out, long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox,
+                void* stream) {
+  if (ks < 1 || D % 8) return -1;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, bias, pos, slot, cs,
                      (__bf16*)q_out, ldq, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, D, neox);
   return (int)hipGetLastError();
 }

@@ -226,7 +226,7 @@ class Engine:
         if tokenizer is not None and getattr(tokenizer, "eos_id", None) is not None:
             self.eos.add(int(tokenizer.eos_id))
         if tokenizer is not None:
-            for name in ("<|eot_id|>", "<|end_of_text|>", "<|eom_id|>", "</s>"):
+            for name in ("<|eot_id|>", "<|end_of_text|>", "<|eom_id|>", "</s>", "<|im_end|>", "<|endoftext|>"):
                 tid = tokenizer.vocab.get(name) if hasattr(tokenizer, "vocab") else None
                 if tid is not None:
                     self.eos.add(int(tid))

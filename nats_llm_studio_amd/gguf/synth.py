@@ -61,6 +61,8 @@ SPECS: Dict[str, ModelSpec] = {
     "tiny-llama": ModelSpec("tiny-llama", "llama", 2, 512, 4, 2, 768, 1024, 512, 10000.0),
     "tiny-mixtral": ModelSpec("tiny-mixtral", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,
                               n_expert=4, n_expert_used=2, tokenizer="llama"),
+    "qwen2.5-7b": ModelSpec("qwen2.5-7b", "qwen2", 28, 3584, 28, 4, 18944, 152064, 32768, 1e6, eps=1e-6),
+    "tiny-qwen2": ModelSpec("tiny-qwen2", "qwen2", 2, 512, 4, 2, 768, 1000, 512, 1e6, eps=1e-6, tied_embeddings=True),
     "tiny-llama31": ModelSpec("tiny-llama31", "llama", 2, 512, 4, 2, 768, 1024, 512, 500000.0, rope_freqs=True),
     "tiny-granite": ModelSpec("tiny-granite", "granite", 2, 512, 8, 2, 768, 1000, 512, 10000.0,
                               tied_embeddings=True, embedding_scale=12.0, residual_scale=0.22,
@@ -100,6 +102,8 @@ def tensor_plan(spec: ModelSpec, ftype: str):
             (p + "attn_k.weight", (nkv, d), base, std),
             (p + "attn_v.weight", (nkv, d), more if mb else base, std),
             (p + "attn_output.weight", (d, nq), base, std / np.sqrt(2 * spec.n_layer) * 4),
+        ] + ([(p + "attn_q.bias", (nq,), GGMLType.F32, -3.0), (p + "attn_k.bias", (nkv,), GGMLType.F32, -3.0),
+              (p + "attn_v.bias", (nkv,), GGMLType.F32, -3.0)] if spec.arch == "qwen2" else []) + [
             (p + "ffn_norm.weight", (d,), GGMLType.F32, -1.0),
         ]
         if spec.n_expert:
@@ -148,7 +152,12 @@ def _metadata(w: GGUFWriter, spec: ModelSpec, ftype: str, name: str):
         w.add(f"{a}.attention.scale", float(spec.attention_scale))
         w.add(f"{a}.logit_scale", float(spec.logit_scale))
     if spec.tokenizer == "gpt2":
-        if a == "granite":
+        if a == "qwen2":
+            tokens, types, merges, ids = tsyn.bytelevel_vocab(spec.vocab, tsyn.QWEN2_SPECIALS)
+            bos, eos = ids["<|endoftext|>"], ids["<|im_end|>"]
+            tmpl, add_bos = tsyn.CHATML_TEMPLATE, False
+            pre = "qwen2"
+        elif a == "granite":
             specials = ["<|end_of_text|>", "<|start_of_role|>", "<|end_of_role|>", "<|tool_call|>"]
             tokens, types, merges, ids = tsyn.bytelevel_vocab(spec.vocab, specials)
             bos = eos = ids["<|end_of_text|>"]
@@ -201,6 +210,9 @@ def write_synthetic_gguf(path: str, spec_name: str, ftype: str = "Q4_K_M", seed:
         if std == -2.0:   # rope frequency factors (llama.cpp llama3 recipe: factor 8, low/high 1/4)
             def prod(n=n):
                 return llama3_rope_factors(2 * n, spec.rope_base).astype(np.float32).view(np.uint8)
+        elif std == -3.0:   # projection biases: small
+            def prod(n=n):
+                return (0.1 * rng.standard_normal(n)).astype(np.float32).view(np.uint8)
         elif std < 0:   # norm weights: ~1
             def prod(n=n):
                 return (1.0 + 0.1 * rng.standard_normal(n).astype(np.float32)).view(np.uint8)

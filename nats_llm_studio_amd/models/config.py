@@ -3,7 +3,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
-SUPPORTED_ARCHS = ("llama", "granite", "mistral", "mixtral")
+SUPPORTED_ARCHS = ("llama", "granite", "mistral", "mixtral", "qwen2")
+NEOX_ARCHS = ("qwen2",)           # llama.cpp LLAMA_ROPE_TYPE_NEOX families
 
 
 @dataclass
@@ -65,6 +66,7 @@ class ModelConfig:
             tied_embeddings="output.weight" not in set(tensor_names) if tensor_names else False,
             embedding_scale=float(g("embedding_scale", 1.0)), residual_scale=float(g("residual_scale", 1.0)),
             attention_scale=float(g("attention.scale", 0.0)), logit_scale=float(g("logit_scale", 1.0)),
+            rope_neox=a in NEOX_ARCHS,
             rope_pos_scale=(1.0 / float(g("rope.scaling.factor", 1.0) or 1.0)
                             if str(g("rope.scaling.type", "none")) == "linear" else 1.0),
         )

@@ -58,6 +58,7 @@ class LayerWeights:
     wo: QWeight
     gateup: Optional[QWeight] = None
     down: Optional[QWeight] = None
+    qkv_bias: Optional[torch.Tensor] = None     # Qwen2: f32 [(Hq + 2*Hkv) * D] (this shard)
     # MoE
     router: Optional[QWeight] = None
     exp_gateup: List[QWeight] = field(default_factory=list)
@@ -189,6 +190,11 @@ class LlamaModel:
             qkv = [Seg(wq, 0), Seg(wk, Hq * D), Seg(wv, (Hq + Hkv) * D)]
             wo = self._matrix(p + "attn_output.weight", None, (r * Hq * D, (r + 1) * Hq * D))
             lw = LayerWeights(self._vec(p + "attn_norm.weight"), self._vec(p + "ffn_norm.weight"), qkv, wo)
+            if p + "attn_q.bias" in self.reader.tensors:
+                bq = self.reader.dequantized(p + "attn_q.bias").reshape(-1)[r * Hq * D:(r + 1) * Hq * D]
+                bk = self.reader.dequantized(p + "attn_k.bias").reshape(-1)[r * Hkv * D:(r + 1) * Hkv * D]
+                bv = self.reader.dequantized(p + "attn_v.bias").reshape(-1)[r * Hkv * D:(r + 1) * Hkv * D]
+                lw.qkv_bias = torch.from_numpy(np.concatenate([bq, bk, bv]).astype(np.float32)).to(self.device)
             if cfg.n_expert:
                 lw.router = self._matrix(p + "ffn_gate_inp.weight")
                 F = self.exp_ffn
@@ -285,7 +291,7 @@ class LlamaModel:
             if L > 0 and not fused_prev:
                 ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
             ops.qkv_rope_kv(lw.qkv, b.h, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
-                            cfg.rope_neox)
+                            cfg.rope_neox, bias=lw.qkv_bias)
             if qblocks is not None and nqb > 0 and ops.attention_prefill_ok(Hq, Hkv, D):
                 ops.attention_prefill(b.q, kc[L], vc[L], b.block_tables, qblocks, nqb, b.tok_seq, b.ctx_len, b.ao,
                                       T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)

@@ -36,6 +36,9 @@ class ReferenceModel:
             inv = inv / self.w("rope_freqs.weight").double().reshape(-1)[:D // 2]
         ang = ((pos.double() * cfg.rope_pos_scale)[:, None] * inv[None, :]).float()
         c, s = torch.cos(ang)[:, None, :], torch.sin(ang)[:, None, :]
+        if cfg.rope_neox:                                  # (i, i + D/2) pairs (Qwen2)
+            x0, x1 = x[..., :D // 2], x[..., D // 2:]
+            return torch.cat([x0 * c - x1 * s, x0 * s + x1 * c], dim=-1)
         x0, x1 = x[..., 0::2], x[..., 1::2]
         return torch.stack([x0 * c - x1 * s, x0 * s + x1 * c], dim=-1).flatten(-2)
 
@@ -52,9 +55,9 @@ class ReferenceModel:
         for i in range(cfg.n_layer):
             p = f"blk.{i}."
             h = self._rms(x, self.w(p + "attn_norm.weight"), cfg.eps)
-            q = (h @ self.w(p + "attn_q.weight").t()).view(S, H, D)
-            k = (h @ self.w(p + "attn_k.weight").t()).view(S, Hkv, D)
-            v = (h @ self.w(p + "attn_v.weight").t()).view(S, Hkv, D)
+            q, k, v = (h @ self.w(p + f"attn_{n}.weight").t() + (self.w(p + f"attn_{n}.bias")
+                       if p + f"attn_{n}.bias" in self.r.tensors else 0.0) for n in "qkv")
+            q, k, v = q.view(S, H, D), k.view(S, Hkv, D), v.view(S, Hkv, D)
             q, k = self._rope(q, pos), self._rope(k, pos)
             k = k.repeat_interleave(G, dim=1)
             v = v.repeat_interleave(G, dim=1)

@@ -323,14 +323,19 @@ def rope_table(max_pos: int, head_dim: int, base: float, device, freq_factors=No
 
 
 def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.Tensor, q_out: torch.Tensor,
-            kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, neox: bool = False):
-    """kc/vc: [slots, Hkv, D] bf16 for one layer. slot (int32) < 0 skips the cache write."""
+            kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, neox: bool = False,
+            bias: Optional[torch.Tensor] = None):
+    """kc/vc: [slots, Hkv, D] bf16 for one layer. slot (int32) < 0 skips the cache write.
+    `bias` (f32 [(Hq+2*Hkv)*D], Qwen2 QKV bias) is added before the rotation."""
     if qkv.is_cuda:
-        _lib.check(_lib.lib().nls_rope_kv(qkv.data_ptr(), qkv.stride(0), 1, 0, pos.data_ptr(), slot.data_ptr(),
-                                          cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(),
-                                          vc.data_ptr(), T, Hq, Hkv, D, int(neox), _stream_ptr(qkv)), "nls_rope_kv")
+        _lib.check(_lib.lib().nls_rope_kv(qkv.data_ptr(), qkv.stride(0), 1, 0, _p(bias), pos.data_ptr(),
+                                          slot.data_ptr(), cs.data_ptr(), q_out.data_ptr(), q_out.stride(0),
+                                          kc.data_ptr(), vc.data_ptr(), T, Hq, Hkv, D, int(neox), _stream_ptr(qkv)),
+                   "nls_rope_kv")
         return
     x = qkv[:T].float()
+    if bias is not None:
+        x = x + bias.float()[None, :x.shape[1]]
     p = pos[:T].long()
     c, s = cs[p, :, 0], cs[p, :, 1]                      # [T, D/2]
 
@@ -357,7 +362,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.
 
 def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
                 cs: torch.Tensor, q_out: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int,
-                D: int, neox: bool = False, cfg=None):
+                D: int, neox: bool = False, cfg=None, bias: Optional[torch.Tensor] = None):
     """QKV projection + RoPE + paged KV append. With a split-K launch config the partial slabs
     are summed inside the RoPE kernel (no separate reduce pass, no fp32 qkv round trip)."""
     if h.is_cuda and all(s.xmap is None for s in segs):
@@ -373,12 +378,12 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
             st = _stream_ptr(h)
             _lib.check(L.nls_qgemv(arr, len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
                                    EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
-            _lib.check(L.nls_rope_kv(ws.data_ptr(), ncol, ks, T * ncol, pos.data_ptr(), slot.data_ptr(),
+            _lib.check(L.nls_rope_kv(ws.data_ptr(), ncol, ks, T * ncol, _p(bias), pos.data_ptr(), slot.data_ptr(),
                                      cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(), vc.data_ptr(),
                                      T, Hq, Hkv, D, int(neox), st), "nls_rope_kv")
             return
     qgemv(segs, h, qkv, T)
-    rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox)
+    rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox, bias)
 
 
 def embed(ids: torch.Tensor, w: QWeight, out: torch.Tensor, T: int, scale: float = 1.0):

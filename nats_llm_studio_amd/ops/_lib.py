@@ -31,7 +31,7 @@ _SIGS = {
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
     "nls_splitk_add_rmsnorm": [c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int,
                                c_float, c_void_p],
-    "nls_rope_kv": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
+    "nls_rope_kv": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                     c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nls_embed": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_float, c_void_p],
     "nls_dequant": [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p],

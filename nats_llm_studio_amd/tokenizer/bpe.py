@@ -19,6 +19,9 @@ import regex as re
 # Llama-3 pre-tokeniser (llama.cpp LLAMA_VOCAB_PRE_TYPE_LLAMA3)
 LLAMA3_PRETOK = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*"
                  r"|\s*[\r\n]+|\s+(?!\S)|\s+")
+# Qwen2 pre-tokeniser (llama.cpp LLAMA_VOCAB_PRE_TYPE_QWEN2): single digits
+QWEN2_PRETOK = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*"
+                r"|\s*[\r\n]+|\s+(?!\S)|\s+")
 GPT2_PRETOK = r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+"
 
 TOKEN_TYPE_NORMAL = 1
@@ -99,7 +102,8 @@ class ByteLevelBPE(_Base):
             self.ranks[(a, b)] = i
         self.b2u = bytes_to_unicode()
         self.u2b = {v: k for k, v in self.b2u.items()}
-        self.pretok = re.compile(GPT2_PRETOK if pre in ("gpt2", "default") else LLAMA3_PRETOK)
+        self.pretok = re.compile(GPT2_PRETOK if pre in ("gpt2", "default") else
+                                 QWEN2_PRETOK if pre == "qwen2" else LLAMA3_PRETOK)
         self._cache: Dict[str, List[int]] = {}
 
     def _bpe(self, word: str) -> List[str]:

@@ -169,3 +169,14 @@ def spm_vocab(n_vocab: int, n_merges: int = 400):
         scores.append(-1e9)
         k += 1
     return tokens[:n_vocab], types[:n_vocab], scores[:n_vocab]
+
+
+# Qwen2 / ChatML
+QWEN2_SPECIALS = ["<|endoftext|>", "<|im_start|>", "<|im_end|>"]
+CHATML_TEMPLATE = (
+    "{% for message in messages %}"
+    "{% if loop.first and message['role'] != 'system' %}<|im_start|>system\nYou are a helpful assistant.<|im_end|>\n{% endif %}"
+    "<|im_start|>{{ message['role'] }}\n{{ message['content'] }}<|im_end|>\n"
+    "{% endfor %}"
+    "{% if add_generation_prompt %}<|im_start|>assistant\n{% endif %}"
+)

@@ -19,7 +19,7 @@ def tiny_models(tmp_path_factory):
     from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
     d = tmp_path_factory.mktemp("models")
     out = {}
-    for name in ("tiny-llama", "tiny-mixtral", "tiny-granite", "tiny-llama31"):
+    for name in ("tiny-llama", "tiny-mixtral", "tiny-granite", "tiny-llama31", "tiny-qwen2"):
         p = str(d / f"{name}.gguf")
         write_synthetic_gguf(p, name, "Q4_K_M", seed=0)
         out[name] = p

@@ -9,7 +9,7 @@ from nats_llm_studio_amd.models.llama import LlamaModel
 from nats_llm_studio_amd.models.reference import ReferenceModel
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama31", "tiny-granite"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama31", "tiny-granite", "tiny-qwen2"])
 def test_cpu_prefill_matches_reference(tiny_models, name):
     r = GGUFReader(tiny_models[name])
     m = LlamaModel(r, "cpu")

@@ -12,7 +12,7 @@ from nats_llm_studio_amd.models.reference import ReferenceModel
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite", "tiny-llama31", "tiny-qwen2"])
 def test_prefill_logits_match_reference(gpu, tiny_models, name):
     r = GGUFReader(tiny_models[name])
     m = LlamaModel(r, gpu)

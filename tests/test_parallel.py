@@ -18,6 +18,7 @@ _TP_SPECS = {
     "llama": dataclasses.replace(SPECS["tiny-llama"], name="tp-llama", d_ff=1024),
     "mixtral": dataclasses.replace(SPECS["tiny-mixtral"], name="tp-mixtral"),
     "granite": dataclasses.replace(SPECS["tiny-granite"], name="tp-granite", d_ff=1024),
+    "qwen2": dataclasses.replace(SPECS["tiny-qwen2"], name="tp-qwen2", d_ff=1024),
 }
 PROMPTS = [[1, 5, 9, 200, 31, 7, 77], [1, 300, 301, 302]]
 
@@ -75,7 +76,8 @@ def _worker(rank, world, port, path, ep, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fam,ep", [("llama", False), ("granite", False), ("mixtral", False), ("mixtral", True)])
+@pytest.mark.parametrize("fam,ep", [("llama", False), ("granite", False), ("mixtral", False), ("mixtral", True),
+                                    ("qwen2", False)])
 def test_tp2_matches_tp1(tmp_path, fam, ep):
     spec = _TP_SPECS[fam]
     path = str(tmp_path / f"{spec.name}.gguf")

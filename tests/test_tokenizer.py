@@ -9,7 +9,7 @@ TEXTS = ["Hello world!", "The capital of France is Paris.", "  spaces  and\nnewl
          "def main(): return 42", ""]
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite", "tiny-qwen2"])
 def test_roundtrip(tiny_models, name):
     md = GGUFReader(tiny_models[name]).metadata
     tok = tokenizer_from_metadata(md)
@@ -45,7 +45,7 @@ def test_multipart_content(tiny_models):
     assert "<|start_of_role|>user<|end_of_role|>ab" in s
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-granite", "tiny-qwen2"])
 def test_stream_decoder_reassembles_text(tiny_models, name):
     """Streamed deltas concatenate to the full decode: multi-byte UTF-8 split over byte tokens is held
     back until complete, SentencePiece word spaces survive token-by-token emission."""
@@ -57,3 +57,13 @@ def test_stream_decoder_reassembles_text(tiny_models, name):
         deltas = [sd.push(i) for i in ids]
         assert "".join(deltas) == tok.decode(ids), (name, t, deltas)
         assert all("�" not in d for d in deltas)
+
+
+def test_qwen2_chatml_and_single_digit_pretokeniser(tiny_models):
+    md = GGUFReader(tiny_models["tiny-qwen2"]).metadata
+    tok = tokenizer_from_metadata(md)
+    ct = ChatTemplate(md["tokenizer.chat_template"])
+    s = ct.render([{"role": "user", "content": "Hi"}])
+    assert s.startswith("<|im_start|>system\n") and s.endswith("<|im_start|>assistant\n")
+    assert tok.tokens[tok.eos_id] == "<|im_end|>"
+    assert [p for p in tok.pretok.findall("x 2024")] == ["x", " ", "2", "0", "2", "4"]
