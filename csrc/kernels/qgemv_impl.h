@@ -53,7 +53,11 @@ DEVI unsigned long long argmax_key(float v, int idx) {
 
 DEVI float silu(float g) { return g / (1.f + __expf(-g)); }
 
-template <int T, int WAVES, int RT, int MT>
+// XL: the activation rows are first staged into LDS (batch <= a few rows, no row maps), so the
+// main loop's x reads are ds_reads and the VMEM queue holds only the weight stream: its in-order
+// vmcnt waits then never drain the DEPTH-deep weight prefetch (global x loads issued each step
+// would: waiting for step s's x also waits for every older weight reload).
+template <int T, int WAVES, int RT, int MT, bool XL = false>
 DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
@@ -70,12 +74,27 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   // a lane-conditional load would compile to a branch + vmcnt(0) per K-step that drains the
   // whole weight prefetch (cdna_hip_programming.md §5 "Three .s-level traps" (c)).
   const act_t* xr[MT];
+  if constexpr (XL) {
+    act_t* xs = reinterpret_cast<act_t*>(lds + (WAVES + 1) * RT * MT * 256);
+    const int kc = S.K >> 3;                       // 16-B chunks per row
+    for (int i = threadIdx.x; i < mcount * kc; i += WAVES * 64) {
+      const int row = i / kc, c = i - row * kc;
+      *reinterpret_cast<u32x4*>(xs + (size_t)row * S.K + c * 8) = ld16(a.x + (size_t)row * a.ldx + c * 8);
+    }
+    __syncthreads();
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = mt * 16 + r;
-    int src = m < mcount ? m : -1;
-    if (S.xmap) src = (m < mcount) ? S.xmap[m] : -1;
-    xr[mt] = a.x + (size_t)(src >= 0 ? src : 0) * a.ldx;
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + r;
+      xr[mt] = xs + (size_t)(m < mcount ? m : 0) * S.K;
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + r;
+      int src = m < mcount ? m : -1;
+      if (S.xmap) src = (m < mcount) ? S.xmap[m] : -1;
+      xr[mt] = a.x + (size_t)(src >= 0 ? src : 0) * a.ldx;
+    }
   }
   int rowc[RT];
 #pragma unroll
@@ -91,7 +110,11 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   // loop unrolled by two, so a buffer is reloaded (sb + 2) right after its dequant and no
   // register holding an in-flight load is ever copied (a copy would force vmcnt(0)).
   typedef typename RawOf<T>::type Raw;
-  Raw wA[RT], wB[RT];
+  // Weight-stream depth: 4 super-blocks in flight per wave for the K-quants (<= 68 VGPRs of raw
+  // blocks at RT = 1), 2 for the wide plain-float tiles. Decode at batch 1 is latency-bound on
+  // this stream (each wave owns only K/WAVES of a 16-row tile).
+  constexpr int DEPTH = (RT == 1 && sizeof(Raw) <= 80) ? 4 : 2;
+  Raw wA[RT], wB[RT], wC[RT], wD[RT];
   // All weight loads are unconditional (super-block index clamped into [sb0, sb1)): a
   // conditional load breaks hipcc's vmcnt bookkeeping at the join and it falls back to
   // vmcnt(0). The clamped tail reloads hit L2 and are never consumed.
@@ -101,6 +124,12 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
+    if constexpr (DEPTH == 4) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wC[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 2, sbl), g);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wD[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 3, sbl), g);
+    }
   }
   auto step = [&](Raw (&w)[RT], int sb) {
     // 1) activation fragments of this super-block (issued before this step's weight reload)
@@ -118,9 +147,9 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
     __builtin_amdgcn_sched_barrier(0);
-    // 3) reload the buffer two super-blocks ahead
+    // 3) reload the buffer DEPTH super-blocks ahead
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+    for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + DEPTH, sbl), g);
     __builtin_amdgcn_sched_barrier(0);
     // 4) MFMA
 #pragma unroll
@@ -135,11 +164,23 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     }
   };
   int sb = sb0;
-  for (; sb + 1 < sb1; sb += 2) {
-    step(wA, sb);
-    step(wB, sb + 1);
+  if constexpr (DEPTH == 4) {
+    for (; sb + 3 < sb1; sb += 4) {
+      step(wA, sb);
+      step(wB, sb + 1);
+      step(wC, sb + 2);
+      step(wD, sb + 3);
+    }
+    if (sb < sb1) step(wA, sb);
+    if (sb + 1 < sb1) step(wB, sb + 1);
+    if (sb + 2 < sb1) step(wC, sb + 2);
+  } else {
+    for (; sb + 1 < sb1; sb += 2) {
+      step(wA, sb);
+      step(wB, sb + 1);
+    }
+    if (sb < sb1) step(wA, sb);
   }
-  if (sb < sb1) step(wA, sb);
 
   // ---- cross-wave reduction through LDS -------------------------------------
   // red: [WAVES][RT][MT][4][64] ; tile: [RT*16 rows][MT*16 batch]
@@ -210,7 +251,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 // KSET 0: Q4_K/Q6_K (the Q4_K_M mix); KSET 1: Q5_K/Q6_K/Q8_0; KSET 2: plain F16/BF16/F32. Splitting the format
 // switch keeps the register budget of the quantised kernels small (a switch case's
 // VGPR demand is paid by every case).
-template <int WAVES, int RT, int MT, int KSET>
+template <int WAVES, int RT, int MT, int KSET, bool XL = false>
 __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tile = blockIdx.x;
@@ -222,22 +263,22 @@ __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArg
   const int row0 = (tile - S.tile_begin) * RT * 16;
   if constexpr (KSET == 0) {
     switch (S.type) {
-      case QT_Q4_K: gemv_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_Q4_K: gemv_tile<QT_Q4_K, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, a, lds); break;
       default: break;
     }
   } else if constexpr (KSET == 1) {
     switch (S.type) {
-      case QT_Q5_K: gemv_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_Q5_K: gemv_tile<QT_Q5_K, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, a, lds); break;
       default: break;
     }
   } else {
     switch (S.type) {
-      case QT_F16: gemv_tile<QT_F16, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_BF16: gemv_tile<QT_BF16, WAVES, RT, MT>(S, row0, a, lds); break;
-      case QT_F32: gemv_tile<QT_F32, WAVES, RT, MT>(S, row0, a, lds); break;
+      case QT_F16: gemv_tile<QT_F16, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_BF16: gemv_tile<QT_BF16, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_F32: gemv_tile<QT_F32, WAVES, RT, MT, XL>(S, row0, a, lds); break;
       default: break;
     }
   }
@@ -535,6 +576,16 @@ static __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks
 template <int WAVES, int RT, int MT, int KSET>
 int launch_t(const SegList& sl, int ntiles, const GemvArgs& a, hipStream_t st) {
   const size_t lds = (size_t)(WAVES + 1) * RT * MT * 256 * sizeof(float);
+  if constexpr (MT == 1) {      // stage the activation rows in LDS when they fit (batch-1 decode)
+    bool mapped = false;
+    for (int i = 0; i < sl.nseg; ++i) mapped |= sl.s[i].xmap != nullptr || sl.s[i].mcount != nullptr;
+    const size_t xbytes = (size_t)a.M * sl.s[0].K * sizeof(act_t);
+    if (!mapped && lds + xbytes <= 64 * 1024) {
+      hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, KSET, true>), dim3(ntiles), dim3(WAVES * 64), lds + xbytes,
+                         st, sl, a);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, KSET>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
   return (int)hipGetLastError();
 }
