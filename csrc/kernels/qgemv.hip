@@ -25,9 +25,10 @@ struct NlsSeg {
 // mode 3: large-M LDS-DMA GEMM (qgemm_dma.h; Q4_K/Q5_K/Q6_K only): 4 waves, `rt` = activation
 //         tiles per block (16: 256 rows, 8: 128 rows), optional split-K as mode 1.
 // Returns 0 on success, a hipError_t, or -1 on bad arguments.
-int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
-              float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
-              void* stream) {
+static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
+                      float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
+                      void* stream, const float* xf, long ldxf, const float* nw, float eps) {
+  if (xf && (mode != 0 || M > 16 || !nw)) return -1;
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
   if (mode == 3) {
     if (waves != 4 || (rt != 8 && rt != 16)) return -1;
@@ -69,7 +70,8 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
   }
   if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
   const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
-  GemvArgs a{(const act_t*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax, 0, M};
+  GemvArgs a{(const act_t*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax, 0, M,
+             xf, ldxf, nw, eps};
   const int mt = M > 64 ? 8 : (M + 15) / 16;
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
@@ -97,6 +99,20 @@ int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, lo
     return (int)hipGetLastError();
   }
   return launch(0, waves, rt, mt, sl, tiles, 1, nullptr, a, st, 1);
+}
+
+int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
+              float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
+              void* stream) {
+  return qgemv_impl(segs, nseg, x, ldx, y, ldy, M, alpha, epi, argmax, waves, rt, mode, ks, ws, stream, nullptr, 0,
+                    nullptr, 0.f);
+}
+
+// Path A with the input RMSNorm fused into the activation staging: x rows = f16(rmsnorm(xf) * nw).
+int nls_qgemv_norm(const NlsSeg* segs, int nseg, const float* xf, long ldxf, const float* nw, float eps, void* y,
+                   long ldy, int M, float alpha, int epi, void* argmax, int waves, int rt, void* stream) {
+  return qgemv_impl(segs, nseg, xf, 0, y, ldy, M, alpha, epi, argmax, waves, rt, 0, 1, nullptr, stream, xf, ldxf,
+                    nw, eps);
 }
 
 }  // extern "C"

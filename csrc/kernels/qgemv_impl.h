@@ -43,6 +43,9 @@ struct GemvArgs {
   int pad;            // path B split-K: total raw output columns
   unsigned long long* argmax;   // optional [M] packed (ordered value << 32 | ~idx)
   int m0, mtot;       // large-M split-K: first activation row of this block, total rows (slab index)
+  // optional fused input RMSNorm (path A, staged rows): x = f16(rmsnorm(xf[m]) * nw), xf f32
+  const float* xf; long ldxf;
+  const float* nw; float eps;
 };
 
 DEVI unsigned long long argmax_key(float v, int idx) {
@@ -76,10 +79,40 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   const act_t* xr[MT];
   if constexpr (XL) {
     act_t* xs = reinterpret_cast<act_t*>(lds + (WAVES + 1) * RT * MT * 256);
-    const int kc = S.K >> 3;                       // 16-B chunks per row
-    for (int i = threadIdx.x; i < mcount * kc; i += WAVES * 64) {
-      const int row = i / kc, c = i - row * kc;
-      *reinterpret_cast<u32x4*>(xs + (size_t)row * S.K + c * 8) = ld16(a.x + (size_t)row * a.ldx + c * 8);
+    if (a.xf) {
+      // fused RMSNorm of the residual rows (the decode-time `rmsnorm` launch folded into the GEMV
+      // that consumes it: every workgroup normalises the few rows itself, reading them from L2)
+      const int K = S.K;
+      typedef act_t act4 __attribute__((ext_vector_type(4)));
+      for (int m = 0; m < mcount; ++m) {
+        const float* xrow = a.xf + (size_t)m * a.ldxf;
+        float ss = 0.f;
+        for (int i = threadIdx.x * 4; i < K; i += WAVES * 256) {
+          const float4 v = *reinterpret_cast<const float4*>(xrow + i);
+          ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+        if (lane == 0) lds[wave] = ss;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) tot += lds[w];
+        __syncthreads();
+        const float inv = rsqrtf(tot / (float)K + a.eps);
+        for (int i = threadIdx.x * 4; i < K; i += WAVES * 256) {
+          const float4 v = *reinterpret_cast<const float4*>(xrow + i);
+          const float4 w = *reinterpret_cast<const float4*>(a.nw + i);
+          *reinterpret_cast<act4*>(xs + (size_t)m * K + i) =
+              act4{(act_t)(v.x * inv * w.x), (act_t)(v.y * inv * w.y), (act_t)(v.z * inv * w.z), (act_t)(v.w * inv * w.w)};
+        }
+      }
+    } else {
+      const int kc = S.K >> 3;                       // 16-B chunks per row
+      for (int i = threadIdx.x; i < mcount * kc; i += WAVES * 64) {
+        const int row = i / kc, c = i - row * kc;
+        *reinterpret_cast<u32x4*>(xs + (size_t)row * S.K + c * 8) = ld16(a.x + (size_t)row * a.ldx + c * 8);
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -586,6 +619,7 @@ int launch_t(const SegList& sl, int ntiles, const GemvArgs& a, hipStream_t st) {
       return (int)hipGetLastError();
     }
   }
+  if (a.xf) return -1;          // fused input norm needs the staged (MT = 1, unmapped, fitting) path
   hipLaunchKernelGGL((qgemv_kernel<WAVES, RT, MT, KSET>), dim3(ntiles), dim3(WAVES * 64), lds, st, sl, a);
   return (int)hipGetLastError();
 }

@@ -188,9 +188,38 @@ def gemv_config(segs: Sequence[Seg], M: int):
     return tuning.select(segs, M)
 
 
+NORM_FUSE_LDS = 54 * 1024      # staged-row budget of the fused-norm GEMV (64 KiB LDS minus the reduce area)
+
+
+def norm_fusable(M: int, K: int) -> bool:
+    """Can a path-A GEMV fold the RMSNorm of its M input rows (K wide) into its activation staging?"""
+    return M <= 16 and M * K * 2 <= NORM_FUSE_LDS
+
+
 def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
-          argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1):
-    """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K]."""
+          argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1,
+          norm=None):
+    """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K].
+    norm = (xf f32 [M, K], w f32 [K], eps): the GEMV input is f16(rmsnorm(xf) * w), computed inside the
+    kernel (batch <= a few rows; `x` is then ignored on the GPU)."""
+    if norm is not None and x.is_cuda:
+        xf, nw, eps = norm
+        if any(s.xmap is not None for s in segs) or not norm_fusable(M, segs[0].w.K):
+            raise ValueError("fused-norm GEMV needs unmapped rows and M*K*2 <= NORM_FUSE_LDS")
+        mode, waves, rt, ks = gemv_config(segs, M)
+        if mode != 0:
+            waves, rt = 4, 2
+        arr = (_lib.NlsSeg * len(segs))()
+        for i, s in enumerate(segs):
+            arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), None, None, None, s.w.type, s.w.rows, s.w.K, s.ycol)
+        _lib.check(_lib.lib().nls_qgemv_norm(arr, len(segs), xf.data_ptr(), xf.stride(0), nw.data_ptr(), float(eps),
+                                             y.data_ptr(), y.stride(0), M, float(alpha), EPI[epi], _p(argmax), waves,
+                                             rt, _stream_ptr(xf)), "nls_qgemv_norm")
+        return y
+    if norm is not None:
+        xf, nw, eps = norm
+        xs = xf[:M].float()
+        x = (xs * torch.rsqrt(xs.pow(2).mean(dim=1, keepdim=True) + eps) * nw.float()).to(ACT_DTYPE)
     if x.is_cuda:
         if x.dtype != ACT_DTYPE:
             raise TypeError(f"qgemv: activations must be {ACT_DTYPE}, got {x.dtype}")
@@ -362,10 +391,10 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.
 
 def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
                 cs: torch.Tensor, q_out: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int,
-                D: int, neox: bool = False, cfg=None, bias: Optional[torch.Tensor] = None):
+                D: int, neox: bool = False, cfg=None, bias: Optional[torch.Tensor] = None, norm=None):
     """QKV projection + RoPE + paged KV append. With a split-K launch config the partial slabs
     are summed inside the RoPE kernel (no separate reduce pass, no fp32 qkv round trip)."""
-    if h.is_cuda and all(s.xmap is None for s in segs):
+    if h.is_cuda and all(s.xmap is None for s in segs) and norm is None:
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
@@ -382,7 +411,7 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
                                      cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(), vc.data_ptr(),
                                      T, Hq, Hkv, D, int(neox), st), "nls_rope_kv")
             return
-    qgemv(segs, h, qkv, T)
+    qgemv(segs, h, qkv, T, norm=norm)
     rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox, bias)
 
 

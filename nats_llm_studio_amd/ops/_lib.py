@@ -28,6 +28,8 @@ class NlsSeg(ctypes.Structure):
 _SIGS = {
     "nls_qgemv": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_float, c_int,
                   c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "nls_qgemv_norm": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_float, c_void_p, c_long, c_int,
+                       c_float, c_int, c_void_p, c_int, c_int, c_void_p],
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
     "nls_splitk_add_rmsnorm": [c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int,
                                c_float, c_void_p],

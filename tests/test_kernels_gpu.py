@@ -515,3 +515,31 @@ def test_qgemm_dma_swiglu_multiseg(gpu, ks):
     yq = torch.zeros(x.shape[0], 512, device=gpu)
     ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)], x, yq, M, mode=3, waves=4, rt=16, ks=ks)
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("M", [1, 3, 6])
+@pytest.mark.parametrize("epi", ["f32", "add", "swiglu", "argmax"])
+def test_qgemv_fused_rmsnorm(gpu, t, M, epi):
+    """Path A with the input RMSNorm folded into the staged activation rows == rmsnorm kernel + GEMV."""
+    rows, K = 272, 2048
+    w, Wd = _qw(rows, K, t, gpu)
+    g = torch.Generator().manual_seed(5)
+    xf = (torch.randn(16, K, generator=g) * 3).to(gpu)
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(gpu)
+    h = torch.zeros(16, K, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.rmsnorm(xf, nw, h, M, 1e-5)
+    ncol = rows // 2 if epi == "swiglu" else rows
+    dt = ops.ACT_DTYPE if epi == "swiglu" else torch.float32
+    base = torch.randn(16, ncol, device=gpu).to(dt)
+    outs = []
+    for fused in (False, True):
+        y = base.clone()
+        keys = torch.zeros(16, dtype=torch.int64, device=gpu)
+        ops.qgemv([ops.Seg(w)], h, y, M, alpha=0.5, epi=epi, argmax=keys if epi == "argmax" else None,
+                  norm=(xf, nw, 1e-5) if fused else None, mode=0 if not fused else -1, waves=4, rt=2)
+        outs.append((y[:M].float().cpu(), keys[:M].cpu()))
+    if epi == "argmax":     # same winning index (the value may differ in its last ulp: rms summation order)
+        assert ((outs[0][1] & 0xFFFFFFFF) == (outs[1][1] & 0xFFFFFFFF)).all()
+    else:
+        _close(outs[1][0], outs[0][0], 5e-3)

@@ -39,3 +39,20 @@ def test_rope_freqs_change_the_rotation(tiny_models):
     m = LlamaModel(r, "cpu")
     plain = ops.rope_table(m.cfg.ctx, m.D, m.cfg.rope_base, "cpu")
     assert not torch.allclose(m.cs[100], plain[100])
+
+
+def test_fused_norm_decode_matches_unfused(tiny_models):
+    """Few-row decode with the RMSNorms folded into the GEMVs (NLS_FUSE_NORM) == the plain path."""
+    from nats_llm_studio_amd.engine.engine import Engine, GenRequest
+    from nats_llm_studio_amd.engine.sampling import SamplingParams
+    r = GGUFReader(tiny_models["tiny-llama"])
+    outs = []
+    for fuse in (False, True):
+        m = LlamaModel(r, "cpu", fuse_norm=fuse)
+        eng = Engine(m, None, max_batch=4, num_blocks=32, use_graphs=False, ctx=256)
+        futs = [eng.submit(GenRequest([1, 2, 3, 40 + i], SamplingParams(max_tokens=6, ignore_eos=True)))
+                for i in range(3)]
+        while not all(f.done() for f in futs):
+            eng.step()
+        outs.append([f.result().token_ids for f in futs])
+    assert outs[0] == outs[1]
