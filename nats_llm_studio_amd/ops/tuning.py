@@ -42,8 +42,16 @@ def heuristic(segs, M: int):
     K = segs[0].w.K
     if M <= 8:
         return (0, 8, 1, 1)
-    if M > 64:                   # MFMA GEMM: 128 weight rows x 128 activation rows per workgroup
-        return (1, 8, 1, 1)
+    if M > 64:
+        if all(int(s.w.type) in (12, 13, 14) for s in segs):
+            # LDS-dequant GEMM (mode 2): 128 weight rows x 256 (or 128) activation rows per workgroup;
+            # split K until the grid covers the 256 CUs (the measured winners on the 8B shapes)
+            tiles = sum((s.w.rows + 127) // 128 for s in segs) * ((M + 255) // 256)
+            ks, nb = 1, K // 256
+            while tiles * ks < 256 and ks * 2 <= max(1, nb // 4):
+                ks *= 2
+            return (2, 8, 4 if M >= 192 else 2, ks)
+        return (1, 8, 1, 1)      # MFMA GEMM: 128 weight rows x 128 activation rows per workgroup
     waves, rt = 8, 1
     tiles = sum((s.w.rows + waves * rt * 16 - 1) // (waves * rt * 16) for s in segs)
     ks = 1
