@@ -1,11 +1,12 @@
 #!/bin/bash
-# rocprofv3 kernel trace + stats of the bench (B given as $1, default 64)
-mkdir -p gpurun_out
+# rocprofv3 kernel traces of the bench at B=512 and B=1 + per-step breakdowns
+set -u
+cd "$GRAFT_REPO_ROOT"
 export PYTHONPATH=$PWD
-B=${1:-64}
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-python -m nats_llm_studio_amd.build > gpurun_out/build.log 2>&1 || exit 3
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b$B -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-rtt --concurrency $B > gpurun_out/prof_b$B.log 2>&1; rc=$?
-echo "rc=$rc"; tail -3 gpurun_out/prof_b$B.log
-find gpurun_out/prof_b$B -name "*stats*"
-exit $rc
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for B in 512 1; do
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b$B -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-rtt --concurrency $B > gpurun_out/prof_b$B.log 2>&1 || { echo "prof B=$B failed"; tail -5 gpurun_out/prof_b$B.log; exit 1; }
+  python tools/analyze_trace.py $(find gpurun_out/prof_b$B -name "*kernel_trace.csv" | head -1) > gpurun_out/prof_b${B}_breakdown.txt
+  cat gpurun_out/prof_b${B}_breakdown.txt
+done
