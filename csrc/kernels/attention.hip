@@ -235,8 +235,11 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
     launch_attn<DD, GG>(grid, st, qq, ldq, k, v, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \
                         scale, chunk, n_split, o, ldo, part_o, part_ml);                                     \
   } else
-  NLS_ATTN_CASE(128, 1) NLS_ATTN_CASE(128, 2) NLS_ATTN_CASE(128, 4) NLS_ATTN_CASE(128, 8)
-  NLS_ATTN_CASE(64, 1) NLS_ATTN_CASE(64, 2) NLS_ATTN_CASE(64, 4) NLS_ATTN_CASE(64, 8) { return -1; }
+  // G = Hq/Hkv of the supported families: 1 (MHA), 2/4/8 (Llama/Mixtral), 3/5/6/7 (Qwen2 sizes, e.g. 28/4)
+  NLS_ATTN_CASE(128, 1) NLS_ATTN_CASE(128, 2) NLS_ATTN_CASE(128, 3) NLS_ATTN_CASE(128, 4) NLS_ATTN_CASE(128, 5)
+  NLS_ATTN_CASE(128, 6) NLS_ATTN_CASE(128, 7) NLS_ATTN_CASE(128, 8)
+  NLS_ATTN_CASE(64, 1) NLS_ATTN_CASE(64, 2) NLS_ATTN_CASE(64, 3) NLS_ATTN_CASE(64, 4) NLS_ATTN_CASE(64, 5)
+  NLS_ATTN_CASE(64, 6) NLS_ATTN_CASE(64, 7) NLS_ATTN_CASE(64, 8) { return -1; }
 #undef NLS_ATTN_CASE
   if (n_split > 1) {
     if (D == 128)

@@ -30,7 +30,8 @@ namespace nls_gemm {
 using namespace nls_gemv;
 
 template <int T, int WM>
-DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds) {
+DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds,
+                   const int* xm, const int* ym) {
   constexpr int MTW = 4;                 // 16-row activation tiles per wave
   constexpr int WN = 8 / WM;
   constexpr int NTW = 8 / WN;            // 16-row weight tiles per wave
@@ -57,12 +58,19 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 xr[NXU];
+  // the activation row each thread stages (fixed for the whole K loop); rows >= M only feed
+  // outputs that are never stored: clamp, never branch. xm: MoE gather (block-local row -> x row)
+  int xrow[NXU];
+#pragma unroll
+  for (int u = 0; u < NXU; ++u) {
+    const int row = min((int)((threadIdx.x + 512 * u) >> 3), M - 1);
+    xrow[u] = xm ? xm[row] : row;
+  }
   auto load_x = [&](int sb, int q) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NXU; ++u) {
-      const int idx = threadIdx.x + 512 * u, row = idx >> 3, ch = idx & 7;
-      // rows >= M only feed outputs that are never stored: clamp, never branch
-      xr[u] = ld16(a.x + (size_t)min(row, M - 1) * a.ldx + sb * 256 + q * 64 + ch * 8);
+      const int ch = (threadIdx.x + 512 * u) & 7;
+      xr[u] = ld16(a.x + (size_t)xrow[u] * a.ldx + sb * 256 + q * 64 + ch * 8);
     }
   };
   auto store_x = [&](int buf) __attribute__((always_inline)) {
@@ -194,12 +202,13 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
           const float u = __shfl_xor(v, 8, 64);
           if (r < 8 && b < M && row < S.rows) {
             const int n = S.ycol + ((rbase + 16 * j) >> 1) + r;
-            reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
+            const int yb = ym ? ym[b] : b;
+            reinterpret_cast<act_t*>(a.y)[(size_t)yb * a.ldy + n] = (act_t)(silu(v) * u);
           }
           continue;
         }
         if (b < M && row < S.rows) {
-          const size_t off = (size_t)b * a.ldy + S.ycol + row;
+          const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
           if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
           else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
           else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
@@ -251,28 +260,34 @@ __global__ __launch_bounds__(512) void qmm_lds_kernel(SegList segs, GemvArgs a, 
   const int tile = (j / ks / nmb) * 8 + xcd;
   if (tile >= ntiles) return;
   const int m0 = mb * BM;
-  a.m0 = m0;
-  a.x += (size_t)m0 * a.ldx;
-  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-  a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-  if (a.argmax) a.argmax += m0;
-  a.M = min(BM, a.M - m0);
   Seg S = segs.s[0];
 #pragma unroll
   for (int s = 1; s < 8; ++s)
     if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
+  // MoE grouped GEMM: the expert's routed-row count lives on the device; m-blocks past it exit
+  // before reading any weights (the grid is sized for the worst case, every token on one expert)
+  const int mrows = S.mcount ? min(*S.mcount, a.M) : a.M;
+  if (m0 >= mrows) return;
+  const int* xm = S.xmap ? S.xmap + m0 : nullptr;
+  const int* ym = S.ymap ? S.ymap + m0 : nullptr;
+  a.m0 = m0;
+  if (!xm) a.x += (size_t)m0 * a.ldx;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+  if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (a.argmax) a.argmax += m0;
+  a.M = min(BM, mrows - m0);
   const int row0 = (tile - S.tile_begin) * 128;
   if constexpr (KSET == 0) {
     switch (S.type) {
-      case QT_Q4_K: lds_tile<QT_Q4_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
-      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      case QT_Q4_K: lds_tile<QT_Q4_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
       default: break;
     }
   } else {
     switch (S.type) {
-      case QT_Q5_K: lds_tile<QT_Q5_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
-      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds); break;
-      case QT_Q8_0: lds_tile<QT_Q8_0, WM>(S, row0, kslice, ks, a, ws, lds); break;
+      case QT_Q5_K: lds_tile<QT_Q5_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q8_0: lds_tile<QT_Q8_0, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
       default: break;
     }
   }
@@ -299,6 +314,7 @@ template <int KSET>
 int launch_lds_kset(int wm, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
   if (wm == 4) return launch_lds_t<4, KSET>(sl, ntiles, ks, ws, a, st);
   if (wm == 2) return launch_lds_t<2, KSET>(sl, ntiles, ks, ws, a, st);
+  if (wm == 1) return launch_lds_t<1, KSET>(sl, ntiles, ks, ws, a, st);   // 64-row blocks (MoE experts)
   return -1;
 }
 

@@ -32,7 +32,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
   if (mode == 3) {
     if (waves != 4 || (rt != 8 && rt != 16)) return -1;
-  } else if (mode == 2 ? (waves != 8 || (rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) {
+  } else if (mode == 2 ? (waves != 8 || (rt != 1 && rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) {
     return -1;
   }
   if (M > 64 && mode == 0) return -1;   // large M: path B / LDS GEMM
@@ -44,7 +44,10 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
-    if (mode != 0 && segs[i].xmap) return -1;
+    // mapped rows (MoE): path A, or the LDS GEMM without split-K / arg-max
+    if ((segs[i].xmap || segs[i].ymap || segs[i].mcount) && mode != 0 &&
+        (mode != 2 || ks > 1 || argmax || epi == EPI_SLABS))
+      return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;
     sl.s[i].ymap = segs[i].ymap;

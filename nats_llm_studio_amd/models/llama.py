@@ -390,18 +390,30 @@ class LlamaModel:
         k, E = cfg.n_expert_used, cfg.n_expert
         cap = b.x.shape[0]
         ops.qgemv([Seg(lw.router)], b.h, m["rlogits"], T)
-        for c0 in range(0, T, 64):
-            n = min(64, T - c0)
+        # few tokens: path-A GEMV over each expert's gathered rows; many tokens: ONE route and the
+        # LDS-dequant GEMM (mode 2) over all experts, each m-block of an expert gathering its rows
+        # through xrows and exiting when it lies past the expert's device-side count
+        gemm = T > 64 and self.device.type == "cuda"
+        step = T if gemm else 64
+        # m-block = 64*rt rows. Every m-block re-dequantises the expert's weights, so the largest
+        # block wins even at ~64 routed rows per expert (Mixtral B=256, tools/moe_ab.sh: gate/up
+        # rt 4 / down rt 2 = 32.0 ms/step, 2/2 = 34.3, 2/1 = 39.6, 1/1 = 50.8)
+        gu = dn = {}
+        if gemm:
+            gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", 4)), ks=1)
+            dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", 2)), ks=1)
+        for c0 in range(0, T, step):
+            n = min(step, T - c0)
             ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap)
             loc = list(zip(self.experts, lw.exp_gateup, lw.exp_down))
             segs = [Seg(gu, 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, gu, _ in loc]
             for s0 in range(0, len(segs), 8):
-                ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu")
+                ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu", **gu)
             if self.ep:                        # rows routed to other ranks' experts stay zero
                 m["yexp"][:n * k].zero_()
             segs = [Seg(dn, 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, _, dn in loc]
             for s0 in range(0, len(segs), 8):
-                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32")
+                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32", **dn)
             if self.shard.size > 1:
                 self.comm.all_reduce(m["yexp"][:n * k])
             ops.moe_combine(m["yexp"], m["topw"], n, k, b.x[c0:], cfg.residual_scale)

@@ -227,7 +227,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         mapped = any(s.xmap is not None for s in segs)
         if mode < 0 or waves == 0:
             mode, waves, rt, ks = gemv_config(segs, M) if not mapped else (0, 8, 1, 1)
-        if M > 64 and (mapped or mode == 0):
+        if M > 64 and mode == 0:
             # mapped (MoE) rows / path A: chunks of 64 rows
             for m0 in range(0, M, 64):
                 mm = min(64, M - m0)

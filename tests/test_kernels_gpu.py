@@ -124,6 +124,48 @@ def test_qgemv_mapped_rows(gpu):
     assert (y[1].cpu() == 7.0).all()
 
 
+@pytest.mark.parametrize("T,rt,qt", [(200, 2, GGMLType.Q4_K), (300, 4, GGMLType.Q5_K), (150, 1, GGMLType.Q6_K)])
+def test_qgemm_mapped_moe(gpu, T, rt, qt):
+    """Grouped MoE GEMM (mode 2, mapped rows): one route over T tokens, SwiGLU gate/up and f32 down
+    over every expert in one launch each, against the per-row fp32 reference."""
+    E, k, K, F = 4, 2, 512, 256
+    logits = torch.randn(T, E, device=gpu)
+    cap = T
+    topw = torch.zeros(T * k, device=gpu)
+    counts = torch.zeros(E, dtype=torch.int32, device=gpu)
+    xrows = torch.zeros(E * cap, dtype=torch.int32, device=gpu)
+    yrows = torch.zeros(E * cap, dtype=torch.int32, device=gpu)
+    ops.moe_route(logits, T, k, topw, counts, xrows, yrows, cap)
+    rng = np.random.default_rng(9)
+    gus, G, U = [], [], []
+    for e in range(E):
+        g_raw = Q.random_blocks(qt, F * K, 0.05, rng)
+        u_raw = Q.random_blocks(qt, F * K, 0.05, rng)
+        gus.append(ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, qt, F, K), qt, 2 * F, K, gpu))
+        G.append(ops.QWeight(g_raw, qt, F, K, "cpu").dense())
+        U.append(ops.QWeight(u_raw, qt, F, K, "cpu").dense())
+    dns = [_qw(K, F, qt, gpu, 40 + e) for e in range(E)]
+    x = _x(T, K, gpu)
+    act = torch.zeros(T * k, F, dtype=ops.ACT_DTYPE, device=gpu)
+    yexp = torch.full((T * k, K), 5.0, device=gpu)
+    cfg = dict(mode=2, waves=8, rt=rt, ks=1)
+    segs = [ops.Seg(gus[e], 0, xrows[e * cap:], yrows[e * cap:], counts[e:e + 1]) for e in range(E)]
+    ops.qgemv(segs, x, act, T, epi="swiglu", **cfg)
+    segs = [ops.Seg(dns[e][0], 0, yrows[e * cap:], yrows[e * cap:], counts[e:e + 1]) for e in range(E)]
+    ops.qgemv(segs, act, yexp, T, epi="f32", **cfg)
+    torch.cuda.synchronize()
+    cnt, xr, yr = counts.cpu(), xrows.cpu(), yrows.cpu()
+    assert int(cnt.sum()) == T * k and sorted(yr[e * cap + i].item() for e in range(E)
+                                              for i in range(int(cnt[e]))) == list(range(T * k))
+    xf = x.float().cpu()
+    for e in range(E):
+        n = int(cnt[e])
+        xi, yi = xr[e * cap:e * cap + n].long(), yr[e * cap:e * cap + n].long()
+        ref = torch.nn.functional.silu(xf[xi] @ G[e].t()) * (xf[xi] @ U[e].t())
+        _close(act[yi], ref, 3e-2)
+        _close(yexp[yi], act[yi].float().cpu() @ dns[e][1].t(), 3e-2)
+
+
 def test_rmsnorm_embed(gpu):
     x = torch.randn(5, 1024, device=gpu)
     w = torch.randn(1024, device=gpu)
@@ -159,7 +201,7 @@ def test_rope_kv(gpu, neox):
         torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1)])
+@pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1), (128, 7), (64, 6), (128, 5)])
 @pytest.mark.parametrize("n_split,chunk", [(1, 0), (4, 0), (32, 0), (8, -16), (3, 512)])
 def test_attention_paged(gpu, D, G, n_split, chunk):
     Hkv = 2

@@ -35,6 +35,28 @@ def test_prefill_logits_match_reference(gpu, tiny_models, name):
     assert agree > 0.9
 
 
+def test_moe_grouped_gemm_prefill(gpu, tiny_models):
+    """T > 64 routes every token at once and runs the experts as mapped-row LDS GEMMs (mode 2)."""
+    r = GGUFReader(tiny_models["tiny-mixtral"])
+    m = LlamaModel(r, gpu)
+    ref = ReferenceModel(r)
+    S, n = 150, 48
+    ids = list(np.random.default_rng(1).integers(0, 900, S))
+    b = m.step_buffers(256, 4, 16)
+    kc, vc = m.kv_cache(16, 16)
+    b.ids[:S] = torch.tensor(ids, dtype=torch.int32)
+    b.pos[:S] = torch.arange(S)
+    b.slot[:S] = torch.arange(S)
+    b.tok_seq[:S] = 0
+    b.ctx_len[:S] = torch.arange(S) + 1
+    b.block_tables[0] = torch.arange(16)
+    rows = torch.arange(S - n, S, dtype=torch.int32, device=gpu)
+    m.forward(b, kc, vc, S, 16, n_split=2, logit_rows=rows, n_logits=n)
+    rl = ref.logits(ids)[S - n:]
+    err = (b.logits[:n].cpu() - rl).abs().max().item()
+    assert err < 0.05 * rl.abs().max().item(), err
+
+
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
 @pytest.mark.parametrize("graphs", [False, True])
 def test_engine_greedy_matches_reference(gpu, tiny_models, name, graphs):
