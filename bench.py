@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-rtt", action="store_true")
     ap.add_argument("--single-stream", action="store_true", help="also time batch-1 decode (reported, not the headline)")
+    ap.add_argument("--step-breakdown", action="store_true",
+                    help="report host time vs time blocked on the previous step's tokens (diagnostic)")
     args = ap.parse_args()
 
     import numpy as np
@@ -100,6 +102,20 @@ def main():
         eng.step()
     assert len(eng.running) == B, "all requests must still be decoding in the timed region"
 
+    wait = [0.0]
+    if args.step_breakdown:   # time the host spends blocked on step N's event (GPU-bound share)
+        orig = eng._process
+
+        def timed(infl):
+            eng._ev[infl[1]].synchronize() if eng.dev.type == "cuda" else None
+            t = time.perf_counter()
+            orig(infl)
+            wait[0] -= time.perf_counter() - t
+        def timed_outer(infl):
+            t = time.perf_counter()
+            timed(infl)
+            wait[0] += time.perf_counter() - t
+        eng._process = timed_outer
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -111,6 +127,21 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tokens = B * args.steps
+    if args.step_breakdown:
+        eng._process = orig
+        eng._drain()
+        # steady-state replay of the same decode graph, GPU-only (diagnostic: the replays rewrite
+        # the last step's KV slots; nothing after this point is checked)
+        g = eng.graphs.get((eng._bucket(B), False))
+        if g is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g.replay()
+            e0.record()
+            for _ in range(10):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            wait.append(e0.elapsed_time(e1) / 10)
 
     t_max = elapsed
     tok_sum = tokens
@@ -129,6 +160,10 @@ def main():
         f.result()
 
     extra = {}
+    if args.step_breakdown:
+        extra["step_breakdown_ms"] = {"gpu_wait": round(wait[0] / args.steps * 1e3, 3),
+                                      "host_other": round((elapsed - wait[0]) / args.steps * 1e3, 3),
+                                      "graph_replay_only": round(wait[1], 3) if len(wait) > 1 else None}
     if args.single_stream:
         r = eng.generate(list(rng.integers(0, 1000, args.prompt_len)), SamplingParams(max_tokens=64, ignore_eos=True))
         extra["single_stream_tok_s"] = round(r.tokens_per_second, 1)
