@@ -1,21 +1,33 @@
 #!/usr/bin/env python3
 """Headline benchmark (BASELINE.json): output tokens/sec of `lmstudio.chat_model`-style greedy
-generation on a random-init Llama-3-8B Q4_K_M GGUF, one engine replica per GPU.
+generation on a random-init Llama-3-8B Q4_K_M GGUF, plus the p50 NATS request-reply RTT.
 
-    python bench.py --gpus N --steps K --warmup W [--concurrency B] [--prompt-len P]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--concurrency B] [--tp T] [--ep]
+                    [--model llama-3-8b|llama-3-70b|mixtral-8x7b|...] [--device cuda|cpu]
 
-One step = one continuous-batching decode step over B in-flight requests per GPU
-(hipGraph replay + per-step scheduling + the host<-device next-token copy: the real
-serving loop, nothing skipped). N > 1 is launched by torch.distributed.run, one rank per
-GPU; every rank is an independent replica (the reference's NATS queue-group scale-out,
-README.md:478-484), so scaling is weak (fixed per-GPU work). Rank 0 prints ONE JSON line;
-`value` is the whole-job aggregate (sum over ranks of tokens / max-over-ranks time).
+One step = one continuous-batching decode step over B in-flight requests per model replica
+(hipGraph replay + per-step scheduling + the host<-device next-token copy: the real serving
+loop, nothing skipped).
+
+Multi-GPU: `--gpus N` runs N ranks, one per GPU. Launched by `torch.distributed.run` (the driver
+does this, setting WORLD_SIZE) or, when WORLD_SIZE is unset, bench.py starts
+`torch.distributed.run` itself as a child process BEFORE touching the GPU and exits with its
+code. The N ranks form N/T model replicas of T-way tensor parallelism:
+  * T = 1 (default, BASELINE config 2): N independent replicas -- the reference's NATS
+    queue-group scale-out (`/root/reference/README.md:478-484`); scaling is weak.
+  * T > 1 (`--tp`, BASELINE config 3: Llama-3-70B TP=8): rank 0 of each replica schedules,
+    the others replay its steps; row-parallel all-reduces over RCCL/xGMI.
+  * `--ep` (BASELINE config 5: Mixtral): experts are owned whole by ranks (expert parallel).
+Rank 0 prints ONE JSON line; `value` is the whole-job aggregate (sum over replicas of tokens /
+max-over-ranks time of the K timed steps, bracketed by a world barrier + device sync).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,46 +37,111 @@ sys.path.insert(0, ROOT)
 METRIC = "output tokens/sec + p50 NATS req-reply RTT, Llama-3-8B Q4_K chat_model"
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--concurrency", type=int, default=512, help="in-flight chat requests per GPU")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU) of the job")
+    ap.add_argument("--steps", type=int, default=200, help="timed decode steps (sustained run by default)")
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--concurrency", type=int, default=512, help="in-flight chat requests per model replica")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--ftype", default="Q4_K_M")
+    ap.add_argument("--ftype", default=None, help="default: Q5_K_M for mixtral, else Q4_K_M")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (divides --gpus)")
+    ap.add_argument("--ep", action="store_true", help="MoE: expert parallel over the TP group")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"), help="cpu: gloo rehearsal of the path")
     ap.add_argument("--model-dir", default=os.environ.get("NLS_BENCH_DIR", "/tmp/nls_bench"))
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-rtt", action="store_true")
     ap.add_argument("--single-stream", action="store_true", help="also time batch-1 decode (reported, not the headline)")
     ap.add_argument("--step-breakdown", action="store_true",
                     help="report host time vs time blocked on the previous step's tokens (diagnostic)")
-    args = ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.ftype is None:
+        a.ftype = "Q5_K_M" if "mixtral" in a.model else "Q4_K_M"
+    return a
 
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(args, argv) -> int:
+    """--gpus N > 1 without a launcher: run torch.distributed.run as a CHILD process (this process
+    has not imported torch, let alone touched the GPU) and return its exit code."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn(args, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if world % args.tp:
+        raise SystemExit(f"bench.py: --tp {args.tp} must divide --gpus {world}")
+    return run(args, world)
+
+
+def run(args, world: int):
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    cuda = args.device == "cuda"
+    if cuda:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, min(4, (os.cpu_count() or 2) // max(1, world))))
+    sync = torch.cuda.synchronize if cuda else (lambda *a: None)
+    tp = args.tp
+    replica, tp_rank = rank // tp, rank % tp
+    comm = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        import datetime
+        kw = dict(backend="nccl" if cuda else "gloo", timeout=datetime.timedelta(seconds=1800))
+        if cuda:
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    if tp > 1:
+        from nats_llm_studio_amd.parallel.comm import Comm
+        mine = None
+        for g in range(world // tp):     # every rank creates every group, in the same order
+            ranks = list(range(g * tp, (g + 1) * tp))
+            pg = dist.new_group(ranks) if world > tp else dist.group.WORLD
+            cg = dist.new_group(ranks, backend="gloo") if cuda else pg
+            if g == replica:
+                mine = (pg, cg)
+        comm = Comm(mine[0], mine[1], dev)
+        if cuda and os.environ.get("NLS_ONESHOT_AR", "0") == "1":
+            from nats_llm_studio_amd.parallel.oneshot import OneShotAllReduce
+            comm.oneshot = OneShotAllReduce(comm)
 
     from nats_llm_studio_amd import build as nbuild
     from nats_llm_studio_amd.gguf.reader import GGUFReader
     from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
-    from nats_llm_studio_amd.models.llama import LlamaModel
+    from nats_llm_studio_amd.models.llama import LlamaModel, ShardSpec
     from nats_llm_studio_amd.engine.engine import Engine, GenRequest
     from nats_llm_studio_amd.engine.sampling import SamplingParams
 
     path = os.path.join(args.model_dir, f"{args.model}-{args.ftype}.gguf")
     t0 = time.time()
     if local == 0:
-        nbuild.build_kernels()
+        if cuda:
+            nbuild.build_kernels()
         if not os.path.exists(path):
             os.makedirs(args.model_dir, exist_ok=True)
             write_synthetic_gguf(path, args.model, args.ftype, seed=0)
@@ -74,8 +151,8 @@ def main():
 
     t0 = time.time()
     reader = GGUFReader(path)
-    model = LlamaModel(reader, dev)
-    torch.cuda.synchronize()
+    model = LlamaModel(reader, dev, ShardSpec(tp_rank, tp, args.ep), comm)
+    sync()
     t_load = time.time() - t0
 
     B = args.concurrency
@@ -84,8 +161,27 @@ def main():
     prefill_steps = (B * args.prompt_len + max_prefill - 1) // max_prefill
     gen_tokens = args.warmup + args.steps + prefill_steps + 8
     need_tokens = args.prompt_len + gen_tokens
-    eng = Engine(model, None, max_batch=B, max_prefill_tokens=max_prefill, use_graphs=not args.no_graphs,
+    eng = Engine(model, None, max_batch=B, max_prefill_tokens=max_prefill, use_graphs=cuda and not args.no_graphs,
                  ctx=max(need_tokens + 16, 512), num_blocks=B * ((need_tokens + 15) // 16 + 1))
+    marks = []
+
+    def barrier_hook():                 # both sides of the timed region, on every rank
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+        marks.append(time.perf_counter())
+
+    leader = tp_rank == 0
+    if not leader:                      # follower: replay the leader's steps until STOP
+        eng.sync_hook = barrier_hook
+        eng.follow()
+        elapsed = marks[1] - marks[0] if len(marks) >= 2 else 0.0
+        _reduce_and_report(args, world, dist, torch, dev, elapsed, 0.0, None, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
+
     eng.capture_all()
     rng = np.random.default_rng(rank)
     vocab = model.cfg.vocab
@@ -96,127 +192,135 @@ def main():
     t0 = time.time()
     while any(s.n_prefilled < s.n_prompt for s in eng.running) or eng.waiting:
         eng.step()
-    torch.cuda.synchronize()
+    sync()
     t_prefill = time.time() - t0
     for _ in range(args.warmup):
         eng.step()
     assert len(eng.running) == B, "all requests must still be decoding in the timed region"
 
     wait = [0.0]
-    if args.step_breakdown:   # time the host spends blocked on step N's event (GPU-bound share)
-        orig = eng._process
-
-        def timed(infl):
-            eng._ev[infl[1]].synchronize() if eng.dev.type == "cuda" else None
-            t = time.perf_counter()
-            orig(infl)
-            wait[0] -= time.perf_counter() - t
+    orig = eng._process
+    if args.step_breakdown and cuda:    # time the host spends blocked on step N's event (GPU-bound share)
         def timed_outer(infl):
             t = time.perf_counter()
-            timed(infl)
+            eng._ev[infl[1]].synchronize()
             wait[0] += time.perf_counter() - t
+            orig(infl)
         eng._process = timed_outer
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    st0 = dict(comm.stats) if comm is not None else None
+    eng.sync(barrier_hook) if tp > 1 else barrier_hook()
     for _ in range(args.steps):
         eng.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    eng.sync(barrier_hook) if tp > 1 else barrier_hook()
+    elapsed = marks[1] - marks[0]
     tokens = B * args.steps
-    if args.step_breakdown:
-        eng._process = orig
+    eng._process = orig
+    comm_stats = None
+    if comm is not None:
+        d = {k: comm.stats[k] - st0.get(k, 0) for k in comm.stats}
+        comm_stats = {"all_reduce_per_step": round(d["all_reduce"] / args.steps, 2),
+                      "all_reduce_bytes_per_step": int(d["all_reduce_bytes"] / args.steps),
+                      "ctrl_msgs_per_step": round(d["ctrl"] / args.steps, 2),
+                      "oneshot": comm.oneshot is not None}
+
+    extra = {}
+    if args.step_breakdown and cuda:
         eng._drain()
-        # steady-state replay of the same decode graph, GPU-only (diagnostic: the replays rewrite
-        # the last step's KV slots; nothing after this point is checked)
         g = eng.graphs.get((eng._bucket(B), False))
-        if g is not None:
+        replay = None
+        if g is not None and tp == 1:   # GPU-only replay of the same decode graph (diagnostic)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             g.replay()
             e0.record()
             for _ in range(10):
                 g.replay()
             e1.record()
-            torch.cuda.synchronize()
-            wait.append(e0.elapsed_time(e1) / 10)
-
-    t_max = elapsed
-    tok_sum = tokens
-    if world > 1:
-        tt = torch.tensor([elapsed, float(tokens)], dtype=torch.float64, device=dev)
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        t_max = float(mx[0])
-        tok_sum = float(tt[1])
-
+            sync()
+            replay = round(e0.elapsed_time(e1) / 10, 3)
+        extra["step_breakdown_ms"] = {"gpu_wait": round(wait[0] / args.steps * 1e3, 3),
+                                      "host_other": round((elapsed - wait[0]) / args.steps * 1e3, 3),
+                                      "graph_replay_only": replay}
     # drain
     while eng.running or eng.waiting:
         eng.step()
     for f in futs:
         f.result()
-
-    extra = {}
-    if args.step_breakdown:
-        extra["step_breakdown_ms"] = {"gpu_wait": round(wait[0] / args.steps * 1e3, 3),
-                                      "host_other": round((elapsed - wait[0]) / args.steps * 1e3, 3),
-                                      "graph_replay_only": round(wait[1], 3) if len(wait) > 1 else None}
     if args.single_stream:
         r = eng.generate(list(rng.integers(0, 1000, args.prompt_len)), SamplingParams(max_tokens=64, ignore_eos=True))
         extra["single_stream_tok_s"] = round(r.tokens_per_second, 1)
         extra["single_stream_ttft_ms"] = round(r.time_to_first_token * 1e3, 2)
 
-    rtt = None
-    chat_rtt = None
+    rtt = chat_rtt = None
     if not args.no_rtt and rank == 0:
         try:
             from nats_llm_studio_amd.service.bench_rtt import measure_rtt
             rtt = measure_rtt(n=500)
         except Exception as e:  # natscore missing -> report null, never fake
             extra["rtt_error"] = str(e)[:200]
-        try:   # chat_model on the real 8B engine (after the timed region; engine idle)
+        try:   # chat_model on the real engine (after the timed region; engine idle)
             from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_rtt
             chat_rtt = measure_engine_chat_rtt(eng, reader.metadata, n=30)
         except Exception as e:
             extra["chat_rtt_error"] = str(e)[:300]
+    eng.stop_followers()
 
-    if rank == 0:
-        value = tok_sum / t_max
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "output tokens/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(t_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp16",   # f16 activations + f16 MFMA on Q4_K_M weights, fp32 accumulate and residual
-            "data": "synthetic prompts, random-init GGUF weights (Q4_K_M mix: Q4_K + Q6_K), no network",
-            "config": {
-                "model": f"{args.model} {args.ftype}",
-                "global_batch": B * world,
-                "seq_len": args.prompt_len,
-                "parallelism": f"dp{world}",
-                "concurrency_per_gpu": B,
-                "hipgraph": not args.no_graphs,
-            },
-            "p50_rtt_ms": (chat_rtt or {}).get("p50_ms", None if rtt is None else rtt.get("p50_ms")),
-            "rtt_chat_model_engine": chat_rtt,
-            "rtt": rtt,
-            "weights_gb": round(model.weight_bytes / 1e9, 3),
-            "timings_s": {"gguf_write": round(t_gen, 1), "load": round(t_load, 1), "prefill_all": round(t_prefill, 3)},
-            **extra,
-        }
-        print(json.dumps(out), flush=True)
+    info = dict(model=model, B=B, tp=tp, t_gen=t_gen, t_load=t_load, t_prefill=t_prefill, rtt=rtt,
+                chat_rtt=chat_rtt, comm_stats=comm_stats, extra=extra)
+    _reduce_and_report(args, world, dist, torch, dev, elapsed, float(tokens), info, rank)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, rank):
+    t_max, tok_sum = elapsed, tokens
+    if world > 1:
+        tt = torch.tensor([elapsed, tokens], dtype=torch.float64, device=dev)
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        t_max, tok_sum = float(mx[0]), float(tt[1])
+    if rank != 0:
+        return
+    model, B, tp = info["model"], info["B"], info["tp"]
+    dp = world // tp
+    par = f"dp{dp}" if tp == 1 else (f"tp{tp}" if dp == 1 else f"dp{dp}xtp{tp}")
+    if args.ep and model.cfg.n_expert:
+        par += "+ep"
+    rtt, chat_rtt = info["rtt"], info["chat_rtt"]
+    out = {
+        "metric": METRIC,
+        "value": round(tok_sum / t_max, 2),
+        "unit": "output tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if tp == 1 else "strong",   # tp: one replica's fixed batch over more GPUs
+        "vs_baseline": None,
+        "dtype": "fp16",   # f16 activations + f16 MFMA on K-quant weights, fp32 accumulate and residual
+        "data": f"synthetic prompts, random-init GGUF weights ({args.ftype} mix), no network",
+        "config": {
+            "model": f"{args.model} {args.ftype}",
+            "global_batch": B * dp,
+            "seq_len": args.prompt_len,
+            "parallelism": par,
+            "concurrency_per_replica": B,
+            "hipgraph": args.device == "cuda" and not args.no_graphs,
+            "device": args.device,
+        },
+        "p50_rtt_ms": (chat_rtt or {}).get("p50_ms", None if rtt is None else rtt.get("p50_ms")),
+        "rtt_chat_model_engine": chat_rtt,
+        "rtt": rtt,
+        "weights_gb_per_rank": round(model.weight_bytes / 1e9, 3),
+        "comm": info["comm_stats"],
+        "timings_s": {"gguf_write": round(info["t_gen"], 1), "load": round(info["t_load"], 1),
+                      "prefill_all": round(info["t_prefill"], 3)},
+        **info["extra"],
+    }
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -33,7 +33,7 @@ from .sampling import SamplingParams, sample_rows, sample_rows_gpu
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512)
 
 # tensor-parallel control messages (rank 0 -> followers), see Engine.follow()
-_OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE = 0, 1, 2, 3
+_OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE, _OP_SYNC = 0, 1, 2, 3, 4
 _HDR = 8
 _NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
 
@@ -239,6 +239,7 @@ class Engine:
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0)
         self.full_logits: Optional[torch.Tensor] = None
         self._ctrl_hdr = torch.zeros(_HDR + self.max_batch, dtype=torch.int32)
+        self.sync_hook: Optional[Callable[[], None]] = None   # follower side of Engine.sync()
 
     # ------------------------------------------------------------------ API
     def submit(self, req: GenRequest) -> Future:
@@ -448,6 +449,13 @@ class Engine:
         if op in (_OP_PREFILL, _OP_DECODE):
             self.tp.bcast_ctrl(hmeta[:_NSEG * pad + nseq * nb].clone())
 
+    def sync(self, hook: Callable[[], None]):
+        """Rank 0: make every follower run its `sync_hook` now, then run `hook` here (used by the
+        benchmark to bracket a timed region with a world-wide barrier while followers replay)."""
+        self._drain()
+        self._ctrl(_OP_SYNC, 0, 0, False, [], 0, None, 0)
+        hook()
+
     def stop_followers(self):
         if self.tp is not None and self.rank == 0 and not getattr(self, "_followers_stopped", False):
             self._followers_stopped = True
@@ -464,6 +472,10 @@ class Engine:
                 return
             if op == _OP_CAPTURE:
                 self._capture(T, LlamaModel.attn_splits(T, self.model.Hkv))
+                continue
+            if op == _OP_SYNC:
+                if self.sync_hook is not None:
+                    self.sync_hook()
                 continue
             hm = self.h_meta_p if op == _OP_PREFILL else self.h_meta_d
             buf = torch.zeros(_NSEG * pad + nseq * nb, dtype=torch.int32)

@@ -59,6 +59,10 @@ SPECS: Dict[str, ModelSpec] = {
                                 attention_scale=0.015625, logit_scale=8.0),
     # tiny shapes for CPU / kernel tests (all dims multiples of 256)
     "tiny-llama": ModelSpec("tiny-llama", "llama", 2, 512, 4, 2, 768, 1024, 512, 10000.0),
+    # TP-shardable tiny shape (TP=2: per-rank FFN 512, one kv head each) for CPU multi-rank benches
+    "tiny-llama-tp": ModelSpec("tiny-llama-tp", "llama", 2, 512, 4, 2, 1024, 1024, 512, 10000.0),
+    "tiny-mixtral-tp": ModelSpec("tiny-mixtral-tp", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,
+                                 n_expert=4, n_expert_used=2, tokenizer="llama"),
     "tiny-mixtral": ModelSpec("tiny-mixtral", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,
                               n_expert=4, n_expert_used=2, tokenizer="llama"),
     "qwen2.5-7b": ModelSpec("qwen2.5-7b", "qwen2", 28, 3584, 28, 4, 18944, 152064, 32768, 1e6, eps=1e-6),

@@ -1,0 +1,44 @@
+"""bench.py contract on CPU (gloo): `--gpus N` starts N ranks itself when no launcher set
+WORLD_SIZE, TP/EP replicas replay the leader's steps, and rank 0 prints ONE JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(tmp_path, *args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--steps", "3", "--warmup", "1",
+           "--concurrency", "4", "--prompt-len", "16", "--no-rtt", "--model-dir", str(tmp_path), *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("extra,par,scaling", [
+    (["--gpus", "2", "--tp", "2", "--model", "tiny-llama-tp"], "tp2", "strong"),
+    (["--gpus", "2", "--model", "tiny-llama-tp"], "dp2", "weak"),
+    (["--gpus", "2", "--tp", "2", "--ep", "--model", "tiny-mixtral-tp"], "tp2+ep", "strong"),
+])
+def test_bench_spawns_ranks(tmp_path, extra, par, scaling):
+    out = _bench(tmp_path, *extra)
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == par
+    assert out["scaling"] == scaling
+    assert out["steps"] == 3 and out["value"] > 0
+    if "tp" in par:
+        assert out["comm"]["all_reduce_per_step"] > 0
+    assert out["config"]["global_batch"] == (4 if "tp" in par else 8)
+
+
+def test_bench_rejects_mismatched_world(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
