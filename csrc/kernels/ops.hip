@@ -299,7 +299,7 @@ __global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E,
                                  float* __restrict__ topw, int* __restrict__ counts,
                                  int* __restrict__ xrows, int* __restrict__ yrows, int cap) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
+  if (t >= T || E > 64 || k > 8 || k > E) return;    // p[64] / sel[8] bounds (host checks these too)
   const float* l = logits + (size_t)t * E;
   float mx = -INFINITY;
   for (int e = 0; e < E; ++e) mx = fmaxf(mx, l[e]);
@@ -311,10 +311,12 @@ __global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E,
   int sel[8];
   float sw[8];
   for (int j = 0; j < k; ++j) {
+    // NaN / inf router logits: NaN never wins a comparison, so start from the first unused expert
+    // (be stays a valid index whatever the values are)
     int be = -1;
-    float bv = -1.f;
+    float bv = 0.f;
     for (int e = 0; e < E; ++e)
-      if (!((used >> e) & 1) && p[e] > bv) { bv = p[e]; be = e; }
+      if (!((used >> e) & 1) && (be < 0 || p[e] > bv)) { bv = p[e]; be = e; }
     used |= 1ull << be;
     sel[j] = be;
     sw[j] = bv / sum;

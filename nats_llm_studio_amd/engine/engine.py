@@ -14,7 +14,9 @@ each decode step:
 from __future__ import annotations
 
 import collections
+import hashlib
 import itertools
+import os
 import math
 import threading
 import time
@@ -84,15 +86,22 @@ class BlockAllocator:
         self.free: Deque[int] = deque(range(n))           # never-cached / invalidated blocks
         self.lru: "collections.OrderedDict[int, None]" = collections.OrderedDict()   # cached, ref 0
         self.ref = [0] * n
-        self.key_of: Dict[int, int] = {}                   # block -> chain hash
-        self.block_of: Dict[int, int] = {}                 # chain hash -> block
+        self.key_of: Dict[int, bytes] = {}                 # block -> chain digest
+        self.block_of: Dict[bytes, int] = {}               # chain digest -> block
         self.hits = 0                                      # prompt tokens served from the cache
 
+    _KEY = os.urandom(16)        # per-process key: block digests cannot be precomputed by a client
+
     @staticmethod
-    def chain_keys(tokens: Seq[int], bs: int, n_blocks: int) -> List[int]:
-        keys, h = [], 0
+    def chain_keys(tokens: Seq[int], bs: int, n_blocks: int) -> List[bytes]:
+        """Keyed BLAKE2b chain over the token ids: block i's key commits to tokens [0, (i+1)*bs),
+        so a cached block is reused only for the exact same prefix (no hash-collision reuse of
+        another request's KV)."""
+        keys, h = [], b""
+        arr = np.asarray(tokens[:n_blocks * bs], dtype=np.int64)
         for i in range(n_blocks):
-            h = hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+            h = hashlib.blake2b(h + arr[i * bs:(i + 1) * bs].tobytes(), digest_size=16,
+                                key=BlockAllocator._KEY).digest()
             keys.append(h)
         return keys
 
@@ -169,7 +178,7 @@ class _Seq:
         self.done = False
         self.row = -1          # decode-batch row (stable for the sequence's life)
         self.n_fed = 0         # positions whose KV is written or being written
-        self.keys: List[int] = []   # prefix-cache chain hashes of the full prompt blocks
+        self.keys: List[bytes] = []   # prefix-cache chain digests of the full prompt blocks
         self.n_cached = 0      # prompt tokens whose KV came from the prefix cache
 
     @property
@@ -257,6 +266,9 @@ class Engine:
         if req.params.seed is not None and not req.params.greedy:
             s.gen = torch.Generator(device="cpu").manual_seed(int(req.params.seed))
         with self.lock:
+            if self.stop_flag or self.model is None:    # unloaded / shut down: never park a request
+                fut.set_exception(RuntimeError("engine is not running (model unloaded)"))
+                return fut
             self.waiting.append(s)
             self.counters["requests"] += 1
             self.lock.notify_all()

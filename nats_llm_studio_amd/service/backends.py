@@ -102,7 +102,12 @@ class StubBackend:
 
 
 class EngineBackend:
-    """GGUF models served by the HIP engine; JIT-loaded, LRU-evicted."""
+    """GGUF models served by the HIP engine; JIT-loaded, LRU-evicted.
+
+    Loading never holds the registry lock: a model is built outside it (concurrent chats for the
+    same model wait on one per-model future), so `list_models` / `health` / chats of loaded models
+    keep answering during a tens-of-seconds load. Every chat pins its model state (`inflight`);
+    an evicted or deleted model is unloaded only when its last in-flight chat has finished."""
 
     name = "engine"
 
@@ -110,6 +115,8 @@ class EngineBackend:
         self.cfg = cfg
         self._lock = threading.RLock()
         self._loaded: "collections.OrderedDict[str, dict]" = collections.OrderedDict()
+        self._loading: Dict[str, "Future"] = {}
+        self._ids: tuple = ()          # lock-free snapshot of the loaded model ids
         self._device = None
         self.pinned = False          # tensor-parallel worker: serves only its preloaded model
 
@@ -123,8 +130,10 @@ class EngineBackend:
         return self._device
 
     def loaded_ids(self):
-        with self._lock:
-            return list(self._loaded)
+        return list(self._ids)
+
+    def _publish(self):
+        self._ids = tuple(self._loaded)
 
     def build_state(self, entry: ModelEntry, shard=None, comm=None, start: bool = True) -> dict:
         """GGUF -> device model + tokenizer + chat template + engine (one TP shard if `shard`)."""
@@ -147,36 +156,87 @@ class EngineBackend:
         if start:
             eng.start()
         return {"engine": eng, "tok": tok, "tmpl": ChatTemplate(tmpl, bos, eos), "entry": entry,
-                "load_s": time.time() - t0}
+                "load_s": time.time() - t0, "inflight": 0, "evicted": False}
 
     def adopt(self, st: dict, pinned: bool = True):
         """Serve an already-built state (tensor-parallel rank 0); other models are refused."""
+        st.setdefault("inflight", 0)
+        st.setdefault("evicted", False)
         with self._lock:
             self._loaded[st["entry"].id] = st
             self.pinned = pinned
+            self._publish()
+
+    def _evict_locked(self, keep: int) -> list:
+        """Drop LRU models until at most `keep` remain; returns the idle ones to unload now."""
+        idle = []
+        while len(self._loaded) > keep:
+            _, st = self._loaded.popitem(last=False)
+            st["evicted"] = True
+            if st["inflight"] == 0:
+                idle.append(st)
+        self._publish()
+        return idle
 
     def load(self, entry: ModelEntry) -> dict:
-        with self._lock:
-            if entry.id in self._loaded:
-                self._loaded.move_to_end(entry.id)
-                return self._loaded[entry.id]
-            if self.pinned:
-                raise RuntimeError(f"this tensor-parallel worker serves only {list(self._loaded)}")
-            while len(self._loaded) >= max(1, self.cfg.max_loaded_models):
-                old, st = self._loaded.popitem(last=False)
-                st["engine"].unload()
-            st = self.build_state(entry)
-            self._loaded[entry.id] = st
+        """The model's state, pinned for one chat (pair with `release`)."""
+        from concurrent.futures import Future
+        while True:
+            with self._lock:
+                st = self._loaded.get(entry.id)
+                if st is not None:
+                    self._loaded.move_to_end(entry.id)
+                    st["inflight"] += 1
+                    return st
+                if self.pinned:
+                    raise RuntimeError(f"this tensor-parallel worker serves only {list(self._loaded)}")
+                fut = self._loading.get(entry.id)
+                owner = fut is None
+                if owner:
+                    fut = self._loading[entry.id] = Future()
+                    idle = self._evict_locked(max(1, self.cfg.max_loaded_models) - 1)
+            if not owner:
+                fut.result()            # another chat is loading this model; then pin it (loop)
+                continue
+            for old in idle:
+                old["engine"].unload()
+            try:
+                st = self.build_state(entry)
+            except BaseException as e:
+                with self._lock:
+                    self._loading.pop(entry.id, None)
+                fut.set_exception(e)
+                raise
+            with self._lock:
+                idle = self._evict_locked(max(1, self.cfg.max_loaded_models) - 1)
+                self._loaded[entry.id] = st
+                st["inflight"] += 1
+                self._publish()
+                self._loading.pop(entry.id, None)
+            for old in idle:
+                old["engine"].unload()
+            fut.set_result(st)
             return st
+
+    def release(self, st: dict):
+        with self._lock:
+            st["inflight"] -= 1
+            gone = st["evicted"] and st["inflight"] == 0
+        if gone:
+            st["engine"].unload()
 
     def unload(self, model_id: str) -> bool:
         with self._lock:
             if self.pinned:
                 return False
             st = self._loaded.pop(model_id, None)
-        if st is None:
-            return False
-        st["engine"].unload()
+            self._publish()
+            if st is None:
+                return False
+            st["evicted"] = True
+            idle = st["inflight"] == 0
+        if idle:
+            st["engine"].unload()
         return True
 
     def chat(self, model_id: str, entry: Optional[ModelEntry], req: dict, done: Done, deadline: float = None,
@@ -196,27 +256,41 @@ class EngineBackend:
         except Exception as e:
             done(500, _error_body(f"failed to load model '{model_id}': {e}"))
             return
-        eng, tok, tmpl = st["engine"], st["tok"], st["tmpl"]
-        try:
-            prompt = tmpl.render(msgs, add_generation_prompt=True)
-        except Exception as e:
-            done(400, _error_body(f"chat template error: {e}"))
-            return
-        ids = tok.encode(prompt, add_bos=False)
-        params = SamplingParams.from_request(req, default_max=self.cfg.default_max_tokens)
-        on_token = None
-        if stream_cb is not None:
-            from ..tokenizer.bpe import StreamDecoder
-            sd = StreamDecoder(tok)
+        released = [False]
 
-            def on_token(t, _sd=sd):
-                d = _sd.push(t)
-                if d:
-                    stream_cb(d)
-        fut = eng.submit(GenRequest(ids, params, on_token=on_token, deadline=deadline))
-        ctx = eng.ctx
+        def release():
+            if not released[0]:
+                released[0] = True
+                self.release(st)
+
+        try:
+            eng, tok, tmpl = st["engine"], st["tok"], st["tmpl"]
+            try:
+                prompt = tmpl.render(msgs, add_generation_prompt=True)
+            except Exception as e:
+                release()
+                done(400, _error_body(f"chat template error: {e}"))
+                return
+            ids = tok.encode(prompt, add_bos=False)
+            params = SamplingParams.from_request(req, default_max=self.cfg.default_max_tokens)
+            on_token = None
+            if stream_cb is not None:
+                from ..tokenizer.bpe import StreamDecoder
+                sd = StreamDecoder(tok)
+
+                def on_token(t, _sd=sd):
+                    d = _sd.push(t)
+                    if d:
+                        stream_cb(d)
+            fut = eng.submit(GenRequest(ids, params, on_token=on_token, deadline=deadline))
+            ctx = eng.ctx
+        except Exception as e:
+            release()
+            done(500, _error_body(f"generation failed: {e}"))
+            return
 
         def finished(f):
+            release()
             try:
                 r = f.result()
             except Exception as e:
@@ -224,6 +298,9 @@ class EngineBackend:
                 return
             if r.finish_reason == "error":
                 done(500, _error_body(r.error or "generation failed"))
+                return
+            if r.finish_reason == "cancelled":     # engine stopped under the request (unload / shutdown)
+                done(503, _error_body(f"generation cancelled: model '{model_id}' was unloaded"))
                 return
             if r.finish_reason == "timeout":       # handler context expired (reference: 2 min, `:328`)
                 done(0, _error_body("context deadline exceeded"))
@@ -237,9 +314,11 @@ class EngineBackend:
 
     def stats(self):
         with self._lock:
-            return {"backend": "engine", "device": str(self._device),
-                    "models": {k: dict(v["engine"].stats(), load_s=round(v["load_s"], 3))
-                               for k, v in self._loaded.items()}}
+            items = list(self._loaded.items())
+        return {"backend": "engine", "device": str(self._device),
+                "loading": list(self._loading),
+                "models": {k: dict(v["engine"].stats(), load_s=round(v["load_s"], 3), inflight=v["inflight"])
+                           for k, v in items}}
 
 
 class HttpBackend:

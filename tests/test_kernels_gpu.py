@@ -254,6 +254,30 @@ def test_moe_route(gpu):
         assert toks == sorted([t for t in range(T) if ex in e[t].tolist()])
 
 
+def test_moe_route_nan_rows_stay_in_bounds(gpu):
+    """A router row of NaN / inf logits must still pick k distinct valid experts (no index -1)."""
+    T, E, k, cap = 6, 8, 2, 64
+    lg = torch.randn(T, E, device=gpu)
+    lg[1] = float("nan")
+    lg[2, 3] = float("inf")
+    lg[3, :4] = float("-inf")
+    lg[4, 5] = float("nan")
+    topw = torch.zeros(T * k, device=gpu)
+    counts = torch.zeros(E, dtype=torch.int32, device=gpu)
+    xr = torch.full((E * cap + 64,), -7, dtype=torch.int32, device=gpu)   # guard tail: never written
+    yr = torch.full((E * cap + 64,), -7, dtype=torch.int32, device=gpu)
+    ops.moe_route(lg, T, k, topw, counts, xr, yr, cap)
+    torch.cuda.synchronize()
+    c = counts.cpu()
+    assert c.sum().item() == T * k and (c >= 0).all()
+    assert (xr[E * cap:] == -7).all() and (yr[E * cap:] == -7).all()
+    seen = {t: [] for t in range(T)}
+    for ex in range(E):
+        for t in xr[ex * cap:ex * cap + c[ex]].cpu().tolist():
+            seen[t].append(ex)
+    assert all(len(v) == k and len(set(v)) == k for v in seen.values()), seen
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2])
 def test_oneshot_allreduce_simulated(gpu, world):
