@@ -8,7 +8,9 @@
 // Lane map: D/8 lanes per key (16 B each = 8 dims), 64/(D/8) keys per wave in flight;
 // every lane group keeps its own online-softmax state (m, l, o) which the workgroup
 // merges through LDS at the end. With n_split > 1 unnormalised partials go to a
-// workspace and attn_combine merges them (log-sum-exp in base 2).
+// workspace and are merged (log-sum-exp in base 2) either by the LAST active split of each
+// (token, kv head) to finish -- an agent-scope ticket in `cnt`, no second launch -- or, without
+// counters, by attn_combine.
 #include "common.h"
 
 namespace {
@@ -20,7 +22,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     const __bf16* __restrict__ q, long ldq, const __bf16* __restrict__ kc, const __bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
     const int* __restrict__ ctx_len, int Hkv, int bs, float scale, int chunk, int n_split,
-    act_t* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml) {
+    act_t* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int* __restrict__ cnt) {
   constexpr int LPT = D / 8;          // lanes per key
   constexpr int TPW = 64 / LPT;       // keys per wave per step
   constexpr int NSTREAM = 4 * TPW;    // independent softmax streams per workgroup
@@ -174,6 +177,45 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       }
     }
   }
+  if (n_split == 1 || !cnt) return;
+  // Fused combine. Splits past the context returned before reaching here (ctx == 0 rows: all run),
+  // so the active count is known; the last one to arrive merges them (Guideline 16 ticket).
+  const int na = ctx > 0 ? min(n_split, (ctx + chunk - 1) / chunk) : n_split;
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* c = cnt + (size_t)t * Hkv + kh;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == na - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int e = threadIdx.x; e < G * D; e += 256) {
+    const int h = e / D, d = e - h * D;
+    const int qh = kh * G + h;
+    const size_t pb = ((size_t)t * Hq + qh) * n_split;
+    float M = -INFINITY;
+    for (int s2 = 0; s2 < na; ++s2) M = fmaxf(M, part_ml[2 * (pb + s2)]);
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+      for (int s2 = 0; s2 < na; ++s2) {
+        const float ms = part_ml[2 * (pb + s2)];
+        if (ms == -INFINITY) continue;
+        const float f = exp2f(ms - M);
+        L += part_ml[2 * (pb + s2) + 1] * f;
+        O += part_o[(pb + s2) * D + d] * f;
+      }
+    }
+    out[(size_t)t * ldo + (size_t)qh * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
+  }
 }
 
 template <int D>
@@ -206,20 +248,21 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
 template <int D, int G>
 void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const __bf16* kc, const __bf16* vc,
                  const int* bt, int bts, const int* ts, const int* cl, int Hkv, int bs, float scale, int chunk,
-                 int ns, act_t* out, long ldo, float* po, float* pml) {
+                 int ns, act_t* out, long ldo, float* po, float* pml, int* cnt) {
   hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, q, ldq, kc, vc, bt, bts, ts, cl, Hkv, bs,
-                     scale, chunk, ns, out, ldo, po, pml);
+                     scale, chunk, ns, out, ldo, po, pml, cnt);
 }
 
 }  // namespace
 
 extern "C" {
 
-// workspace: part_o [T*Hq*n_split*D] f32, part_ml [T*Hq*n_split*2] f32 (only if n_split > 1)
+// workspace: part_o [T*Hq*n_split*D] f32, part_ml [T*Hq*n_split*2] f32 (only if n_split > 1);
+// cnt: int32 [T*Hkv], zero (re-armed by every launch): the splits merge in-kernel; null: attn_combine
 int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
                     int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
                     int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
-                    float* part_ml, void* stream) {
+                    float* part_ml, int* cnt, void* stream) {
   if (Hq % Hkv || n_split < 1 || (chunk > 0 && chunk % block_size) || 64 % (64 / (D / 8)) ||
       (4 * 64 / (D / 8)) > 64 * block_size)
     return -1;
@@ -233,7 +276,7 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
 #define NLS_ATTN_CASE(DD, GG)                                                                                 \
   if (D == DD && G == GG) {                                                                                  \
     launch_attn<DD, GG>(grid, st, qq, ldq, k, v, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \
-                        scale, chunk, n_split, o, ldo, part_o, part_ml);                                     \
+                        scale, chunk, n_split, o, ldo, part_o, part_ml, cnt);                                \
   } else
   // G = Hq/Hkv of the supported families: 1 (MHA), 2/4/8 (Llama/Mixtral), 3/5/6/7 (Qwen2 sizes, e.g. 28/4)
   NLS_ATTN_CASE(128, 1) NLS_ATTN_CASE(128, 2) NLS_ATTN_CASE(128, 3) NLS_ATTN_CASE(128, 4) NLS_ATTN_CASE(128, 5)
@@ -241,7 +284,7 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
   NLS_ATTN_CASE(64, 1) NLS_ATTN_CASE(64, 2) NLS_ATTN_CASE(64, 3) NLS_ATTN_CASE(64, 4) NLS_ATTN_CASE(64, 5)
   NLS_ATTN_CASE(64, 6) NLS_ATTN_CASE(64, 7) NLS_ATTN_CASE(64, 8) { return -1; }
 #undef NLS_ATTN_CASE
-  if (n_split > 1) {
+  if (n_split > 1 && !cnt) {
     if (D == 128)
       hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
                          n_split, chunk, block_size, o, ldo);

@@ -17,6 +17,14 @@ struct NlsSeg {
   int type, rows, K, ycol;
 };
 
+// Optional fused operands of a launch (plain C layout for ctypes; every pointer may be null).
+struct NlsFuse {
+  const float* xf; long ldxf; const float* nw; float eps;                    // input RMSNorm (path A)
+  const int* pos; const int* slot; const float* cs; const float* bias;      // EPI_ROPE
+  void* q_out; long ldq; void* kc; void* vc; int Hq, Hkv, D, pad0;
+  void* hout; long ldh; const float* onw; int* cnt;                          // residual add + RMSNorm
+};
+
 // mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
 // mode 1: path B (waves split rows, LDS-staged activations, optional split-K `ks` with workspace
 //         `ws` of ks*M*sum(rows) floats).
@@ -27,8 +35,25 @@ struct NlsSeg {
 // Returns 0 on success, a hipError_t, or -1 on bad arguments.
 static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
                       float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
-                      void* stream, const float* xf, long ldxf, const float* nw, float eps) {
-  if (xf && (mode != 0 || M > 16 || !nw)) return -1;
+                      void* stream, const NlsFuse* fz) {
+  static const NlsFuse none{};
+  if (!fz) fz = &none;
+  const float* xf = fz->xf;
+  if (xf && (mode != 0 || M > 16 || !fz->nw)) return -1;
+  if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A, plain rows, contiguous Q|K|V segments
+    if (mode != 0 || argmax || !fz->pos || !fz->slot || !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 ||
+        fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
+      return -1;
+    int c = 0;
+    for (int i = 0; i < nseg; ++i) {
+      if (segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].rows % 16 || segs[i].ycol != c) return -1;
+      c += segs[i].rows;
+    }
+    if (c != (fz->Hq + 2 * fz->Hkv) * fz->D) return -1;
+  }
+  if (fz->onw && (mode != 0 || epi != EPI_ADD_F32 || nseg != 1 || segs[0].ycol || segs[0].xmap || segs[0].ymap ||
+                  segs[0].mcount || !fz->cnt || !fz->hout || segs[0].rows % 4 || argmax))
+    return -1;
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
   if (mode == 3) {
     if (waves != 4 || (rt != 8 && rt != 16)) return -1;
@@ -73,8 +98,37 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
   const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
-  GemvArgs a{(const act_t*)x, ldx, y, ldy, M, epi, alpha, cols, (unsigned long long*)argmax, 0, M,
-             xf, ldxf, nw, eps};
+  GemvArgs a{};
+  a.x = (const act_t*)x;
+  a.ldx = ldx;
+  a.y = y;
+  a.ldy = ldy;
+  a.M = M;
+  a.epi = epi;
+  a.alpha = alpha;
+  a.pad = cols;
+  a.argmax = (unsigned long long*)argmax;
+  a.m0 = 0;
+  a.mtot = M;
+  a.xf = xf;
+  a.ldxf = fz->ldxf;
+  a.nw = fz->nw;
+  a.eps = fz->eps;
+  a.pos = fz->pos;
+  a.slot = fz->slot;
+  a.cs = fz->cs;
+  a.bias = fz->bias;
+  a.q_out = (__bf16*)fz->q_out;
+  a.ldq = fz->ldq;
+  a.kc = (__bf16*)fz->kc;
+  a.vc = (__bf16*)fz->vc;
+  a.Hq = fz->Hq;
+  a.Hkv = fz->Hkv;
+  a.D = fz->D;
+  a.hout = (act_t*)fz->hout;
+  a.ldh = fz->ldh;
+  a.onw = fz->onw;
+  a.cnt = fz->cnt;
   const int mt = M > 64 ? 8 : (M + 15) / 16;
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
@@ -107,15 +161,28 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
 int nls_qgemv(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
               float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
               void* stream) {
-  return qgemv_impl(segs, nseg, x, ldx, y, ldy, M, alpha, epi, argmax, waves, rt, mode, ks, ws, stream, nullptr, 0,
-                    nullptr, 0.f);
+  return qgemv_impl(segs, nseg, x, ldx, y, ldy, M, alpha, epi, argmax, waves, rt, mode, ks, ws, stream, nullptr);
 }
 
 // Path A with the input RMSNorm fused into the activation staging: x rows = f16(rmsnorm(xf) * nw).
 int nls_qgemv_norm(const NlsSeg* segs, int nseg, const float* xf, long ldxf, const float* nw, float eps, void* y,
                    long ldy, int M, float alpha, int epi, void* argmax, int waves, int rt, void* stream) {
-  return qgemv_impl(segs, nseg, xf, 0, y, ldy, M, alpha, epi, argmax, waves, rt, 0, 1, nullptr, stream, xf, ldxf,
-                    nw, eps);
+  NlsFuse fz{};
+  fz.xf = xf;
+  fz.ldxf = ldxf;
+  fz.nw = nw;
+  fz.eps = eps;
+  return qgemv_impl(segs, nseg, xf, 0, y, ldy, M, alpha, epi, argmax, waves, rt, 0, 1, nullptr, stream, &fz);
 }
+
+// Any launch with fused operands (input norm, RoPE/KV-append epilogue, residual + output norm).
+int nls_qgemv_ex(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M, float alpha,
+                 int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws, void* stream,
+                 const NlsFuse* fz) {
+  return qgemv_impl(segs, nseg, fz && fz->xf ? (const void*)fz->xf : x, ldx, y, ldy, M, alpha, epi, argmax, waves,
+                    rt, mode, ks, ws, stream, fz);
+}
+
+int nls_fuse_size() { return (int)sizeof(NlsFuse); }
 
 }  // extern "C"

@@ -23,7 +23,10 @@ namespace nls_gemv {
 
 // EPI_SLABS: split-K partial slabs only (the caller fuses the reduce, e.g. with RMSNorm);
 // EPI_ARGMAX: fused arg-max keys only, no logits stored (greedy decode)
-enum Epi : int { EPI_F32 = 0, EPI_ACT = 1, EPI_ADD_F32 = 2, EPI_SWIGLU = 3, EPI_SLABS = 4, EPI_ARGMAX = 5 };
+// EPI_ROPE: the Q|K|V projection's rows leave the tile rotated (adjacent-pair RoPE, + optional bias)
+//           straight into q (bf16) and the paged K/V cache: no fp32 qkv round trip, no RoPE launch
+enum Epi : int { EPI_F32 = 0, EPI_ACT = 1, EPI_ADD_F32 = 2, EPI_SWIGLU = 3, EPI_SLABS = 4, EPI_ARGMAX = 5,
+                 EPI_ROPE = 6 };
 
 struct Seg {
   const uint8_t* w;
@@ -46,7 +49,67 @@ struct GemvArgs {
   // optional fused input RMSNorm (path A, staged rows): x = f16(rmsnorm(xf[m]) * nw), xf f32
   const float* xf; long ldxf;
   const float* nw; float eps;
+  // EPI_ROPE operands (see rope_kv_kernel in ops.hip for the cache layout)
+  const int* pos; const int* slot; const float* cs; const float* bias;
+  __bf16* q_out; long ldq; __bf16* kc; __bf16* vc; int Hq, Hkv, D;
+  // EPI_ADD_F32 + onw: after the residual update the LAST workgroup to finish (agent-scope ticket
+  // `cnt`, zero between launches) normalises the updated rows: hout = f16(rmsnorm(y) * onw)
+  act_t* hout; long ldh; const float* onw; int* cnt;
 };
+
+// Workgroup ticket: true in exactly one workgroup, the last of `n` to arrive, after which every
+// global store of the others is visible to it (cdna_hip_programming.md Guideline 16: each wave drains
+// its stores, barrier, one lane releases at agent scope then bumps the counter; the last arriver
+// acquires). The last arriver re-arms the counter for the next launch. `flag`: one LDS int.
+DEVI bool last_arriver(int* cnt, int n, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == n - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// rows [0, M) of y (f32, width D, stride ldy) -> hout = f16(rmsnorm(row) * w); one workgroup of NT threads
+template <int NT>
+DEVI void rows_rmsnorm(const float* y, long ldy, int M, int D, const float* w, float eps, act_t* hout, long ldh,
+                       float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  typedef act_t act4 __attribute__((ext_vector_type(4)));
+  for (int m = 0; m < M; ++m) {
+    const float* yr = y + (size_t)m * ldy;
+    float ss = 0.f;
+    for (int i = threadIdx.x * 4; i < D; i += NT * 4) {
+      const float4 v = *reinterpret_cast<const float4*>(yr + i);
+      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) tot += red[i];
+    __syncthreads();
+    const float inv = rsqrtf(tot / (float)D + eps);
+    for (int i = threadIdx.x * 4; i < D; i += NT * 4) {
+      const float4 v = *reinterpret_cast<const float4*>(yr + i);
+      const float4 g = *reinterpret_cast<const float4*>(w + i);
+      *reinterpret_cast<act4*>(hout + (size_t)m * ldh + i) =
+          act4{(act_t)(v.x * inv * g.x), (act_t)(v.y * inv * g.y), (act_t)(v.z * inv * g.z), (act_t)(v.w * inv * g.w)};
+    }
+  }
+}
 
 DEVI unsigned long long argmax_key(float v, int idx) {
   uint32_t u = __builtin_bit_cast(uint32_t, v);
@@ -72,6 +135,44 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   int mcount = a.M;
   if (S.mcount) mcount = min(*S.mcount, a.M);
 
+  int rowc[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(row0 + rt * 16 + r, S.rows - 1);
+
+  f32x4 acc[RT][MT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Weight stream: two register buffers with FIXED roles (A: even, B: odd super-blocks), the
+  // loop unrolled by two, so a buffer is reloaded (sb + 2) right after its dequant and no
+  // register holding an in-flight load is ever copied (a copy would force vmcnt(0)).
+  typedef typename RawOf<T>::type Raw;
+  // Weight-stream depth: 4 super-blocks in flight per wave for the K-quants (<= 68 VGPRs of raw
+  // blocks at RT = 1), 2 for the wide plain-float tiles. Decode at batch 1 is latency-bound on
+  // this stream (each wave owns only K/WAVES of a 16-row tile).
+  constexpr int DEPTH = (RT == 1 && sizeof(Raw) <= 80) ? 4 : 2;
+  Raw wA[RT], wB[RT], wC[RT], wD[RT];
+  // All weight loads are unconditional (super-block index clamped into [sb0, sb1)): a
+  // conditional load breaks hipcc's vmcnt bookkeeping at the join and it falls back to
+  // vmcnt(0). The clamped tail reloads hit L2 and are never consumed.
+  const int sbl = max(sb1 - 1, sb0);
+  if (sb0 < sb1) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
+    if constexpr (DEPTH == 4) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wC[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 2, sbl), g);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wD[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 3, sbl), g);
+    }
+  }
+  // (the prologue weight loads above are issued BEFORE the activation rows are staged: at batch 1 the
+  // x round trip -- and the fused RMSNorm's reduction -- then overlaps the first weight fetch instead of
+  // preceding it on the critical path)
   // Activation rows (A operand row = batch row r of tile mt). Padded / unmapped rows load a
   // valid row (row 0: broadcast, cache-resident) and are zeroed with a select after the load:
   // a lane-conditional load would compile to a branch + vmcnt(0) per K-step that drains the
@@ -127,41 +228,6 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
       int src = m < mcount ? m : -1;
       if (S.xmap) src = (m < mcount) ? S.xmap[m] : -1;
       xr[mt] = a.x + (size_t)(src >= 0 ? src : 0) * a.ldx;
-    }
-  }
-  int rowc[RT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(row0 + rt * 16 + r, S.rows - 1);
-
-  f32x4 acc[RT][MT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // Weight stream: two register buffers with FIXED roles (A: even, B: odd super-blocks), the
-  // loop unrolled by two, so a buffer is reloaded (sb + 2) right after its dequant and no
-  // register holding an in-flight load is ever copied (a copy would force vmcnt(0)).
-  typedef typename RawOf<T>::type Raw;
-  // Weight-stream depth: 4 super-blocks in flight per wave for the K-quants (<= 68 VGPRs of raw
-  // blocks at RT = 1), 2 for the wide plain-float tiles. Decode at batch 1 is latency-bound on
-  // this stream (each wave owns only K/WAVES of a 16-row tile).
-  constexpr int DEPTH = (RT == 1 && sizeof(Raw) <= 80) ? 4 : 2;
-  Raw wA[RT], wB[RT], wC[RT], wD[RT];
-  // All weight loads are unconditional (super-block index clamped into [sb0, sb1)): a
-  // conditional load breaks hipcc's vmcnt bookkeeping at the join and it falls back to
-  // vmcnt(0). The clamped tail reloads hit L2 and are never consumed.
-  const int sbl = max(sb1 - 1, sb0);
-  if (sb0 < sb1) {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
-    if constexpr (DEPTH == 4) {
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) wC[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 2, sbl), g);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) wD[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 3, sbl), g);
     }
   }
   auto step = [&](Raw (&w)[RT], int sb) {
@@ -241,6 +307,38 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 
   // ---- epilogue ----------------------------------------------------------------
   const int ncols = MT * 16;
+  if (a.epi == EPI_ROPE) {
+    // a head's pair (2i, 2i+1) = tile rows (rr, rr+1): tiles are 16-row aligned and D is even
+    for (int e = threadIdx.x; e < RT * 8 * ncols; e += WAVES * 64) {
+      const int bb = e % ncols, rr = 2 * (e / ncols);
+      const int row = row0 + rr;
+      if (bb >= mcount || row >= S.rows) continue;
+      const int col = S.ycol + row;              // column of the fused Q|K|V output
+      float x0 = tile[rr * ncols + bb], x1 = tile[(rr + 1) * ncols + bb];
+      if (a.bias) {
+        x0 += a.bias[col];
+        x1 += a.bias[col + 1];
+      }
+      const int h = col / a.D, dd = col - h * a.D;
+      const long s = a.slot[bb];
+      __bf16* d = nullptr;
+      if (h < a.Hq + a.Hkv) {
+        const float2 c = reinterpret_cast<const float2*>(a.cs + (size_t)a.pos[bb] * a.D)[dd >> 1];
+        const float y0 = x0 * c.x - x1 * c.y, y1 = x0 * c.y + x1 * c.x;
+        x0 = y0;
+        x1 = y1;
+        if (h < a.Hq) d = a.q_out + (size_t)bb * a.ldq + col;
+        else if (s >= 0) d = a.kc + ((size_t)s * a.Hkv + (h - a.Hq)) * a.D + dd;
+      } else if (s >= 0) {
+        d = a.vc + ((size_t)s * a.Hkv + (h - a.Hq - a.Hkv)) * a.D + dd;
+      }
+      if (d) {
+        typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<bf2*>(d) = bf2{(__bf16)x0, (__bf16)x1};
+      }
+    }
+    return;
+  }
   if (a.epi == EPI_SWIGLU) {
     // tile rows [16i, 16i+8) = gate, [16i+8, 16i+16) = up of outputs (row0/2 + 8i + j)
     for (int e = threadIdx.x; e < RT * 8 * ncols; e += WAVES * 64) {
@@ -266,6 +364,14 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
     else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
     else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
+  }
+  if (a.onw) {
+    // residual + RMSNorm fusion: the next layer's input norm runs in the last workgroup
+    int* flag = reinterpret_cast<int*>(lds);
+    if (!last_arriver(a.cnt, gridDim.x, flag)) return;
+    rows_rmsnorm<WAVES * 64>(reinterpret_cast<const float*>(a.y), a.ldy, mcount, a.pad, a.onw, a.eps, a.hout, a.ldh,
+                             lds + 16);
+    return;
   }
   if (a.argmax) {
     for (int bb = threadIdx.x; bb < min(mcount, ncols); bb += WAVES * 64) {
@@ -325,12 +431,21 @@ __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArg
 // split-K over workgroups (KS > 1) writes fp32 partial slabs; splitk_reduce applies
 // the epilogue in a fixed order (deterministic, no float atomics).
 // ===========================================================================
+constexpr size_t XL_LDS_BYTES = 48 * 1024;    // path-B XL: largest staged x slice
+#ifndef NLS_XL_DEPTH
+#define NLS_XL_DEPTH 8
+#endif
+constexpr int XL_DEPTH = NLS_XL_DEPTH;         // path-B XL: weight super-blocks in flight per wave
+
 DEVI int lds_off(int row, int k) {            // element offset in a [rows][256] f16 tile
   const int ch = (k >> 3) ^ (row & 15);
   return row * 256 + ch * 8 + (k & 7);
 }
 
-template <int T, int WAVES, int RT, int MT>
+// XL (few rows, MT = 1): the workgroup's whole x slice [M][K/ks] is staged in LDS once, so the main
+// loop issues only weight loads -- no per-step global x load whose in-order vmcnt wait would drain the
+// DEPTH-deep weight prefetch, and no per-step barrier (batch-1 gate|up / down / lm_head streaming).
+template <int T, int WAVES, int RT, int MT, bool XL = false>
 DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -345,6 +460,63 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(base + rt * 16 + r, S.rows - 1);
 
   constexpr int NT = WAVES * 64;
+  f32x4 acc[RT][MT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (XL) {
+    static_assert(MT == 1, "XL stages one activation tile");
+    typedef typename RawOf<T>::type Raw;
+    // no per-step x traffic here, so the weight stream can run XL_DEPTH super-blocks ahead
+    constexpr int DEPTH = RT == 1 ? (sizeof(Raw) <= 48 ? XL_DEPTH : (sizeof(Raw) <= 80 ? 4 : 2)) : 2;
+    Raw wb[DEPTH][RT];
+    const int sbl = max(sb1 - 1, sb0);
+    if (sb0 < sb1) {      // weight prologue first: the x staging below overlaps its latency
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) wb[d][rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + d, sbl), g);
+    }
+    // x slice -> LDS [sb - sb0][M][256] (XOR-swizzled 16-B chunks)
+    const int kc = (sb1 - sb0) * 32;
+    for (int i = threadIdx.x; i < M * kc; i += NT) {
+      const int row = i / kc, c = i - row * kc;
+      *reinterpret_cast<u32x4*>(lds + (size_t)(c >> 5) * M * 256 + lds_off(row, (c & 31) * 8)) =
+          ld16(a.x + (size_t)row * a.ldx + (size_t)sb0 * 256 + c * 8);
+    }
+    __syncthreads();
+    const int xrow = min(r, M - 1);      // rows >= M feed outputs that are never stored
+    auto step = [&](Raw (&w)[RT], int sb) {
+      const act_t* xb = lds + (size_t)(sb - sb0) * M * 256;
+      f16x8 xa[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) xa[t] = *reinterpret_cast<const f16x8*>(xb + lds_off(xrow, xoff<T>(t, g)));
+      __builtin_amdgcn_sched_barrier(0);
+      f16x8 wf[RT][8];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + DEPTH, sbl), g);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt][0] = mfma16(xa[t], wf[rt][t], acc[rt][0]);
+    };
+    // buffer d always holds super-blocks = d (mod DEPTH): fixed roles, fully unrolled (no copies of
+    // registers with loads in flight, no runtime-indexed register arrays)
+    int sb = sb0;
+    for (; sb + DEPTH - 1 < sb1; sb += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) step(wb[d], sb + d);
+    }
+#pragma unroll
+    for (int d = 0; d < DEPTH - 1; ++d)
+      if (sb + d < sb1) step(wb[d], sb + d);
+  } else {
   constexpr int NCH = (MT * 16 * 32) / NT;               // 16-B chunks staged per thread
   static_assert((MT * 16 * 32) % NT == 0, "staging must divide evenly");
   // large tiles stage x in two halves (half the staging registers)
@@ -377,20 +549,23 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     }
   };
 
-  f32x4 acc[RT][MT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   typedef typename RawOf<T>::type Raw;
-  Raw wA[RT], wB[RT];
+  // weight-stream depth: few-row launches (MT <= 2) are latency-bound on the weight stream (batch-1
+  // gate|up: one 128-row workgroup per CU), so keep 4 super-blocks in flight per wave there
+  constexpr int DEPTH = (MT <= 2 && RT == 1 && sizeof(Raw) <= 80) ? 4 : 2;
+  Raw wA[RT], wB[RT], wC[RT], wD[RT];
   const int sbl = max(sb1 - 1, sb0);
   if (sb0 < sb1) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wB[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 1, sbl), g);
+    if constexpr (DEPTH == 4) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wC[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 2, sbl), g);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) wD[rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + 3, sbl), g);
+    }
     stage_full(sb0, 0);
   }
   __syncthreads();
@@ -428,7 +603,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + DEPTH, sbl), g);
       store_xh(buf ^ 1, SPLITX ? 1 : 0);
     } else {
       f16x8 wf[RT][8];
@@ -436,7 +611,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       for (int rt = 0; rt < RT; ++rt) dequant<T>(w[rt], g, wf[rt]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + 2, sbl), g);
+      for (int rt = 0; rt < RT; ++rt) w[rt] = load_raw<T, true>(W, rowc[rt], min(sb + DEPTH, sbl), g);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -454,11 +629,24 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     __syncthreads();
   };
   int sb = sb0;
-  for (; sb + 1 < sb1; sb += 2) {
-    step(wA, sb);
-    step(wB, sb + 1);
+  if constexpr (DEPTH == 4) {
+    for (; sb + 3 < sb1; sb += 4) {
+      step(wA, sb);
+      step(wB, sb + 1);
+      step(wC, sb + 2);
+      step(wD, sb + 3);
+    }
+    if (sb < sb1) step(wA, sb);
+    if (sb + 1 < sb1) step(wB, sb + 1);
+    if (sb + 2 < sb1) step(wC, sb + 2);
+  } else {
+    for (; sb + 1 < sb1; sb += 2) {
+      step(wA, sb);
+      step(wB, sb + 1);
+    }
+    if (sb < sb1) step(wA, sb);
   }
-  if (sb < sb1) step(wA, sb);
+  }   // !XL
 
   // ---- epilogue straight from the accumulators ---------------------------------
   // lane holds rows (base + rt*16 + r), batch rows mt*16 + 4g + i
@@ -515,7 +703,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   }
 }
 
-template <int WAVES, int RT, int MT, int KSET>
+template <int WAVES, int RT, int MT, int KSET, bool XL = false>
 __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                          int nmb) {
   extern __shared__ __attribute__((aligned(16))) act_t xlds[];
@@ -548,22 +736,22 @@ __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs 
   const int row0 = (tile - S.tile_begin) * WAVES * RT * 16;
   if constexpr (KSET == 0) {
     switch (S.type) {
-      case QT_Q4_K: mm_tile<QT_Q4_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q4_K: mm_tile<QT_Q4_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
       default: break;
     }
   } else if constexpr (KSET == 1) {
     switch (S.type) {
-      case QT_Q5_K: mm_tile<QT_Q5_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q8_0: mm_tile<QT_Q8_0, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q5_K: mm_tile<QT_Q5_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q8_0: mm_tile<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
       default: break;
     }
   } else {
     switch (S.type) {
-      case QT_F16: mm_tile<QT_F16, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_BF16: mm_tile<QT_BF16, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_F32: mm_tile<QT_F32, WAVES, RT, MT>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_F16: mm_tile<QT_F16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_BF16: mm_tile<QT_BF16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_F32: mm_tile<QT_F32, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
       default: break;
     }
   }
@@ -639,6 +827,20 @@ template <int WAVES, int RT, int MT, int KSET>
 int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st, int nmb) {
   const size_t lds = (size_t)2 * MT * 16 * 256 * sizeof(act_t);
   const int grid = nmb > 1 ? ((ntiles + 7) / 8) * 8 * nmb * ks : ntiles * ks;
+  if constexpr (MT == 1) {      // few rows: stage the whole x slice once (XL) when it fits
+    bool mapped = false;
+    int kmax = 0;
+    for (int i = 0; i < sl.nseg; ++i) {
+      mapped |= sl.s[i].xmap != nullptr || sl.s[i].mcount != nullptr;
+      kmax = max(kmax, sl.s[i].K);
+    }
+    const size_t xbytes = (size_t)a.M * (((kmax >> 8) + ks - 1) / ks) * 256 * sizeof(act_t);
+    if (nmb == 1 && !mapped && xbytes <= XL_LDS_BYTES) {
+      hipLaunchKernelGGL((qmm_kernel<WAVES, RT, 1, KSET, true>), dim3(grid), dim3(WAVES * 64), max(xbytes, lds), st,
+                         sl, a, ks, ws, ntiles, nmb);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, KSET>), dim3(grid), dim3(WAVES * 64), lds, st, sl, a, ks, ws,
                      ntiles, nmb);
   return (int)hipGetLastError();

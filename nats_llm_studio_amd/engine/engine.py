@@ -32,7 +32,7 @@ from .. import ops
 from ..models.llama import LlamaModel
 from .sampling import SamplingParams, sample_rows, sample_rows_gpu
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512)
+BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 640, 768, 1024)
 
 # tensor-parallel control messages (rank 0 -> followers), see Engine.follow()
 _OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE, _OP_SYNC = 0, 1, 2, 3, 4

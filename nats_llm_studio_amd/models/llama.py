@@ -4,11 +4,13 @@ quantised weights with the gfx950 kernels of `nats_llm_studio_amd.ops`.
 This is the co-located engine that replaces LM Studio's llama.cpp runtime behind
 `POST /api/v0/chat/completions` (`/root/reference/nats_llm_studio.go:158-179`).
 
-Per layer the decode step is 8 launches (7 for a dense FFN with fused epilogues):
-  rmsnorm -> QKV GEMV (Q|K|V segments, per-tensor quant type) -> RoPE + paged KV append
-  -> paged GQA attention -> O GEMV (+residual, fused) -> rmsnorm
-  -> gate|up GEMV with fused SwiGLU -> down GEMV (+residual, fused)
-and the whole step is captured once per batch bucket in a hipGraph by the engine.
+Per layer a few-row decode step (single GPU) is 5 launches:
+  QKV GEMV (Q|K|V segments, per-tensor quant type) with RoPE + paged KV append in its epilogue
+  -> paged GQA attention (flash-decoding splits merged in-kernel by the last split)
+  -> O GEMV + residual, the next RMSNorm run by its last workgroup
+  -> gate|up GEMV with fused SwiGLU -> down GEMV + residual + next RMSNorm (last workgroup)
+Large batches use the split-K / LDS GEMMs with fused reduce+RoPE and reduce+residual+RMSNorm
+kernels instead. The whole step is captured once per batch bucket in a hipGraph by the engine.
 """
 from __future__ import annotations
 
@@ -91,6 +93,8 @@ class StepBuffers:
     moe: Dict[str, torch.Tensor] = field(default_factory=dict)
     meta: Optional[torch.Tensor] = None
     pad: int = 0
+    attn_cnt: Optional[torch.Tensor] = None    # int32 [pad*Hkv] split-merge tickets (zero between launches)
+    cnt: Optional[torch.Tensor] = None         # int32 tickets of the last-workgroup residual+RMSNorm GEMVs
 
 
 class LlamaModel:
@@ -255,6 +259,8 @@ class LlamaModel:
         )
         b.meta = meta
         b.pad = pad
+        b.attn_cnt = torch.zeros(pad * self.Hkv, dtype=torch.int32, device=dev)
+        b.cnt = torch.zeros(16, dtype=torch.int32, device=dev)
         b.slot.fill_(-1)
         if cfg.n_expert:
             E = cfg.n_expert
@@ -309,9 +315,11 @@ class LlamaModel:
                                       T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)
             else:
                 ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
-                              block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws)
+                              block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws,
+                              counters=b.attn_cnt)
             if fused:
-                ops.qgemv_add_rmsnorm(Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps)
+                ops.qgemv_add_rmsnorm(Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps,
+                                      counter=b.cnt)
             else:
                 self._row_parallel(lw.wo, b.ao, x, T, cfg.residual_scale)
                 ops.rmsnorm(x, lw.ffn_norm, b.h, T, cfg.eps)
@@ -322,7 +330,8 @@ class LlamaModel:
             else:
                 ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
                 if fused:
-                    ops.qgemv_add_rmsnorm(Seg(lw.down), b.act, x, nxt, b.h, T, cfg.residual_scale, cfg.eps)
+                    ops.qgemv_add_rmsnorm(Seg(lw.down), b.act, x, nxt, b.h, T, cfg.residual_scale, cfg.eps,
+                                          counter=b.cnt)
                     fused_prev = True
                 else:
                     self._row_parallel(lw.down, b.act, x, T, cfg.residual_scale)
@@ -355,7 +364,8 @@ class LlamaModel:
             ops.qkv_rope_kv(lw.qkv, b.h, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
                             cfg.rope_neox, bias=lw.qkv_bias, norm=(x, lw.attn_norm, cfg.eps))
             ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
-                          block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws)
+                          block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws,
+                          counters=b.attn_cnt)
             ops.qgemv([Seg(lw.wo)], b.ao, x, T, alpha=cfg.residual_scale, epi="add")
             ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu", norm=(x, lw.ffn_norm, cfg.eps))
             ops.qgemv([Seg(lw.down)], b.act, x, T, alpha=cfg.residual_scale, epi="add")

@@ -19,7 +19,13 @@ from ..gguf.constants import GGMLType, GGML_BLOCK
 from ..gguf.quants import dequantize
 from . import _lib
 
-EPI = {"f32": 0, "act": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5}
+EPI = {"f32": 0, "act": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5, "rope": 6}
+import os as _os
+# Path-A row-parallel GEMVs of up to this many rows run the next RMSNorm in their last workgroup.
+# Off by default: measured on MI355X at batch 1 it LENGTHENS the step (2.43 vs 2.25 ms/token) -- the
+# last workgroup's ticket + acquire + row reload sit on the critical path and cost more than the
+# separate norm launch inside a hipGraph (profiles/rocprof_b1_r02_addnorm.txt). NLS_ADDNORM=8 enables.
+ADDNORM_MAX_M = int(_os.environ.get("NLS_ADDNORM", "0"))
 ACT_DTYPE = torch.float16   # activation dtype of every GEMM/GEMV input and SwiGLU/RMSNorm/attention output
 
 
@@ -278,12 +284,30 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
     return y
 
 
+def _segs(segs: Sequence[Seg]):
+    arr = (_lib.NlsSeg * len(segs))()
+    for i, s in enumerate(segs):
+        arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows, s.w.K,
+                             s.ycol)
+    return arr
+
+
 def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torch.Tensor, h: torch.Tensor, M: int,
-                      alpha: float, eps: float, cfg=None):
+                      alpha: float, eps: float, cfg=None, counter: Optional[torch.Tensor] = None):
     """x[:M] += alpha * xin @ W^T, then h[:M] = rmsnorm(x[:M]) * norm_w (f16). With a split-K
-    launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel."""
+    launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel; a few-row
+    path-A launch (M <= ADDNORM_MAX_M, `counter`: a zeroed int32 device word) normalises in its last
+    workgroup, so the norm costs no launch at all."""
     if x.is_cuda and seg.xmap is None:
         mode, waves, rt, ks = cfg or gemv_config([seg], M)
+        if (mode == 0 and counter is not None and M <= ADDNORM_MAX_M and seg.ycol == 0
+                and seg.w.rows == x.shape[1]):
+            fz = _lib.NlsFuse(hout=h.data_ptr(), ldh=h.stride(0), onw=norm_w.data_ptr(), cnt=counter.data_ptr(),
+                              eps=float(eps))
+            _lib.check(_lib.lib().nls_qgemv_ex(_segs([seg]), 1, xin.data_ptr(), xin.stride(0), x.data_ptr(),
+                                               x.stride(0), M, float(alpha), EPI["add"], None, waves, rt, 0, 1, None,
+                                               _stream_ptr(x), ctypes.byref(fz)), "nls_qgemv_ex(addnorm)")
+            return h
         if mode != 0 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
             L = _lib.lib()
             ws = _workspace(x.device, ks * M * seg.w.rows)
@@ -391,9 +415,29 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.
 
 def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
                 cs: torch.Tensor, q_out: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int,
-                D: int, neox: bool = False, cfg=None, bias: Optional[torch.Tensor] = None, norm=None):
-    """QKV projection + RoPE + paged KV append. With a split-K launch config the partial slabs
-    are summed inside the RoPE kernel (no separate reduce pass, no fp32 qkv round trip)."""
+                D: int, neox: bool = False, cfg=None, bias: Optional[torch.Tensor] = None, norm=None,
+                fuse_rope: bool = True):
+    """QKV projection + RoPE + paged KV append. A path-A (few-row) launch rotates in the GEMV epilogue
+    and writes q / K / V directly (one launch); with a split-K launch config the partial slabs are
+    summed inside the RoPE kernel (no separate reduce pass, no fp32 qkv round trip)."""
+    if h.is_cuda and all(s.xmap is None for s in segs):
+        mode, waves, rt, ks = cfg or gemv_config(segs, T)
+        ncol = sum(s.w.rows for s in segs)
+        contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
+        if mode == 0 and T <= 64 and not neox and contiguous and ncol == (Hq + 2 * Hkv) * D and fuse_rope:
+            # path A: RoPE + KV append in the GEMV epilogue (no qkv round trip, no RoPE launch)
+            fz = _lib.NlsFuse(pos=pos.data_ptr(), slot=slot.data_ptr(), cs=cs.data_ptr(), bias=_p(bias),
+                              q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
+                              Hq=Hq, Hkv=Hkv, D=D)
+            if norm is not None:
+                xf, nw, eps = norm
+                if not norm_fusable(T, segs[0].w.K):
+                    raise ValueError("fused-norm GEMV needs M*K*2 <= NORM_FUSE_LDS")
+                fz.xf, fz.ldxf, fz.nw, fz.eps = xf.data_ptr(), xf.stride(0), nw.data_ptr(), float(eps)
+            _lib.check(_lib.lib().nls_qgemv_ex(_segs(segs), len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(),
+                                               qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt, 0, 1, None,
+                                               _stream_ptr(h), ctypes.byref(fz)), "nls_qgemv_ex(rope)")
+            return
     if h.is_cuda and all(s.xmap is None for s in segs) and norm is None:
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
@@ -427,10 +471,14 @@ def embed(ids: torch.Tensor, w: QWeight, out: torch.Tensor, T: int, scale: float
 def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables: torch.Tensor,
               tok_seq: torch.Tensor, ctx_len: torch.Tensor, out: torch.Tensor, T: int, Hq: int, Hkv: int, D: int,
               block_size: int, scale: float, chunk: int = 256, n_split: int = 1,
-              workspace: Optional[torch.Tensor] = None):
-    """Paged GQA attention; query t attends to the first ctx_len[t] positions of sequence tok_seq[t]."""
+              workspace: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None):
+    """Paged GQA attention; query t attends to the first ctx_len[t] positions of sequence tok_seq[t].
+    n_split > 1 (flash-decoding): `counters` (zeroed int32 [>= T*Hkv]) lets the last split of each
+    (token, kv head) merge the partials in-kernel; without it a combine kernel runs."""
     if q.is_cuda:
         po = pml = None
+        if counters is not None and (counters.numel() < T * Hkv or counters.dtype != torch.int32):
+            raise ValueError("attention counters must be int32 with >= T*Hkv entries")
         if n_split > 1:
             need = T * Hq * n_split * (D + 2)
             if workspace is None or workspace.numel() < need:
@@ -440,7 +488,8 @@ def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables:
         _lib.check(_lib.lib().nls_attn_decode(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
                                               block_tables.data_ptr(), block_tables.stride(0), tok_seq.data_ptr(),
                                               ctx_len.data_ptr(), T, Hq, Hkv, D, block_size, float(scale), chunk,
-                                              n_split, out.data_ptr(), out.stride(0), po, pml, _stream_ptr(q)),
+                                              n_split, out.data_ptr(), out.stride(0), po, pml,
+                                              _p(counters) if n_split > 1 else None, _stream_ptr(q)),
                    "nls_attn_decode")
         return out
     G = Hq // Hkv

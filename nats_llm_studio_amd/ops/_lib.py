@@ -25,9 +25,21 @@ class NlsSeg(ctypes.Structure):
                 ("type", c_int), ("rows", c_int), ("K", c_int), ("ycol", c_int)]
 
 
+class NlsFuse(ctypes.Structure):
+    """Optional fused operands of one GEMV launch (csrc/kernels/qgemv.hip NlsFuse)."""
+    _fields_ = [("xf", c_void_p), ("ldxf", c_long), ("nw", c_void_p), ("eps", c_float),
+                ("pos", c_void_p), ("slot", c_void_p), ("cs", c_void_p), ("bias", c_void_p),
+                ("q_out", c_void_p), ("ldq", c_long), ("kc", c_void_p), ("vc", c_void_p),
+                ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("pad0", c_int),
+                ("hout", c_void_p), ("ldh", c_long), ("onw", c_void_p), ("cnt", c_void_p)]
+
+
 _SIGS = {
     "nls_qgemv": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_float, c_int,
                   c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "nls_qgemv_ex": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_float, c_int,
+                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, ctypes.POINTER(NlsFuse)],
+    "nls_fuse_size": [],
     "nls_qgemv_norm": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_float, c_void_p, c_long, c_int,
                        c_float, c_int, c_void_p, c_int, c_int, c_void_p],
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
@@ -44,7 +56,7 @@ _SIGS = {
     "nls_moe_combine": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p],
     "nls_attn_decode": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                         c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p,
-                        c_void_p],
+                        c_void_p, c_void_p],
     "nls_attn_prefill": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_sample": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
@@ -69,6 +81,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = c_int
+        if L.nls_fuse_size() != ctypes.sizeof(NlsFuse):
+            raise RuntimeError("stale _kernels.so: NlsFuse layout mismatch (rebuild the kernels)")
         _lib = L
     return _lib
 

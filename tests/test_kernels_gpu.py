@@ -203,7 +203,10 @@ def test_rope_kv(gpu, neox):
 
 @pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1), (128, 7), (64, 6), (128, 5)])
 @pytest.mark.parametrize("n_split,chunk", [(1, 0), (4, 0), (32, 0), (8, -16), (3, 512)])
-def test_attention_paged(gpu, D, G, n_split, chunk):
+@pytest.mark.parametrize("fused", [False, True])
+def test_attention_paged(gpu, D, G, n_split, chunk, fused):
+    """fused: flash-decoding splits merged in-kernel by the last split (ticket counters), called twice
+    to check the counters re-arm; else the separate combine kernel."""
     Hkv = 2
     Hq = Hkv * G
     bs = 16
@@ -221,10 +224,14 @@ def test_attention_paged(gpu, D, G, n_split, chunk):
     cl = torch.tensor(ctx, dtype=torch.int32)
     ref = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE)
     ops.attention(q, kc, vc, bt, ts, cl, ref, T, Hq, Hkv, D, bs, D ** -0.5)
-    out = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE, device=gpu)
-    ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), ts.to(gpu), cl.to(gpu), out, T, Hq, Hkv, D, bs,
-                  D ** -0.5, chunk=chunk, n_split=n_split)
-    torch.testing.assert_close(out.cpu().float(), ref.float(), rtol=2e-2, atol=2e-2)
+    cnt = torch.zeros(T * Hkv, dtype=torch.int32, device=gpu) if fused else None
+    for _ in range(2 if fused else 1):
+        out = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE, device=gpu)
+        ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), ts.to(gpu), cl.to(gpu), out, T, Hq, Hkv, D, bs,
+                      D ** -0.5, chunk=chunk, n_split=n_split, counters=cnt)
+        torch.testing.assert_close(out.cpu().float(), ref.float(), rtol=2e-2, atol=2e-2)
+    if fused:
+        assert int(cnt.abs().sum()) == 0
 
 
 def test_argmax_kernel(gpu):
@@ -417,22 +424,30 @@ def test_sample_kernel(gpu):
 
 
 @pytest.mark.parametrize("M,cfg", [(5, (1, 8, 1, 4)), (64, (1, 4, 1, 2)), (200, (1, 8, 1, 3)), (200, (1, 8, 1, 1)),
-                                   (7, (0, 4, 1, 1)), (256, (2, 8, 4, 4)), (130, (2, 8, 2, 2))])
-def test_qgemv_add_rmsnorm_fused(gpu, M, cfg):
-    """Row-parallel projection + residual + next RMSNorm (split-K slabs reduced by the fused kernel)."""
+                                   (7, (0, 4, 1, 1)), (256, (2, 8, 4, 4)), (130, (2, 8, 2, 2)),
+                                   (1, (0, 8, 1, 1)), (3, (0, 4, 2, 1)), (8, (0, 8, 2, 1))])
+@pytest.mark.parametrize("ticket", [False, True])
+def test_qgemv_add_rmsnorm_fused(gpu, M, cfg, ticket):
+    """Row-parallel projection + residual + next RMSNorm (split-K slabs reduced by the fused kernel;
+    few-row path A with `ticket`: the norm runs in the GEMV's last workgroup, repeated to check the
+    counter re-arms)."""
     D, K = 512, 768
     w, Wd = _qw(D, K, GGMLType.Q4_K, gpu, 11)
     xin = _x(M, K, gpu)
     pad = xin.shape[0]
     base = torch.randn(pad, D, device=gpu)
-    x = base.clone()
     nw = (1 + 0.1 * torch.randn(D)).to(gpu)
-    h = torch.zeros(pad, D, dtype=ops.ACT_DTYPE, device=gpu)
-    ops.qgemv_add_rmsnorm(ops.Seg(w), xin, x, nw, h, M, 0.7, 1e-5, cfg=cfg)
+    cnt = torch.zeros(4, dtype=torch.int32, device=gpu) if ticket else None
     xr = base[:M].cpu() + 0.7 * (xin[:M].float().cpu() @ Wd.t())
-    _close(x[:M], xr)
     hr = xr * torch.rsqrt(xr.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu()
-    _close(h[:M], hr, 3e-2)
+    for _ in range(3 if ticket else 1):
+        x = base.clone()
+        h = torch.zeros(pad, D, dtype=ops.ACT_DTYPE, device=gpu)
+        ops.qgemv_add_rmsnorm(ops.Seg(w), xin, x, nw, h, M, 0.7, 1e-5, cfg=cfg, counter=cnt)
+        _close(x[:M], xr)
+        _close(h[:M], hr, 3e-2)
+    if ticket:
+        assert int(cnt.abs().sum()) == 0
 
 
 def test_lm_head_argmax_only_epilogue(gpu):
@@ -452,10 +467,13 @@ def test_lm_head_argmax_only_epilogue(gpu):
         assert bool((y == 7.0).all())
 
 
-@pytest.mark.parametrize("cfg", [(1, 8, 1, 2), (1, 8, 1, 3), (0, 4, 1, 1), (2, 8, 4, 2), (2, 8, 2, 1)])
-@pytest.mark.parametrize("M", [3, 70, 256])
-def test_qkv_rope_kv_fused(gpu, cfg, M):
-    """QKV projection (3 segments) + RoPE + KV append, split-K slabs summed inside the RoPE kernel."""
+@pytest.mark.parametrize("cfg", [(1, 8, 1, 2), (1, 8, 1, 3), (0, 4, 1, 1), (2, 8, 4, 2), (2, 8, 2, 1), (0, 8, 2, 1),
+                                 (0, 8, 1, 1)])
+@pytest.mark.parametrize("M", [1, 3, 16, 70, 256])
+@pytest.mark.parametrize("bias", [False, True])
+def test_qkv_rope_kv_fused(gpu, cfg, M, bias):
+    """QKV projection (3 segments) + RoPE + KV append: path A rotates in the GEMV epilogue, split-K
+    launches sum their slabs inside the RoPE kernel. `bias`: Qwen2 QKV bias added before rotating."""
     Hq, Hkv, D, K = 4, 2, 128, 512
     wq, Wq = _qw(Hq * D, K, GGMLType.Q4_K, gpu, 21)
     wk, Wk = _qw(Hkv * D, K, GGMLType.Q4_K, gpu, 22)
@@ -467,6 +485,7 @@ def test_qkv_rope_kv_fused(gpu, cfg, M):
     pos = torch.arange(pad, dtype=torch.int32, device=gpu) * 3
     slot = torch.arange(pad, dtype=torch.int32, device=gpu)
     qkv = torch.zeros(pad, (Hq + 2 * Hkv) * D, device=gpu)
+    bv = torch.randn((Hq + 2 * Hkv) * D, device=gpu) if bias else None
     outs = []
     for c in (cfg, None):
         q = torch.zeros(pad, Hq * D, dtype=torch.bfloat16, device=gpu)
@@ -475,10 +494,11 @@ def test_qkv_rope_kv_fused(gpu, cfg, M):
         if c is None:       # reference: plain GEMM then the rope kernel on the CPU path
             qkv_ref = x[:M].float().cpu() @ torch.cat([Wq, Wk, Wv]).t()
             qc, kcc, vcc = q.cpu(), kc.cpu(), vc.cpu()
-            ops.rope_kv(qkv_ref, pos.cpu(), slot.cpu(), cs.cpu(), qc, kcc, vcc, M, Hq, Hkv, D)
+            ops.rope_kv(qkv_ref, pos.cpu(), slot.cpu(), cs.cpu(), qc, kcc, vcc, M, Hq, Hkv, D,
+                        bias=None if bv is None else bv.cpu())
             outs.append((qc, kcc, vcc))
         else:
-            ops.qkv_rope_kv(segs, x, qkv, pos, slot, cs, q, kc, vc, M, Hq, Hkv, D, cfg=c)
+            ops.qkv_rope_kv(segs, x, qkv, pos, slot, cs, q, kc, vc, M, Hq, Hkv, D, cfg=c, bias=bv)
             outs.append((q.cpu(), kc.cpu(), vc.cpu()))
     for a, b in zip(outs[0], outs[1]):
         _close(a[:M], b[:M], 3e-2)
