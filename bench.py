@@ -53,6 +53,10 @@ def parse(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-rtt", action="store_true")
     ap.add_argument("--single-stream", action="store_true", help="also time batch-1 decode (reported, not the headline)")
+    ap.add_argument("--serve-load", type=int, default=512,
+                    help="after the timed region: N concurrent lmstudio.chat_model requests through NATS (half "
+                         "sampled at temperature 0.7) against the same engine; 0 disables")
+    ap.add_argument("--serve-tokens", type=int, default=256, help="max_tokens of each --serve-load request")
     ap.add_argument("--step-breakdown", action="store_true",
                     help="report host time vs time blocked on the previous step's tokens (diagnostic)")
     a = ap.parse_args(argv)
@@ -262,6 +266,13 @@ def run(args, world: int):
             chat_rtt = measure_engine_chat_rtt(eng, reader.metadata, n=30)
         except Exception as e:
             extra["chat_rtt_error"] = str(e)[:300]
+        if args.serve_load > 0 and tp == 1:
+            try:   # service-path throughput: concurrent chat_model burst through natscore
+                from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_load
+                extra["service_load"] = measure_engine_chat_load(eng, reader.metadata, n=args.serve_load,
+                                                                 max_tokens=args.serve_tokens)
+            except Exception as e:
+                extra["service_load_error"] = str(e)[:300]
     eng.stop_followers()
 
     info = dict(model=model, B=B, tp=tp, t_gen=t_gen, t_load=t_load, t_prefill=t_prefill, rtt=rtt,
@@ -323,4 +334,12 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # multi-rank: results are printed and the process groups destroyed; skip interpreter teardown,
+        # where torch's gloo helper threads occasionally abort on a still-joinable std::thread
+        # ("terminate called without an active exception", ~1 in 6 CPU tp2+ep runs)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(rc or 0)
+    sys.exit(rc)

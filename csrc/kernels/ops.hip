@@ -295,39 +295,55 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
 // MoE router: softmax over E logits -> top-k (renormalised) -> per-expert row lists.
 // logits [T][E] f32; outputs: topw [T][k], counts [E] (must be zeroed), rows [E][T*k]
 // (segment-local x row = token t, y row = t*k + j).
-__global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k, int renorm,
-                                 float* __restrict__ topw, int* __restrict__ counts,
-                                 int* __restrict__ xrows, int* __restrict__ yrows, int cap) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T || E > 64 || k > 8 || k > E) return;    // p[64] / sel[8] bounds (host checks these too)
-  const float* l = logits + (size_t)t * E;
-  float mx = -INFINITY;
-  for (int e = 0; e < E; ++e) mx = fmaxf(mx, l[e]);
-  float p[64];
-  float sum = 0.f;
-  for (int e = 0; e < E; ++e) { p[e] = __expf(l[e] - mx); sum += p[e]; }
-  unsigned long long used = 0;
-  float wsum = 0.f;
-  int sel[8];
-  float sw[8];
+// One wave per token, lane e holds expert e (E <= 64): softmax and the k arg-max rounds are wave
+// reductions, so nothing is indexed at run time (no scratch). NaN / inf logits: a NaN never wins a
+// comparison, ties and NaNs resolve to the lowest unused expert, so k distinct valid experts are
+// always chosen.
+__global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k,
+                                                        int renorm, float* __restrict__ topw,
+                                                        int* __restrict__ counts, int* __restrict__ xrows,
+                                                        int* __restrict__ yrows, int cap) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T || E > 64 || k > 8 || k > E) return;    // host checks these too
+  const bool live = lane < E;
+  const float l = live ? logits[(size_t)t * E + lane] : -INFINITY;
+  float mx = l;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  const float p = live ? __expf(l - mx) : 0.f;
+  float sum = p;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  bool used = !live;
+  float wsum = 0.f, myw = 0.f;
+  int myj = -1;
   for (int j = 0; j < k; ++j) {
-    // NaN / inf router logits: NaN never wins a comparison, so start from the first unused expert
-    // (be stays a valid index whatever the values are)
-    int be = -1;
-    float bv = 0.f;
-    for (int e = 0; e < E; ++e)
-      if (!((used >> e) & 1) && (be < 0 || p[e] > bv)) { bv = p[e]; be = e; }
-    used |= 1ull << be;
-    sel[j] = be;
-    sw[j] = bv / sum;
-    wsum += sw[j];
+    // arg-max over unused experts: key = (value ordered, lowest index wins ties); NaN -> lowest key
+    const float v = used ? -INFINITY : p;
+    uint32_t u = __float_as_uint(v);
+    u = (v != v) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+    unsigned long long key = used ? 0ull : (((unsigned long long)u << 32) | (uint32_t)(63 - lane) | (1ull << 31));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long ok = __shfl_xor(key, o, 64);
+      key = ok > key ? ok : key;
+    }
+    const int be = 63 - (int)(key & 63);
+    const float bv = __shfl(p, be, 64);
+    const float w = bv / sum;
+    wsum += w;
+    if (lane == be) {
+      used = true;
+      myw = w;
+      myj = j;
+    }
   }
-  for (int j = 0; j < k; ++j) {
-    topw[t * k + j] = renorm ? sw[j] / wsum : sw[j];
-    const int e = sel[j];
-    const int pos = atomicAdd(counts + e, 1);
-    xrows[e * cap + pos] = t;
-    yrows[e * cap + pos] = t * k + j;
+  if (myj >= 0) {
+    topw[t * k + myj] = renorm ? myw / wsum : myw;
+    const int pos = atomicAdd(counts + lane, 1);
+    xrows[lane * cap + pos] = t;
+    yrows[lane * cap + pos] = t * k + myj;
   }
 }
 
@@ -408,7 +424,7 @@ int nls_argmax_unpack(const void* keys, int n, int* out, void* stream) {
 int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* topw, int* counts, int* xrows,
                   int* yrows, int cap, void* stream) {
   if (E > 64 || k > 8) return -1;
-  hipLaunchKernelGGL(moe_route_kernel, dim3((T + 63) / 64), dim3(64), 0, (hipStream_t)stream, logits, T, E, k,
+  hipLaunchKernelGGL(moe_route_kernel, dim3((T + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits, T, E, k,
                      renorm, topw, counts, xrows, yrows, cap);
   return (int)hipGetLastError();
 }

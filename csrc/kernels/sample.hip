@@ -2,8 +2,8 @@
 // temperature, top-k, min-p, top-p and the final draw -- one workgroup per row, one launch
 // for every sampled request of a step (SURVEY.md §2F sample_topk_topp).
 //
-// No sort over the vocabulary: top-k and top-p become VALUE thresholds found by bisection
-// over block-wide counts / sums (k-th largest logit; the logit above which the kept
+// No sort over the vocabulary: top-k and top-p become VALUE thresholds found by two histogram
+// passes over block-wide counts / masses (k-th largest logit; the logit above which the kept
 // probability mass reaches top_p), and the draw is an inverse-CDF walk in INDEX order over
 // the kept tokens (same distribution as sampling in sorted order). The uniform variate comes
 // from the host (per-request seeded generator), so seeded requests stay reproducible.
@@ -44,25 +44,81 @@ DEVI float block_max(float v, float* red) {
   return s;
 }
 
-__global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, long ld, int V,
-                                                    const SampleParams* __restrict__ params,
-                                                    const int* __restrict__ hist, int hist_stride,
-                                                    int* __restrict__ out) {
-  __shared__ float red[NT / 64];
-  __shared__ float s_chunk[NT];
-  const int row = blockIdx.x;
-  const SampleParams p = params[row];
-  float* l = logits + (size_t)row * ld;
+// Keep-threshold by two histogram passes (instead of ~32 bisection scans of the vocabulary): bins
+// over [a, b] (bin 0 = highest logits) accumulate the weight w of each kept logit (count: 1; mass:
+// exp((l - mx) * it)); the bin where the running weight from the top reaches `target` is refined by a
+// second histogram over that bin alone. Returns t: keeping l >= t reaches `target` (sub-bin ties are
+// kept, resolution (b - a) / NB^2).
+constexpr int NB = 1024;
+DEVI float hist_threshold(const float* __restrict__ l, int V, float a, float b, float keep_lo, bool count, float mx,
+                          float it, float target, float* hbin, float* red) {
+  float above = 0.f;                    // weight strictly above the current search range
+  for (int pass = 0; pass < 2; ++pass) {
+    if (!(b > a)) break;
+    for (int i = threadIdx.x; i < NB; i += NT) hbin[i] = 0.f;
+    __syncthreads();
+    const float scale = (float)NB / (b - a);
+    for (int i = threadIdx.x; i < V; i += NT) {
+      const float v = l[i];
+      if (v >= a && v <= b && v >= keep_lo) {
+        const int bin = min(NB - 1, (int)((b - v) * scale));
+        atomicAdd(&hbin[bin], count ? 1.f : __expf((v - mx) * it));
+      }
+    }
+    __syncthreads();
+    // running weight from the top: one wave scans the bins, 16 per lane
+    __shared__ int s_bin;
+    __shared__ float s_before;
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      float mine = 0.f;
+#pragma unroll
+      for (int j = 0; j < NB / 64; ++j) mine += hbin[lane * (NB / 64) + j];
+      float incl = mine;                              // inclusive prefix over lanes
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+      }
+      const float excl = incl - mine;
+      const bool cross = above + incl >= target && above + excl < target;
+      const unsigned long long m = __ballot(cross);
+      const int owner = m ? __ffsll((long long)m) - 1 : 63;
+      if (lane == owner) {
+        float acc = above + excl;
+        int bin = lane * (NB / 64) + NB / 64 - 1;
+        for (int j = 0; j < NB / 64; ++j) {
+          const float w = hbin[lane * (NB / 64) + j];
+          if (acc + w >= target) { bin = lane * (NB / 64) + j; break; }
+          acc += w;
+        }
+        s_bin = bin;
+        s_before = acc;
+      }
+    }
+    __syncthreads();
+    const int bin = s_bin;
+    above = s_before;
+    const float nb = b - (float)bin / scale, na = b - (float)(bin + 1) / scale;
+    b = nb;
+    a = na;
+    __syncthreads();
+  }
+  return a;
+}
 
+// One row: penalties over the history window h[0, n_hist) (any order), then greedy / temperature /
+// top-k / min-p / top-p and the draw with uniform u. The token is returned in EVERY thread.
+DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u, const int* __restrict__ h,
+                    int n_hist, float* red, float* s_chunk, int* s_tok, float* hbin) {
   // 1) penalties on the distinct ids of the history window (llama.cpp-style semantics)
-  if (p.n_hist > 0 && (p.repeat_penalty != 1.f || p.presence_penalty != 0.f || p.frequency_penalty != 0.f)) {
-    const int* h = hist + (size_t)row * hist_stride;
+  if (n_hist > 0 && (p.repeat_penalty != 1.f || p.presence_penalty != 0.f || p.frequency_penalty != 0.f)) {
     const int j = threadIdx.x;
-    if (j < p.n_hist) {
+    if (j < n_hist) {
       const int id = h[j];
       bool first = true;
       int cnt = 0;
-      for (int i = 0; i < p.n_hist; ++i) {
+      for (int i = 0; i < n_hist; ++i) {
         if (h[i] == id) {
           ++cnt;
           if (i < j) first = false;
@@ -87,30 +143,16 @@ __global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, 
       if (l[i] == mx) best = min(best, i);
     float b = (float)best;   // exact for V < 2^24
     b = -block_max(-b, red);
-    if (threadIdx.x == 0) out[row] = (int)b;
-    return;
+    return (int)b;
   }
   const float it = 1.f / p.temperature;
   // 3) keep-threshold on the logit scale: top-k (k-th largest) and min-p (p >= min_p * p_max)
   float lo = -INFINITY;
   if (p.top_k > 0 && p.top_k < V) {
-    float a = mx - 1.f, b = mx;         // find the largest t with count(l >= t) >= k
-    // widen the lower bracket until it holds k values
-    for (int it2 = 0; it2 < 40; ++it2) {
-      float c = 0.f;
-      for (int i = threadIdx.x; i < V; i += NT) c += l[i] >= a ? 1.f : 0.f;
-      c = block_sum(c, red);
-      if (c >= (float)p.top_k) break;
-      a = mx - 2.f * (mx - a);
-    }
-    for (int it2 = 0; it2 < 32; ++it2) {
-      const float t = 0.5f * (a + b);
-      float c = 0.f;
-      for (int i = threadIdx.x; i < V; i += NT) c += l[i] >= t ? 1.f : 0.f;
-      c = block_sum(c, red);
-      if (c >= (float)p.top_k) a = t; else b = t;
-    }
-    lo = a;
+    float mn = INFINITY;
+    for (int i = threadIdx.x; i < V; i += NT) mn = fminf(mn, l[i]);
+    mn = -block_max(-mn, red);
+    lo = hist_threshold(l, V, mn, mx, -INFINITY, true, mx, it, (float)p.top_k, hbin, red);
   }
   if (p.min_p > 0.f) lo = fmaxf(lo, mx + p.temperature * __logf(p.min_p));
   // 4) top-p: logit threshold above which the kept mass reaches top_p of the kept total
@@ -119,16 +161,9 @@ __global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, 
     if (l[i] >= lo) Z += __expf((l[i] - mx) * it);
   Z = block_sum(Z, red);
   if (p.top_p < 1.f) {
-    float a = lo == -INFINITY ? mx - 80.f * p.temperature : lo, b = mx;
-    for (int it2 = 0; it2 < 32; ++it2) {
-      const float t = 0.5f * (a + b);
-      float s = 0.f;
-      for (int i = threadIdx.x; i < V; i += NT)
-        if (l[i] >= t && l[i] >= lo) s += __expf((l[i] - mx) * it);
-      s = block_sum(s, red);
-      if (s >= p.top_p * Z) a = t; else b = t;
-    }
-    lo = fmaxf(lo, a);
+    // tokens more than 30 temperatures below the max carry < e^-30 of the mass each: search above them
+    const float a = fmaxf(lo, mx - 30.f * p.temperature);
+    lo = fmaxf(lo, hist_threshold(l, V, a, mx, lo, false, mx, it, p.top_p * Z, hbin, red));
     Z = 0.f;
     for (int i = threadIdx.x; i < V; i += NT)
       if (l[i] >= lo) Z += __expf((l[i] - mx) * it);
@@ -143,7 +178,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, 
   s_chunk[threadIdx.x] = cs;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float target = p.u * Z;
+    const float target = u * Z;
     float acc = 0.f;
     int owner = -1;
     for (int t = 0; t < NT; ++t) {
@@ -165,7 +200,63 @@ __global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, 
       for (int i = V - 1; i >= 0; --i)
         if (l[i] >= lo) { tok = i; break; }
     }
-    out[row] = tok;
+    *s_tok = tok;
+  }
+  __syncthreads();
+  return *s_tok;
+}
+
+__global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, long ld, int V,
+                                                    const SampleParams* __restrict__ params,
+                                                    const int* __restrict__ hist, int hist_stride,
+                                                    int* __restrict__ out) {
+  __shared__ float red[NT / 64];
+  __shared__ float s_chunk[NT];
+  __shared__ int s_tok;
+  __shared__ float hbin[NB];
+  const int row = blockIdx.x;
+  const SampleParams p = params[row];
+  const int tok = sample_one(logits + (size_t)row * ld, V, p, p.u, hist + (size_t)row * hist_stride, p.n_hist, red,
+                             s_chunk, &s_tok, hbin);
+  if (threadIdx.x == 0) out[row] = tok;
+}
+
+// counter-based uniform in [0, 1): splitmix64 of (seed, position) -- reproducible per seeded request
+DEVI float uniform01(unsigned long long seed, int pos) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (unsigned long long)(pos + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.f / 16777216.f);
+}
+
+// In-graph sampling of a decode step: rows whose params ask for sampling replace the fused arg-max
+// token in next_ids with a draw; the uniform comes from (seed, position), the penalty window is a
+// per-row ring of the last HIST tokens indexed by absolute position (the host fills it when the row
+// is assigned, every sampled step appends its token), so sampled rows stay on the chained
+// asynchronous decode path (no host round trip, no logits copy).
+__global__ __launch_bounds__(NT) void sample_decode_kernel(float* __restrict__ logits, long ld, int V,
+                                                           const SampleParams* __restrict__ params,
+                                                           const unsigned long long* __restrict__ seeds,
+                                                           const int* __restrict__ pos, const int* __restrict__ ctx_len,
+                                                           int* __restrict__ hist, int hist_stride,
+                                                           int* __restrict__ next_ids) {
+  __shared__ float red[NT / 64];
+  __shared__ float s_chunk[NT];
+  __shared__ int s_tok;
+  __shared__ float hbin[NB];
+  const int row = blockIdx.x;
+  const SampleParams p = params[row];
+  const bool penal = p.repeat_penalty != 1.f || p.presence_penalty != 0.f || p.frequency_penalty != 0.f;
+  if (ctx_len[row] <= 0 || (p.temperature <= 0.f && !penal)) return;     // padding / greedy row
+  const int ps = pos[row];
+  int* h = hist + (size_t)row * hist_stride;
+  const int n_hist = min(hist_stride, ps + 1);
+  const int tok = sample_one(logits + (size_t)row * ld, V, p, uniform01(seeds[row], ps), h, n_hist, red, s_chunk,
+                             &s_tok, hbin);
+  if (threadIdx.x == 0) {
+    next_ids[row] = tok;
+    h[(ps + 1) % hist_stride] = tok;
   }
 }
 
@@ -180,3 +271,13 @@ extern "C" int nls_sample(void* logits, long ld, int n, int V, const void* param
 }
 
 extern "C" int nls_sample_params_size() { return (int)sizeof(SampleParams); }
+
+extern "C" int nls_sample_decode(void* logits, long ld, int n, int V, const void* params, const void* seeds,
+                                 const int* pos, const int* ctx_len, int* hist, int hist_stride, int* next_ids,
+                                 void* stream) {
+  if (n < 1 || V < 1 || hist_stride < 1 || hist_stride > NT) return -1;
+  hipLaunchKernelGGL(sample_decode_kernel, dim3(n), dim3(NT), 0, (hipStream_t)stream, (float*)logits, ld, V,
+                     (const SampleParams*)params, (const unsigned long long*)seeds, pos, ctx_len, hist, hist_stride,
+                     next_ids);
+  return (int)hipGetLastError();
+}

@@ -30,7 +30,7 @@ import torch
 
 from .. import ops
 from ..models.llama import LlamaModel
-from .sampling import SamplingParams, sample_rows, sample_rows_gpu
+from .sampling import HIST, SamplingParams, sample_rows, sample_rows_gpu
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 640, 768, 1024)
 
@@ -245,9 +245,19 @@ class Engine:
         self.thread: Optional[threading.Thread] = None
         self.stop_flag = False
         self._ids = itertools.count()
-        self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0)
+        self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0,
+                             device_sampled_steps=0)
         self.full_logits: Optional[torch.Tensor] = None
         self._ctrl_hdr = torch.zeros(_HDR + self.max_batch, dtype=torch.int32)
+        # In-graph sampling (single GPU): per-row sampling params / seeds / penalty-history rings live on
+        # the device, written once when a sequence takes its decode row; sampled rows then stay on the
+        # chained asynchronous decode path (ops.sample_decode after the lm-head, inside the hipGraph).
+        self.device_sampling = (self.dev.type == "cuda" and self.tp is None
+                                and os.environ.get("NLS_DEVICE_SAMPLING", "1") == "1")
+        if self.device_sampling:
+            self.d_sparams = torch.zeros(self.max_batch, ops.SAMPLE_PARAMS_BYTES, dtype=torch.uint8, device=self.dev)
+            self.d_seeds = torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev)
+            self.d_hist = torch.full((self.max_batch, HIST), -1, dtype=torch.int32, device=self.dev)
         self.sync_hook: Optional[Callable[[], None]] = None   # follower side of Engine.sync()
 
     # ------------------------------------------------------------------ API
@@ -547,6 +557,26 @@ class Engine:
             bt = hm.numpy()[_NSEG * self.db.pad:].reshape(self.max_batch, self.max_blocks)
             bt[r, :nb] = s.blocks
             bt[r, nb:] = 0
+        if self.device_sampling:
+            self._upload_sampling_row(r, s)
+
+    def _upload_sampling_row(self, r: int, s: _Seq):
+        """Row r's sampling state on the device: params (greedy rows: temperature 0, neutral penalties,
+        skipped by the sampler), seed, and the last HIST tokens at ring slots (position % HIST)."""
+        p = s.req.params
+        if p.greedy:
+            raw = ops.sample_params_bytes()
+            seed = 0
+        else:
+            raw = ops.sample_params_bytes(p)
+            seed = int(p.seed) if p.seed is not None else int.from_bytes(os.urandom(8), "little") >> 1
+        hist = np.full(HIST, -1, dtype=np.int32)
+        n = len(s.tokens)
+        for q in range(max(0, n - HIST), n):
+            hist[q % HIST] = s.tokens[q]
+        self.d_sparams[r].copy_(torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()))
+        self.d_seeds[r] = seed & 0x7FFFFFFFFFFFFFFF
+        self.d_hist[r].copy_(torch.from_numpy(hist))
 
     def _release_rows(self, keep=()):
         keep = set(id(x) for x in keep)
@@ -588,7 +618,7 @@ class Engine:
         slot[rows] = bt[rows, p // self.bs] * self.bs + p % self.bs
         return Bp
 
-    def _launch(self, launch: List[_Seq], prev: set, need: bool = False):
+    def _launch(self, launch: List[_Seq], prev: set, need: bool = False, dsamp: bool = False):
         k = self._kbuf = self._kbuf ^ 1
         Bp = self._build_meta(k, launch, prev)
         pad = self.db.pad
@@ -598,7 +628,9 @@ class Engine:
             b.meta.copy_(self.h_meta_d2[k], non_blocking=True)
         else:
             b.meta.copy_(self.h_meta_d2[k])
-        self._run_decode(Bp, need)
+        self._run_decode(Bp, need, dsamp)
+        if dsamp:
+            self.counters["device_sampled_steps"] += 1
         for s in launch:
             s.n_fed += 1
         if self.dev.type == "cuda":
@@ -629,7 +661,8 @@ class Engine:
             if s.row < 0:
                 self._assign_row(s)
         greedy = all(s.req.params.greedy for s in seqs)
-        chain = self.async_decode and greedy
+        dsamp = not greedy and self.device_sampling    # sampled rows drawn inside the decode graph
+        chain = self.async_decode and (greedy or dsamp)
         if not chain:
             self._drain()
         n_rows = max(s.row for s in seqs) + 1
@@ -651,7 +684,7 @@ class Engine:
                 self._process_sync(new, launch, need)
             self._release_rows()
             return
-        new = self._launch(launch, prev) if launch else None
+        new = self._launch(launch, prev, dsamp=dsamp) if launch else None
         self._inflight = None
         if infl is not None:
             self._process(infl)
@@ -680,26 +713,41 @@ class Engine:
             if not s.done:
                 self._append(s, t)
 
-    def _run_decode(self, Bp: int, need_logits: bool = False):
+    def _step_forward(self, Bp: int, ns: int, need_logits: bool, dsamp: bool):
+        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True,
+                           need_logits=need_logits or dsamp)
+        if dsamp:
+            b = self.db
+            ops.sample_decode(b.logits, Bp, self.d_sparams, self.d_seeds, b.pos, b.ctx_len, self.d_hist, b.next_ids)
+
+    def _run_decode(self, Bp: int, need_logits: bool = False, dsamp: bool = False):
         ns = LlamaModel.attn_splits(Bp, self.model.Hkv)
         if not self.use_graphs:
-            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True, need_logits=need_logits)
+            self._step_forward(Bp, ns, need_logits, dsamp)
             return
-        g = self.graphs.get((Bp, need_logits))
-        if g is None:                          # TP followers capture lazily in the same step
-            g = self._capture(Bp, ns, need_logits)
+        key = (Bp, need_logits, dsamp) if dsamp else (Bp, need_logits)
+        g = self.graphs.get(key)
+        if g is None:
+            # first use of this graph (TP followers, sampled / logits variants): THIS step runs eagerly --
+            # exactly once, it has side effects (chained ids, KV append, history ring) -- and the capture
+            # that follows only records the kernels for the next steps
+            self._step_forward(Bp, ns, need_logits, dsamp)
+            self._capture(Bp, ns, need_logits, dsamp, warm=False)
+            return
         g.replay()
         self.counters["graph_replays"] += 1
 
-    def _capture(self, Bp: int, ns: int, need_logits: bool = False):
-        # eager warm-up allocates every lazily sized workspace before capture
-        self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True, need_logits=need_logits)
+    def _capture(self, Bp: int, ns: int, need_logits: bool = False, dsamp: bool = False, warm: bool = True):
+        # eager warm-up allocates every lazily sized workspace before capture (callers whose step already
+        # ran eagerly pass warm=False)
+        if warm:
+            self._step_forward(Bp, ns, need_logits, dsamp)
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True, need_logits=need_logits)
+            self._step_forward(Bp, ns, need_logits, dsamp)
         torch.cuda.synchronize(self.dev)
-        self.graphs[(Bp, need_logits)] = g
+        self.graphs[(Bp, need_logits, dsamp) if dsamp else (Bp, need_logits)] = g
         return g
 
     def capture_all(self, buckets: Seq[int] = None):

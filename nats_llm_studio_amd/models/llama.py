@@ -404,7 +404,9 @@ class LlamaModel:
         # LDS-dequant GEMM (mode 2) over all experts, each m-block of an expert gathering its rows
         # through xrows and exiting when it lies past the expert's device-side count
         gemm = T > 64 and self.device.type == "cuda"
-        step = T if gemm else 64
+        # path-A chunks of <= 32 tokens: the mapped GEMV then runs with <= 2 activation tiles, whose
+        # kernels keep every fragment in registers (3-4 tiles spill: -Rpass-analysis scratch > 0)
+        step = T if gemm else 32
         # m-block = 64*rt rows. Every m-block re-dequantises the expert's weights, so the largest
         # block wins even at ~64 routed rows per expert (Mixtral B=256, tools/moe_ab.sh: gate/up
         # rt 4 / down rt 2 = 32.0 ms/step, 2/2 = 34.3, 2/1 = 39.6, 1/1 = 50.8)
@@ -424,6 +426,14 @@ class LlamaModel:
             segs = [Seg(dn, 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, _, dn in loc]
             for s0 in range(0, len(segs), 8):
                 ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32", **dn)
+            xs = b.x[c0:c0 + n]
             if self.shard.size > 1:
-                self.comm.all_reduce(m["yexp"][:n * k])
-            ops.moe_combine(m["yexp"], m["topw"], n, k, b.x[c0:], cfg.residual_scale)
+                # combine locally first, then ONE all-reduce of the combined [n, d] rows (k x fewer bytes
+                # than reducing the per-slot expert outputs): rank 0 adds into the residual, the others
+                # contribute their partial combine from zero (EP: own experts; TP: own FFN slice)
+                if self.shard.rank != 0:
+                    xs.zero_()
+                ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale)
+                self.comm.all_reduce(xs)
+            else:
+                ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale)

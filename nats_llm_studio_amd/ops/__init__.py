@@ -564,6 +564,33 @@ def argmax_unpack(keys: torch.Tensor, n: int, out: torch.Tensor):
     return out
 
 
+SAMPLE_PARAMS_BYTES = 40      # csrc/kernels/sample.hip SampleParams
+
+
+def sample_params_bytes(p=None) -> bytes:
+    """Device SampleParams of one row; None: a greedy row (skipped by the in-graph sampler)."""
+    if p is None:
+        sp = _lib.SampleParams(0.0, 1.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0, 0, 0)
+    else:
+        sp = _lib.SampleParams(p.temperature, p.top_p, p.min_p, p.repeat_penalty, p.presence_penalty,
+                               p.frequency_penalty, 0.0, int(p.top_k or 0), 0, 0)
+    raw = bytes(sp)
+    assert len(raw) == SAMPLE_PARAMS_BYTES
+    return raw
+
+
+def sample_decode(logits: torch.Tensor, n: int, params: torch.Tensor, seeds: torch.Tensor, pos: torch.Tensor,
+                  ctx_len: torch.Tensor, hist: torch.Tensor, next_ids: torch.Tensor):
+    """In-graph sampling of decode rows [0, n): rows whose device params ask for sampling overwrite
+    next_ids with a draw (uniform from (seed, position)), appending it to their history ring."""
+    if logits.dtype != torch.float32 or logits.stride(1) != 1:
+        raise TypeError("sample_decode: fp32 row-major logits")
+    _lib.check(_lib.lib().nls_sample_decode(logits.data_ptr(), logits.stride(0), n, logits.shape[1], params.data_ptr(),
+                                            seeds.data_ptr(), pos.data_ptr(), ctx_len.data_ptr(), hist.data_ptr(),
+                                            hist.shape[1], next_ids.data_ptr(), _stream_ptr(logits)),
+               "nls_sample_decode")
+
+
 def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
               yrows: torch.Tensor, cap: int, renorm: bool = True):
     E = logits.shape[1]

@@ -61,6 +61,8 @@ _SIGS = {
                          c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_sample": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "nls_sample_params_size": [],
+    "nls_sample_decode": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                          c_void_p, c_void_p],
     "nls_ar_alloc": [c_long, c_int, c_void_p, c_void_p],
     "nls_ar_open": [c_void_p, c_void_p],
     "nls_ar_close": [c_void_p],

@@ -100,5 +100,115 @@ def measure_engine_chat_rtt(engine, metadata: dict, model_id: str = "llama-3-8b"
             "prompt_tokens": r["data"]["response"]["usage"]["prompt_tokens"]}
 
 
+def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b", n: int = 512,
+                             max_tokens: int = 64, sampled_frac: float = 0.5, timeout_s: float = 600.0,
+                             seed: int = 0) -> dict:
+    """Service-path throughput: `n` concurrent `lmstudio.chat_model` requests published at once through
+    the embedded NATS server (natscore) -> Python handlers -> chat template / tokenizer -> the REAL
+    continuous-batching engine -> JSON replies to per-request inboxes. A fraction `sampled_frac` of the
+    requests carries the reference README's sampling payload (`temperature: 0.7`,
+    /root/reference/README.md:200-203); the rest are greedy. Reports output tok/s over the whole
+    burst (first publish -> last reply, from the replies' usage.completion_tokens) and per-request
+    RTT p50/p99."""
+    import random
+    import threading
+    import time
+    from ..natsio import Client, EmbeddedServer
+    from ..tokenizer.bpe import tokenizer_from_metadata
+    from ..tokenizer.chat_template import ChatTemplate, default_template
+    from .backends import EngineBackend
+    from .config import WorkerConfig
+    from .registry import ModelEntry
+    from .service import Service
+    tok = tokenizer_from_metadata(metadata)
+    tmpl = metadata.get("tokenizer.chat_template") or default_template(engine.cfg.arch,
+                                                                       metadata.get("tokenizer.ggml.model", "gpt2"))
+    bos = tok.tokens[tok.bos_id] if tok.bos_id is not None else ""
+    eos = tok.tokens[tok.eos_id] if tok.eos_id is not None else ""
+    engine.tok = tok
+    started = engine.thread is None
+    engine.start()
+    rnd = random.Random(seed)
+    words = ("the model of a system that runs on eight GPUs with fast links between them and a large cache "
+             "tell me about history science music art code data network latency token batch kernel memory").split()
+    done = threading.Event()
+    t_send, t_recv, bodies = {}, {}, {}
+    lock = threading.Lock()
+    with tempfile.TemporaryDirectory() as d:
+        srv = EmbeddedServer(max_payload=8 << 20).start()
+        cfg = WorkerConfig(nats_url=srv.url, models_dir=d, backend="engine")
+        cfg.handler_workers = max(cfg.handler_workers, 8)
+        backend = EngineBackend(cfg)
+        entry = ModelEntry(id=model_id, publisher="synthetic", model_dir=model_id, path="", dir=d,
+                           arch=engine.cfg.arch, quantization="Q4_K_M", max_context_length=engine.ctx)
+        backend.adopt({"engine": engine, "tok": tok, "tmpl": ChatTemplate(tmpl, bos, eos), "entry": entry,
+                       "load_s": 0.0})
+        svc = Service(cfg, backend=backend)
+        svc.start()
+        svc.registry.add(entry)
+        cli = Client().connect(srv.url)
+
+        def on_reply(m):
+            now = time.perf_counter()
+            i = int(m.subject.rsplit(".", 1)[1])
+            with lock:
+                t_recv[i] = now
+                bodies[i] = m.data
+                if len(t_recv) == n:
+                    done.set()
+
+        sub = cli.subscribe("_INBOX.load.>", "", on_reply, 4)
+        cli.flush()
+        payloads = []
+        for i in range(n):
+            text = " ".join(rnd.choice(words) for _ in range(rnd.randint(40, 90)))
+            req = {"model": model_id, "messages": [{"role": "system", "content": "You are a helpful assistant."},
+                                                   {"role": "user", "content": text}],
+                   "max_tokens": max_tokens, "ignore_eos": True}
+            if i < int(round(sampled_frac * n)):
+                req.update(temperature=0.7, top_p=0.95, seed=i)
+            else:
+                req["temperature"] = 0
+            payloads.append(json.dumps(req).encode())
+        order = list(range(n))
+        rnd.shuffle(order)                  # sampled and greedy requests interleave in the batch
+        try:
+            t0 = time.perf_counter()
+            for i in order:
+                t_send[i] = time.perf_counter()
+                cli.publish("lmstudio.chat_model", payloads[i], reply=f"_INBOX.load.{i}")
+            cli.flush()
+            ok = done.wait(timeout_s)
+            t1 = max(t_recv.values()) if t_recv else time.perf_counter()
+        finally:
+            sub.unsubscribe()
+            cli.close()
+            for s2 in svc.subs:
+                s2.unsubscribe()
+            svc.client.close()
+            srv.stop()
+            if started:
+                engine.shutdown()
+    comp, good, rtts, ttft, gen = 0, 0, [], [], []
+    for i, b in bodies.items():
+        r = json.loads(b)
+        if r.get("ok") and r["data"].get("http_status") == 200:
+            good += 1
+            resp = r["data"]["response"]
+            comp += resp["usage"]["completion_tokens"]
+            st = resp.get("stats", {})
+            if "time_to_first_token" in st:
+                ttft.append(st["time_to_first_token"] * 1e3)
+                gen.append(st["generation_time"] * 1e3)
+        rtts.append((t_recv[i] - t_send[i]) * 1e3)
+    wall = t1 - t0
+    return {"requests": n, "ok": good, "complete": bool(ok), "sampled_frac": sampled_frac, "max_tokens": max_tokens,
+            "completion_tokens": comp, "wall_s": round(wall, 3), "tok_s": round(comp / wall, 1) if wall > 0 else None,
+            "rtt_p50_ms": round(_pct(rtts, 50), 1) if rtts else None,
+            "rtt_p99_ms": round(_pct(rtts, 99), 1) if rtts else None,
+            "ttft_p50_ms": round(_pct(ttft, 50), 1) if ttft else None,
+            "generation_p50_ms": round(_pct(gen, 50), 1) if gen else None}
+
+
 if __name__ == "__main__":
     print(json.dumps(measure_rtt()))

@@ -42,3 +42,17 @@ def test_bench_rejects_mismatched_world(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_service_load_generator_cpu(tiny_models):
+    """The bench's service-path burst: concurrent chat_model requests (half sampled) all answered 200
+    through natscore by the real engine, tokens counted from the replies' usage."""
+    from nats_llm_studio_amd.engine.engine import Engine
+    from nats_llm_studio_amd.gguf.reader import GGUFReader
+    from nats_llm_studio_amd.models.llama import LlamaModel
+    from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_load
+    r = GGUFReader(tiny_models["tiny-llama"])
+    eng = Engine(LlamaModel(r, "cpu"), None, max_batch=8, use_graphs=False, ctx=512)
+    out = measure_engine_chat_load(eng, r.metadata, n=8, max_tokens=3)
+    assert out["complete"] and out["ok"] == 8 and out["completion_tokens"] == 24
+    assert out["tok_s"] > 0 and out["rtt_p99_ms"] >= out["rtt_p50_ms"]

@@ -92,3 +92,32 @@ def test_graph_equals_eager(gpu, tiny_models):
             eng.step()
         outs.append([f.result().token_ids for f in futs])
     assert outs[0] == outs[1]
+
+
+def test_device_sampling_in_graph(gpu, tiny_models):
+    """Sampled rows stay on the chained decode graph (ops.sample_decode): top_k=1 sampling equals
+    greedy, seeded draws reproduce, and the device penalty window (history ring filled at row
+    assignment, appended in-graph) bans every recent token under a huge presence penalty."""
+    r = GGUFReader(tiny_models["tiny-llama"])
+    m = LlamaModel(r, gpu)
+    prompt = [5, 17, 99, 3, 250, 7, 81, 12]
+
+    def run(params_list):
+        eng = Engine(m, None, max_batch=8, use_graphs=True)
+        futs = [eng.submit(GenRequest(list(prompt), p)) for p in params_list]
+        while not all(f.done() for f in futs):
+            eng.step()
+        return [f.result().token_ids for f in futs], eng.counters["device_sampled_steps"]
+
+    g = SamplingParams(max_tokens=12, ignore_eos=True)
+    k1 = SamplingParams(max_tokens=12, ignore_eos=True, temperature=1.0, top_k=1)
+    (a, b), n = run([g, k1])
+    assert a == b and n > 0
+    s1 = SamplingParams(max_tokens=12, ignore_eos=True, temperature=1.5, seed=11)
+    s2 = SamplingParams(max_tokens=12, ignore_eos=True, temperature=1.5, seed=12)
+    (x1, y1), _ = run([s1, s2])
+    (x2, y2), _ = run([s1, s2])
+    assert x1 == x2 and y1 == y2
+    ban = SamplingParams(max_tokens=20, ignore_eos=True, temperature=1.0, top_k=1, presence_penalty=1e9)
+    (t,), _ = run([ban])
+    assert len(set(t)) == len(t) and not (set(t[1:]) & set(prompt)), t
