@@ -26,8 +26,16 @@
 #pragma once
 #include "qgemv_impl.h"
 
+#ifndef NLS_GEMM_MFMA32
+#define NLS_GEMM_MFMA32 0     // 1: 32x32x16 MFMA tiles (A/B variant, tools/gemm_ab.py)
+#endif
+#ifndef NLS_GEMM_SETPRIO
+#define NLS_GEMM_SETPRIO 0    // 1: s_setprio(1) around each MFMA cluster (A/B variant)
+#endif
+
 namespace nls_gemm {
 using namespace nls_gemv;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int T, int WM>
 DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds,
@@ -51,11 +59,26 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   const int M = a.M;
   const int drow = min(row0 + wave * 16 + r, S.rows - 1);   // this wave's dequant rows (clamped)
 
-  f32x4 acc[MTW][NTW];
+  // 32x32x16 MFMA tiles (variant): the wave's 64 x (128*WM/8) output as (MTW/2) x (NTW/2) 32x32
+  // accumulators; blocks with a single 16-row weight tile per wave keep 16x16x32
+  constexpr bool M32 = NLS_GEMM_MFMA32 && NTW >= 2;
+  constexpr int MT2 = M32 ? MTW / 2 : 1, NT2 = M32 ? NTW / 2 : 1;
+  f32x16 acc32[MT2][NT2];
+  f32x4 acc[M32 ? 1 : MTW][M32 ? 1 : NTW];
+  if constexpr (M32) {
 #pragma unroll
-  for (int i = 0; i < MTW; ++i)
+    for (int i = 0; i < MT2; ++i)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NT2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int r32 = lane & 31, h32 = lane >> 5;
 
   u32x4 xr[NXU];
   // the activation row each thread stages (fixed for the whole K loop); rows >= M only feed
@@ -96,16 +119,48 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int co = ((4 * s + g) ^ (r & 7)) << 3;
+      if constexpr (M32) {
+      // two K-steps of 16: lane half h32 reads 16-B chunk 4s + 2kk + h32 of its row (row & 7 == r32 & 7)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c2 = ((4 * s + 2 * kk + h32) ^ (r32 & 7)) << 3;
+        f16x8 A[MT2], B[NT2];
+#pragma unroll
+        for (int i = 0; i < MT2; ++i)
+          A[i] = *reinterpret_cast<const f16x8*>(xb + (wm * MTW * 16 + 32 * i + r32) * 64 + c2);
+#pragma unroll
+        for (int j = 0; j < NT2; ++j)
+          B[j] = *reinterpret_cast<const f16x8*>(wb + (wn * NTW * 16 + 32 * j + r32) * 64 + c2);
+        if (kk == 0) *reinterpret_cast<f16x8*>(wn_ + co) = f[s];
+#if NLS_GEMM_SETPRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int i = 0; i < MT2; ++i)
+#pragma unroll
+          for (int j = 0; j < NT2; ++j) acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i], B[j], acc32[i][j], 0, 0, 0);
+#if NLS_GEMM_SETPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      }
+      } else {
       f16x8 A[MTW], B[NTW];
 #pragma unroll
       for (int i = 0; i < MTW; ++i) A[i] = *reinterpret_cast<const f16x8*>(xb + (wm * MTW * 16 + 16 * i + r) * 64 + co);
 #pragma unroll
       for (int j = 0; j < NTW; ++j) B[j] = *reinterpret_cast<const f16x8*>(wb + (wn * NTW * 16 + 16 * j + r) * 64 + co);
       *reinterpret_cast<f16x8*>(wn_ + co) = f[s];
+#if NLS_GEMM_SETPRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < MTW; ++i)
 #pragma unroll
         for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(A[i], B[j], acc[i][j]);
+#if NLS_GEMM_SETPRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      }
     }
   };
   auto deq_w = [&](const Raw& rw, const Sc& sc, int q, int buf) __attribute__((always_inline)) {
@@ -170,38 +225,48 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
   if (sb < sb1) sb_step(rA, sA, rB, sB, sb);
 
-  // ---- epilogue from the accumulators: lane holds weight row rbase + 16j + r and
-  // activation rows mbase + 16i + 4g + e
+  // ---- epilogue from the accumulators ------------------------------------------------------------
+  // 16x16 tiles: lane holds weight row rbase + 16j + r and activation rows mbase + 16i + 4g + e;
+  // 32x32 tiles: weight row rbase + 32j + r32, activation rows mbase + 32i + (e&3) + 8(e>>2) + 4 h32
   const int rbase = row0 + wn * NTW * 16, mbase = wm * MTW * 16;
+  constexpr int NJ = M32 ? NT2 : NTW, NI = M32 ? MT2 : MTW, NE = M32 ? 16 : 4;
+  constexpr int RED_LANES = M32 ? 32 : 16;       // lanes sharing an activation row (argmax reduction)
+  auto wrow = [&](int j) { return M32 ? rbase + 32 * j + r32 : rbase + 16 * j + r; };
+  auto arow = [&](int i, int e) { return M32 ? mbase + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h32 : mbase + 16 * i + 4 * g + e; };
+  auto accv = [&](int i, int j, int e) -> float {
+    if constexpr (M32) return acc32[i][j][e];
+    else return acc[i][j][e];
+  };
   if (ks > 1) {
     const int ntot = a.pad;
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int row = rbase + 16 * j + r;
+    for (int j = 0; j < NJ; ++j) {
+      const int row = wrow(j);
       if (row >= S.rows) continue;
 #pragma unroll
-      for (int i = 0; i < MTW; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int b = mbase + 16 * i + 4 * g + e;
-          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[i][j][e];
+        for (int e = 0; e < NE; ++e) {
+          const int b = arow(i, e);
+          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = accv(i, j, e);
         }
     }
     return;
   }
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int row = rbase + 16 * j + r;
+  for (int j = 0; j < NJ; ++j) {
+    const int row = wrow(j);
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) {
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int b = mbase + 16 * i + 4 * g + e;
-        const float v = acc[i][j][e] * a.alpha;
+      for (int e = 0; e < NE; ++e) {
+        const int b = arow(i, e);
+        const float v = accv(i, j, e) * a.alpha;
         if (a.epi == EPI_SWIGLU) {
+          // interleaved [g0..g7, u0..u7] per 16 weight rows: the partner row is lane ^ 8 (same b)
           const float u = __shfl_xor(v, 8, 64);
-          if (r < 8 && b < M && row < S.rows) {
-            const int n = S.ycol + ((rbase + 16 * j) >> 1) + r;
+          if ((row & 8) == 0 && b < M && row < S.rows) {
+            const int n = S.ycol + ((row & ~15) >> 1) + (row & 7);
             const int yb = ym ? ym[b] : b;
             reinterpret_cast<act_t*>(a.y)[(size_t)yb * a.ldy + n] = (act_t)(silu(v) * u);
           }
@@ -217,8 +282,8 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     }
   }
   if (a.argmax) {
-    // greedy arg-max: max over the lane's NTW rows, then the 16 lanes of a row group, then the
-    // workgroup's waves through LDS (free after the main loop) -> ONE global atomic per
+    // greedy arg-max: max over the lane's weight rows, then the lanes sharing an activation row, then
+    // the workgroup's waves through LDS (free after the main loop) -> ONE global atomic per
     // activation row per workgroup (vs one per 16 rows: 1M contended 64-bit atomics on the
     // 128K-row lm_head otherwise)
     unsigned long long* red = reinterpret_cast<unsigned long long*>(lds);
@@ -226,22 +291,22 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     for (int idx = threadIdx.x; idx < BM; idx += 512) red[idx] = 0ull;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < MTW; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < NE; ++e) {
         unsigned long long k = 0ull;
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int row = rbase + 16 * j + r;
-          const unsigned long long kj = (row < S.rows) ? argmax_key(acc[i][j][e] * a.alpha, S.ycol + row) : 0ull;
+        for (int j = 0; j < NJ; ++j) {
+          const int row = wrow(j);
+          const unsigned long long kj = (row < S.rows) ? argmax_key(accv(i, j, e) * a.alpha, S.ycol + row) : 0ull;
           k = kj > k ? kj : k;
         }
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
+        for (int o = 1; o < RED_LANES; o <<= 1) {
           const unsigned long long ok = __shfl_xor(k, o, 64);
           k = ok > k ? ok : k;
         }
-        if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
+        if ((lane & (RED_LANES - 1)) == 0) atomicMax(red + arow(i, e), k);
       }
     __syncthreads();
     for (int idx = threadIdx.x; idx < M; idx += 512) atomicMax(a.argmax + idx, red[idx]);

@@ -262,8 +262,79 @@ std::string ObjectStore::get_file(const std::string& name, const std::string& pa
     fwrite(s.data(), 1, s.size(), ix);
     fclose(ix);
   };
+  auto put_chunk = [&](const std::string& data, uint64_t sseq) {
+    sha.update(data.data(), data.size());
+    size_t off = 0;
+    while (off < data.size()) {
+      ssize_t w = ::write(fd, data.data() + off, data.size() - off);
+      if (w <= 0) throw std::runtime_error("write failed: " + part);
+      off += (size_t)w;
+    }
+    got += data.size();
+    seq = sseq + 1;
+    ++nread;
+    if ((nread & 63) == 0) save_idx();
+    if (progress) progress(got, size);
+  };
   try {
-    while (nread < nchunks) {
+    // 1) ordered push consumer (what nats.go's ObjectStore.Get does): raw chunk payloads streamed to an
+    //    inbox, no per-chunk request round trip and no base64; flow-control requests are answered as
+    //    the chunks are consumed, so the server never runs more than a window ahead of the disk
+    bool streamed = false;
+    if (nread < nchunks) {
+      const std::string inbox = c_.new_inbox();
+      int64_t sid = c_.subscribe(inbox);
+      const std::string cname = "get" + nuid_next();
+      Json cfg = Json::O();
+      cfg.set("name", Json::S(cname));
+      cfg.set("deliver_subject", Json::S(inbox));
+      cfg.set("filter_subject", Json::S(csubj));
+      cfg.set("deliver_policy", Json::S("by_start_sequence"));
+      cfg.set("opt_start_seq", Json::N((double)seq));
+      cfg.set("ack_policy", Json::S("none"));
+      cfg.set("max_deliver", Json::N(1));
+      cfg.set("flow_control", Json::B(true));
+      cfg.set("idle_heartbeat", Json::N(5e9));
+      cfg.set("mem_storage", Json::B(true));
+      Json creq = Json::O();
+      creq.set("stream_name", Json::S(stream()));
+      creq.set("config", cfg);
+      std::string cerr;
+      try {
+        cerr = api_err(api("$JS.API.CONSUMER.CREATE." + stream() + "." + cname + "." + csubj, creq.dump()));
+      } catch (const std::exception& ex) {
+        cerr = ex.what();
+      }
+      if (cerr.empty()) {
+        try {
+          while (nread < nchunks) {
+            Msg m = c_.next_msg(sid, to_);
+            if (m.status == 100) {                    // flow control request / idle heartbeat
+              if (!m.reply.empty()) c_.publish(m.reply, "");
+              continue;
+            }
+            // reply: $JS.ACK.<stream>.<consumer>.<delivered>.<stream seq>.<consumer seq>.<ts>.<pending>
+            std::vector<std::string> tok;
+            size_t a = 0;
+            for (size_t b; (b = m.reply.find('.', a)) != std::string::npos; a = b + 1) tok.push_back(m.reply.substr(a, b - a));
+            tok.push_back(m.reply.substr(a));
+            if (tok.size() < 9 || tok[0] != "$JS" || tok[1] != "ACK") throw std::runtime_error("object store get: bad delivery");
+            const uint64_t sseq = std::stoull(tok[5]);
+            if (sseq < seq) continue;                 // duplicate (never expected)
+            put_chunk(m.data, sseq);
+          }
+          streamed = true;
+        } catch (...) {
+          try { api("$JS.API.CONSUMER.DELETE." + stream() + "." + cname, ""); } catch (...) {}
+          c_.unsubscribe(sid);
+          throw;
+        }
+        try { api("$JS.API.CONSUMER.DELETE." + stream() + "." + cname, ""); } catch (...) {}
+      }
+      c_.unsubscribe(sid);
+    }
+    // 2) fallback (servers without push consumers): one direct get per chunk
+    while (!streamed && nread < nchunks) {
       Json req = Json::O();
       req.set("seq", Json::N((double)seq));
       req.set("next_by_subj", Json::S(csubj));
@@ -271,19 +342,7 @@ std::string ObjectStore::get_file(const std::string& name, const std::string& pa
       std::string e = api_err(r);
       if (!e.empty()) throw std::runtime_error("object store get: " + e);
       const Json* m = r.get("message");
-      std::string data = b64decode(m->str("data"));
-      sha.update(data.data(), data.size());
-      size_t off = 0;
-      while (off < data.size()) {
-        ssize_t w = ::write(fd, data.data() + off, data.size() - off);
-        if (w <= 0) throw std::runtime_error("write failed: " + part);
-        off += (size_t)w;
-      }
-      got += data.size();
-      seq = (uint64_t)m->num("seq") + 1;
-      ++nread;
-      if ((nread & 63) == 0) save_idx();
-      if (progress) progress(got, size);
+      put_chunk(b64decode(m->str("data")), (uint64_t)m->num("seq"));
     }
   } catch (...) {
     save_idx();

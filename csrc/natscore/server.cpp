@@ -68,6 +68,7 @@ int Server::start() {
 
 void Server::stop() {
   if (!running_.exchange(false)) return;
+  stop_consumers("");
   ::shutdown(lfd_, SHUT_RDWR);
   ::close(lfd_);
   if (accept_th_.joinable()) accept_th_.join();
@@ -259,8 +260,26 @@ void Server::route(const std::string& subj, const std::string& reply, const std:
                    const std::string& payload, Conn* from) {
   bool handled = false;
   if (opt_.jetstream) {
-    if (subj.rfind("$JS.API.", 0) == 0) handled = js_handle(subj, reply, hdr, payload);
-    else handled = js_capture(subj, reply, hdr, payload);
+    if (subj.rfind("$JS.API.", 0) == 0) {
+      handled = js_handle(subj, reply, hdr, payload);
+    } else if (subj.rfind("$JS.FC.", 0) == 0) {
+      // a consumer's flow-control request answered by its subscriber: release the next window
+      std::vector<std::shared_ptr<Consumer>> cs;
+      {
+        std::lock_guard<std::mutex> g(js_mu_);
+        for (auto& kv : consumers_) cs.push_back(kv.second);
+      }
+      for (auto& c : cs) {
+        std::lock_guard<std::mutex> g(c->m);
+        if (c->fc_wait == subj) {
+          c->fc_wait.clear();
+          c->cv.notify_all();
+        }
+      }
+      return;
+    } else {
+      handled = js_capture(subj, reply, hdr, payload);
+    }
   }
   std::vector<std::shared_ptr<Sub>> targets;
   {
@@ -317,7 +336,10 @@ Json Server::stream_info(const Stream& s) {
   st.set("bytes", Json::N((double)s.bytes));
   st.set("first_seq", Json::N(s.msgs.empty() ? (double)(s.last_seq + 1) : (double)s.msgs.begin()->first));
   st.set("last_seq", Json::N((double)s.last_seq));
-  st.set("consumer_count", Json::N(0));
+  uint64_t nc = 0;
+  for (auto& kv : consumers_)
+    if (kv.second->stream == s.name) ++nc;
+  st.set("consumer_count", Json::N((double)nc));
   j.set("state", st);
   return j;
 }
@@ -383,6 +405,7 @@ bool Server::js_capture(const std::string& subj, const std::string& reply, const
         }
       }
       store_msg(s, subj, hdr, payload, true);
+      js_cv_.notify_all();
       Json a = Json::O();
       a.set("stream", Json::S(s.name));
       a.set("seq", Json::N((double)s.last_seq));
@@ -558,12 +581,228 @@ bool Server::js_handle(const std::string& subj, const std::string& reply, const 
           out = "{\"type\":\"io.nats.jetstream.api.v1.stream_msg_delete_response\",\"success\":true}";
         }
       }
+    } else if (!tail("CONSUMER.CREATE.").empty() || !tail("CONSUMER.DURABLE.CREATE.").empty()) {
+      // CONSUMER.CREATE.<stream>[.<name>[.<filter>]] (nats.go >= 2.9) | DURABLE.CREATE.<stream>.<name>
+      std::string rest = !tail("CONSUMER.CREATE.").empty() ? tail("CONSUMER.CREATE.") : tail("CONSUMER.DURABLE.CREATE.");
+      const size_t d1 = rest.find('.');
+      const std::string sname = rest.substr(0, d1);
+      std::string cname;
+      if (d1 != std::string::npos) {
+        const std::string r2 = rest.substr(d1 + 1);
+        cname = r2.substr(0, r2.find('.'));
+      }
+      out = consumer_create(sname, cname, req);
+    } else if (!tail("CONSUMER.DELETE.").empty() || !tail("CONSUMER.INFO.").empty()) {
+      const bool del = !tail("CONSUMER.DELETE.").empty();
+      const std::string key = del ? tail("CONSUMER.DELETE.") : tail("CONSUMER.INFO.");
+      auto it = consumers_.find(key);
+      if (it == consumers_.end()) {
+        out = js_error(404, 10014, "consumer not found", del ? "io.nats.jetstream.api.v1.consumer_delete_response"
+                                                            : "io.nats.jetstream.api.v1.consumer_info_response");
+      } else if (del) {
+        it->second->stop = true;
+        it->second->cv.notify_all();
+        js_cv_.notify_all();
+        out = "{\"type\":\"io.nats.jetstream.api.v1.consumer_delete_response\",\"success\":true}";
+      } else {
+        Json j = consumer_info(*it->second);
+        j.set("type", Json::S("io.nats.jetstream.api.v1.consumer_info_response"));
+        out = j.dump();
+      }
     } else {
       out = js_error(501, 10000, "not supported by the embedded server: " + api, "io.nats.jetstream.api.v1.error");
     }
   }
   respond(reply, out);
   return true;
+}
+
+// ---- push consumers (caller holds js_mu_ for create/info) ---------------------------------------
+Json Server::consumer_info(const Consumer& c) {
+  Json j = Json::O();
+  j.set("stream_name", Json::S(c.stream));
+  j.set("name", Json::S(c.name));
+  j.set("created", Json::S(rfc3339(c.created_ns)));
+  Json cfg = Json::O();
+  cfg.set("deliver_subject", Json::S(c.deliver));
+  if (!c.filter.empty()) cfg.set("filter_subject", Json::S(c.filter));
+  cfg.set("ack_policy", Json::S("none"));
+  cfg.set("flow_control", Json::B(c.flow_control));
+  if (c.heartbeat_ns) cfg.set("idle_heartbeat", Json::N((double)c.heartbeat_ns));
+  j.set("config", cfg);
+  Json dl = Json::O();
+  dl.set("consumer_seq", Json::N((double)c.delivered));
+  dl.set("stream_seq", Json::N((double)(c.next_seq ? c.next_seq - 1 : 0)));
+  j.set("delivered", dl);
+  j.set("num_pending", Json::N(0));
+  j.set("push_bound", Json::B(true));
+  return j;
+}
+
+std::string Server::consumer_create(const std::string& sname, const std::string& cname, const Json& req) {
+  const std::string type = "io.nats.jetstream.api.v1.consumer_create_response";
+  auto sit = streams_.find(sname);
+  if (sit == streams_.end()) return js_error(404, 10059, "stream not found", type);
+  const Json* cfg = req.get("config");
+  if (!cfg) return js_error(400, 10025, "consumer config required", type);
+  auto c = std::make_shared<Consumer>();
+  c->stream = sname;
+  c->name = !cname.empty() ? cname : (!cfg->str("name").empty() ? cfg->str("name")
+                                                                 : (!cfg->str("durable_name").empty() ? cfg->str("durable_name")
+                                                                                                      : nuid_next()));
+  c->deliver = cfg->str("deliver_subject");
+  if (c->deliver.empty()) return js_error(400, 10137, "pull consumers are not supported by the embedded server", type);
+  c->filter = cfg->str("filter_subject");
+  if (c->filter.empty()) {
+    const Json* fs = cfg->get("filter_subjects");
+    if (fs && fs->a.size() == 1) c->filter = fs->a[0].s;
+    else if (fs && fs->a.size() > 1) return js_error(400, 10136, "multiple filter subjects are not supported", type);
+  }
+  const std::string ack = cfg->str("ack_policy");
+  if (!ack.empty() && ack != "none") return js_error(400, 10138, "only ack_policy none is supported", type);
+  Stream& s = *sit->second;
+  const std::string pol = cfg->str("deliver_policy");
+  if (pol.empty() || pol == "all") c->next_seq = s.msgs.empty() ? s.last_seq + 1 : s.msgs.begin()->first;
+  else if (pol == "by_start_sequence") c->next_seq = std::max<uint64_t>(1, (uint64_t)cfg->num("opt_start_seq", 1));
+  else if (pol == "new") c->next_seq = s.last_seq + 1;
+  else if (pol == "last") c->next_seq = s.msgs.empty() ? s.last_seq + 1 : s.msgs.rbegin()->first;
+  else return js_error(400, 10025, "deliver_policy " + pol + " is not supported", type);
+  c->flow_control = cfg->boolean("flow_control", false);
+  c->heartbeat_ns = (int64_t)cfg->num("idle_heartbeat", 0);
+  c->created_ns = now_ns();
+  const std::string key = sname + "." + c->name;
+  auto old = consumers_.find(key);
+  if (old != consumers_.end()) {
+    old->second->stop = true;
+    old->second->cv.notify_all();
+  }
+  consumers_[key] = c;
+  for (auto it = consumer_threads_.begin(); it != consumer_threads_.end();) {   // reap finished deliveries
+    if ((*it)->done) {
+      if ((*it)->th.joinable()) (*it)->th.join();
+      it = consumer_threads_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  c->th = std::thread([this, c] { consumer_loop(c); });
+  consumer_threads_.push_back(c);
+  Json j = consumer_info(*c);
+  j.set("type", Json::S(type));
+  return j.dump();
+}
+
+bool Server::has_interest(const std::string& subj) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& s : subs_)
+    if (s->conn->alive && subject_matches(s->subject, subj)) return true;
+  return false;
+}
+
+void Server::stop_consumers(const std::string& stream) {
+  std::vector<std::shared_ptr<Consumer>> join;
+  {
+    std::lock_guard<std::mutex> g(js_mu_);
+    for (auto it = consumers_.begin(); it != consumers_.end();) {
+      if (stream.empty() || it->second->stream == stream) it = consumers_.erase(it);
+      else ++it;
+    }
+    for (auto it = consumer_threads_.begin(); it != consumer_threads_.end();) {
+      if (stream.empty() || (*it)->stream == stream) {
+        (*it)->stop = true;
+        (*it)->cv.notify_all();
+        join.push_back(*it);
+        it = consumer_threads_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    js_cv_.notify_all();
+  }
+  for (auto& c : join)
+    if (c->th.joinable()) c->th.join();
+}
+
+// Delivery: every stored message on the filter, in stream order, raw payload + original headers, reply
+// subject "$JS.ACK.<stream>.<consumer>.<delivered>.<stream seq>.<consumer seq>.<ts>.<pending>" (the
+// metadata nats.go ordered consumers check for gaps). Flow control: after each FC_WINDOW bytes a
+// "100 FlowControl Request" status message is sent and delivery waits until the subscriber answers it,
+// so a slow consumer (disk-bound pull) never makes the server queue an unbounded amount of data. Idle
+// consumers send "100 Idle Heartbeat"; a consumer whose deliver subject lost all interest ends itself.
+void Server::consumer_loop(std::shared_ptr<Consumer> c) {
+  constexpr uint64_t FC_WINDOW = 32ull << 20;
+  uint64_t since_fc = 0, fc_n = 0;
+  auto last_activity = std::chrono::steady_clock::now();
+  auto last_interest = last_activity;
+  while (!c->stop && running_) {
+    StoredMsg m;
+    bool have = false;
+    uint64_t pending = 0;
+    {
+      std::unique_lock<std::mutex> g(js_mu_);
+      auto sit = streams_.find(c->stream);
+      if (sit == streams_.end()) break;
+      Stream& s = *sit->second;
+      for (auto it = s.msgs.lower_bound(c->next_seq); it != s.msgs.end(); ++it) {
+        if (!c->filter.empty() && !subject_matches(c->filter, it->second.subject)) continue;
+        m = it->second;
+        have = true;
+        break;
+      }
+      if (have) {
+        c->next_seq = m.seq + 1;
+        pending = s.last_seq > m.seq ? s.last_seq - m.seq : 0;   // upper bound (ignores the filter)
+      } else {
+        c->next_seq = s.last_seq + 1;
+        js_cv_.wait_for(g, std::chrono::milliseconds(200));
+      }
+    }
+    const auto now = std::chrono::steady_clock::now();
+    if (!have) {
+      if (c->heartbeat_ns > 0 && now - last_activity >= std::chrono::nanoseconds(c->heartbeat_ns)) {
+        route(c->deliver, "", "NATS/1.0 100 Idle Heartbeat\r\nNats-Last-Consumer: " + std::to_string(c->delivered) +
+                                  "\r\nNats-Last-Stream: " + std::to_string(c->next_seq - 1) + "\r\n\r\n",
+              "", nullptr);
+        last_activity = now;
+      }
+      if (has_interest(c->deliver)) last_interest = now;
+      else if (now - last_interest > std::chrono::seconds(5)) break;    // ephemeral consumer abandoned
+      continue;
+    }
+    ++c->delivered;
+    const std::string ack = "$JS.ACK." + c->stream + "." + c->name + ".1." + std::to_string(m.seq) + "." +
+                            std::to_string(c->delivered) + "." + std::to_string(m.time_ns) + "." +
+                            std::to_string(pending);
+    route(c->deliver, ack, m.hdr, m.data, nullptr);
+    last_activity = now;
+    since_fc += m.data.size() + m.hdr.size();
+    if (c->flow_control && since_fc >= FC_WINDOW) {
+      since_fc = 0;
+      const std::string fc = "$JS.FC." + c->stream + "." + c->name + "." + std::to_string(++fc_n);
+      {
+        std::lock_guard<std::mutex> g(c->m);
+        c->fc_wait = fc;
+      }
+      route(c->deliver, fc, "NATS/1.0 100 FlowControl Request\r\n\r\n", "", nullptr);
+      std::unique_lock<std::mutex> g(c->m);
+      for (int waited = 0; !c->fc_wait.empty() && !c->stop && running_; ++waited) {
+        c->cv.wait_for(g, std::chrono::milliseconds(100));
+        if (waited % 50 == 49) {                       // every 5 s: give up if nobody listens any more
+          g.unlock();
+          const bool alive = has_interest(c->deliver);
+          g.lock();
+          if (!alive) {
+            c->stop = true;
+            break;
+          }
+        }
+      }
+    }
+  }
+  std::lock_guard<std::mutex> g(js_mu_);
+  auto it = consumers_.find(c->stream + "." + c->name);
+  if (it != consumers_.end() && it->second == c) consumers_.erase(it);
+  c->done = true;
 }
 
 // ---- persistence: <store_dir>/<stream>.cfg (JSON) + <stream>.log (binary records) ----

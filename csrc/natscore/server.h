@@ -2,10 +2,13 @@
 // nats-server binary): core pub/sub with `*`/`>` wildcards, queue groups, request-reply
 // with no-responders (503) status, headers, max_payload enforcement, PING/PONG, and a
 // JetStream subset sufficient for the Object Store (streams, publish acks, rollup,
-// purge, direct message get incl. next_by_subj, optional file persistence).
+// purge, direct message get incl. next_by_subj, optional file persistence) and the
+// ephemeral push consumers nats.go's ObjectStore.Get uses (ordered consumer: raw chunk
+// delivery to an inbox, flow control, idle heartbeats, by_start_sequence resume).
 // Fault-injection hooks (drop/delay/disconnect) back the failure-detection tests.
 #pragma once
 #include <atomic>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -48,6 +51,19 @@ class Server {
     std::string subject, hdr, data;
     int64_t time_ns;
   };
+  struct Consumer {
+    std::string stream, name, deliver, filter;
+    uint64_t next_seq = 1;                 // next stream sequence to examine
+    uint64_t delivered = 0;                // consumer sequence
+    bool flow_control = false;
+    int64_t heartbeat_ns = 0;
+    int64_t created_ns = 0;
+    std::atomic<bool> stop{false}, done{false};
+    std::mutex m;
+    std::condition_variable cv;
+    std::string fc_wait;                   // reply subject of the outstanding flow-control request
+    std::thread th;
+  };
   struct Stream {
     std::string name;
     Json config;
@@ -74,6 +90,11 @@ class Server {
   void load_store();
   void store_msg(Stream& s, const std::string& subj, const std::string& hdr, const std::string& data, bool log);
   void purge(Stream& s, const std::string& filter, uint64_t* n, bool log);
+  std::string consumer_create(const std::string& stream, const std::string& name, const Json& req);
+  Json consumer_info(const Consumer& c);
+  void consumer_loop(std::shared_ptr<Consumer> c);
+  bool has_interest(const std::string& subj);
+  void stop_consumers(const std::string& stream);
 
   ServerOptions opt_;
   int lfd_ = -1;
@@ -85,6 +106,9 @@ class Server {
   std::vector<std::shared_ptr<Sub>> subs_;
   std::mutex js_mu_;
   std::map<std::string, std::unique_ptr<Stream>> streams_;
+  std::map<std::string, std::shared_ptr<Consumer>> consumers_;   // "<stream>.<name>" -> consumer (js_mu_)
+  std::vector<std::shared_ptr<Consumer>> consumer_threads_;       // every started consumer, joined (js_mu_)
+  std::condition_variable js_cv_;                                 // new stream messages (js_mu_)
   std::mt19937 rng_{12345};
   std::atomic<uint64_t> next_cid_{1};
   std::atomic<double> drop_rate_{0.0};

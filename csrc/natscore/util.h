@@ -71,7 +71,8 @@ class Sha256 {
   void update(const void* data, size_t len);
   std::string digest();   // 32 raw bytes
  private:
-  void block(const uint8_t* p);
+  void block(const uint8_t* p);                 // scalar compression of one block
+  void blocks(const uint8_t* p, size_t n);      // n blocks (SHA-NI when the CPU has it)
   uint32_t h_[8];
   uint8_t buf_[64];
   size_t blen_ = 0;

@@ -31,17 +31,20 @@ def _run(cmd):
     subprocess.check_call(cmd)
 
 
-def build_kernels(force: bool = False) -> str:
-    """Compile each .hip translation unit to an object in parallel, then link one .so."""
-    out = os.path.join(PKG, "_kernels.so")
+def build_kernels(force: bool = False, defines=(), tag: str = "") -> str:
+    """Compile each .hip translation unit to an object in parallel, then link one .so.
+    `defines` + `tag`: an A/B variant library `_kernels_<tag>.so` (e.g. tools/gemm_ab.py), built in
+    its own object directory; the default build is `_kernels.so`."""
+    out = os.path.join(PKG, f"_kernels_{tag}.so" if tag else "_kernels.so")
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     if force or _stale(out, deps):
         from concurrent.futures import ThreadPoolExecutor
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-        bdir = os.path.join(ROOT, "build", "kernels")
+        bdir = os.path.join(ROOT, "build", f"kernels_{tag}" if tag else "kernels")
         os.makedirs(bdir, exist_ok=True)
-        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics"]
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+                 *[f"-D{d}" for d in defines]]
         objs = [os.path.join(bdir, os.path.basename(s) + ".o") for s in srcs]
         jobs = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + glob.glob(os.path.join(CSRC, "kernels", "*.h")))]
         with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:

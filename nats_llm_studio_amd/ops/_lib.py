@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_kernels.so")
+LIB_PATH = os.environ.get("NLS_KERNELS_SO") or os.path.join(os.path.dirname(_HERE), "_kernels.so")
 
 _lib = None
 
@@ -71,6 +71,16 @@ _SIGS = {
     "nls_ar_blocks": [],
     "nls_ar_run": [c_void_p, c_long, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_long, c_void_p],
 }
+
+
+def load(path: str):
+    """Load (and type) a kernel library without installing it (A/B of kernel variants in one process)."""
+    L = ctypes.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = c_int
+    return L
 
 
 def lib():

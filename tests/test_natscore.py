@@ -259,3 +259,47 @@ def test_jetstream_persistence(tmp_path):
     assert ObjectStore(c2, "persist").get_bytes("p/m/f.gguf") == b"hello world" * 100
     c2.close()
     s2.stop()
+
+
+def test_object_store_get_streams_over_push_consumer(server, tmp_path):
+    """get_file streams raw chunks over an ordered push consumer: > 2 flow-control windows (32 MiB
+    each) of data, interrupted half way then resumed from the .part checkpoint, digest verified, and
+    the ephemeral consumer is gone afterwards (stream consumer_count back to 0)."""
+    import hashlib
+    import json
+    c = client(server)
+    os_ = ObjectStore(c, "big")
+    os_.create()
+    data = os.urandom(80 << 20)
+    os_.put_bytes("p/m/big.gguf", data, chunk_size=512 * 1024)
+    dest = tmp_path / "big.gguf"
+
+    class Cut(Exception):
+        pass
+
+    def cut(got, total):
+        if got > total // 2:
+            raise Cut()
+    with pytest.raises(Exception):
+        os_.get_file("p/m/big.gguf", str(dest), True, cut)
+    part = (tmp_path / "big.gguf.part").stat().st_size
+    assert 0 < part < len(data)
+    info = os_.get_file("p/m/big.gguf", str(dest), True)
+    assert dest.stat().st_size == len(data) and hashlib.sha256(dest.read_bytes()).digest() == hashlib.sha256(data).digest()
+    assert info["digest"] == sha256_digest(data)
+    import time
+    for _ in range(100):          # the interrupted consumer ends once its inbox has no subscriber
+        st = json.loads(c.request("$JS.API.STREAM.INFO.OBJ_big", b"", 5).data)
+        if st["state"]["consumer_count"] == 0:
+            break
+        time.sleep(0.1)
+    assert st["state"]["consumer_count"] == 0
+    c.close()
+
+
+def test_sha256_matches_hashlib():
+    import hashlib
+    from nats_llm_studio_amd.natsio import _natscore as n
+    for L in (0, 1, 55, 56, 63, 64, 65, 127, 128, 129, 1000, 65536 + 7):
+        b = os.urandom(L)
+        assert n.sha256(b) == hashlib.sha256(b).digest(), L

@@ -74,7 +74,11 @@ def test_chat_stub_echo(env):
 def test_metrics_health(env):
     _, _, _, cli = env
     req(cli, "list_models", {})
-    m = req(cli, "metrics", {})
+    for _ in range(50):   # the handler records its latency just after it has replied
+        m = req(cli, "metrics", {})
+        if "list_models" in m["data"]["latency_ms"]:
+            break
+        time.sleep(0.01)
     assert m["ok"] and m["data"]["requests"]["list_models"] >= 1 and "p50" in m["data"]["latency_ms"]["list_models"]
     h = req(cli, "health", {})
     assert h["data"]["status"] == "ok" and h["data"]["backend"] == "stub"
