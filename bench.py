@@ -130,9 +130,9 @@ def run(args, world: int):
             if g == replica:
                 mine = (pg, cg)
         comm = Comm(mine[0], mine[1], dev)
-        if cuda and os.environ.get("NLS_ONESHOT_AR", "0") == "1":
-            from nats_llm_studio_amd.parallel.oneshot import OneShotAllReduce
-            comm.oneshot = OneShotAllReduce(comm)
+        if cuda and os.environ.get("NLS_ONESHOT_AR", "1") == "1":
+            from nats_llm_studio_amd.parallel.oneshot import try_oneshot
+            comm.oneshot = try_oneshot(comm)
 
     from nats_llm_studio_amd import build as nbuild
     from nats_llm_studio_amd.gguf.reader import GGUFReader

@@ -94,6 +94,7 @@ class StepBuffers:
     meta: Optional[torch.Tensor] = None
     pad: int = 0
     attn_cnt: Optional[torch.Tensor] = None    # int32 [pad*Hkv] split-merge tickets (zero between launches)
+    part: Optional[torch.Tensor] = None        # f32 [pad, d] row-parallel partial sums (TP fused all-reduce)
     cnt: Optional[torch.Tensor] = None         # int32 tickets of the last-workgroup residual+RMSNorm GEMVs
 
 
@@ -260,6 +261,8 @@ class LlamaModel:
         b.meta = meta
         b.pad = pad
         b.attn_cnt = torch.zeros(pad * self.Hkv, dtype=torch.int32, device=dev)
+        if self.shard.size > 1:
+            b.part = torch.zeros(pad, cfg.d_model, dtype=torch.float32, device=dev)
         b.cnt = torch.zeros(16, dtype=torch.int32, device=dev)
         b.slot.fill_(-1)
         if cfg.n_expert:
@@ -320,7 +323,8 @@ class LlamaModel:
             if fused:
                 ops.qgemv_add_rmsnorm(Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps,
                                       counter=b.cnt)
-            else:
+            elif not self.comm.row_parallel_add_norm(lw.wo, b.ao, b.part, x, lw.ffn_norm, b.h, T,
+                                                     cfg.residual_scale, cfg.eps):
                 self._row_parallel(lw.wo, b.ao, x, T, cfg.residual_scale)
                 ops.rmsnorm(x, lw.ffn_norm, b.h, T, cfg.eps)
             nxt = self.layers[L + 1].attn_norm if L + 1 < len(self.layers) else self.out_norm
@@ -332,6 +336,9 @@ class LlamaModel:
                 if fused:
                     ops.qgemv_add_rmsnorm(Seg(lw.down), b.act, x, nxt, b.h, T, cfg.residual_scale, cfg.eps,
                                           counter=b.cnt)
+                    fused_prev = True
+                elif self.comm.row_parallel_add_norm(lw.down, b.act, b.part, x, nxt, b.h, T, cfg.residual_scale,
+                                                     cfg.eps):
                     fused_prev = True
                 else:
                     self._row_parallel(lw.down, b.act, x, T, cfg.residual_scale)

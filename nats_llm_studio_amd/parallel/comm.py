@@ -55,6 +55,21 @@ class Comm:
         ops.qgemv([Seg(w)], xin, resid, T, alpha=alpha, epi="add" if self.rank == 0 else "f32")
         self.all_reduce(resid[:T])
 
+    def row_parallel_add_norm(self, w, xin: torch.Tensor, part: torch.Tensor, resid: torch.Tensor,
+                              nw: torch.Tensor, h: torch.Tensor, T: int, alpha: float, eps: float) -> bool:
+        """Decode fast path: partial GEMV into `part`, then ONE fused one-shot kernel sums the ranks'
+        partials in rank order into the residual and writes the next RMSNorm (h) -- 2 launches per
+        row-parallel projection instead of GEMV + all-reduce + norm. False: not applicable (caller
+        falls back to row_parallel_add + rmsnorm)."""
+        os_ = self.oneshot
+        if os_ is None or not resid.is_cuda or not os_.addnorm_ok(T, resid.shape[1]):
+            return False
+        ops.qgemv([Seg(w)], xin, part, T, alpha=alpha, epi="f32")
+        self.stats["all_reduce"] += 1
+        self.stats["all_reduce_bytes"] += T * resid.shape[1] * 4
+        os_.add_norm(part, resid, nw, h, T, eps)
+        return True
+
     def vocab_parallel_argmax(self, keys: torch.Tensor, n: int, vocab_lo: int, next_ids: torch.Tensor):
         """Per-rank fused-argmax keys (value<<32 | ~local_idx) -> global greedy ids on every rank."""
         k = keys[:n]
@@ -108,7 +123,7 @@ def init_distributed(device_type: Optional[str] = None, timeout_s: float = 600.0
         dist.init_process_group(**kw)
     ctrl = dist.new_group(backend="gloo") if device_type == "cuda" else None
     comm = Comm(dist.group.WORLD, ctrl, dev)
-    if device_type == "cuda" and comm.size > 1 and os.environ.get("NLS_ONESHOT_AR", "0") == "1":
-        from .oneshot import OneShotAllReduce
-        comm.oneshot = OneShotAllReduce(comm)
+    if device_type == "cuda" and comm.size > 1 and os.environ.get("NLS_ONESHOT_AR", "1") == "1":
+        from .oneshot import try_oneshot
+        comm.oneshot = try_oneshot(comm)
     return comm

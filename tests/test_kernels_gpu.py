@@ -312,6 +312,33 @@ def test_oneshot_allreduce_simulated(gpu, world):
         g.close()
 
 
+@pytest.mark.parametrize("rows,D", [(1, 4096), (3, 8192), (16, 4096), (5, 2048)])
+def test_oneshot_allreduce_addnorm_simulated(gpu, rows, D):
+    """Fused TP decode epilogue (one launch): x += sum of the ranks' partials in rank order, then
+    h = f16(rmsnorm(x) * w) -- vs the fp32 reference, bit-identical x across ranks, repeated to
+    exercise both epoch parities."""
+    from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
+    world = 2
+    g = SimulatedGroup(world, 1 << 16, gpu)
+    try:
+        nw = (1 + 0.1 * torch.randn(D, device=gpu)).float()
+        for it in range(3):
+            base = torch.randn(rows, D, device=gpu)
+            parts = torch.randn(world, rows, D, device=gpu)
+            xs = base.unsqueeze(0).repeat(world, 1, 1).contiguous()
+            hs = torch.zeros(world, rows, D, dtype=ops.ACT_DTYPE, device=gpu)
+            g.add_norm(parts, xs, nw, hs, rows, 1e-5)
+            torch.cuda.synchronize()
+            assert int(g.err.item()) == 0, f"timeout at call {it}"
+            ref = base + parts[0] + parts[1]
+            href = ref * torch.rsqrt(ref.pow(2).mean(1, keepdim=True) + 1e-5) * nw
+            assert torch.equal(xs[0], xs[1]) and torch.equal(hs[0], hs[1])
+            torch.testing.assert_close(xs[0], ref, rtol=1e-6, atol=1e-5)
+            _close(hs[0], href, 1e-2)
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q8_0, GGMLType.BF16])
 @pytest.mark.parametrize("M", [65, 128, 200, 300])
 @pytest.mark.parametrize("wr", [(8, 1, 1), (4, 2, 1), (8, 1, 3)])
