@@ -225,6 +225,8 @@ def run(args, world: int):
         comm_stats = {"all_reduce_per_step": round(d["all_reduce"] / args.steps, 2),
                       "all_reduce_bytes_per_step": int(d["all_reduce_bytes"] / args.steps),
                       "ctrl_msgs_per_step": round(d["ctrl"] / args.steps, 2),
+                      "ctrl_us_per_step": round(d["ctrl_s"] / args.steps * 1e6, 1),
+                      "ctrl_transport": "shm-ring" if comm.ring is not None else "gloo",
                       "oneshot": comm.oneshot is not None}
 
     extra = {}

@@ -12,8 +12,9 @@ Studio's concern. Here one process drives one GPU and the ranks of a model shard
     row instead of gathering [B, V] logits), and a logits all-gather only when a request
     samples. Small all-reduces can be routed to the IPC one-shot kernel
     (`parallel/oneshot.py`) instead of RCCL.
-  * control plane (`ctrl`, always gloo/TCP on the host): rank 0 (the scheduler) broadcasts
-    each step's header + packed int32 metadata so follower ranks launch the same step.
+  * control plane: rank 0 (the scheduler) broadcasts each step's header + packed int32 metadata
+    so follower ranks launch the same step -- through a shared-memory ring when the group is on
+    one host (`parallel/shm_ctrl.py`), else over the gloo `ctrl` group.
 """
 from __future__ import annotations
 
@@ -38,7 +39,15 @@ class Comm:
         self.src = dist.get_global_rank(group, 0) if group is not None else 0
         self.device = torch.device(device) if device is not None else None
         self.oneshot = None          # optional small-message all-reduce (parallel/oneshot.py)
-        self.stats = dict(all_reduce=0, all_reduce_bytes=0, ctrl=0)
+        self.stats = dict(all_reduce=0, all_reduce_bytes=0, ctrl=0, ctrl_s=0.0)
+        self.ring = None             # shared-memory control ring (ranks on one host), else gloo broadcasts
+        if self.size > 1 and os.environ.get("NLS_SHM_CTRL", "1") == "1":
+            import socket
+            hosts = [None] * self.size
+            dist.all_gather_object(hosts, socket.gethostname(), group=self.ctrl)
+            if len(set(hosts)) == 1:
+                from .shm_ctrl import ShmCtrlRing
+                self.ring = ShmCtrlRing(self.ctrl, self.rank, self.size)
 
     # ------------------------------------------------------------------ data plane
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
@@ -50,10 +59,30 @@ class Comm:
         dist.all_reduce(t, op=op, group=self.group)
         return t
 
+    OVERLAP_ROWS = 256      # prefill: row chunk of the GEMM / all-reduce pipeline
+
     def row_parallel_add(self, w, xin: torch.Tensor, resid: torch.Tensor, T: int, alpha: float):
-        """resid[:T] += alpha * sum_r x_r @ W_r^T  (W row-parallel: K split across ranks)."""
-        ops.qgemv([Seg(w)], xin, resid, T, alpha=alpha, epi="add" if self.rank == 0 else "f32")
-        self.all_reduce(resid[:T])
+        """resid[:T] += alpha * sum_r x_r @ W_r^T  (W row-parallel: K split across ranks).
+        Prefill-size T on GPUs: the GEMM runs in row chunks and chunk c's all-reduce runs on a side
+        stream while chunk c+1's GEMM computes (RCCL overlapped with the dequant GEMM); the caller's
+        stream waits for the last reduction."""
+        epi = "add" if self.rank == 0 else "f32"
+        C = self.OVERLAP_ROWS
+        if not resid.is_cuda or T < 2 * C:
+            ops.qgemv([Seg(w)], xin, resid, T, alpha=alpha, epi=epi)
+            self.all_reduce(resid[:T])
+            return
+        cur = torch.cuda.current_stream(resid.device)
+        if getattr(self, "_comm_stream", None) is None:
+            self._comm_stream = torch.cuda.Stream(resid.device)
+        cs = self._comm_stream
+        for r0 in range(0, T, C):
+            n = min(C, T - r0)
+            ops.qgemv([Seg(w)], xin[r0:], resid[r0:], n, alpha=alpha, epi=epi)
+            cs.wait_stream(cur)
+            with torch.cuda.stream(cs):
+                self.all_reduce(resid[r0:r0 + n])
+        cur.wait_stream(cs)
 
     def row_parallel_add_norm(self, w, xin: torch.Tensor, part: torch.Tensor, resid: torch.Tensor,
                               nw: torch.Tensor, h: torch.Tensor, T: int, alpha: float, eps: float) -> bool:
@@ -92,9 +121,16 @@ class Comm:
 
     # ------------------------------------------------------------------ control plane
     def bcast_ctrl(self, t: torch.Tensor):
-        """Host int32 tensor from rank 0 to all ranks (gloo)."""
+        """Host int32 tensor from rank 0 to all ranks: the shared-memory ring when every rank of the
+        group is on this host (one memcpy + a sequence store per step), else a gloo broadcast."""
+        import time
         self.stats["ctrl"] += 1
-        dist.broadcast(t, src=self.src, group=self.ctrl)
+        t0 = time.perf_counter()
+        if self.ring is not None:
+            self.ring.bcast(t)
+        else:
+            dist.broadcast(t, src=self.src, group=self.ctrl)
+        self.stats["ctrl_s"] += time.perf_counter() - t0
         return t
 
     def min_int(self, v: int) -> int:
