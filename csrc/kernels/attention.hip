@@ -13,6 +13,12 @@
 // counters, by attn_combine.
 #include "common.h"
 
+// NLS_ATTN_PREFETCH2=1 streams K/V two tiles ahead; A/B on MI355X (B=1/16, P=4096) measured it
+// 0.3-0.8 % slower than one tile ahead (profiles/attn_prefetch_split_ab.txt), so it is off.
+#ifndef NLS_ATTN_PREFETCH2
+#define NLS_ATTN_PREFETCH2 0
+#endif
+
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -84,20 +90,28 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   };
   auto kv_off = [&](int pos, int base) -> size_t { return ((size_t)slot_of(pos, base) * Hkv + kh) * D + 8 * dl; };
 
-  u32x4 kr = {0, 0, 0, 0}, vr = {0, 0, 0, 0};
+  // K/V rows PF steps ahead in flight (long contexts at small batch are latency-bound on this chain)
+  u32x4 kr = {0, 0, 0, 0}, vr = {0, 0, 0, 0}, k1 = kr, v1 = vr;
   if (start < end) {
     const int p0 = min(start + stream, end - 1);
     const size_t off = kv_off(p0, start);
     kr = ld16(kc + off);
     vr = ld16(vc + off);
+    if (NLS_ATTN_PREFETCH2 && start + NSTREAM < end) {
+      const int p1 = min(start + NSTREAM + stream, end - 1);
+      const size_t o1 = kv_off(p1, start + NSTREAM);
+      k1 = ld16(kc + o1);
+      v1 = ld16(vc + o1);
+    }
   }
   for (int base = start; base < end; base += NSTREAM) {
     const int pos = base + stream;
     const bool valid = pos < end;
-    u32x4 kn = kr, vn = vr;
-    if (base + NSTREAM < end) {
-      const int pn = min(pos + NSTREAM, end - 1);
-      const size_t off = kv_off(pn, base + NSTREAM);
+    constexpr int PF = NLS_ATTN_PREFETCH2 ? 2 : 1;
+    u32x4 kn = PF == 2 ? k1 : kr, vn = PF == 2 ? v1 : vr;
+    if (base + PF * NSTREAM < end) {
+      const int pn = min(pos + PF * NSTREAM, end - 1);
+      const size_t off = kv_off(pn, base + PF * NSTREAM);
       kn = ld16(kc + off);
       vn = ld16(vc + off);
     }
@@ -130,8 +144,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * c + p * vf[i];
     }
-    kr = kn;
-    vr = vn;
+    if constexpr (PF == 2) {
+      kr = k1;
+      vr = v1;
+      k1 = kn;
+      v1 = vn;
+    } else {
+      kr = kn;
+      vr = vn;
+    }
   }
 
   // ---- merge the NSTREAM streams through LDS ----------------------------------
@@ -203,9 +224,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     const int qh = kh * G + h;
     const size_t pb = ((size_t)t * Hq + qh) * n_split;
     float M = -INFINITY;
+#pragma unroll 8
     for (int s2 = 0; s2 < na; ++s2) M = fmaxf(M, part_ml[2 * (pb + s2)]);
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
+#pragma unroll 8
       for (int s2 = 0; s2 < na; ++s2) {
         const float ms = part_ml[2 * (pb + s2)];
         if (ms == -INFINITY) continue;

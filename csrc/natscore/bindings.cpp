@@ -72,17 +72,24 @@ PYBIND11_MODULE(_natscore, m) {
 
   py::class_<Server>(m, "Server")
       .def(py::init([](const std::string& host, int port, size_t max_payload, bool jetstream,
-                       const std::string& store_dir) {
+                       const std::string& store_dir, const std::string& auth_token,
+                       const std::vector<std::pair<std::string, std::string>>& users,
+                       const std::vector<std::string>& nkeys) {
              ServerOptions o;
              o.host = host;
              o.port = port;
              o.max_payload = max_payload;
              o.jetstream = jetstream;
              o.store_dir = store_dir;
+             o.auth_token = auth_token;
+             o.users = users;
+             o.nkeys = nkeys;
              return new Server(o);
            }),
            py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("max_payload") = 1 << 20,
-           py::arg("jetstream") = true, py::arg("store_dir") = "")
+           py::arg("jetstream") = true, py::arg("store_dir") = "", py::arg("auth_token") = "",
+           py::arg("users") = std::vector<std::pair<std::string, std::string>>(),
+           py::arg("nkeys") = std::vector<std::string>())
       .def("start", &Server::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Server::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &Server::port)
@@ -96,18 +103,25 @@ PYBIND11_MODULE(_natscore, m) {
       .def(
           "connect",
           [](Client& c, const std::string& url, const std::string& name, int timeout_ms, bool reconnect,
-             int max_reconnect, int reconnect_wait_ms) {
+             int max_reconnect, int reconnect_wait_ms, const std::string& token, const std::string& user,
+             const std::string& password, const std::string& nkey_seed, const std::string& jwt) {
             ClientOptions o;
             o.name = name;
             o.connect_timeout_ms = timeout_ms;
             o.allow_reconnect = reconnect;
             o.max_reconnect = max_reconnect;
             o.reconnect_wait_ms = reconnect_wait_ms;
+            o.token = token;
+            o.user = user;
+            o.pass = password;
+            o.nkey_seed = nkey_seed;
+            o.jwt = jwt;
             py::gil_scoped_release r;
             c.connect(url, o);
           },
           py::arg("url"), py::arg("name") = "natscore", py::arg("timeout_ms") = 2000, py::arg("reconnect") = true,
-          py::arg("max_reconnect") = 60, py::arg("reconnect_wait_ms") = 250)
+          py::arg("max_reconnect") = 60, py::arg("reconnect_wait_ms") = 250, py::arg("token") = "",
+          py::arg("user") = "", py::arg("password") = "", py::arg("nkey_seed") = "", py::arg("jwt") = "")
       .def("close", &Client::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("connected", &Client::connected)
       .def(
@@ -204,6 +218,35 @@ PYBIND11_MODULE(_natscore, m) {
   m.def("b64encode", [](py::bytes d, bool url) { return b64encode(std::string(d), url); }, py::arg("data"),
         py::arg("url") = false);
   m.def("nuid", &nuid_next);
+  m.def("nkey_public", [](const std::string& seed) {
+    std::string raw;
+    if (!nkey_seed_raw(seed, raw)) throw std::runtime_error("invalid nkey seed");
+    return nkey_public(raw);
+  });
+  m.def("nkey_sign", [](const std::string& seed, py::bytes msg) {
+    std::string raw;
+    if (!nkey_seed_raw(seed, raw)) throw std::runtime_error("invalid nkey seed");
+    return py::bytes(nkey_sign(raw, std::string(msg)));
+  });
+  m.def("nkey_verify", [](const std::string& pub, py::bytes msg, py::bytes sig) {
+    return nkey_verify(pub, std::string(msg), std::string(sig));
+  });
+  m.def("nkey_user_seed_from_raw", [](py::bytes raw32) {
+    // "SU..." text form of a raw 32-byte ed25519 seed (key generation / tests)
+    std::string r = raw32;
+    if (r.size() != 32) throw std::runtime_error("need 32 bytes");
+    std::string body;
+    body += (char)(NKEY_PREFIX_SEED | (NKEY_PREFIX_USER >> 5));
+    body += (char)((NKEY_PREFIX_USER & 31) << 3);
+    body += r;
+    const uint16_t crc = crc16_xmodem(body);
+    return base32_encode(body + std::string(1, (char)(crc & 0xFF)) + std::string(1, (char)(crc >> 8)));
+  });
+  m.def("parse_creds", [](const std::string& text) {
+    std::string jwt, seed;
+    if (!parse_creds(text, jwt, seed)) throw std::runtime_error("no user nkey seed in creds");
+    return py::make_tuple(jwt, seed);
+  });
   m.def("subject_matches", &subject_matches);
   m.def("parse_headers", [](py::bytes raw) {
     Headers h = parse_headers(std::string(raw));

@@ -11,12 +11,36 @@ Client::Client() {}
 
 Client::~Client() { close(); }
 
-static void parse_url(const std::string& url, std::string& host, int& port) {
+static std::string pct_decode(const std::string& s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size()) {
+      o += (char)std::strtol(s.substr(i + 1, 2).c_str(), nullptr, 16);
+      i += 2;
+    } else {
+      o += s[i];
+    }
+  }
+  return o;
+}
+
+// nats://[user:pass@ | token@]host[:port]: URL credentials fill the options the caller left empty
+static void parse_url(const std::string& url, std::string& host, int& port, ClientOptions& opt) {
   std::string u = url;
   auto p = u.find("://");
   if (p != std::string::npos) u = u.substr(p + 3);
-  auto at = u.rfind('@');               // user:pass@ (ignored: no auth in this build)
-  if (at != std::string::npos) u = u.substr(at + 1);
+  auto at = u.rfind('@');
+  if (at != std::string::npos) {
+    const std::string ui = u.substr(0, at);
+    const auto c = ui.find(':');
+    if (c != std::string::npos) {
+      if (opt.user.empty()) opt.user = pct_decode(ui.substr(0, c));
+      if (opt.pass.empty()) opt.pass = pct_decode(ui.substr(c + 1));
+    } else if (opt.token.empty()) {
+      opt.token = pct_decode(ui);
+    }
+    u = u.substr(at + 1);
+  }
   auto sl = u.find('/');
   if (sl != std::string::npos) u = u.substr(0, sl);
   auto c = u.rfind(':');
@@ -44,16 +68,33 @@ bool Client::dial() {
     if (line.size() > 65536) { ::close(fd); return false; }
   }
   if (line.rfind("INFO ", 0) != 0) { ::close(fd); return false; }
+  std::string nonce;
   {
     std::lock_guard<std::mutex> g(mu_);
     info_ = line.substr(5, line.size() - 7);
     try {
       Json j = Json::parse(info_);
       max_payload_ = (size_t)j.num("max_payload", 1 << 20);
+      nonce = j.str("nonce");
     } catch (...) {
     }
   }
   Json c = Json::O();
+  if (!opt_.token.empty()) c.set("auth_token", Json::S(opt_.token));
+  if (!opt_.user.empty()) {
+    c.set("user", Json::S(opt_.user));
+    c.set("pass", Json::S(opt_.pass));
+  }
+  if (!opt_.jwt.empty()) c.set("jwt", Json::S(opt_.jwt));
+  if (!opt_.nkey_seed.empty()) {
+    std::string raw;
+    if (!nkey_seed_raw(opt_.nkey_seed, raw)) {
+      ::close(fd);
+      throw std::runtime_error("nats: invalid nkey seed");
+    }
+    if (opt_.jwt.empty()) c.set("nkey", Json::S(nkey_public(raw)));
+    c.set("sig", Json::S(b64encode(nkey_sign(raw, nonce), true, false)));
+  }
   c.set("verbose", Json::B(opt_.verbose));
   c.set("pedantic", Json::B(false));
   c.set("tls_required", Json::B(false));
@@ -89,11 +130,27 @@ bool Client::dial() {
 void Client::connect(const std::string& url, ClientOptions opt) {
   if (connected_) throw std::runtime_error("already connected");
   opt_ = opt;
-  parse_url(url, host_, port_);
+  parse_url(url, host_, port_, opt_);
   closing_ = false;
   if (!dial()) throw ConnectionClosedError("nats: cannot connect to " + url);
   rth_ = std::thread([this] { reader(); });
-  flush(opt_.connect_timeout_ms);
+  try {
+    flush(opt_.connect_timeout_ms);
+  } catch (...) {
+    std::string e;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      e = last_err_;
+    }
+    close();
+    if (!e.empty()) throw ConnectionClosedError("nats: " + e);
+    throw;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  if (!last_err_.empty() && last_err_.find("Authorization") != std::string::npos) {
+    const std::string e = last_err_;
+    throw ConnectionClosedError("nats: " + e);
+  }
 }
 
 void Client::close() {
@@ -314,6 +371,11 @@ void Client::on_op(Op& op) {
     case Op::INFO: {
       std::lock_guard<std::mutex> g(mu_);
       info_ = op.arg;
+      break;
+    }
+    case Op::ERR: {
+      std::lock_guard<std::mutex> g(mu_);
+      last_err_ = op.arg;
       break;
     }
     default: break;

@@ -31,6 +31,9 @@ struct ClientOptions {
   int max_reconnect = 60;            // attempts (-1 = forever)
   int reconnect_wait_ms = 250;
   bool verbose = false;
+  // authentication (CONNECT fields): token, user/password, an nkey seed ("SU..." signing the server
+  // nonce) and/or a user JWT (from a .creds file, also signed with its seed)
+  std::string token, user, pass, nkey_seed, jwt;
 };
 
 class TimeoutError : public std::runtime_error {
@@ -100,6 +103,7 @@ class Client {
   std::map<int64_t, std::shared_ptr<Sub>> subs_;
   int64_t next_sid_ = 1;
   std::string info_;
+  std::string last_err_;               // last -ERR text from the server (e.g. 'Authorization Violation')
   size_t max_payload_ = 1 << 20;
   // request/reply
   std::mutex resp_setup_mu_;

@@ -28,6 +28,8 @@ struct Server::Conn {
   std::mutex wmu;
   std::atomic<bool> alive{true};
   bool headers = false, no_responders = false, verbose = false, echo = true;
+  bool authed = false;
+  std::string nonce;
   std::thread th;
   bool write(const std::string& s) {
     std::lock_guard<std::mutex> g(wmu);
@@ -154,6 +156,13 @@ void Server::accept_loop() {
     info.set("max_payload", Json::N((double)opt_.max_payload));
     info.set("jetstream", Json::B(opt_.jetstream));
     info.set("client_id", Json::N((double)c->id));
+    if (opt_.auth_required()) {
+      info.set("auth_required", Json::B(true));
+      c->nonce = random_b64url(11);
+      info.set("nonce", Json::S(c->nonce));
+    } else {
+      c->authed = true;
+    }
     c->write("INFO " + info.dump() + "\r\n");
     c->th = std::thread([this, c] { conn_loop(c); });
   }
@@ -179,7 +188,39 @@ void Server::conn_loop(std::shared_ptr<Conn> c) {
   // the Conn object stays in conns_ until stop() (its thread handle must be joined there)
 }
 
+bool Server::authorize(const Conn& c, const Json& j) {
+  if (!opt_.auth_required()) return true;
+  if (!opt_.auth_token.empty() && ct_equal(j.str("auth_token"), opt_.auth_token)) return true;
+  const std::string user = j.str("user");
+  if (!user.empty())
+    for (auto& up : opt_.users)
+      if (up.first == user && ct_equal(j.str("pass"), up.second)) return true;
+  const std::string nk = j.str("nkey");
+  if (!nk.empty() && std::find(opt_.nkeys.begin(), opt_.nkeys.end(), nk) != opt_.nkeys.end()) {
+    std::string sig;
+    std::string b = j.str("sig");
+    while (b.size() % 4) b += '=';
+    for (char& ch : b) {                      // base64url -> base64
+      if (ch == '-') ch = '+';
+      else if (ch == '_') ch = '/';
+    }
+    try {
+      sig = b64decode(b);
+    } catch (...) {
+      return false;
+    }
+    return nkey_verify(nk, c.nonce, sig);
+  }
+  return false;
+}
+
 void Server::handle(const std::shared_ptr<Conn>& c, Op& op) {
+  if (!c->authed && op.kind != Op::CONNECT && op.kind != Op::PING && op.kind != Op::PONG) {
+    c->write("-ERR 'Authorization Violation'\r\n");
+    c->alive = false;
+    ::shutdown(c->fd, SHUT_RDWR);
+    return;
+  }
   switch (op.kind) {
     case Op::CONNECT: {
       try {
@@ -188,6 +229,15 @@ void Server::handle(const std::shared_ptr<Conn>& c, Op& op) {
         c->no_responders = j.boolean("no_responders", false);
         c->verbose = j.boolean("verbose", false);
         c->echo = j.boolean("echo", true);
+        if (!c->authed) {
+          if (!authorize(*c, j)) {
+            c->write("-ERR 'Authorization Violation'\r\n");
+            c->alive = false;
+            ::shutdown(c->fd, SHUT_RDWR);
+            return;
+          }
+          c->authed = true;
+        }
       } catch (...) {
         c->write("-ERR 'Invalid CONNECT'\r\n");
         return;

@@ -29,6 +29,12 @@ struct ServerOptions {
   bool jetstream = true;
   std::string store_dir;              // "" = memory only
   std::string server_name = "natscore";
+  // authentication (any configured -> auth_required): a shared token, user/password pairs, and/or
+  // user nkeys (public "U..." keys; the client signs the per-connection INFO nonce)
+  std::string auth_token;
+  std::vector<std::pair<std::string, std::string>> users;
+  std::vector<std::string> nkeys;
+  bool auth_required() const { return !auth_token.empty() || !users.empty() || !nkeys.empty(); }
 };
 
 class Server {
@@ -77,6 +83,7 @@ class Server {
   void accept_loop();
   void conn_loop(std::shared_ptr<Conn> c);
   void handle(const std::shared_ptr<Conn>& c, Op& op);
+  bool authorize(const Conn& c, const Json& connect);
   void route(const std::string& subj, const std::string& reply, const std::string& hdr,
              const std::string& payload, Conn* from);
   bool js_handle(const std::string& subj, const std::string& reply, const std::string& hdr,

@@ -1,5 +1,8 @@
 #include "util.h"
 
+#include <openssl/evp.h>
+#include <openssl/rand.h>
+
 #include <cpuid.h>
 #include <immintrin.h>
 #include <cstdlib>
@@ -519,6 +522,159 @@ bool send_all(int fd, const char* p, size_t n) {
     n -= (size_t)w;
   }
   return true;
+}
+
+}  // namespace natscore
+
+
+// ============================== nkeys / auth ===============================
+namespace natscore {
+
+static const char B32[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZ234567";
+
+std::string base32_encode(const std::string& raw) {
+  std::string out;
+  uint32_t buf = 0;
+  int bits = 0;
+  for (unsigned char c : raw) {
+    buf = (buf << 8) | c;
+    bits += 8;
+    while (bits >= 5) {
+      out += B32[(buf >> (bits - 5)) & 31];
+      bits -= 5;
+    }
+  }
+  if (bits > 0) out += B32[(buf << (5 - bits)) & 31];
+  return out;
+}
+
+bool base32_decode(const std::string& s, std::string& raw) {
+  raw.clear();
+  uint32_t buf = 0;
+  int bits = 0;
+  for (char ch : s) {
+    int v;
+    if (ch >= 'A' && ch <= 'Z') v = ch - 'A';
+    else if (ch >= '2' && ch <= '7') v = ch - '2' + 26;
+    else if (ch == '=') break;
+    else return false;
+    buf = (buf << 5) | (uint32_t)v;
+    bits += 5;
+    if (bits >= 8) {
+      raw += (char)((buf >> (bits - 8)) & 0xFF);
+      bits -= 8;
+    }
+  }
+  return true;
+}
+
+uint16_t crc16_xmodem(const std::string& data) {
+  uint16_t crc = 0;
+  for (unsigned char c : data) {
+    crc ^= (uint16_t)c << 8;
+    for (int i = 0; i < 8; ++i) crc = (crc & 0x8000) ? (uint16_t)((crc << 1) ^ 0x1021) : (uint16_t)(crc << 1);
+  }
+  return crc;
+}
+
+static bool nkey_unwrap(const std::string& text, std::string& body) {
+  std::string raw;
+  if (!base32_decode(text, raw) || raw.size() < 3) return false;
+  body = raw.substr(0, raw.size() - 2);
+  const uint16_t crc = (uint16_t)((unsigned char)raw[raw.size() - 2] | ((unsigned char)raw[raw.size() - 1] << 8));
+  return crc16_xmodem(body) == crc;
+}
+
+static std::string nkey_wrap(const std::string& body) {
+  const uint16_t crc = crc16_xmodem(body);
+  return base32_encode(body + std::string(1, (char)(crc & 0xFF)) + std::string(1, (char)(crc >> 8)));
+}
+
+bool nkey_seed_raw(const std::string& seed, std::string& raw32) {
+  std::string body;
+  if (!nkey_unwrap(seed, body) || body.size() != 34) return false;
+  const uint8_t b0 = (uint8_t)body[0], b1 = (uint8_t)body[1];
+  if ((b0 & 0xF8) != NKEY_PREFIX_SEED) return false;
+  const uint8_t kind = (uint8_t)(((b0 & 7) << 5) | ((b1 & 0xF8) >> 3));
+  if (kind != NKEY_PREFIX_USER) return false;           // user seeds only ("SU...")
+  raw32 = body.substr(2, 32);
+  return true;
+}
+
+static EVP_PKEY* ed_priv(const std::string& raw32) {
+  return EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, nullptr, (const unsigned char*)raw32.data(), 32);
+}
+
+std::string nkey_public(const std::string& raw32) {
+  EVP_PKEY* k = ed_priv(raw32);
+  if (!k) throw std::runtime_error("nkey: bad seed");
+  unsigned char pub[32];
+  size_t n = sizeof pub;
+  EVP_PKEY_get_raw_public_key(k, pub, &n);
+  EVP_PKEY_free(k);
+  return nkey_wrap(std::string(1, (char)NKEY_PREFIX_USER) + std::string((const char*)pub, 32));
+}
+
+std::string nkey_sign(const std::string& raw32, const std::string& msg) {
+  EVP_PKEY* k = ed_priv(raw32);
+  if (!k) throw std::runtime_error("nkey: bad seed");
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  unsigned char sig[64];
+  size_t n = sizeof sig;
+  const bool ok = EVP_DigestSignInit(ctx, nullptr, nullptr, nullptr, k) == 1 &&
+                  EVP_DigestSign(ctx, sig, &n, (const unsigned char*)msg.data(), msg.size()) == 1;
+  EVP_MD_CTX_free(ctx);
+  EVP_PKEY_free(k);
+  if (!ok) throw std::runtime_error("nkey: signing failed");
+  return std::string((const char*)sig, n);
+}
+
+bool nkey_verify(const std::string& pub, const std::string& msg, const std::string& sig) {
+  std::string body;
+  if (!nkey_unwrap(pub, body) || body.size() != 33 || (uint8_t)body[0] != NKEY_PREFIX_USER || sig.size() != 64)
+    return false;
+  EVP_PKEY* k = EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, nullptr, (const unsigned char*)body.data() + 1, 32);
+  if (!k) return false;
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  const bool ok = EVP_DigestVerifyInit(ctx, nullptr, nullptr, nullptr, k) == 1 &&
+                  EVP_DigestVerify(ctx, (const unsigned char*)sig.data(), sig.size(), (const unsigned char*)msg.data(),
+                                   msg.size()) == 1;
+  EVP_MD_CTX_free(ctx);
+  EVP_PKEY_free(k);
+  return ok;
+}
+
+std::string random_b64url(size_t nbytes) {
+  std::string r(nbytes, '\0');
+  RAND_bytes((unsigned char*)&r[0], (int)nbytes);
+  std::string s = b64encode(r, true);
+  while (!s.empty() && s.back() == '=') s.pop_back();
+  return s;
+}
+
+bool ct_equal(const std::string& a, const std::string& b) {
+  unsigned char d = a.size() != b.size();
+  for (size_t i = 0; i < std::min(a.size(), b.size()); ++i) d |= (unsigned char)(a[i] ^ b[i]);
+  return d == 0;
+}
+
+static std::string between(const std::string& t, const std::string& begin) {
+  size_t a = t.find(begin);
+  if (a == std::string::npos) return "";
+  a = t.find('\n', a);
+  if (a == std::string::npos) return "";
+  size_t b = t.find("---", a + 1);
+  std::string s = t.substr(a + 1, (b == std::string::npos ? t.size() : b) - a - 1);
+  std::string out;
+  for (char c : s)
+    if (!isspace((unsigned char)c)) out += c;
+  return out;
+}
+
+bool parse_creds(const std::string& text, std::string& jwt, std::string& seed) {
+  jwt = between(text, "BEGIN NATS USER JWT");
+  seed = between(text, "BEGIN USER NKEY SEED");
+  return !seed.empty();
 }
 
 }  // namespace natscore

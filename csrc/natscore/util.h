@@ -82,6 +82,23 @@ class Sha256 {
 std::string nuid_next();          // 22-char base62 unique id
 
 // ---------------------------------------------------------------------------
+// NATS nkeys (ed25519 identities, base32 + CRC16 text form) and auth helpers
+// ---------------------------------------------------------------------------
+std::string base32_encode(const std::string& raw);               // RFC 4648, no padding
+bool base32_decode(const std::string& s, std::string& raw);
+uint16_t crc16_xmodem(const std::string& data);
+constexpr uint8_t NKEY_PREFIX_SEED = 18 << 3, NKEY_PREFIX_USER = 20 << 3;
+// "SU..." user seed -> raw 32-byte ed25519 private seed (false: malformed / bad checksum)
+bool nkey_seed_raw(const std::string& seed, std::string& raw32);
+std::string nkey_public(const std::string& raw32);               // "U..." public key of a seed
+std::string nkey_sign(const std::string& raw32, const std::string& msg);    // 64-byte signature
+bool nkey_verify(const std::string& pub, const std::string& msg, const std::string& sig);
+std::string random_b64url(size_t nbytes);
+bool ct_equal(const std::string& a, const std::string& b);      // constant-time compare
+// creds file: the user JWT and the nkey seed between the BEGIN/END markers
+bool parse_creds(const std::string& text, std::string& jwt, std::string& seed);
+
+// ---------------------------------------------------------------------------
 // Subject helpers
 // ---------------------------------------------------------------------------
 std::vector<std::string> split_tokens(const std::string& subj);

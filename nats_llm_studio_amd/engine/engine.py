@@ -316,7 +316,17 @@ class Engine:
         self.waiting.clear()
 
     def unload(self):
-        """Free device memory (KV cache, graphs, weights)."""
+        """Free device memory (KV cache, graphs, weights).
+
+        May be reached from the engine thread itself (a request's completion callback releasing the
+        last reference of an evicted model): then the loop is told to stop and the teardown runs on
+        a helper thread once the loop has returned, never by joining the current thread."""
+        if self.thread is not None and threading.current_thread() is self.thread:
+            with self.lock:
+                self.stop_flag = True
+                self.lock.notify_all()
+            threading.Thread(target=self.unload, name="nls-engine-unload", daemon=True).start()
+            return
         self.shutdown()
         self.graphs.clear()
         self.kc = self.vc = None

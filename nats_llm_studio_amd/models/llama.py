@@ -29,6 +29,10 @@ from ..ops import QWeight, Seg
 from .config import ModelConfig
 
 
+_SPLIT_CAP = int(os.environ.get("NLS_ATTN_SPLIT_CAP", "32"))     # flash-decoding splits per (token, kv head)
+_SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgroups of a decode attention launch
+
+
 @dataclass
 class ShardSpec:
     """Model shard of this process (rank of size); size 1 = whole model.
@@ -279,10 +283,13 @@ class LlamaModel:
 
     @staticmethod
     def attn_splits(T: int, Hkv: int) -> int:
+        """Flash-decoding splits per (token, kv head): enough workgroups to cover the chip. The kernel
+        sizes each split from the actual context (>= 64 keys) and skips splits past it, so a large
+        split count only costs parallelism headroom for long contexts."""
         wg = T * Hkv
         if wg >= 512:
             return 1
-        return int(min(32, max(1, 512 // wg)))
+        return int(min(_SPLIT_CAP, max(1, _SPLIT_WG // wg)))
 
     # ------------------------------------------------------------------ forward
     def forward(self, b: StepBuffers, kc: torch.Tensor, vc: torch.Tensor, T: int, block_size: int,

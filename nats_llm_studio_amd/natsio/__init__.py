@@ -11,6 +11,7 @@ sides of the wire are implemented natively here.
 from __future__ import annotations
 
 import json
+import os
 import threading
 from typing import Callable, Dict, Optional
 
@@ -81,8 +82,16 @@ class Client:
         self.subs = []
 
     def connect(self, url: str = "nats://127.0.0.1:4222", name: str = "nats-llm-studio-amd", timeout: float = 2.0,
-                reconnect: bool = True, max_reconnect: int = 60, reconnect_wait: float = 0.25) -> "Client":
-        self._c.connect(url, name, int(timeout * 1000), reconnect, max_reconnect, int(reconnect_wait * 1000))
+                reconnect: bool = True, max_reconnect: int = 60, reconnect_wait: float = 0.25, token: str = "",
+                user: str = "", password: str = "", nkey_seed: str = "", creds: str = "") -> "Client":
+        """Authentication as nats.go: `token`, `user`/`password` (or in the URL), `nkey_seed` ("SU..."),
+        or a `.creds` file (user JWT + seed); nkey-based methods sign the server's INFO nonce."""
+        jwt = ""
+        if creds:
+            with open(os.path.expanduser(creds)) as f:
+                jwt, nkey_seed = _nc.parse_creds(f.read())
+        self._c.connect(url, name, int(timeout * 1000), reconnect, max_reconnect, int(reconnect_wait * 1000), token,
+                        user, password, nkey_seed, jwt)
         return self
 
     @property
@@ -131,8 +140,10 @@ class Client:
 
 class EmbeddedServer:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, max_payload: int = 1 << 20, jetstream: bool = True,
-                 store_dir: str = ""):
-        self._s = _nc.Server(host, port, max_payload, jetstream, store_dir)
+                 store_dir: str = "", auth_token: str = "", users=(), nkeys=()):
+        """`auth_token` / `users` [(user, password)] / `nkeys` ["U..." public keys]: any of them makes
+        the server require authentication (INFO auth_required + a per-connection nonce)."""
+        self._s = _nc.Server(host, port, max_payload, jetstream, store_dir, auth_token, list(users), list(nkeys))
         self.host = host
 
     def start(self) -> "EmbeddedServer":
@@ -164,6 +175,13 @@ class EmbeddedServer:
 
     def __exit__(self, *a):
         self.stop()
+
+
+def nkey_keypair(raw32: bytes = None):
+    """(seed "SU...", public "U...") of a new (or given 32-byte) user nkey."""
+    raw32 = raw32 if raw32 is not None else os.urandom(32)
+    seed = _nc.nkey_user_seed_from_raw(raw32)
+    return seed, _nc.nkey_public(seed)
 
 
 class ObjectStore:

@@ -60,6 +60,17 @@ class WorkerConfig:
     timeout_chat: float = 120.0
     handler_workers: int = 4
     lmstudio_base_url: str = "http://127.0.0.1:1234"   # used by the `http` backend only
+    # NATS authentication (nats.go options): token, user/password, nkey seed or a .creds file
+    nats_token: str = ""
+    nats_user: str = ""
+    nats_password: str = ""
+    nats_nkey_seed: str = ""
+    nats_creds: str = ""
+
+    def nats_auth(self) -> dict:
+        """Keyword arguments of natsio.Client.connect for the configured credentials."""
+        return dict(token=self.nats_token, user=self.nats_user, password=self.nats_password,
+                    nkey_seed=self.nats_nkey_seed, creds=self.nats_creds)
 
     def subject(self, name: str) -> str:
         return f"{self.subject_prefix}.{name}"
@@ -84,6 +95,15 @@ class WorkerConfig:
         c.subject_prefix = e.get("SUBJECT_PREFIX", c.subject_prefix)
         c.embedded_server = e.get("EMBEDDED_NATS", "0") in ("1", "true", "yes")
         c.store_dir = e.get("NATS_STORE_DIR", c.store_dir)
+        c.nats_token = e.get("NATS_TOKEN", c.nats_token)
+        c.nats_user = e.get("NATS_USER", c.nats_user)
+        c.nats_password = e.get("NATS_PASSWORD", c.nats_password)
+        c.nats_nkey_seed = e.get("NATS_NKEY_SEED", c.nats_nkey_seed)
+        seed_file = e.get("NATS_NKEY_SEED_FILE", "")
+        if seed_file and not c.nats_nkey_seed:
+            with open(os.path.expanduser(seed_file)) as f:
+                c.nats_nkey_seed = f.read().strip()
+        c.nats_creds = e.get("NATS_CREDS", c.nats_creds)
         return c
 
     @classmethod
@@ -106,6 +126,7 @@ class WorkerConfig:
         ap.add_argument("--embedded-server", action="store_true", default=c.embedded_server)
         ap.add_argument("--store-dir", default=c.store_dir)
         ap.add_argument("--subject-prefix", default=c.subject_prefix)
+        ap.add_argument("--nats-creds", default=c.nats_creds, help="NATS .creds file (user JWT + nkey seed)")
         a = ap.parse_args(argv)
         for k, v in vars(a).items():
             setattr(c, k, v)

@@ -59,7 +59,8 @@ class Service:
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "Service":
         if self.client is None:
-            self.client = Client().connect(self.cfg.nats_url, name=f"nats-llm-studio-amd-{os.getpid()}")
+            self.client = Client().connect(self.cfg.nats_url, name=f"nats-llm-studio-amd-{os.getpid()}",
+                                           **self.cfg.nats_auth())
         self.store = ModelStore(self.client, self.cfg.models_dir, self.cfg.bucket)
         self.registry.scan()
         q = self.cfg.queue_group

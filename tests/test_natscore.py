@@ -303,3 +303,46 @@ def test_sha256_matches_hashlib():
     for L in (0, 1, 55, 56, 63, 64, 65, 127, 128, 129, 1000, 65536 + 7):
         b = os.urandom(L)
         assert n.sha256(b) == hashlib.sha256(b).digest(), L
+
+
+# ---------------------------------------------------------------- authentication
+def test_nkeys_sign_verify_roundtrip():
+    from nats_llm_studio_amd.natsio import _natscore as n, nkey_keypair
+    seed, pub = nkey_keypair(bytes(range(32)))
+    assert seed.startswith("SU") and pub.startswith("U") and len(pub) == 56 and len(seed) == 58
+    assert nkey_keypair(bytes(range(32))) == (seed, pub)            # deterministic from the raw seed
+    sig = n.nkey_sign(seed, b"nonce-123")
+    assert len(sig) == 64 and n.nkey_verify(pub, b"nonce-123", sig)
+    assert not n.nkey_verify(pub, b"nonce-124", sig)
+    bad = bytes([sig[0] ^ 1]) + sig[1:]
+    assert not n.nkey_verify(pub, b"nonce-123", bad)
+    with pytest.raises(Exception):
+        n.nkey_public(seed[:-1] + ("A" if seed[-1] != "A" else "B"))   # checksum mismatch
+
+
+def test_server_auth_token_user_nkey(tmp_path):
+    from nats_llm_studio_amd.natsio import _natscore as n, nkey_keypair
+    seed, pub = nkey_keypair()
+    other_seed, _ = nkey_keypair()
+    s = EmbeddedServer(auth_token="s3cret", users=[("alice", "pw")], nkeys=[pub]).start()
+    try:
+        url = s.url
+        ok = [Client().connect(url, token="s3cret", reconnect=False),
+              Client().connect(url.replace("nats://", "nats://alice:pw@"), reconnect=False),
+              Client().connect(url, nkey_seed=seed, reconnect=False)]
+        creds = tmp_path / "u.creds"
+        creds.write_text("-----BEGIN NATS USER JWT-----\neyJhbGciOi.fake.jwt\n------END NATS USER JWT------\n\n"
+                         "************************* IMPORTANT *************************\n"
+                         f"-----BEGIN USER NKEY SEED-----\n{seed}\n------END USER NKEY SEED------\n")
+        assert n.parse_creds(creds.read_text()) == ("eyJhbGciOi.fake.jwt", seed)
+        for c in ok:
+            sub = c.subscribe("auth.echo", cb=lambda m, c=c: c.publish(m.reply, m.data))
+            c.flush()
+            assert c.request("auth.echo", b"hi", 2).data == b"hi"
+            sub.unsubscribe()
+            c.close()
+        for kw in (dict(token="wrong"), dict(user="alice", password="nope"), dict(nkey_seed=other_seed), {}):
+            with pytest.raises(Exception, match="Authorization|cannot connect|timeout|closed"):
+                Client().connect(url, reconnect=False, timeout=1.0, **kw)
+    finally:
+        s.stop()
