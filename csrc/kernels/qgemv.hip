@@ -5,6 +5,11 @@
 
 using namespace nls_gemv;
 
+namespace nls_hgemm {
+int launch_dense(int wm, int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
+                 hipStream_t st);
+}
+
 
 extern "C" {
 
@@ -32,6 +37,10 @@ struct NlsFuse {
 //         activation blocks, 2: 128-row), optional split-K as mode 1.
 // mode 3: large-M LDS-DMA GEMM (qgemm_dma.h; Q4_K/Q5_K/Q6_K only): 4 waves, `rt` = activation
 //         tiles per block (16: 256 rows, 8: 128 rows), optional split-K as mode 1.
+// mode 4: large-M dense f16 GEMM (hgemm.hip): every segment is type F16 with `w` = a ROW-MAJOR
+//         [rows][K] f16 matrix (not the tiled layout); 8 waves, `rt` = WM (4: 256-row activation
+//         blocks, 2: 128-row), optional split-K as mode 1.
+// mode 5: mode 4 with 256-row weight tiles (twice the MFMA work per fetched activation byte).
 // Returns 0 on success, a hipError_t, or -1 on bad arguments.
 static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
                       float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
@@ -55,7 +64,11 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
                   segs[0].mcount || !fz->cnt || !fz->hout || segs[0].rows % 4 || argmax))
     return -1;
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
-  if (mode == 3) {
+  if (mode == 4 || mode == 5) {
+    if (waves != 8 || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount) return -1;
+  } else if (mode == 3) {
     if (waves != 4 || (rt != 8 && rt != 16)) return -1;
   } else if (mode == 2 ? (waves != 8 || (rt != 1 && rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) {
     return -1;
@@ -65,7 +78,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16;
+  const int tile_rows = mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16);
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -133,14 +146,16 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
   auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : launch_k2);
-  if (mode >= 2 && kset == 2) return -1;   // plain float weights: path B only
+  if (mode >= 2 && mode <= 3 && kset == 2) return -1;   // tiled float weights: path B only
   if (mode == 3)
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type == QT_Q8_0) return -1;   // raw Q8_0 tiles do not fit the DMA LDS budget
   if (mode != 0) {
     if (ks < 1) ks = 1;
     int rc;
-    if (mode == 3)
+    if (mode >= 4)
+      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, sl, tiles, ks, (float*)ws, a, st);
+    else if (mode == 3)
       rc = (kset == 0 ? nls_dma::launch_dma_k0 : nls_dma::launch_dma_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 2)
       rc = (kset == 0 ? nls_gemm::launch_lds_k0 : nls_gemm::launch_lds_k1)(rt, sl, tiles, ks, (float*)ws, a, st);

@@ -108,6 +108,12 @@ bool Client::dial() {
   // re-establish subscriptions
   {
     std::lock_guard<std::mutex> g(mu_);
+    // PING/PONG accounting: PINGs of a previous connection will never be answered (release their
+    // waiters), and the handshake PING above counts like any flush PING -- otherwise its PONG runs
+    // pongs_recv_ one ahead and the next flush() returns before the server has seen what preceded it
+    pongs_recv_ = pings_sent_;
+    ++pings_sent_;
+    pong_cv_.notify_all();
     for (auto& kv : subs_) {
       if (kv.second->closed) continue;
       hello += "SUB " + kv.second->subject + (kv.second->queue.empty() ? "" : " " + kv.second->queue) + " " +

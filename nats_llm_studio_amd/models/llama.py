@@ -226,6 +226,30 @@ class LlamaModel:
         head = "token_embd.weight" if cfg.tied_embeddings else "output.weight"
         self.lm_head = self._matrix(head, (self.vocab_lo, self.vocab_hi))
 
+    def dense_matrices(self) -> List[QWeight]:
+        """The projection matrices that get an f16 copy for the large-M dense GEMM (mode 4):
+        attention, dense FFN and the LM head (MoE experts stay quantised: their grouped GEMM
+        gathers rows and runs the LDS-dequant kernel)."""
+        out = []
+        for lw in self.layers:
+            out += [s.w for s in lw.qkv] + [lw.wo]
+            if lw.gateup is not None:
+                out += [lw.gateup, lw.down]
+        out.append(self.lm_head)
+        return out
+
+    def expand_dense(self, budget_bytes: Optional[int] = None) -> int:
+        """Give every dense_matrices() entry its f16 copy (ops.QWeight.expand_dense) when the whole set
+        fits in `budget_bytes` (None: no limit). All or nothing, so every large-M step takes one path;
+        returns the bytes added (0 if skipped or already expanded)."""
+        ws = self.dense_matrices()
+        need = sum(w.dense_bytes for w in ws if w.d16 is None)
+        if self.device.type != "cuda" or need == 0 or (budget_bytes is not None and need > budget_bytes):
+            return 0
+        added = sum(w.expand_dense() for w in ws)
+        self.dense_bytes = getattr(self, "dense_bytes", 0) + added
+        return added
+
     # ------------------------------------------------------------------ buffers
     def kv_cache(self, num_blocks: int, block_size: int = 16):
         L, slots = self.cfg.n_layer, num_blocks * block_size

@@ -26,6 +26,9 @@ import os as _os
 # last workgroup's ticket + acquire + row reload sit on the critical path and cost more than the
 # separate norm launch inside a hipGraph (profiles/rocprof_b1_r02_addnorm.txt). NLS_ADDNORM=8 enables.
 ADDNORM_MAX_M = int(_os.environ.get("NLS_ADDNORM", "0"))
+# Large-M GEMMs switch to the dense f16 kernel (mode 4, csrc/kernels/hgemm.hip) from this many rows
+# on, for weights that carry an f16 copy (QWeight.expand_dense)
+DENSE_MIN_M = int(_os.environ.get("NLS_DENSE_GEMM_M", "128"))
 ACT_DTYPE = torch.float16   # activation dtype of every GEMM/GEMV input and SwiGLU/RMSNorm/attention output
 
 
@@ -136,6 +139,20 @@ class QWeight:
                 self.data = tile_layout(t, ggml_type, rows, K)
         self._raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1) if self.device.type == "cpu" else None
         self._dense = None
+        self.d16: Optional[torch.Tensor] = None    # row-major f16 copy for the large-M GEMM (mode 4)
+
+    def expand_dense(self) -> int:
+        """Keep a dequantised row-major f16 copy next to the quantised tiles (GPU; idempotent).
+        Returns the bytes it added. Large-M GEMMs then run on MFMA without in-kernel dequantisation;
+        the copy is the HIP dequant kernel's output, i.e. the very f16 values modes 2/3 feed their MFMAs."""
+        if self.device.type != "cuda" or self.layout != "tiled" or self.d16 is not None:
+            return 0
+        self.d16 = self.dense(torch.float16).contiguous()
+        return self.d16.numel() * 2
+
+    @property
+    def dense_bytes(self) -> int:
+        return self.rows * self.K * 2
 
     @property
     def nbytes(self) -> int:
@@ -186,12 +203,35 @@ def _workspace(dev, n: int) -> torch.Tensor:
     return w
 
 
+def dense_ok(segs: Sequence[Seg], M: int) -> bool:
+    """Does this launch run on the dense f16 GEMM (mode 4)?"""
+    return M >= DENSE_MIN_M and all(s.w.d16 is not None and s.xmap is None and s.ymap is None for s in segs)
+
+
 def gemv_config(segs: Sequence[Seg], M: int):
     """(mode, waves, rt, ks) for a launch. mode 0 = waves split K (small batch, mapped rows);
     mode 1 = waves split rows over an LDS-staged activation tile (+ split-K across workgroups);
-    mode 2 = large-M LDS-dequant GEMM (K-quants; rt = waves along M: 256- or 128-row blocks)."""
+    mode 2 = large-M LDS-dequant GEMM (K-quants; rt = waves along M: 256- or 128-row blocks);
+    mode 4/5 = large-M dense f16 GEMM on the weights' f16 copies, 128/256 weight rows per workgroup
+    (rt as mode 2)."""
     from . import tuning
+    if dense_ok(segs, M):
+        return tuning.select_dense(segs, M)
     return tuning.select(segs, M)
+
+
+def _seg_arr(segs: Sequence[Seg], mode: int):
+    """ctypes segment list of a launch: modes 4/5 point at the row-major f16 copies."""
+    arr = (_lib.NlsSeg * len(segs))()
+    for i, s in enumerate(segs):
+        if mode in (4, 5):
+            if s.w.d16 is None:
+                raise ValueError(f"{s.w.name}: mode 4 needs QWeight.expand_dense()")
+            arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), None, None, None, 1, s.w.rows, s.w.K, s.ycol)
+        else:
+            arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
+                                 s.w.K, s.ycol)
+    return arr
 
 
 NORM_FUSE_LDS = 54 * 1024      # staged-row budget of the fused-norm GEMV (64 KiB LDS minus the reduce area)
@@ -240,10 +280,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
                 qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt,
                       mode, ks)
             return y
-        arr = (_lib.NlsSeg * len(segs))()
-        for i, s in enumerate(segs):
-            arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
-                                 s.w.K, s.ycol)
+        arr = _seg_arr(segs, mode)
         ws = None
         if mode != 0 and ks > 1:
             ws = _workspace(x.device, ks * M * sum(s.w.rows for s in segs)).data_ptr()
@@ -311,8 +348,7 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
         if mode != 0 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
             L = _lib.lib()
             ws = _workspace(x.device, ks * M * seg.w.rows)
-            arr = (_lib.NlsSeg * 1)()
-            arr[0] = _lib.NlsSeg(seg.w.data.data_ptr(), None, None, None, seg.w.type, seg.w.rows, seg.w.K, 0)
+            arr = _seg_arr([seg], mode)
             st = _stream_ptr(x)
             _lib.check(L.nls_qgemv(arr, 1, xin.data_ptr(), xin.stride(0), x.data_ptr(), x.stride(0), M, float(alpha),
                                    EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
@@ -445,9 +481,7 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         if mode != 0 and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
             L = _lib.lib()
             ws = _workspace(h.device, ks * T * ncol)
-            arr = (_lib.NlsSeg * len(segs))()
-            for i, s in enumerate(segs):
-                arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), None, None, None, s.w.type, s.w.rows, s.w.K, s.ycol)
+            arr = _seg_arr(segs, mode)
             st = _stream_ptr(h)
             _lib.check(L.nls_qgemv(arr, len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
                                    EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")

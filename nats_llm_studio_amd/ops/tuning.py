@@ -61,6 +61,34 @@ def heuristic(segs, M: int):
     return (1, waves, rt, ks)
 
 
+def dense_key(segs, M: int) -> str:
+    return f"d:{sum(s.w.rows for s in segs)}:{segs[0].w.K}:{_mb(M)}"
+
+
+def dense_heuristic(segs, M: int):
+    """Modes 4/5 (dense f16 GEMM): 256-row activation blocks from M >= 192 with 256-row weight tiles
+    (mode 5), then the split-K that minimises (workgroup rounds over the 256 CUs) / ks, with a small
+    per-slice cost."""
+    wm = 4 if M >= 192 else 2
+    bm = 64 * wm
+    mode, bn = (5, 256) if M >= 192 else (4, 128)
+    tiles = sum((s.w.rows + bn - 1) // bn for s in segs) * ((M + bm - 1) // bm)
+    nkt = segs[0].w.K // 64
+    best, best_ks = None, 1
+    for ks in range(1, 9):
+        if ks > 1 and nkt // ks < 8:
+            break
+        cost = -(-tiles * ks // 256) / ks + 0.03 * ks
+        if best is None or cost < best - 1e-9:
+            best, best_ks = cost, ks
+    return (mode, 8, wm, best_ks)
+
+
+def select_dense(segs, M: int):
+    hit = table().get(dense_key(segs, M))
+    return hit if hit is not None else dense_heuristic(segs, M)
+
+
 def select(segs, M: int):
     hit = table().get(key(segs, M))
     return hit if hit is not None else heuristic(segs, M)

@@ -656,3 +656,85 @@ def test_qgemv_fused_rmsnorm(gpu, t, M, epi):
         assert ((outs[0][1] & 0xFFFFFFFF) == (outs[1][1] & 0xFFFFFFFF)).all()
     else:
         _close(outs[1][0], outs[0][0], 5e-3)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("M", [65, 128, 300, 520])
+@pytest.mark.parametrize("mode,wm,ks", [(4, 4, 1), (4, 2, 1), (4, 4, 3), (4, 2, 5), (5, 4, 1), (5, 2, 1), (5, 4, 3),
+                                        (5, 2, 2)])
+def test_hgemm_dense(gpu, t, M, mode, wm, ks):
+    """Dense f16 GEMM (mode 4) on the weights' f16 copy: both operands by LDS-DMA into a 3-deep ring;
+    partial last 128-row weight tile and activation block, K slices of 2..12 steps; store, add, argmax."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, t, gpu)
+    assert w.expand_dense() == rows * K * 2 and w.expand_dense() == 0
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=mode, waves=8, rt=wm, ks=ks, argmax=keys)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    assert float(y[M:].abs().max().cpu()) == 0.0 if M < pad else True
+    ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+    ops.argmax_unpack(keys, M, ids)
+    assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=mode, waves=8, rt=wm, ks=ks)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+    # the same launch through the quantised LDS GEMM agrees to accumulation order
+    y3 = torch.zeros(pad, rows, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y3, M, mode=2, waves=8, rt=wm, ks=1)
+    _close(y3[:M], y[:M], 1e-3)
+
+
+@pytest.mark.parametrize("mode,ks", [(4, 1), (4, 2), (5, 1), (5, 2)])
+def test_hgemm_dense_swiglu_multiseg_auto(gpu, mode, ks):
+    """Mode 4 with the SwiGLU epilogue and a Q|K|V-style multi-segment launch; then the automatic
+    selection (gemv_config) picks mode 4 exactly when every segment carries an f16 copy and M is large."""
+    K, F = 512, 256
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    w.expand_dense()
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 333
+    x = _x(M, K, gpu)
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=mode, waves=8, rt=4, ks=ks)
+    xf = x[:M].float().cpu()
+    _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(128, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(128, K, GGMLType.Q6_K, gpu, 3)
+    segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)]
+    assert ops.gemv_config(segs, M)[0] != 4
+    for q in (a, b, c):
+        q.expand_dense()
+    assert ops.gemv_config(segs, M)[0] in (4, 5) and ops.gemv_config(segs, 8)[0] not in (4, 5)
+    yq = torch.zeros(x.shape[0], 512, device=gpu)
+    ops.qgemv(segs, x, yq, M, mode=mode, waves=8, rt=4, ks=ks)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+    yq.zero_()
+    ops.qgemv(segs, x, yq, M)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+
+
+def test_hgemm_dense_add_rmsnorm_slabs(gpu):
+    """Mode 4 split-K slabs feeding the fused reduce + residual + RMSNorm kernel (o / down projections)."""
+    D, K, M = 512, 1024, 200
+    w, Wd = _qw(D, K, GGMLType.Q4_K, gpu, 4)
+    w.expand_dense()
+    xin = _x(M, K, gpu)
+    x = torch.randn(xin.shape[0], D, device=gpu)
+    x0 = x.clone()
+    nw = torch.rand(D, device=gpu) + 0.5
+    h = torch.zeros(xin.shape[0], D, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv_add_rmsnorm(ops.Seg(w), xin, x, nw, h, M, 1.0, 1e-5, cfg=(5, 8, 4, 4))
+    ref = x0[:M].cpu() + xin[:M].float().cpu() @ Wd.t()
+    _close(x[:M], ref)
+    hn = ref * torch.rsqrt(ref.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu()
+    _close(h[:M], hn, 2e-2)

@@ -346,3 +346,22 @@ def test_server_auth_token_user_nkey(tmp_path):
                 Client().connect(url, reconnect=False, timeout=1.0, **kw)
     finally:
         s.stop()
+
+
+def test_flush_waits_for_server_after_connect():
+    """flush() must not return on the PONG of the CONNECT handshake PING (which once ran the
+    PONG count one ahead): a SUB followed by flush() is registered before the peer publishes."""
+    lost = 0
+    for _ in range(40):
+        s = EmbeddedServer().start()
+        a, b = client(s), client(s)
+        sub = b.subscribe("x.*")
+        b.flush()
+        a.publish("x.y", b"1")
+        a.flush()
+        try:
+            sub.next_msg(2)
+        except TimeoutError:
+            lost += 1
+        a.close(); b.close(); s.stop()
+    assert lost == 0

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--cfg", default="")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--type", default="Q4_K")
+    ap.add_argument("--dense", action="store_true", help="give the weight its f16 copy (mode 4 eligible)")
     args = ap.parse_args()
     spec = SPECS[args.model]
     d, hd = spec.d_model, spec.head_dim
@@ -42,6 +43,8 @@ def main():
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(0)
     w = ops.QWeight(Q.random_blocks(t, rows * K, 0.02, rng), t, rows, K, dev)
+    if args.dense:
+        w.expand_dense()
     segs = [ops.Seg(w, 0)]
     M = args.M
     x = (torch.randn(M, K, device=dev) * 0.5).to(ops.ACT_DTYPE)

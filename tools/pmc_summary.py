@@ -20,7 +20,7 @@ for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=Tru
         did = max(d)
         vals[k].update(d[did])
 for k, c in vals.items():
-    if "qmm" not in k and "qgemv" not in k and len(vals) > 1:
+    if "qmm" not in k and "qgemv" not in k and "hgemm" not in k and len(vals) > 1:
         continue
     print(k)
     for n in sorted(c):

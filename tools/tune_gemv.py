@@ -4,6 +4,9 @@ write the per-shape winners to nats_llm_studio_amd/ops/gemv_tuning.json.
 
 Each config is timed as a hipGraph of REPS back-to-back launches (so host launch cost is
 excluded), median of 5 replays. Usage: python tools/tune_gemv.py [--model llama-3-8b] [--out f.json]
+
+--dense: tune the dense f16 GEMM (mode 4, weights' f16 copies) at the large-M buckets instead, next to
+the current quantised winner of the same shape ("d:<rows>:<K>:<Mbucket>" entries).
 """
 import argparse
 import json
@@ -60,6 +63,11 @@ def configs(K, M=1, quant=True):
     return c
 
 
+def dense_configs(K):
+    nkt = K // 64
+    return [(mode, 8, wm, ks) for mode in (5, 4) for wm in (4, 2) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
+
+
 def time_cfg(copies, x, y, M, epi, keys, cfg):
     """copies: weight-copy segment lists cycled through by the REPS launches, so small matrices are
     streamed from HBM as in a real decode step (one copy would sit in L2 / the 256 MB MALL)."""
@@ -97,6 +105,7 @@ def main():
     ap.add_argument("--out", default=tuning._PATH)
     ap.add_argument("--log", default="gpurun_out/tune_gemv.log")
     ap.add_argument("--only", default="", help="comma list of shape names (qkv,qkv6,o,gateup,down,down6,lm_head)")
+    ap.add_argument("--dense", action="store_true", help="tune mode 4 (dense f16) at M > 64")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     spec = SPECS[args.model]
@@ -126,6 +135,11 @@ def main():
                 w = s_new.w
                 w.__dict__.update(s_old.w.__dict__)
                 w.data = s_old.w.data.clone()
+        if args.dense:
+            for cp in copies:
+                for s_ in cp:
+                    s_.w.d16 = None
+                    s_.w.expand_dense()
         ncol = col // 2 if epi == "swiglu" else col
         mmax = max(64, max(Ms))
         x = torch.randn(mmax, K, device=dev).to(ops.ACT_DTYPE)
@@ -133,6 +147,24 @@ def main():
         keys = torch.zeros(mmax, dtype=torch.int64, device=dev)
         for M in Ms:
             res = []
+            if args.dense:
+                qcfg = tuning.select(segs, M)
+                qus = time_cfg(copies, x, y, M, epi, keys, tuple(qcfg))
+                for cfg in dense_configs(K):
+                    us = time_cfg(copies, x, y, M, epi, keys, cfg)
+                    if us is not None:
+                        res.append((us, cfg))
+                res.sort()
+                best_us, best = res[0]
+                table[tuning.dense_key(segs, M)] = list(best)
+                tf = 2.0 * M * col * K
+                line = (f"{name:8s} M={M:4d} quant {tuple(qcfg)} {qus:8.2f}us {tf / qus / 1e6:7.1f} TF | dense best={best} "
+                        f"{best_us:8.2f}us {tf / best_us / 1e6:7.1f} TF x{qus / best_us:4.2f} | "
+                        + " ".join(f"{c}:{u:.1f}" for u, c in res[:4]))
+                print(line, flush=True)
+                log.write(line + "\n")
+                log.flush()
+                continue
             for cfg in configs(K, M, all(int(t) in (8, 12, 13, 14) for t, _ in segdef)):
                 us = time_cfg(copies, x, y, M, epi, keys, cfg)
                 if us is not None:
