@@ -24,7 +24,8 @@ from nats_llm_studio_amd.ops import tuning
 pytestmark = pytest.mark.gpu
 
 _TABLE = json.load(open(tuning._PATH))
-_SHAPES = sorted({k.rsplit(":", 1)[0] for k in _TABLE})
+_SHAPES = sorted({k.rsplit(":", 1)[0] for k in _TABLE if not k.startswith("d:")})
+_DENSE = sorted({k.rsplit(":", 1)[0] for k in _TABLE if k.startswith("d:")})
 
 
 def _weights(types, rows, K, dev, rng):
@@ -68,6 +69,35 @@ def test_tuning_table_entries_at_real_shapes(gpu, shape):
         scale = ref.abs().max().item()
         assert err <= 2e-2 * scale, f"{shape} M={M} cfg={cfg}: err {err:.4g} vs {scale:.4g}"
         assert not torch.isnan(y[:M]).any(), f"{shape} M={M} cfg={cfg}: unwritten outputs"
+
+
+@pytest.mark.parametrize("shape", _DENSE)
+def test_dense_tuning_entries_at_real_shapes(gpu, shape):
+    """Every dense f16 GEMM entry (modes 4/5, "d:<rows>:<K>:<M>") at its real shape and M bucket."""
+    _, rows_s, K_s = shape.split(":")
+    rows, K = int(rows_s), int(K_s)
+    rng = np.random.default_rng(abs(hash(shape)) % (1 << 31))
+    segs, Wd = _weights([12], rows, K, gpu, rng)
+    segs[0].w.expand_dense()
+    sample = torch.from_numpy(np.sort(rng.choice(rows, size=min(rows, 512), replace=False))).to(gpu)
+    Ws = Wd.index_select(0, sample).float()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    for k, cfg in sorted(_TABLE.items()):
+        if not k.startswith(shape + ":"):
+            continue
+        M = int(k.rsplit(":", 1)[1])
+        mode, waves, rt, ks = cfg
+        x = (torch.randn(M, K, generator=g) * 0.5).to(ops.ACT_DTYPE).to(gpu)
+        y = torch.full((M, rows), float("nan"), device=gpu)
+        ops.qgemv(segs, x, y, M, mode=mode, waves=waves, rt=rt, ks=ks)
+        ref = x.float() @ Ws.t()
+        got = y.index_select(1, sample)
+        err = (got - ref).abs().max().item()
+        assert err <= 2e-2 * ref.abs().max().item(), f"{k} cfg={cfg}: err {err:.4g}"
+        assert not torch.isnan(y).any(), f"{k} cfg={cfg}: unwritten outputs"
+        del x, y
+    del segs, Wd
+    torch.cuda.empty_cache()
 
 
 @pytest.fixture(scope="module")
