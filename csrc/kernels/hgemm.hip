@@ -36,24 +36,26 @@ using nls_dma::glds16;
 using nls_dma::lds_addr;
 using nls_dma::wait_vm_lgkm0;
 
-template <int WM, int BN>
+template <int WM, int BN, int NWV>
 struct HG {
+  static constexpr int NT = 64 * NWV;         // threads per workgroup (8 or 16 waves)
   static constexpr int BM = 64 * WM;          // activation rows per workgroup
-  static constexpr int WN = 8 / WM;           // waves along N
+  static constexpr int WN = NWV / WM;         // waves along N
   static constexpr int NTW = BN / 16 / WN;    // 16-row weight tiles per wave
   static constexpr int MTW = 4;               // 16-row activation tiles per wave
   static constexpr int XS = BM * 128;         // bytes of one activation stage [BM][64] f16
   static constexpr int WSB = BN * 128;        // bytes of one weight stage [BN][64] f16
   static constexpr int NSX = 3;               // activation ring depth
   static constexpr int NSW = (NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2;   // weight ring depth (LDS budget)
-  static constexpr int NX = BM / 64;          // activation DMA instructions per wave per stage
-  static constexpr int NW = BN / 64;          // weight DMA instructions per wave per stage
+  static constexpr int NX = BM / 8 / NWV;     // activation DMA instructions per wave per stage
+  static constexpr int NW = BN / 8 / NWV;     // weight DMA instructions per wave per stage
+  static_assert(NX >= 1 && NW >= 1 && NTW >= 1, "tile too small for the wave count");
   static constexpr size_t LDS = (size_t)NSX * XS + (size_t)NSW * WSB;
 };
 
-template <int WM, int BN>
+template <int WM, int BN, int NWV>
 DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
-  typedef HG<WM, BN> G;
+  typedef HG<WM, BN, NWV> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, NX = G::NX, NW = G::NW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -213,7 +215,7 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
     // max over the lane's weight rows, the 16 lanes of an activation row, then the waves through
     // LDS (free after the main loop): one global atomic per activation row per workgroup
     unsigned long long* red = reinterpret_cast<unsigned long long*>(lds);
-    for (int idx = threadIdx.x; idx < G::BM; idx += 512) red[idx] = 0ull;
+    for (int idx = threadIdx.x; idx < G::BM; idx += G::NT) red[idx] = 0ull;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
@@ -234,15 +236,15 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
         if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
       }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < M; idx += 512) atomicMax(a.argmax + idx, red[idx]);
+    for (int idx = threadIdx.x; idx < M; idx += G::NT) atomicMax(a.argmax + idx, red[idx]);
   }
 }
 
-template <int WM, int BN>
-__global__ __launch_bounds__(512, 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+template <int WM, int BN, int NWV>
+__global__ __launch_bounds__(64 * NWV, 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                        int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
-  constexpr int BM = HG<WM, BN>::BM;
+  constexpr int BM = HG<WM, BN, NWV>::BM;
   // (tile, m-block, k-slice) with all m-blocks and k-slices of a tile on one XCD
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
   const int kslice = j % ks;
@@ -260,32 +262,35 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(SegList segs, GemvArgs a,
 #pragma unroll
   for (int s = 1; s < 8; ++s)
     if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
-  hgemm_tile<WM, BN>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds);
+  hgemm_tile<WM, BN, NWV>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds);
 }
 
-template <int WM, int BN>
+template <int WM, int BN, int NWV>
 int launch_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  typedef HG<WM, BN> G;
+  typedef HG<WM, BN, NWV> G;
   const int nmb = (a.M + G::BM - 1) / G::BM;
   const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
-    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)G::LDS) != hipSuccess)
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL((hgemm_kernel<WM, BN>), dim3(grid), dim3(512), G::LDS, st, sl, a, ks, ws, ntiles, nmb);
+  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles, nmb);
   return (int)hipGetLastError();
 }
 
-// bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at wm 4)
-int launch_dense(int wm, int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
+// bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at
+// wm 4); waves: 8 (2 per SIMD, 64 x 16*bn/128 accumulator tile per wave) or 16 (4 per SIMD, half
+// the tile per wave: more waves to cover each other's LDS and barrier waits)
+int launch_dense(int wm, int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
                  hipStream_t st) {
-  if (bn == 128 && wm == 4) return launch_t<4, 128>(sl, ntiles, ks, ws, a, st);
-  if (bn == 128 && wm == 2) return launch_t<2, 128>(sl, ntiles, ks, ws, a, st);
-  if (bn == 256 && wm == 4) return launch_t<4, 256>(sl, ntiles, ks, ws, a, st);
-  if (bn == 256 && wm == 2) return launch_t<2, 256>(sl, ntiles, ks, ws, a, st);
+#define NLS_HG(W, B, V) \
+  if (wm == W && bn == B && waves == V) return launch_t<W, B, V>(sl, ntiles, ks, ws, a, st);
+  NLS_HG(4, 128, 8) NLS_HG(2, 128, 8) NLS_HG(4, 256, 8) NLS_HG(2, 256, 8)
+  NLS_HG(4, 128, 16) NLS_HG(2, 128, 16) NLS_HG(4, 256, 16) NLS_HG(2, 256, 16)
+#undef NLS_HG
   return -1;
 }
 

@@ -6,7 +6,7 @@
 using namespace nls_gemv;
 
 namespace nls_hgemm {
-int launch_dense(int wm, int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
+int launch_dense(int wm, int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
                  hipStream_t st);
 }
 
@@ -63,9 +63,9 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (fz->onw && (mode != 0 || epi != EPI_ADD_F32 || nseg != 1 || segs[0].ycol || segs[0].xmap || segs[0].ymap ||
                   segs[0].mcount || !fz->cnt || !fz->hout || segs[0].rows % 4 || argmax))
     return -1;
-  if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8)) return -1;
+  if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
   if (mode == 4 || mode == 5) {
-    if (waves != 8 || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
+    if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount) return -1;
   } else if (mode == 3) {
@@ -154,7 +154,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     if (ks < 1) ks = 1;
     int rc;
     if (mode >= 4)
-      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, sl, tiles, ks, (float*)ws, a, st);
+      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 3)
       rc = (kset == 0 ? nls_dma::launch_dma_k0 : nls_dma::launch_dma_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 2)

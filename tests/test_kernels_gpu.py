@@ -660,9 +660,10 @@ def test_qgemv_fused_rmsnorm(gpu, t, M, epi):
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
 @pytest.mark.parametrize("M", [65, 128, 300, 520])
-@pytest.mark.parametrize("mode,wm,ks", [(4, 4, 1), (4, 2, 1), (4, 4, 3), (4, 2, 5), (5, 4, 1), (5, 2, 1), (5, 4, 3),
-                                        (5, 2, 2)])
-def test_hgemm_dense(gpu, t, M, mode, wm, ks):
+@pytest.mark.parametrize("mode,wm,ks,wv", [(4, 4, 1, 8), (4, 2, 1, 8), (4, 4, 3, 8), (4, 2, 5, 8), (5, 4, 1, 8),
+                                           (5, 2, 1, 8), (5, 4, 3, 8), (5, 2, 2, 8), (4, 4, 2, 16), (4, 2, 1, 16),
+                                           (5, 4, 1, 16), (5, 2, 3, 16)])
+def test_hgemm_dense(gpu, t, M, mode, wm, ks, wv):
     """Dense f16 GEMM (mode 4) on the weights' f16 copy: both operands by LDS-DMA into a 3-deep ring;
     partial last 128-row weight tile and activation block, K slices of 2..12 steps; store, add, argmax."""
     rows, K = 264, 768
@@ -672,7 +673,7 @@ def test_hgemm_dense(gpu, t, M, mode, wm, ks):
     pad = x.shape[0]
     y = torch.zeros(pad, rows, device=gpu)
     keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, mode=mode, waves=8, rt=wm, ks=ks, argmax=keys)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=mode, waves=wv, rt=wm, ks=ks, argmax=keys)
     ref = x[:M].float().cpu() @ Wd.t()
     _close(y[:M], ref)
     assert float(y[M:].abs().max().cpu()) == 0.0 if M < pad else True
@@ -681,7 +682,7 @@ def test_hgemm_dense(gpu, t, M, mode, wm, ks):
     assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
     base = torch.randn(pad, rows, device=gpu)
     y2 = base.clone()
-    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=mode, waves=8, rt=wm, ks=ks)
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=mode, waves=wv, rt=wm, ks=ks)
     _close(y2[:M], base[:M].cpu() + 0.5 * ref)
     # the same launch through the quantised LDS GEMM agrees to accumulation order
     y3 = torch.zeros(pad, rows, device=gpu)
@@ -689,8 +690,8 @@ def test_hgemm_dense(gpu, t, M, mode, wm, ks):
     _close(y3[:M], y[:M], 1e-3)
 
 
-@pytest.mark.parametrize("mode,ks", [(4, 1), (4, 2), (5, 1), (5, 2)])
-def test_hgemm_dense_swiglu_multiseg_auto(gpu, mode, ks):
+@pytest.mark.parametrize("mode,ks,wv", [(4, 1, 8), (4, 2, 8), (5, 1, 8), (5, 2, 8), (5, 1, 16), (4, 2, 16)])
+def test_hgemm_dense_swiglu_multiseg_auto(gpu, mode, ks, wv):
     """Mode 4 with the SwiGLU epilogue and a Q|K|V-style multi-segment launch; then the automatic
     selection (gemv_config) picks mode 4 exactly when every segment carries an f16 copy and M is large."""
     K, F = 512, 256
@@ -704,7 +705,7 @@ def test_hgemm_dense_swiglu_multiseg_auto(gpu, mode, ks):
     M = 333
     x = _x(M, K, gpu)
     y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=mode, waves=8, rt=4, ks=ks)
+    ops.qgemv([ops.Seg(w)], x, y, M, epi="swiglu", mode=mode, waves=wv, rt=4, ks=ks)
     xf = x[:M].float().cpu()
     _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
     a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
@@ -716,7 +717,7 @@ def test_hgemm_dense_swiglu_multiseg_auto(gpu, mode, ks):
         q.expand_dense()
     assert ops.gemv_config(segs, M)[0] in (4, 5) and ops.gemv_config(segs, 8)[0] not in (4, 5)
     yq = torch.zeros(x.shape[0], 512, device=gpu)
-    ops.qgemv(segs, x, yq, M, mode=mode, waves=8, rt=4, ks=ks)
+    ops.qgemv(segs, x, yq, M, mode=mode, waves=wv, rt=4, ks=ks)
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
     yq.zero_()
     ops.qgemv(segs, x, yq, M)
