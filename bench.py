@@ -44,6 +44,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--concurrency", type=int, default=512, help="in-flight chat requests per model replica")
     ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--sample-frac", type=float, default=0.0,
+                    help="fraction of the requests decoded with temperature 0.7 / top-p 0.95 / top-k 40 (device sampler)")
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--ftype", default=None, help="default: Q5_K_M for mixtral, else Q4_K_M")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (divides --gpus)")
@@ -189,9 +191,15 @@ def run(args, world: int):
     eng.capture_all()
     rng = np.random.default_rng(rank)
     vocab = model.cfg.vocab
-    futs = [eng.submit(GenRequest(list(rng.integers(0, min(vocab, 100000), args.prompt_len)),
-                                  SamplingParams(max_tokens=gen_tokens, ignore_eos=True)))
-            for _ in range(B)]
+    nsamp = int(round(args.sample_frac * B))        # rows decoded with the reference payload's sampling
+
+    def params(i):
+        if i < nsamp:
+            return SamplingParams(max_tokens=gen_tokens, ignore_eos=True, temperature=0.7, top_p=0.95, top_k=40,
+                                  seed=i)
+        return SamplingParams(max_tokens=gen_tokens, ignore_eos=True)
+    futs = [eng.submit(GenRequest(list(rng.integers(0, min(vocab, 100000), args.prompt_len)), params(i)))
+            for i in range(B)]
     # prefill every request (not timed), then warm up the decode loop
     t0 = time.time()
     while any(s.n_prefilled < s.n_prompt for s in eng.running) or eng.waiting:
@@ -322,6 +330,7 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
             "concurrency_per_replica": B,
             "hipgraph": args.device == "cuda" and not args.no_graphs,
             "device": args.device,
+            "sampled_frac": args.sample_frac,
         },
         "p50_rtt_ms": (chat_rtt or {}).get("p50_ms", None if rtt is None else rtt.get("p50_ms")),
         "rtt_chat_model_engine": chat_rtt,

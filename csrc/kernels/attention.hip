@@ -23,6 +23,16 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// Keys per flash-decoding split. chunk > 0: fixed; chunk < 0: balanced over n_split with at least
+// -chunk keys; chunk == 0: balanced with at least 64 keys below 1024 of context and 128 above (batch-1
+// A/B, profiles/attn_split_policy_b1.txt: 64-key splits win on short contexts, where the split's
+// dependent K/V fetch chain dominates; 128-key splits at 1K-4K, where the merge of many partials does)
+__device__ __forceinline__ int split_chunk(int chunk, int ctx, int n_split, int bs) {
+  if (chunk > 0) return chunk;
+  const int mn = chunk ? -chunk : (ctx >= 1024 ? 128 : 64);
+  return max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
+}
+
 template <int D, int G>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const __bf16* __restrict__ q, long ldq, const __bf16* __restrict__ kc, const __bf16* __restrict__ vc,
@@ -40,11 +50,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int Hq = Hkv * G;
 
   const int ctx = ctx_len[t];
-  // chunk > 0: fixed; chunk <= 0: balanced over n_split with a minimum of (chunk ? -chunk : 64) keys
-  if (chunk <= 0) {
-    const int mn = chunk ? -chunk : 64;
-    chunk = max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
-  }
+  chunk = split_chunk(chunk, ctx, n_split, bs);
   const int start = split * chunk;
   if (n_split > 1 && start >= ctx && ctx > 0) return;       // inactive split: combine skips it
   const int end = min(ctx, start + chunk);
@@ -247,10 +253,7 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
                                     act_t* __restrict__ out, long ldo) {
   const int t = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
   const int ctx = ctx_len[t];
-  if (chunk <= 0) {
-    const int mn = chunk ? -chunk : 64;
-    chunk = max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
-  }
+  chunk = split_chunk(chunk, ctx, n_split, bs);
   const int na = min(n_split, (ctx + chunk - 1) / chunk);   // active splits (others never wrote)
   const size_t pb = ((size_t)t * Hq + h) * n_split;
   float M = -INFINITY;

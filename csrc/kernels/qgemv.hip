@@ -28,6 +28,7 @@ struct NlsFuse {
   const int* pos; const int* slot; const float* cs; const float* bias;      // EPI_ROPE
   void* q_out; long ldq; void* kc; void* vc; int Hq, Hkv, D, pad0;
   void* hout; long ldh; const float* onw; int* cnt;                          // residual add + RMSNorm
+  float* ssq_out; const float* ssq_in; int ldss, nss_in;                     // split RMSNorm (GemvArgs)
 };
 
 // mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
@@ -48,7 +49,14 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   static const NlsFuse none{};
   if (!fz) fz = &none;
   const float* xf = fz->xf;
-  if (xf && (mode != 0 || M > 16 || !fz->nw)) return -1;
+  if (xf && (M > 16 || !fz->nw || (mode != 0 && !(mode == 1 && fz->ssq_in)))) return -1;
+  if (fz->ssq_in && (!xf || fz->nss_in < 1 || fz->nss_in > fz->ldss)) return -1;
+  if (fz->ssq_out) {      // producer of a split RMSNorm: path A residual add, whole tiles of tokens
+    const int ncols = ((M + 15) / 16) * 16;
+    if (mode != 0 || epi != EPI_ADD_F32 || nseg != 1 || segs[0].xmap || segs[0].ymap || segs[0].mcount || argmax ||
+        fz->onw || M > 32 || (waves * 64) % ncols || fz->ldss < (segs[0].rows + 16 * rt - 1) / (16 * rt))
+      return -1;
+  }
   if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A, plain rows, contiguous Q|K|V segments
     if (mode != 0 || argmax || !fz->pos || !fz->slot || !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 ||
         fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
@@ -142,6 +150,10 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   a.ldh = fz->ldh;
   a.onw = fz->onw;
   a.cnt = fz->cnt;
+  a.ssq_out = fz->ssq_out;
+  a.ssq_in = fz->ssq_in;
+  a.ldss = fz->ldss;
+  a.nss_in = fz->nss_in;
   const int mt = M > 64 ? 8 : (M + 15) / 16;
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;

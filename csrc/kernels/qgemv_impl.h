@@ -55,7 +55,27 @@ struct GemvArgs {
   // EPI_ADD_F32 + onw: after the residual update the LAST workgroup to finish (agent-scope ticket
   // `cnt`, zero between launches) normalises the updated rows: hout = f16(rmsnorm(y) * onw)
   act_t* hout; long ldh; const float* onw; int* cnt;
+  // RMSNorm split across a producer / consumer pair (no norm launch, no full-row reduction pass):
+  // an EPI_ADD_F32 path-A launch writes, per token m, its workgroup's share of sum(x^2) over the
+  // rows it updated to ssq_out[m * ldss + blockIdx.x]; a consumer with xf / nw sums the nss_in
+  // shares of ssq_in (fixed order: deterministic) to get the row's inverse RMS.
+  float* ssq_out; const float* ssq_in; int ldss, nss_in;
 };
+
+// inv[m] = 1 / rms of rows m < M from producer partial sums of squares (see GemvArgs::ssq_in); one
+// wave per row, lanes sum the shares in a fixed order; ends with a workgroup barrier
+template <int NT>
+DEVI void ssq_inv(const float* ssq, int ldss, int n, int M, int K, float eps, float* inv) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int m = wave; m < M; m += NT / 64) {
+    float s = 0.f;
+    for (int j = lane; j < n; j += 64) s += ssq[(size_t)m * ldss + j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) inv[m] = rsqrtf(s / (float)K + eps);
+  }
+  __syncthreads();
+}
 
 // Workgroup ticket: true in exactly one workgroup, the last of `n` to arrive, after which every
 // global store of the others is visible to it (cdna_hip_programming.md Guideline 16: each wave drains
@@ -185,22 +205,28 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
       // that consumes it: every workgroup normalises the few rows itself, reading them from L2)
       const int K = S.K;
       typedef act_t act4 __attribute__((ext_vector_type(4)));
+      if (a.ssq_in) ssq_inv<WAVES * 64>(a.ssq_in, a.ldss, a.nss_in, mcount, K, a.eps, lds + 64);
       for (int m = 0; m < mcount; ++m) {
         const float* xrow = a.xf + (size_t)m * a.ldxf;
-        float ss = 0.f;
-        for (int i = threadIdx.x * 4; i < K; i += WAVES * 256) {
-          const float4 v = *reinterpret_cast<const float4*>(xrow + i);
-          ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        float inv;
+        if (a.ssq_in) {
+          inv = lds[64 + m];
+        } else {
+          float ss = 0.f;
+          for (int i = threadIdx.x * 4; i < K; i += WAVES * 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xrow + i);
+            ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+          if (lane == 0) lds[wave] = ss;
+          __syncthreads();
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) tot += lds[w];
+          __syncthreads();
+          inv = rsqrtf(tot / (float)K + a.eps);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-        if (lane == 0) lds[wave] = ss;
-        __syncthreads();
-        float tot = 0.f;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) tot += lds[w];
-        __syncthreads();
-        const float inv = rsqrtf(tot / (float)K + a.eps);
         for (int i = threadIdx.x * 4; i < K; i += WAVES * 256) {
           const float4 v = *reinterpret_cast<const float4*>(xrow + i);
           const float4 w = *reinterpret_cast<const float4*>(a.nw + i);
@@ -354,6 +380,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     }
     return;
   }
+  float sq = 0.f;        // ssq_out: this thread's share of sum(x^2); its token bb = threadIdx.x % ncols
   for (int e = threadIdx.x; e < RT * 16 * ncols; e += WAVES * 64) {
     const int bb = e % ncols, rr = e / ncols;
     const int row = row0 + rr;
@@ -361,9 +388,28 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     const float v = tile[rr * ncols + bb];
     const int yrow = S.ymap ? S.ymap[bb] : bb;
     const size_t off = (size_t)yrow * a.ldy + S.ycol + row;
-    if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
-    else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-    else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
+    if (a.epi == EPI_F32) {
+      reinterpret_cast<float*>(a.y)[off] = v;
+    } else if (a.epi == EPI_ADD_F32) {
+      float* p = reinterpret_cast<float*>(a.y) + off;
+      const float nv = *p + v;
+      *p = nv;
+      sq += nv * nv;
+    } else if (a.epi == EPI_ACT) {
+      reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
+    }
+  }
+  if (a.ssq_out) {
+    // per-token share of sum(x^2) over this workgroup's rows -> slot blockIdx.x (the host checks
+    // (WAVES * 64) % ncols == 0, so a thread's elements all belong to one token)
+    __syncthreads();                       // the tile reads above are done: reuse the reduce area
+    lds[threadIdx.x] = sq;
+    __syncthreads();
+    if (threadIdx.x < min(mcount, ncols)) {
+      float t = 0.f;
+      for (int j = threadIdx.x; j < WAVES * 64; j += ncols) t += lds[j];
+      a.ssq_out[(size_t)threadIdx.x * a.ldss + blockIdx.x] = t;
+    }
   }
   if (a.onw) {
     // residual + RMSNorm fusion: the next layer's input norm runs in the last workgroup
@@ -481,10 +527,29 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     }
     // x slice -> LDS [sb - sb0][M][256] (XOR-swizzled 16-B chunks)
     const int kc = (sb1 - sb0) * 32;
-    for (int i = threadIdx.x; i < M * kc; i += NT) {
-      const int row = i / kc, c = i - row * kc;
-      *reinterpret_cast<u32x4*>(lds + (size_t)(c >> 5) * M * 256 + lds_off(row, (c & 31) * 8)) =
-          ld16(a.x + (size_t)row * a.ldx + (size_t)sb0 * 256 + c * 8);
+    if (a.xf) {
+      // fused input RMSNorm from the producer's partial sums of squares (the slice may be a
+      // split-K part of the row; the norm needs the whole row: launch_b requires ssq_in here)
+      float* inv = reinterpret_cast<float*>(lds + (size_t)M * kc * 8);
+      ssq_inv<NT>(a.ssq_in, a.ldss, a.nss_in, M, S.K, a.eps, inv);
+      typedef act_t act8 __attribute__((ext_vector_type(8)));
+      for (int i = threadIdx.x; i < M * kc; i += NT) {
+        const int row = i / kc, c = i - row * kc;
+        const size_t k0 = (size_t)sb0 * 256 + c * 8;
+        const float* xp = a.xf + (size_t)row * a.ldxf + k0;
+        const float4 v0 = *reinterpret_cast<const float4*>(xp), v1 = *reinterpret_cast<const float4*>(xp + 4);
+        const float4 w0 = *reinterpret_cast<const float4*>(a.nw + k0), w1 = *reinterpret_cast<const float4*>(a.nw + k0 + 4);
+        const float s = inv[row];
+        *reinterpret_cast<act8*>(lds + (size_t)(c >> 5) * M * 256 + lds_off(row, (c & 31) * 8)) =
+            act8{(act_t)(v0.x * s * w0.x), (act_t)(v0.y * s * w0.y), (act_t)(v0.z * s * w0.z), (act_t)(v0.w * s * w0.w),
+                 (act_t)(v1.x * s * w1.x), (act_t)(v1.y * s * w1.y), (act_t)(v1.z * s * w1.z), (act_t)(v1.w * s * w1.w)};
+      }
+    } else {
+      for (int i = threadIdx.x; i < M * kc; i += NT) {
+        const int row = i / kc, c = i - row * kc;
+        *reinterpret_cast<u32x4*>(lds + (size_t)(c >> 5) * M * 256 + lds_off(row, (c & 31) * 8)) =
+            ld16(a.x + (size_t)row * a.ldx + (size_t)sb0 * 256 + c * 8);
+      }
     }
     __syncthreads();
     const int xrow = min(r, M - 1);      // rows >= M feed outputs that are never stored
@@ -766,6 +831,7 @@ static __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks
   const int b = blockIdx.y;
   const bool swiglu = a.epi == EPI_SWIGLU;
   const int nout = swiglu ? ntot / 2 : ntot;
+  unsigned long long best = 0ull;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nout; j += gridDim.x * blockDim.x) {
     int col = swiglu ? (j >> 3) * 16 + (j & 7) : j;
     RedSeg S = rl.s[0];
@@ -788,7 +854,27 @@ static __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int ks
     if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
     else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
     else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
-    if (a.argmax) atomicMax(a.argmax + b, argmax_key(v, S.ycol + row));
+    if (a.argmax) {
+      const unsigned long long k = argmax_key(v, S.ycol + row);
+      best = k > best ? k : best;
+    }
+  }
+  if (a.argmax) {
+    // one atomic per workgroup and row (a per-element atomicMax on the one key of a row serialises
+    // ~128K updates for an lm_head: 27 us of a 2.2 ms batch-1 step)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long ok = __shfl_xor(best, o, 64);
+      best = ok > best ? ok : best;
+    }
+    __shared__ unsigned long long red[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+      if (best) atomicMax(a.argmax + b, best);
+    }
   }
 }
 
@@ -836,11 +922,13 @@ int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a
     }
     const size_t xbytes = (size_t)a.M * (((kmax >> 8) + ks - 1) / ks) * 256 * sizeof(act_t);
     if (nmb == 1 && !mapped && xbytes <= XL_LDS_BYTES) {
-      hipLaunchKernelGGL((qmm_kernel<WAVES, RT, 1, KSET, true>), dim3(grid), dim3(WAVES * 64), max(xbytes, lds), st,
+      const size_t need = a.xf ? xbytes + 64 * sizeof(float) : xbytes;     // + inv-rms scratch
+      hipLaunchKernelGGL((qmm_kernel<WAVES, RT, 1, KSET, true>), dim3(grid), dim3(WAVES * 64), max(need, lds), st,
                          sl, a, ks, ws, ntiles, nmb);
       return (int)hipGetLastError();
     }
   }
+  if (a.xf) return -1;          // fused input norm: the staged (XL) path only
   hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, KSET>), dim3(grid), dim3(WAVES * 64), lds, st, sl, a, ks, ws,
                      ntiles, nmb);
   return (int)hipGetLastError();

@@ -180,6 +180,7 @@ class _Seq:
         self.n_fed = 0         # positions whose KV is written or being written
         self.keys: List[bytes] = []   # prefix-cache chain digests of the full prompt blocks
         self.n_cached = 0      # prompt tokens whose KV came from the prefix cache
+        self.text_cache = None  # [StreamDecoder, text] of the generation (stop-string checks)
 
     @property
     def generated(self) -> List[int]:
@@ -805,9 +806,23 @@ class Engine:
             self._finish(s, "length", "contextLengthReached")
 
     def _stop_string(self, s: _Seq) -> bool:
-        text = self.tok.decode(s.generated)
+        """Incremental: the generated text grows by the stream decoder's delta and only its tail that a
+        new occurrence could overlap is searched (decoding the whole generation every step is O(n^2)
+        host work per request, paid on the engine thread)."""
+        if s.text_cache is None:
+            from ..tokenizer.bpe import StreamDecoder
+            sd = StreamDecoder(self.tok)
+            for t in s.generated[:-1]:
+                sd.push(t)
+            s.text_cache = [sd, ""]
+        sd, text = s.text_cache
+        delta = sd.push(s.tokens[-1])
+        if not delta:
+            return False
+        text += delta
+        s.text_cache[1] = text
         for st in s.req.params.stop:
-            if st and st in text:
+            if st and st in text[-(len(st) + len(delta)):]:
                 return True
         return False
 

@@ -31,6 +31,9 @@ from .config import ModelConfig
 
 _SPLIT_CAP = int(os.environ.get("NLS_ATTN_SPLIT_CAP", "32"))     # flash-decoding splits per (token, kv head)
 _SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgroups of a decode attention launch
+# fewest keys per flash-decoding split (0: the kernel's context-adaptive policy, attention.hip
+# split_chunk: 64 keys below 1K of context, 128 above)
+_MIN_CHUNK = int(os.environ.get("NLS_ATTN_MIN_CHUNK", "0"))
 
 
 @dataclass
@@ -100,15 +103,19 @@ class StepBuffers:
     attn_cnt: Optional[torch.Tensor] = None    # int32 [pad*Hkv] split-merge tickets (zero between launches)
     part: Optional[torch.Tensor] = None        # f32 [pad, d] row-parallel partial sums (TP fused all-reduce)
     cnt: Optional[torch.Tensor] = None         # int32 tickets of the last-workgroup residual+RMSNorm GEMVs
+    ssq: Optional[torch.Tensor] = None         # f32 [pad, ldss] split-RMSNorm partial sums of squares
+    ldss: int = 0
 
 
 class LlamaModel:
     def __init__(self, reader: GGUFReader, device="cpu", shard: ShardSpec = ShardSpec(), comm=None,
                  fuse_norm: Optional[bool] = None):
         self.reader = reader
-        # RMSNorm folded into the consuming GEMVs for few-row decode steps. Measured neutral on MI355X
-        # at batch 1 (2.31 vs 2.28 ms/token: the saved launches are paid back by every workgroup
-        # re-normalising its input rows), so opt-in: NLS_FUSE_NORM=1.
+        # RMSNorm folded into the consuming GEMVs for few-row decode steps, split between the O / down
+        # GEMVs (per-workgroup shares of sum(x^2)) and the consumers (no norm launch, no reduction pass).
+        # Measured neutral on MI355X at batch 1 (2.24 vs 2.22 ms/token, profiles/b1_split_rmsnorm_ab.txt):
+        # the 65 removed launches come back as latency on the producers' and consumers' critical paths,
+        # so opt-in: NLS_FUSE_NORM=1.
         self.fuse_norm = bool(int(os.environ.get("NLS_FUSE_NORM", "0"))) if fuse_norm is None else fuse_norm
         self.device = torch.device(device)
         self.cfg = cfg = ModelConfig.from_gguf(reader.metadata, reader.tensors.keys())
@@ -292,6 +299,8 @@ class LlamaModel:
         if self.shard.size > 1:
             b.part = torch.zeros(pad, cfg.d_model, dtype=torch.float32, device=dev)
         b.cnt = torch.zeros(16, dtype=torch.int32, device=dev)
+        b.ldss = (cfg.d_model + 15) // 16       # one share per 16-row path-A tile of an O / down GEMV
+        b.ssq = torch.zeros(pad * b.ldss, dtype=torch.float32, device=dev)
         b.slot.fill_(-1)
         if cfg.n_expert:
             E = cfg.n_expert
@@ -349,7 +358,7 @@ class LlamaModel:
                                       T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)
             else:
                 ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
-                              block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws,
+                              block_size, cfg.attn_softmax_scale, chunk=-_MIN_CHUNK, n_split=n_split, workspace=b.attn_ws,
                               counters=b.attn_cnt)
             if fused:
                 ops.qgemv_add_rmsnorm(Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps,
@@ -398,15 +407,23 @@ class LlamaModel:
         cfg = self.cfg
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         x = b.x
+        # split RMSNorm: each O / down launch leaves per-workgroup shares of sum(x^2) in b.ssq and the
+        # consuming GEMV sums them instead of re-reading the whole row (ops.qgemv_add_ssq)
+        ssq, ldss = b.ssq, b.ldss
+
+        def nrm(w, parts):
+            return (x, w, cfg.eps, ssq if parts else None, ldss, parts or 0)
+
+        parts = None
         for L, lw in enumerate(self.layers):
             ops.qkv_rope_kv(lw.qkv, b.h, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
-                            cfg.rope_neox, bias=lw.qkv_bias, norm=(x, lw.attn_norm, cfg.eps))
+                            cfg.rope_neox, bias=lw.qkv_bias, norm=nrm(lw.attn_norm, parts))
             ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
-                          block_size, cfg.attn_softmax_scale, chunk=0, n_split=n_split, workspace=b.attn_ws,
+                          block_size, cfg.attn_softmax_scale, chunk=-_MIN_CHUNK, n_split=n_split, workspace=b.attn_ws,
                           counters=b.attn_cnt)
-            ops.qgemv([Seg(lw.wo)], b.ao, x, T, alpha=cfg.residual_scale, epi="add")
-            ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu", norm=(x, lw.ffn_norm, cfg.eps))
-            ops.qgemv([Seg(lw.down)], b.act, x, T, alpha=cfg.residual_scale, epi="add")
+            parts = ops.qgemv_add_ssq(Seg(lw.wo), b.ao, x, T, cfg.residual_scale, ssq, ldss)
+            ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu", norm=nrm(lw.ffn_norm, parts))
+            parts = ops.qgemv_add_ssq(Seg(lw.down), b.act, x, T, cfg.residual_scale, ssq, ldss)
         n = T
         if logit_rows is not None:             # (prefill-style row pick: normalise, then gather)
             ops.rmsnorm(x, self.out_norm, b.h, T, cfg.eps)
@@ -419,7 +436,7 @@ class LlamaModel:
         else:
             ops.argmax_reset(b.keys)
             ops.qgemv([Seg(self.lm_head, 0)], b.h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
-                      epi="f32" if need_logits else "argmax", norm=(x, self.out_norm, cfg.eps))
+                      epi="f32" if need_logits else "argmax", norm=nrm(self.out_norm, parts))
         ops.argmax_unpack(b.keys, n, b.next_ids)
         return n
 

@@ -246,10 +246,33 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
           argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1,
           norm=None):
     """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K].
-    norm = (xf f32 [M, K], w f32 [K], eps): the GEMV input is f16(rmsnorm(xf) * w), computed inside the
-    kernel (batch <= a few rows; `x` is then ignored on the GPU)."""
+    norm = (xf f32 [M, K], w f32 [K], eps[, ssq, ldss, nparts]): the GEMV input is f16(rmsnorm(xf) * w),
+    computed inside the kernel (batch <= a few rows; `x` is then ignored on the GPU). With the partial
+    sums of squares a qgemv_add_ssq producer left in `ssq`, the kernel skips the reduction pass and the
+    tuned path-B (XL) config stays usable."""
+    if norm is not None and x.is_cuda and len(norm) == 6 and norm[3] is not None:
+        xf, nw, eps, ssq, ldss, nparts = norm
+        if any(s.xmap is not None for s in segs) or M > 16:
+            raise ValueError("fused-norm GEMV needs unmapped rows and M <= 16")
+        cfg = gemv_config(segs, M)
+        fz = _lib.NlsFuse(xf=xf.data_ptr(), ldxf=xf.stride(0), nw=nw.data_ptr(), eps=float(eps),
+                          ssq_in=ssq.data_ptr(), ldss=int(ldss), nss_in=int(nparts))
+        cands = [cfg] if cfg[0] in (0, 1) else []
+        cands.append((0, 4, 2, 1))
+        for mode, waves, rt, ks in cands:
+            ws = None
+            if mode == 1 and ks > 1:
+                ws = _workspace(x.device, ks * M * sum(s.w.rows for s in segs)).data_ptr()
+            rc = _lib.lib().nls_qgemv_ex(_segs(segs), len(segs), xf.data_ptr(), xf.stride(0), y.data_ptr(),
+                                         y.stride(0), M, float(alpha), EPI[epi], _p(argmax), waves, rt, mode, ks, ws,
+                                         _stream_ptr(xf), ctypes.byref(fz))
+            if rc == 0:
+                return y
+            if rc != -1:
+                _lib.check(rc, "nls_qgemv_ex(norm)")
+        raise ValueError("no launch config takes the split-RMSNorm operands")
     if norm is not None and x.is_cuda:
-        xf, nw, eps = norm
+        xf, nw, eps = norm[:3]
         if any(s.xmap is not None for s in segs) or not norm_fusable(M, segs[0].w.K):
             raise ValueError("fused-norm GEMV needs unmapped rows and M*K*2 <= NORM_FUSE_LDS")
         mode, waves, rt, ks = gemv_config(segs, M)
@@ -263,7 +286,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
                                              rt, _stream_ptr(xf)), "nls_qgemv_norm")
         return y
     if norm is not None:
-        xf, nw, eps = norm
+        xf, nw, eps = norm[:3]
         xs = xf[:M].float()
         x = (xs * torch.rsqrt(xs.pow(2).mean(dim=1, keepdim=True) + eps) * nw.float()).to(ACT_DTYPE)
     if x.is_cuda:
@@ -319,6 +342,28 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
             key = _argmax_keys(v, idx + s.ycol)
             argmax[yi] = torch.maximum(argmax[yi], key)
     return y
+
+
+def qgemv_add_ssq(seg: Seg, xin: torch.Tensor, x: torch.Tensor, M: int, alpha: float, ssq: torch.Tensor,
+                  ldss: int, cfg=None) -> Optional[int]:
+    """x[:M] += alpha * xin @ W^T, and when the launch runs on path A, each workgroup also leaves its
+    share of sum(x_new^2) per token in ssq[m * ldss + wg] for the next fused-norm GEMV (split RMSNorm:
+    no norm launch, no reduction pass in the consumer). Returns the number of shares, or None when
+    this launch cannot produce them (the consumer then normalises from the full rows)."""
+    if x.is_cuda and seg.xmap is None and M <= 32:
+        mode, waves, rt, ks = cfg or gemv_config([seg], M)
+        ntile = -(-seg.w.rows // (16 * rt))
+        if mode == 0 and ntile <= ldss:
+            fz = _lib.NlsFuse(ssq_out=ssq.data_ptr(), ldss=int(ldss))
+            rc = _lib.lib().nls_qgemv_ex(_segs([seg]), 1, xin.data_ptr(), xin.stride(0), x.data_ptr(), x.stride(0), M,
+                                         float(alpha), EPI["add"], None, waves, rt, 0, 1, None, _stream_ptr(x),
+                                         ctypes.byref(fz))
+            if rc == 0:
+                return ntile
+            if rc != -1:
+                _lib.check(rc, "nls_qgemv_ex(ssq)")
+    qgemv([seg], xin, x, M, alpha=alpha, epi="add")
+    return None
 
 
 def _segs(segs: Sequence[Seg]):
@@ -466,10 +511,12 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
                               q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
                               Hq=Hq, Hkv=Hkv, D=D)
             if norm is not None:
-                xf, nw, eps = norm
+                xf, nw, eps = norm[:3]
                 if not norm_fusable(T, segs[0].w.K):
                     raise ValueError("fused-norm GEMV needs M*K*2 <= NORM_FUSE_LDS")
                 fz.xf, fz.ldxf, fz.nw, fz.eps = xf.data_ptr(), xf.stride(0), nw.data_ptr(), float(eps)
+                if len(norm) == 6 and norm[3] is not None:
+                    fz.ssq_in, fz.ldss, fz.nss_in = norm[3].data_ptr(), int(norm[4]), int(norm[5])
             _lib.check(_lib.lib().nls_qgemv_ex(_segs(segs), len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(),
                                                qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt, 0, 1, None,
                                                _stream_ptr(h), ctypes.byref(fz)), "nls_qgemv_ex(rope)")

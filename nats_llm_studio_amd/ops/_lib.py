@@ -31,7 +31,8 @@ class NlsFuse(ctypes.Structure):
                 ("pos", c_void_p), ("slot", c_void_p), ("cs", c_void_p), ("bias", c_void_p),
                 ("q_out", c_void_p), ("ldq", c_long), ("kc", c_void_p), ("vc", c_void_p),
                 ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("pad0", c_int),
-                ("hout", c_void_p), ("ldh", c_long), ("onw", c_void_p), ("cnt", c_void_p)]
+                ("hout", c_void_p), ("ldh", c_long), ("onw", c_void_p), ("cnt", c_void_p),
+                ("ssq_out", c_void_p), ("ssq_in", c_void_p), ("ldss", c_int), ("nss_in", c_int)]
 
 
 _SIGS = {

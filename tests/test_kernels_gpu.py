@@ -1,4 +1,5 @@
 """HIP kernel numerics vs the fp32 PyTorch reference of the same op (MI355X only)."""
+import ctypes
 import math
 
 import numpy as np
@@ -739,3 +740,41 @@ def test_hgemm_dense_add_rmsnorm_slabs(gpu):
     _close(x[:M], ref)
     hn = ref * torch.rsqrt(ref.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu()
     _close(h[:M], hn, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 3, 16])
+def test_split_rmsnorm_producer_consumer(gpu, M):
+    """Split RMSNorm: a path-A residual-add GEMV leaves per-workgroup shares of sum(x^2); a fused-norm
+    consumer (path A, path B XL, path B XL split-K) sums them instead of re-reading the row."""
+    D, K2 = 1024, 512
+    wo, Wo = _qw(D, K2, GGMLType.Q4_K, gpu, 21)
+    xin = _x(M, K2, gpu, seed=5)
+    x = (torch.randn(xin.shape[0], D) * 0.7).to(gpu)
+    x0 = x.clone()
+    ldss = D // 16
+    ssq = torch.full((xin.shape[0] * ldss,), float("nan"), device=gpu)
+    parts = ops.qgemv_add_ssq(ops.Seg(wo), xin, x, M, 0.5, ssq, ldss, cfg=(0, 8, 1, 1))
+    assert parts == D // 16
+    ref = x0[:M].cpu() + 0.5 * (xin[:M].float().cpu() @ Wo.t())
+    _close(x[:M], ref)
+    tot = ssq.view(-1, ldss)[:M, :parts].double().sum(1).cpu()
+    assert torch.allclose(tot, ref.double().pow(2).sum(1), rtol=1e-4), (tot, ref.pow(2).sum(1))
+    nw = (torch.rand(D) + 0.5).to(gpu)
+    xn = ref * torch.rsqrt(ref.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu()
+    wc, Wc = _qw(768, D, GGMLType.Q4_K, gpu, 22)
+    want = xn @ Wc.t()
+    for cfg in [(0, 8, 1, 1), (0, 4, 2, 1), (1, 4, 2, 1), (1, 8, 1, 2)]:
+        y = torch.zeros(xin.shape[0], 768, device=gpu)
+        fz = ops._lib.NlsFuse(xf=x.data_ptr(), ldxf=x.stride(0), nw=nw.data_ptr(), eps=1e-5, ssq_in=ssq.data_ptr(),
+                              ldss=ldss, nss_in=parts)
+        mode, waves, rt, ks = cfg
+        ws = ops._workspace(gpu, ks * M * 768).data_ptr() if ks > 1 else None
+        rc = ops._lib.lib().nls_qgemv_ex(ops._segs([ops.Seg(wc)]), 1, x.data_ptr(), x.stride(0), y.data_ptr(),
+                                         y.stride(0), M, 1.0, ops.EPI["f32"], None, waves, rt, mode, ks, ws,
+                                         ops._stream_ptr(x), ctypes.byref(fz))
+        assert rc == 0, (cfg, rc)
+        _close(y[:M], want, 3e-2)
+    # the public entry: tuned config, partials tuple
+    y = torch.zeros(xin.shape[0], 768, device=gpu)
+    ops.qgemv([ops.Seg(wc)], x, y, M, norm=(x, nw, 1e-5, ssq, ldss, parts))
+    _close(y[:M], want, 3e-2)

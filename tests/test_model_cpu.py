@@ -56,3 +56,28 @@ def test_fused_norm_decode_matches_unfused(tiny_models):
             eng.step()
         outs.append([f.result().token_ids for f in futs])
     assert outs[0] == outs[1]
+
+
+def test_stop_strings_incremental(tiny_models):
+    """A stop string that appears mid-generation ends the request there (stopStringFound) and is cut
+    from the text; the check is incremental (stream decoder tail), not a re-decode per token."""
+    from nats_llm_studio_amd.engine.engine import Engine, GenRequest
+    from nats_llm_studio_amd.engine.sampling import SamplingParams
+    from nats_llm_studio_amd.tokenizer.bpe import tokenizer_from_metadata
+    r = GGUFReader(tiny_models["tiny-llama"])
+    tok = tokenizer_from_metadata(r.metadata)
+    m = LlamaModel(r, "cpu")
+    eng = Engine(m, tok, max_batch=2, num_blocks=32, use_graphs=False, ctx=256)
+    prompt = [1, 2, 3, 40]
+    full = eng.generate(prompt, SamplingParams(max_tokens=24, ignore_eos=True))
+    text = full.text
+    assert len(text) > 8
+    # a stop string taken from the middle of the generated text
+    cut = len(tok.decode(full.token_ids[:8]))
+    stop = text[cut:cut + 3]
+    assert stop and stop in text
+    first = text.find(stop)
+    res = eng.generate(prompt, SamplingParams(max_tokens=24, ignore_eos=True, stop=[stop]))
+    assert res.finish_reason == "stop" and res.stop_reason == "stopStringFound"
+    assert res.text == text[:first]
+    assert len(res.token_ids) < len(full.token_ids)

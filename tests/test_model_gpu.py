@@ -121,3 +121,26 @@ def test_device_sampling_in_graph(gpu, tiny_models):
     ban = SamplingParams(max_tokens=20, ignore_eos=True, temperature=1.0, top_k=1, presence_penalty=1e9)
     (t,), _ = run([ban])
     assert len(set(t)) == len(t) and not (set(t[1:]) & set(prompt)), t
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_split_rmsnorm_decode_matches_plain(gpu, tiny_models, graphs):
+    """Few-row decode with every RMSNorm split between the O/down GEMVs (shares of sum(x^2)) and the
+    consuming GEMVs == the plain path with norm launches, token for token."""
+    from nats_llm_studio_amd.engine.engine import Engine, GenRequest
+    from nats_llm_studio_amd.engine.sampling import SamplingParams
+    from nats_llm_studio_amd.gguf.reader import GGUFReader
+    from nats_llm_studio_amd.models.llama import LlamaModel
+    r = GGUFReader(tiny_models["tiny-llama"])
+    outs = []
+    for fuse in (False, True):
+        m = LlamaModel(r, gpu, fuse_norm=fuse)
+        eng = Engine(m, None, max_batch=4, num_blocks=64, use_graphs=graphs, ctx=256)
+        futs = [eng.submit(GenRequest([1, 2, 3, 40 + i], SamplingParams(max_tokens=12, ignore_eos=True)))
+                for i in range(3)]
+        while not all(f.done() for f in futs):
+            eng.step()
+        outs.append([f.result().token_ids for f in futs])
+        eng.shutdown()
+    agree = sum(int(a == b) for r0, r1 in zip(*outs) for a, b in zip(r0, r1))
+    assert outs[0][0][:4] == outs[1][0][:4] and agree >= 30, outs
