@@ -292,6 +292,61 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
   }
 }
 
+// combine + the next layer's input RMSNorm in one launch (single rank, few tokens): resid[t] +=
+// alpha * sum_j w[t,j] * y[t*k+j]; h[t] = f16(rmsnorm(resid[t]) * nw). One workgroup per token: every
+// load of a thread's 4-float groups is issued before any arithmetic (a loop that loads, adds and
+// stores per element serialises ~16 dependent round trips per thread: 13 us at batch 1).
+template <int KMAX>
+__global__ __launch_bounds__(256) void moe_combine_norm_kernel(const float* __restrict__ y, const float* __restrict__ w,
+                                                               int topk, float* __restrict__ resid, long ldr, int D,
+                                                               float alpha, const float* __restrict__ nw, float eps,
+                                                               act_t* __restrict__ h, long ldh) {
+  __shared__ float sh[8];
+  constexpr int NV = 4;                        // float4 groups per thread per pass (D <= 4096 in one pass)
+  const int t = blockIdx.x;
+  float* xr = resid + (size_t)t * ldr;
+  float wk[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) wk[j] = j < topk ? w[t * topk + j] * alpha : 0.f;
+  float ss = 0.f;
+  for (int base = threadIdx.x * 4; base < D; base += 256 * 4 * NV) {
+    float4 xv[NV], yv[KMAX][NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i = base + u * 1024;
+      xv[u] = i < D ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j)
+        yv[j][u] = (j < topk && i < D) ? *reinterpret_cast<const float4*>(y + ((size_t)t * topk + j) * D + i)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i = base + u * 1024;
+      float4 v = xv[u];
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        v.x += wk[j] * yv[j][u].x;
+        v.y += wk[j] * yv[j][u].y;
+        v.z += wk[j] * yv[j][u].z;
+        v.w += wk[j] * yv[j][u].w;
+      }
+      xv[u] = v;
+      if (i < D) *reinterpret_cast<float4*>(xr + i) = v;
+      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+  }
+  ss = block_sum<256>(ss, sh);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  typedef act_t act4 __attribute__((ext_vector_type(4)));
+  for (int i = threadIdx.x * 4; i < D; i += 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + i);
+    const float4 g = *reinterpret_cast<const float4*>(nw + i);
+    *reinterpret_cast<act4*>(h + (size_t)t * ldh + i) =
+        act4{(act_t)(v.x * inv * g.x), (act_t)(v.y * inv * g.y), (act_t)(v.z * inv * g.z), (act_t)(v.w * inv * g.w)};
+  }
+}
+
 // MoE router: softmax over E logits -> top-k (renormalised) -> per-expert row lists.
 // logits [T][E] f32; outputs: topw [T][k], counts [E] (must be zeroed), rows [E][T*k]
 // (segment-local x row = token t, y row = t*k + j).
@@ -302,9 +357,13 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
 __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k,
                                                         int renorm, float* __restrict__ topw,
                                                         int* __restrict__ counts, int* __restrict__ xrows,
-                                                        int* __restrict__ yrows, int cap) {
+                                                        int* __restrict__ yrows, int cap, int* __restrict__ sel) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gridDim.x == 1) {      // one workgroup (<= 4 tokens): zero the counts here (no host memset launch)
+    for (int e = threadIdx.x; e < E; e += 256) counts[e] = 0;
+    __syncthreads();
+  }
   if (t >= T || E > 64 || k > 8 || k > E) return;    // host checks these too
   const bool live = lane < E;
   const float l = live ? logits[(size_t)t * E + lane] : -INFINITY;
@@ -340,6 +399,7 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
     }
   }
   if (myj >= 0) {
+    if (sel) sel[t * k + myj] = lane;           // routed expert of (token, slot): device-selected launches
     topw[t * k + myj] = renorm ? myw / wsum : myw;
     const int pos = atomicAdd(counts + lane, 1);
     xrows[lane * cap + pos] = t;
@@ -421,11 +481,13 @@ int nls_argmax_unpack(const void* keys, int n, int* out, void* stream) {
   return (int)hipGetLastError();
 }
 
+// counts: zeroed inside the kernel when T <= 4 (one workgroup), else by the caller; sel (optional):
+// [T*k] expert id of each (token, slot)
 int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* topw, int* counts, int* xrows,
-                  int* yrows, int cap, void* stream) {
+                  int* yrows, int cap, int* sel, void* stream) {
   if (E > 64 || k > 8) return -1;
   hipLaunchKernelGGL(moe_route_kernel, dim3((T + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits, T, E, k,
-                     renorm, topw, counts, xrows, yrows, cap);
+                     renorm, topw, counts, xrows, yrows, cap, sel);
   return (int)hipGetLastError();
 }
 
@@ -433,6 +495,18 @@ int nls_moe_combine(const float* y, const float* w, int T, int topk, float* resi
                     void* stream) {
   hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr, D,
                      alpha);
+  return (int)hipGetLastError();
+}
+
+int nls_moe_combine_norm(const float* y, const float* w, int T, int topk, float* resid, long ldr, int D, float alpha,
+                         const float* nw, float eps, void* h, long ldh, void* stream) {
+  if (D % 4 || topk > 8 || topk < 1) return -1;
+  if (topk <= 2)
+    hipLaunchKernelGGL(moe_combine_norm_kernel<2>, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr,
+                       D, alpha, nw, eps, (act_t*)h, ldh);
+  else
+    hipLaunchKernelGGL(moe_combine_norm_kernel<8>, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr,
+                       D, alpha, nw, eps, (act_t*)h, ldh);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ struct NlsFuse {
   void* q_out; long ldq; void* kc; void* vc; int Hq, Hkv, D, pad0;
   void* hout; long ldh; const float* onw; int* cnt;                          // residual add + RMSNorm
   float* ssq_out; const float* ssq_in; int ldss, nss_in;                     // split RMSNorm (GemvArgs)
+  const int* sel; int sel_slots, sel_base, pad1;                             // device-selected segments
 };
 
 // mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
@@ -71,6 +72,11 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (fz->onw && (mode != 0 || epi != EPI_ADD_F32 || nseg != 1 || segs[0].ycol || segs[0].xmap || segs[0].ymap ||
                   segs[0].mcount || !fz->cnt || !fz->hout || segs[0].rows % 4 || argmax))
     return -1;
+  if (fz->sel) {           // path A over routed experts only: identical segment shapes
+    if (mode != 0 || fz->sel_slots < 1 || fz->sel_slots > 256 || argmax) return -1;
+    for (int i = 1; i < nseg; ++i)
+      if (segs[i].rows != segs[0].rows || segs[i].K != segs[0].K) return -1;
+  }
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
   if (mode == 4 || mode == 5) {
     if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
@@ -150,6 +156,10 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   a.ldh = fz->ldh;
   a.onw = fz->onw;
   a.cnt = fz->cnt;
+  a.sel = fz->sel;
+  a.sel_base = fz->sel_base;
+  a.sel_tiles = (segs[0].rows + tile_rows - 1) / tile_rows;
+  if (fz->sel) tiles = fz->sel_slots * a.sel_tiles;
   a.ssq_out = fz->ssq_out;
   a.ssq_in = fz->ssq_in;
   a.ldss = fz->ldss;

@@ -60,6 +60,10 @@ struct GemvArgs {
   // rows it updated to ssq_out[m * ldss + blockIdx.x]; a consumer with xf / nw sums the nss_in
   // shares of ssq_in (fixed order: deterministic) to get the row's inverse RMS.
   float* ssq_out; const float* ssq_in; int ldss, nss_in;
+  // device-selected segments (MoE decode, few tokens): workgroup i serves segment sel[i / sel_tiles] -
+  // sel_base (out of range or a repeat of an earlier slot: exit), tile i % sel_tiles of it -- only the
+  // routed experts' tiles are launched instead of every expert's (most of which would exit at once)
+  const int* sel; int sel_tiles, sel_base, pad1;
 };
 
 // inv[m] = 1 / rms of rows m < M from producer partial sums of squares (see GemvArgs::ssq_in); one
@@ -439,11 +443,23 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 template <int WAVES, int RT, int MT, int KSET, bool XL = false>
 __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tile = blockIdx.x;
+  int tile = blockIdx.x;
   Seg S = segs.s[0];
+  if (a.sel) {
+    const int slot = blockIdx.x / a.sel_tiles;
+    const int e = a.sel[slot] - a.sel_base;
+    if (e < 0 || e >= segs.nseg) return;
+    for (int s2 = 0; s2 < slot; ++s2)
+      if (a.sel[s2] - a.sel_base == e) return;     // expert already served by an earlier slot
 #pragma unroll
-  for (int i = 1; i < 8; ++i)
-    if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
+    for (int i = 1; i < 8; ++i)
+      if (i == e) S = segs.s[i];                 // static indices: no scratch copy of the arg array
+    tile = S.tile_begin + blockIdx.x % a.sel_tiles;
+  } else {
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+      if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
+  }
   if (S.mcount && *S.mcount <= 0) return;     // MoE expert with no routed tokens
   const int row0 = (tile - S.tile_begin) * RT * 16;
   if constexpr (KSET == 0) {

@@ -310,6 +310,7 @@ class LlamaModel:
                 counts=torch.zeros(E, dtype=torch.int32, device=dev),
                 xrows=torch.zeros(E * pad, dtype=torch.int32, device=dev),
                 yrows=torch.zeros(E * pad, dtype=torch.int32, device=dev),
+                sel=torch.zeros(pad * k, dtype=torch.int32, device=dev),
                 yexp=torch.zeros(pad * k, cfg.d_model, dtype=torch.float32, device=dev),
             )
         return b
@@ -370,7 +371,7 @@ class LlamaModel:
             nxt = self.layers[L + 1].attn_norm if L + 1 < len(self.layers) else self.out_norm
             fused_prev = False
             if cfg.n_expert:
-                self._moe(lw, b, T)
+                fused_prev = self._moe(lw, b, T, nxt if fused else None)
             else:
                 ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
                 if fused:
@@ -446,11 +447,12 @@ class LlamaModel:
         else:
             self.comm.row_parallel_add(w, xin, resid, T, alpha)
 
-    def _moe(self, lw: LayerWeights, b: StepBuffers, T: int):
+    def _moe(self, lw: LayerWeights, b: StepBuffers, T: int, next_norm: Optional[torch.Tensor] = None) -> bool:
         """Top-k routed experts: router GEMV -> route kernel (per-expert row lists on device)
         -> grouped expert GEMVs (tiles of experts with no routed rows exit before reading
         weights) -> deterministic weighted combine into the residual."""
         cfg = self.cfg
+        normed = False
         m = b.moe
         k, E = cfg.n_expert_used, cfg.n_expert
         cap = b.x.shape[0]
@@ -471,16 +473,23 @@ class LlamaModel:
             dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", 2)), ks=1)
         for c0 in range(0, T, step):
             n = min(step, T - c0)
-            ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap)
+            # few tokens: the route kernel also lists each (token, slot)'s expert and the expert GEMVs
+            # launch only those experts' tiles (k of E; the rest would be launched just to exit)
+            use_sel = not gemm and self.device.type == "cuda" and n * k < len(self.experts)
+            ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap,
+                          sel=m["sel"] if use_sel else None)
             loc = list(zip(self.experts, lw.exp_gateup, lw.exp_down))
             segs = [Seg(gu, 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, gu, _ in loc]
+
+            def sel(s0):
+                return (m["sel"], n * k, self.experts[0] + s0) if use_sel else None
             for s0 in range(0, len(segs), 8):
-                ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu", **gu)
+                ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu", sel=sel(s0), **gu)
             if self.ep:                        # rows routed to other ranks' experts stay zero
                 m["yexp"][:n * k].zero_()
             segs = [Seg(dn, 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, _, dn in loc]
             for s0 in range(0, len(segs), 8):
-                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32", **dn)
+                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32", sel=sel(s0), **dn)
             xs = b.x[c0:c0 + n]
             if self.shard.size > 1:
                 # combine locally first, then ONE all-reduce of the combined [n, d] rows (k x fewer bytes
@@ -490,5 +499,10 @@ class LlamaModel:
                     xs.zero_()
                 ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale)
                 self.comm.all_reduce(xs)
+            elif next_norm is not None and n == T:
+                # one chunk: the combine and the next layer's input RMSNorm share a launch
+                ops.moe_combine_norm(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale, next_norm, cfg.eps, b.h)
+                normed = True
             else:
                 ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale)
+        return normed

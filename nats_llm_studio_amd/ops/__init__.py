@@ -29,6 +29,10 @@ ADDNORM_MAX_M = int(_os.environ.get("NLS_ADDNORM", "0"))
 # Large-M GEMMs switch to the dense f16 kernel (mode 4, csrc/kernels/hgemm.hip) from this many rows
 # on, for weights that carry an f16 copy (QWeight.expand_dense)
 DENSE_MIN_M = int(_os.environ.get("NLS_DENSE_GEMM_M", "128"))
+# launch config of the mapped-row (MoE expert) path-A GEMV: mode, waves, row tiles, split
+# (Mixtral-8x7B batch 1 / 16, profiles/moe_selected_experts.txt: 0,4,2,1 3.90 / 10.0 ms per step vs 0,8,1,1
+# 4.94 / 15.1)
+MOE_GEMV = tuple(int(v) for v in _os.environ.get("NLS_MOE_GEMV", "0,4,2,1").split(","))
 ACT_DTYPE = torch.float16   # activation dtype of every GEMM/GEMV input and SwiGLU/RMSNorm/attention output
 
 
@@ -244,7 +248,7 @@ def norm_fusable(M: int, K: int) -> bool:
 
 def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
           argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1,
-          norm=None):
+          norm=None, sel=None):
     """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K].
     norm = (xf f32 [M, K], w f32 [K], eps[, ssq, ldss, nparts]): the GEMV input is f16(rmsnorm(xf) * w),
     computed inside the kernel (batch <= a few rows; `x` is then ignored on the GPU). With the partial
@@ -289,13 +293,25 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         xf, nw, eps = norm[:3]
         xs = xf[:M].float()
         x = (xs * torch.rsqrt(xs.pow(2).mean(dim=1, keepdim=True) + eps) * nw.float()).to(ACT_DTYPE)
+    if x.is_cuda and sel is not None:
+        # MoE decode with few tokens: launch only the routed experts' tiles (path A, mapped rows).
+        # sel = (int32 slots tensor, n_slots, base): slot i serves segment sel[i] - base.
+        if x.dtype != ACT_DTYPE:
+            raise TypeError(f"qgemv: activations must be {ACT_DTYPE}, got {x.dtype}")
+        st, nslots, base = sel
+        mode, waves, rt, ks = MOE_GEMV if mode < 0 or waves == 0 else (mode, waves, rt, ks)
+        fz = _lib.NlsFuse(sel=st.data_ptr(), sel_slots=int(nslots), sel_base=int(base))
+        _lib.check(_lib.lib().nls_qgemv_ex(_segs(segs), len(segs), x.data_ptr(), x.stride(0), y.data_ptr(),
+                                           y.stride(0), M, float(alpha), EPI[epi], _p(argmax), waves, rt, 0, 1, None,
+                                           _stream_ptr(x), ctypes.byref(fz)), "nls_qgemv_ex(sel)")
+        return y
     if x.is_cuda:
         if x.dtype != ACT_DTYPE:
             raise TypeError(f"qgemv: activations must be {ACT_DTYPE}, got {x.dtype}")
         L = _lib.lib()
         mapped = any(s.xmap is not None for s in segs)
         if mode < 0 or waves == 0:
-            mode, waves, rt, ks = gemv_config(segs, M) if not mapped else (0, 8, 1, 1)
+            mode, waves, rt, ks = gemv_config(segs, M) if not mapped else MOE_GEMV
         if M > 64 and mode == 0:
             # mapped (MoE) rows / path A: chunks of 64 rows
             for m0 in range(0, M, 64):
@@ -673,12 +689,15 @@ def sample_decode(logits: torch.Tensor, n: int, params: torch.Tensor, seeds: tor
 
 
 def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
-              yrows: torch.Tensor, cap: int, renorm: bool = True):
+              yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None):
+    """Top-k routing: per-expert row lists (counts / xrows / yrows) and weights topw; `sel` (optional,
+    int32 [>= T*k]) receives each (token, slot)'s expert id for device-selected expert launches."""
     E = logits.shape[1]
     if logits.is_cuda:
-        counts.zero_()
+        if T > 4:                  # one-workgroup launches (T <= 4) zero the counts in-kernel
+            counts.zero_()
         _lib.check(_lib.lib().nls_moe_route(logits.data_ptr(), T, E, k, int(renorm), topw.data_ptr(),
-                                            counts.data_ptr(), xrows.data_ptr(), yrows.data_ptr(), cap,
+                                            counts.data_ptr(), xrows.data_ptr(), yrows.data_ptr(), cap, _p(sel),
                                             _stream_ptr(logits)), "nls_moe_route")
         return
     p = torch.softmax(logits[:T].float(), dim=-1)
@@ -694,6 +713,21 @@ def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: 
             xrows[ex * cap + c] = t
             yrows[ex * cap + c] = t * k + j
             counts[ex] += 1
+            if sel is not None:
+                sel[t * k + j] = ex
+
+
+def moe_combine_norm(y: torch.Tensor, topw: torch.Tensor, T: int, k: int, resid: torch.Tensor, alpha: float,
+                     norm_w: torch.Tensor, eps: float, h: torch.Tensor):
+    """moe_combine, then h[:T] = rmsnorm(resid[:T]) * norm_w (the next layer's input norm) in the same launch."""
+    if y.is_cuda:
+        D = resid.shape[1]
+        _lib.check(_lib.lib().nls_moe_combine_norm(y.data_ptr(), topw.data_ptr(), T, k, resid.data_ptr(),
+                                                   resid.stride(0), D, float(alpha), norm_w.data_ptr(), float(eps),
+                                                   h.data_ptr(), h.stride(0), _stream_ptr(y)), "nls_moe_combine_norm")
+        return h
+    moe_combine(y, topw, T, k, resid, alpha)
+    return rmsnorm(resid, norm_w, h, T, eps)
 
 
 def moe_combine(y: torch.Tensor, topw: torch.Tensor, T: int, k: int, resid: torch.Tensor, alpha: float = 1.0):

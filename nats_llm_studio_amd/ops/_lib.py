@@ -32,7 +32,8 @@ class NlsFuse(ctypes.Structure):
                 ("q_out", c_void_p), ("ldq", c_long), ("kc", c_void_p), ("vc", c_void_p),
                 ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("pad0", c_int),
                 ("hout", c_void_p), ("ldh", c_long), ("onw", c_void_p), ("cnt", c_void_p),
-                ("ssq_out", c_void_p), ("ssq_in", c_void_p), ("ldss", c_int), ("nss_in", c_int)]
+                ("ssq_out", c_void_p), ("ssq_in", c_void_p), ("ldss", c_int), ("nss_in", c_int),
+                ("sel", c_void_p), ("sel_slots", c_int), ("sel_base", c_int), ("pad1", c_int)]
 
 
 _SIGS = {
@@ -53,8 +54,10 @@ _SIGS = {
     "nls_argmax": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
     "nls_argmax_unpack": [c_void_p, c_int, c_void_p, c_void_p],
     "nls_moe_route": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                      c_void_p],
+                      c_void_p, c_void_p],
     "nls_moe_combine": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p],
+    "nls_moe_combine_norm": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p, c_float,
+                             c_void_p, c_long, c_void_p],
     "nls_attn_decode": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                         c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p,
                         c_void_p, c_void_p],

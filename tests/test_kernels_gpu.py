@@ -778,3 +778,56 @@ def test_split_rmsnorm_producer_consumer(gpu, M):
     y = torch.zeros(xin.shape[0], 768, device=gpu)
     ops.qgemv([ops.Seg(wc)], x, y, M, norm=(x, nw, 1e-5, ssq, ldss, parts))
     _close(y[:M], want, 3e-2)
+
+
+@pytest.mark.parametrize("T", [1, 3, 10])
+def test_moe_route_sel_and_selected_expert_launch(gpu, T):
+    """The route kernel lists each (token, slot)'s expert (and zeroes stale counts itself for T <= 4);
+    a device-selected launch over those slots equals the launch over every expert."""
+    E, k, K, R = 8, 2, 512, 64
+    lg = torch.randn(T, E, device=gpu)
+    topw = torch.zeros(T * k, device=gpu)
+    counts = torch.full((E,), 5 if T <= 4 else 0, dtype=torch.int32, device=gpu)   # stale counts: T<=4 zeroes
+    cap = 64
+    xr = torch.zeros(E * cap, dtype=torch.int32, device=gpu)
+    yr = torch.zeros(E * cap, dtype=torch.int32, device=gpu)
+    sel = torch.full((T * k,), -1, dtype=torch.int32, device=gpu)
+    ops.moe_route(lg, T, k, topw, counts, xr, yr, cap, sel=sel)
+    _, e = torch.topk(torch.softmax(lg, -1), k, -1)
+    assert sorted(sel.view(T, k).cpu().tolist()[0]) == sorted(e.cpu().tolist()[0])
+    assert set(sel.cpu().tolist()) == set(e.flatten().cpu().tolist())
+    assert counts.sum().item() == T * k
+    ws = [_qw(R, K, GGMLType.Q5_K, gpu, 30 + i)[0] for i in range(E)]
+    x = _x(T, K, gpu)
+    segs = [ops.Seg(ws[i], 0, xr[i * cap:], yr[i * cap:], counts[i:i + 1]) for i in range(E)]
+    y_all = torch.zeros(64, R, device=gpu)
+    ops.qgemv(segs, x, y_all, T)
+    y_sel = torch.zeros(64, R, device=gpu)
+    ops.qgemv(segs, x, y_sel, T, sel=(sel, T * k, 0))
+    assert torch.equal(y_all[:T * k], y_sel[:T * k])
+    # a base offset (expert group 4..7 of an EP rank / an 8-segment group): out-of-range slots exit
+    y_hi = torch.zeros(64, R, device=gpu)
+    ops.qgemv(segs[4:], x, y_hi, T, sel=(sel, T * k, 4))
+    for t in range(T):
+        for j in range(k):
+            ex = int(e[t, j])
+            row = t * k + j
+            want = y_all[row] if ex >= 4 else torch.zeros(R, device=gpu)
+            assert torch.equal(y_hi[row], want), (t, j, ex)
+
+
+@pytest.mark.parametrize("T,k,D", [(1, 2, 4096), (3, 2, 1024), (2, 4, 4096), (5, 8, 8192)])
+def test_moe_combine_norm(gpu, T, k, D):
+    """Fused MoE combine + next RMSNorm vs the two-step fp32 reference."""
+    g = torch.Generator().manual_seed(T * 100 + k)
+    y = torch.randn(T * k, D, generator=g)
+    w = torch.rand(T * k, generator=g)
+    x = torch.randn(T, D, generator=g)
+    nw = torch.rand(D, generator=g) + 0.5
+    ref = x + 0.7 * (w.view(T, k, 1) * y.view(T, k, D)).sum(1)
+    href = ref * torch.rsqrt(ref.pow(2).mean(1, keepdim=True) + 1e-5) * nw
+    xg = x.to(gpu)
+    h = torch.zeros(T, D, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.moe_combine_norm(y.to(gpu), w.to(gpu), T, k, xg, 0.7, nw.to(gpu), 1e-5, h)
+    _close(xg, ref, 1e-5)
+    _close(h, href, 1e-2)
