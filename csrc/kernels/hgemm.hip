@@ -36,7 +36,7 @@ using nls_dma::glds16;
 using nls_dma::lds_addr;
 using nls_dma::wait_vm_lgkm0;
 
-template <int WM, int BN, int NWV>
+template <int WM, int BN, int NWV, int NST = 3>
 struct HG {
   static constexpr int NT = 64 * NWV;         // threads per workgroup (8 or 16 waves)
   static constexpr int BM = 64 * WM;          // activation rows per workgroup
@@ -45,17 +45,18 @@ struct HG {
   static constexpr int MTW = 4;               // 16-row activation tiles per wave
   static constexpr int XS = BM * 128;         // bytes of one activation stage [BM][64] f16
   static constexpr int WSB = BN * 128;        // bytes of one weight stage [BN][64] f16
-  static constexpr int NSX = 3;               // activation ring depth
-  static constexpr int NSW = (NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2;   // weight ring depth (LDS budget)
+  static constexpr int NSX = NST;             // activation ring depth
+  // weight ring depth (LDS budget); NST = 2: both rings 2 deep, small enough for 2 workgroups per CU
+  static constexpr int NSW = NST == 2 ? 2 : ((NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2);
   static constexpr int NX = BM / 8 / NWV;     // activation DMA instructions per wave per stage
   static constexpr int NW = BN / 8 / NWV;     // weight DMA instructions per wave per stage
   static_assert(NX >= 1 && NW >= 1 && NTW >= 1, "tile too small for the wave count");
   static constexpr size_t LDS = (size_t)NSX * XS + (size_t)NSW * WSB;
 };
 
-template <int WM, int BN, int NWV>
+template <int WM, int BN, int NWV, int NST>
 DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
-  typedef HG<WM, BN, NWV> G;
+  typedef HG<WM, BN, NWV, NST> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, NX = G::NX, NW = G::NW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -141,6 +142,22 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
         dma_x(j + 2);
         step(j);
         wait_vm_lgkm0<NX + NW>();               // step j+1 landed (j+2 in flight)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    } else if constexpr (G::NSX == 2) {
+      // both rings 2 deep (two workgroups per CU hide each other's load waits): step j+1 is issued at
+      // the top of step j and fully waited for at its end
+      dma_w(0);
+      dma_x(0);
+      wait_vm_lgkm0<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      for (int j = 0; j < nq; ++j) {
+        dma_w(j + 1);                           // slots (j+1)%2 were last read in step j-1: retired
+        dma_x(j + 1);
+        step(j);
+        wait_vm_lgkm0<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
@@ -240,11 +257,11 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
   }
 }
 
-template <int WM, int BN, int NWV>
-__global__ __launch_bounds__(64 * NWV, 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+template <int WM, int BN, int NWV, int NST>
+__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                        int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
-  constexpr int BM = HG<WM, BN, NWV>::BM;
+  constexpr int BM = HG<WM, BN, NWV, NST>::BM;
   // (tile, m-block, k-slice) with all m-blocks and k-slices of a tile on one XCD
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
   const int kslice = j % ks;
@@ -262,34 +279,35 @@ __global__ __launch_bounds__(64 * NWV, 1) void hgemm_kernel(SegList segs, GemvAr
 #pragma unroll
   for (int s = 1; s < 8; ++s)
     if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
-  hgemm_tile<WM, BN, NWV>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds);
+  hgemm_tile<WM, BN, NWV, NST>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds);
 }
 
-template <int WM, int BN, int NWV>
+template <int WM, int BN, int NWV, int NST>
 int launch_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  typedef HG<WM, BN, NWV> G;
+  typedef HG<WM, BN, NWV, NST> G;
   const int nmb = (a.M + G::BM - 1) / G::BM;
   const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
-    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)G::LDS) != hipSuccess)
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles, nmb);
+  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV, NST>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles, nmb);
   return (int)hipGetLastError();
 }
 
 // bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at
-// wm 4); waves: 8 (2 per SIMD, 64 x 16*bn/128 accumulator tile per wave) or 16 (4 per SIMD, half
+// wm 4); nst 2: 2-deep rings (64 KiB at wm 2, bn 128: two workgroups per CU); waves: 8 (2 per SIMD, 64 x 16*bn/128 accumulator tile per wave) or 16 (4 per SIMD, half
 // the tile per wave: more waves to cover each other's LDS and barrier waits)
-int launch_dense(int wm, int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
-                 hipStream_t st) {
-#define NLS_HG(W, B, V) \
-  if (wm == W && bn == B && waves == V) return launch_t<W, B, V>(sl, ntiles, ks, ws, a, st);
-  NLS_HG(4, 128, 8) NLS_HG(2, 128, 8) NLS_HG(4, 256, 8) NLS_HG(2, 256, 8)
-  NLS_HG(4, 128, 16) NLS_HG(2, 128, 16) NLS_HG(4, 256, 16) NLS_HG(2, 256, 16)
+int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
+                 const GemvArgs& a, hipStream_t st) {
+#define NLS_HG(W, B, V, S) \
+  if (wm == W && bn == B && waves == V && nst == S) return launch_t<W, B, V, S>(sl, ntiles, ks, ws, a, st);
+  NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
+  NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
+  NLS_HG(2, 128, 8, 2)
 #undef NLS_HG
   return -1;
 }

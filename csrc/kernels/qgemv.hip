@@ -6,8 +6,8 @@
 using namespace nls_gemv;
 
 namespace nls_hgemm {
-int launch_dense(int wm, int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
-                 hipStream_t st);
+int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
+                 const GemvArgs& a, hipStream_t st);
 }
 
 
@@ -43,6 +43,7 @@ struct NlsFuse {
 //         [rows][K] f16 matrix (not the tiled layout); 8 waves, `rt` = WM (4: 256-row activation
 //         blocks, 2: 128-row), optional split-K as mode 1.
 // mode 5: mode 4 with 256-row weight tiles (twice the MFMA work per fetched activation byte).
+// mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
 // Returns 0 on success, a hipError_t, or -1 on bad arguments.
 static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
                       float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
@@ -78,7 +79,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       if (segs[i].rows != segs[0].rows || segs[i].K != segs[0].K) return -1;
   }
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
-  if (mode == 4 || mode == 5) {
+  if (mode < 0 || mode > 6 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode >= 4 && mode <= 6) {
     if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount) return -1;
@@ -176,7 +178,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     if (ks < 1) ks = 1;
     int rc;
     if (mode >= 4)
-      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, sl, tiles, ks, (float*)ws, a, st);
+      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : 3, sl, tiles, ks, (float*)ws, a,
+                                   st);
     else if (mode == 3)
       rc = (kset == 0 ? nls_dma::launch_dma_k0 : nls_dma::launch_dma_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 2)

@@ -228,7 +228,7 @@ def _seg_arr(segs: Sequence[Seg], mode: int):
     """ctypes segment list of a launch: modes 4/5 point at the row-major f16 copies."""
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
-        if mode in (4, 5):
+        if mode in (4, 5, 6):
             if s.w.d16 is None:
                 raise ValueError(f"{s.w.name}: mode 4 needs QWeight.expand_dense()")
             arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), None, None, None, 1, s.w.rows, s.w.K, s.ycol)

@@ -66,7 +66,7 @@ def dense_key(segs, M: int) -> str:
 
 
 def dense_heuristic(segs, M: int):
-    """Modes 4/5 (dense f16 GEMM): 256-row activation blocks from M >= 192 with 256-row weight tiles
+    """Modes 4/5/6 (dense f16 GEMM): 256-row activation blocks from M >= 192 with 256-row weight tiles
     (mode 5), then the split-K that minimises (workgroup rounds over the 256 CUs) / ks, with a small
     per-slice cost."""
     wm = 4 if M >= 192 else 2
