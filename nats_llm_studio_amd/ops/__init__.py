@@ -208,7 +208,8 @@ def _workspace(dev, n: int) -> torch.Tensor:
 
 
 def dense_ok(segs: Sequence[Seg], M: int) -> bool:
-    """Does this launch run on the dense f16 GEMM (mode 4)?"""
+    """May this launch run on the dense f16 GEMM (modes 4-6; the tuning table can still prefer the
+    quantised kernel for the shape)?"""
     return M >= DENSE_MIN_M and all(s.w.d16 is not None and s.xmap is None and s.ymap is None for s in segs)
 
 
@@ -220,7 +221,9 @@ def gemv_config(segs: Sequence[Seg], M: int):
     (rt as mode 2)."""
     from . import tuning
     if dense_ok(segs, M):
-        return tuning.select_dense(segs, M)
+        cfg = tuning.select_dense(segs, M)
+        if cfg is not None:
+            return cfg
     return tuning.select(segs, M)
 
 

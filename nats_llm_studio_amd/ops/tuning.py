@@ -85,7 +85,10 @@ def dense_heuristic(segs, M: int):
 
 
 def select_dense(segs, M: int):
+    """Dense config, or None where the tuner measured the quantised GEMM faster (entry [-1])."""
     hit = table().get(dense_key(segs, M))
+    if hit is not None and hit[0] < 0:
+        return None
     return hit if hit is not None else dense_heuristic(segs, M)
 
 

@@ -86,6 +86,8 @@ def test_dense_tuning_entries_at_real_shapes(gpu, shape):
         if not k.startswith(shape + ":"):
             continue
         M = int(k.rsplit(":", 1)[1])
+        if cfg[0] < 0:                          # quantised GEMM measured faster here: not used
+            continue
         mode, waves, rt, ks = cfg
         x = (torch.randn(M, K, generator=g) * 0.5).to(ops.ACT_DTYPE).to(gpu)
         y = torch.full((M, rows), float("nan"), device=gpu)
