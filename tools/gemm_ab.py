@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--M", type=int, default=512)
     ap.add_argument("--shapes", default="qkv,o,gateup,down,lm_head")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--dense", action="store_true", help="f16 weight copies: the large-M dense GEMM configs")
     a = ap.parse_args()
     libs = [(p, _lib.load(p)) for p in a.libs.split(",")]
     spec = SPECS["llama-3-8b"]
@@ -46,7 +47,9 @@ def main():
         segs, col, nbytes = [], 0, 0
         for t, rows in segdef:
             w = ops.QWeight(Q.random_blocks(t, rows * K, 0.02, rng), t, rows, K, dev)
-            nbytes += w.nbytes
+            if a.dense:
+                w.expand_dense()
+            nbytes += w.nbytes if not a.dense else w.dense_bytes
             segs.append(ops.Seg(w, col))
             col += rows
         ncopy = min(REPS, max(1, -(-(1 << 30) // nbytes)))
@@ -57,9 +60,11 @@ def main():
                 w = ops.QWeight.__new__(ops.QWeight)
                 w.__dict__.update(s.w.__dict__)
                 w.data = s.w.data.clone()
+                if a.dense:
+                    w.d16 = s.w.d16.clone()
                 cp.append(ops.Seg(w, s.ycol))
             copies.append(cp)
-        cfg = tuning.select(segs, M)
+        cfg = ops.gemv_config(segs, M)
         x = (torch.randn(max(M, 64), K, device=dev) * 0.5).to(ops.ACT_DTYPE)
         ncol = col // 2 if epi == "swiglu" else col
         y = torch.zeros(max(M, 64), ncol, dtype=ops.ACT_DTYPE if epi == "swiglu" else torch.float32, device=dev)
