@@ -248,7 +248,11 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
           const int b = arow(i, e);
-          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = accv(i, j, e);
+          if (b >= M) continue;
+          if (ym)        // mapped split-K: slab row = the token's y row, columns shared by every expert
+            ws[((size_t)kslice * a.mtot + ym[b]) * ntot + S.ycol + row] = accv(i, j, e);
+          else
+            ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = accv(i, j, e);
         }
     }
     return;

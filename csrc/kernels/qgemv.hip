@@ -92,15 +92,20 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (M > 64 && mode == 0) return -1;   // large M: path B / LDS GEMM
   if (mode != 0 && ks > 1 && !ws) return -1;
   if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
+  // mapped split-K (MoE down projection at many tokens): slabs indexed by the y row, one reduce
+  bool mks = mode == 2 && ks > 1 && epi == EPI_F32 && !argmax;
+  for (int i = 0; i < nseg && mks; ++i)
+    mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
   const int tile_rows = mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16);
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
-    // mapped rows (MoE): path A, or the LDS GEMM without split-K / arg-max
+    // mapped rows (MoE): path A, or the LDS GEMM without arg-max; split-K only as "mapped split-K"
+    // (every segment an expert writing the same output columns of its own y rows, f32 store)
     if ((segs[i].xmap || segs[i].ymap || segs[i].mcount) && mode != 0 &&
-        (mode != 2 || ks > 1 || argmax || epi == EPI_SLABS))
+        (mode != 2 || argmax || epi == EPI_SLABS || (ks > 1 && !mks)))
       return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;
@@ -135,7 +140,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   a.M = M;
   a.epi = epi;
   a.alpha = alpha;
-  a.pad = cols;
+  a.pad = mks ? segs[0].rows : cols;      // split-K slab width
   a.argmax = (unsigned long long*)argmax;
   a.m0 = 0;
   a.mtot = M;
@@ -188,6 +193,13 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       rc = launch(1, waves, rt, mt, sl, tiles, ks, (float*)ws, a, st, nmb);
     if (rc || ks == 1 || epi == EPI_SLABS) return rc;
     RedList rl{};
+    if (mks) {            // slabs [ks][M y rows][rows]: one shared output segment
+      rl.s[0] = RedSeg{0, segs[0].rows, 0, 0};
+      rl.nseg = 1;
+      dim3 grid((segs[0].rows + 255) / 256, M);
+      hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, ks, M, segs[0].rows, rl, a);
+      return (int)hipGetLastError();
+    }
     for (int i = 0; i < nseg; ++i) rl.s[i] = RedSeg{sl.s[i].tile_begin_col, sl.s[i].rows, sl.s[i].ycol, 0};
     rl.nseg = nseg;
     const int nout = epi == EPI_SWIGLU ? cols / 2 : cols;

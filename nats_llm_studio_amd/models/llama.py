@@ -468,9 +468,19 @@ class LlamaModel:
         # block wins even at ~64 routed rows per expert (Mixtral B=256, tools/moe_ab.sh: gate/up
         # rt 4 / down rt 2 = 32.0 ms/step, 2/2 = 34.3, 2/1 = 39.6, 1/1 = 50.8)
         gu = dn = {}
+        dn_rows = T
         if gemm:
             gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", 4)), ks=1)
             dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", 2)), ks=1)
+            # down projection (K = d_ff): split K over workgroups when ONE launch covers every routed row
+            # (<= 8 local experts, no EP: every y row written by exactly one expert in every K slice);
+            # the slabs are indexed by the y row, so that launch's M is the T*k output rows
+            # (Mixtral-8x7B: B=256 28.5 vs 30.9 ms/step at 4 slices, B=128 25.8 vs 25.1: from ~48 rows per
+            # expert on, profiles/moe_down_splitk.txt)
+            kdn = int(os.environ.get("NLS_MOE_KS_DN", "4"))
+            if kdn > 1 and len(self.experts) <= 8 and not self.ep and T * k >= 48 * len(self.experts):
+                dn["ks"] = kdn
+                dn_rows = T * k
         for c0 in range(0, T, step):
             n = min(step, T - c0)
             # few tokens: the route kernel also lists each (token, slot)'s expert and the expert GEMVs
@@ -489,7 +499,8 @@ class LlamaModel:
                 m["yexp"][:n * k].zero_()
             segs = [Seg(dn, 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, _, dn in loc]
             for s0 in range(0, len(segs), 8):
-                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], n, epi="f32", sel=sel(s0), **dn)
+                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], dn_rows if dn.get("ks", 1) > 1 else n, epi="f32",
+                          sel=sel(s0), **dn)
             xs = b.x[c0:c0 + n]
             if self.shard.size > 1:
                 # combine locally first, then ONE all-reduce of the combined [n, d] rows (k x fewer bytes

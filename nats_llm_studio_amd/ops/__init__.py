@@ -325,7 +325,8 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         arr = _seg_arr(segs, mode)
         ws = None
         if mode != 0 and ks > 1:
-            ws = _workspace(x.device, ks * M * sum(s.w.rows for s in segs)).data_ptr()
+            width = segs[0].w.rows if mapped else sum(s.w.rows for s in segs)   # mapped split-K: shared columns
+            ws = _workspace(x.device, ks * M * width).data_ptr()
         rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
                          EPI[epi], _p(argmax), waves, rt, mode, ks, ws, _stream_ptr(x))
         _lib.check(rc, "nls_qgemv")

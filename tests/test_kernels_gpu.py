@@ -154,7 +154,11 @@ def test_qgemm_mapped_moe(gpu, T, rt, qt):
     ops.qgemv(segs, x, act, T, epi="swiglu", **cfg)
     segs = [ops.Seg(dns[e][0], 0, yrows[e * cap:], yrows[e * cap:], counts[e:e + 1]) for e in range(E)]
     ops.qgemv(segs, act, yexp, T, epi="f32", **cfg)
+    # mapped split-K (the MoE down projection at many tokens): slabs by y row, launch M = T*k rows
+    yks = torch.full((T * k, K), 7.0, device=gpu)
+    ops.qgemv(segs, act, yks, T * k, epi="f32", mode=2, waves=8, rt=rt, ks=3)
     torch.cuda.synchronize()
+    _close(yks, yexp, 1e-3)
     cnt, xr, yr = counts.cpu(), xrows.cpu(), yrows.cpu()
     assert int(cnt.sum()) == T * k and sorted(yr[e * cap + i].item() for e in range(E)
                                               for i in range(int(cnt[e]))) == list(range(T * k))
