@@ -254,6 +254,10 @@ def run(args, world: int):
         extra["step_breakdown_ms"] = {"gpu_wait": round(wait[0] / args.steps * 1e3, 3),
                                       "host_other": round((elapsed - wait[0]) / args.steps * 1e3, 3),
                                       "graph_replay_only": replay}
+    moe = getattr(eng.db, "moe", None)
+    if cuda and moe and "counts" in moe:   # routed rows per local expert, last MoE layer of the last step
+        sync()
+        extra["moe_counts_last_layer"] = moe["counts"][:len(model.experts)].tolist()
     # drain
     while eng.running or eng.waiting:
         eng.step()

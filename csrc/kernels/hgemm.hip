@@ -55,7 +55,8 @@ struct HG {
 };
 
 template <int WM, int BN, int NWV, int NST>
-DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
+DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
+                     const int* xm, const int* ym) {
   typedef HG<WM, BN, NWV, NST> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, NX = G::NX, NW = G::NW, WN = G::WN;
   const int lane = threadIdx.x & 63;
@@ -73,8 +74,9 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
   const act_t* xsrc[NX];
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
-    const int row = 8 * (NX * wave + i) + (lane >> 3);
-    xsrc[i] = a.x + (size_t)min(row, M - 1) * a.ldx + kt0 * 64 + c * 8;   // rows >= M: clamped, never stored
+    // rows >= M: clamped, never stored; xm: MoE gather (block-local row -> x row) on the DMA source
+    const int row = min(8 * (NX * wave + i) + (lane >> 3), M - 1);
+    xsrc[i] = a.x + (size_t)(xm ? xm[row] : row) * a.ldx + kt0 * 64 + c * 8;
   }
   const act_t* wsrc[NW];
   const act_t* Wd = reinterpret_cast<const act_t*>(S.w);
@@ -196,7 +198,11 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int b = mbase + 16 * i + 4 * g + e;
-          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[i][j][e];
+          if (b >= M) continue;
+          if (ym)        // mapped split-K: slab row = the token's y row, columns shared by every expert
+            ws[((size_t)kslice * a.mtot + ym[b]) * ntot + S.ycol + row] = acc[i][j][e];
+          else
+            ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[i][j][e];
         }
     }
     return;
@@ -215,12 +221,12 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
           const float u = __shfl_xor(v, 8, 64);
           if (r < 8 && b < M && row < S.rows) {
             const int n = S.ycol + ((row & ~15) >> 1) + (row & 7);
-            reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
+            reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
           }
           continue;
         }
         if (b < M && row < S.rows) {
-          const size_t off = (size_t)b * a.ldy + S.ycol + row;
+          const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
           if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
           else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
           else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
@@ -269,17 +275,23 @@ __global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegLi
   const int tile = (j / ks / nmb) * 8 + xcd;
   if (tile >= ntiles) return;
   const int m0 = mb * BM;
-  a.m0 = m0;
-  a.x += (size_t)m0 * a.ldx;
-  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-  a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-  if (a.argmax) a.argmax += m0;
-  a.M = min(BM, a.M - m0);
   Seg S = segs.s[0];
 #pragma unroll
   for (int s = 1; s < 8; ++s)
     if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
-  hgemm_tile<WM, BN, NWV, NST>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds);
+  // MoE grouped GEMM (as mode 2): the expert's routed-row count lives on the device; m-blocks past it
+  // exit before issuing any DMA (the grid is sized for every routed row on one expert)
+  const int mrows = S.mcount ? min(*S.mcount, a.M) : a.M;
+  if (m0 >= mrows) return;
+  const int* xm = S.xmap ? S.xmap + m0 : nullptr;
+  const int* ym = S.ymap ? S.ymap + m0 : nullptr;
+  a.m0 = m0;
+  if (!xm) a.x += (size_t)m0 * a.ldx;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+  if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (a.argmax) a.argmax += m0;
+  a.M = min(BM, mrows - m0);
+  hgemm_tile<WM, BN, NWV, NST>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds, xm, ym);
 }
 
 template <int WM, int BN, int NWV, int NST>

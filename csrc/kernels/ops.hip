@@ -216,7 +216,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids, WDesc W, int type,
                                                     float* __restrict__ out, long ldo, float scale) {
   const int t = blockIdx.x;
-  const int id = ids[t];
+  // clamped: a bad id (device-chained decode feeds sampled ids back without a host check) must not
+  // become a wild address
+  const int id = min(max(ids[t], 0), W.rows - 1);
   for (int k = threadIdx.x; k < W.K; k += 256)
     out[(size_t)t * ldo + k] = scale * dequant_elem(W, type, id, k);
 }

@@ -37,15 +37,21 @@ namespace nls_gemm {
 using namespace nls_gemv;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int T, int WM>
+// NA = 16-row activation tiles each wave multiplies (1..4), chosen per m-block from its real row count:
+// wave row wm owns activation tiles i*WM + wm (interleaved), so a block with few rows (MoE experts:
+// ~64 routed rows in a 256-row block) spreads its MFMAs over every wave and skips the padding tiles
+// instead of multiplying them (Mixtral B=256 gate/up: 4x fewer MFMAs), and stages only the rows used.
+template <int T, int WM, int NA>
 DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds,
                    const int* xm, const int* ym) {
-  constexpr int MTW = 4;                 // 16-row activation tiles per wave
+  constexpr int MTW = 4;                 // 16-row activation tiles per wave (at most)
   constexpr int WN = 8 / WM;
   constexpr int NTW = 8 / WN;            // 16-row weight tiles per wave
   constexpr int BM = WM * MTW * 16;
   constexpr int XS = BM * 64, WSZ = 128 * 64;    // f16 elements per buffer
-  constexpr int NXU = BM * 8 / 512;              // 16-B x chunks staged per thread per quarter
+  // 16-B x chunks staged per thread per quarter: 64-row groups up to the NA*WM tiles in use
+  constexpr int NXU = (NA * WM * 16 + 63) / 64;
+  static_assert(NA >= 1 && NA <= MTW && NXU * 512 <= BM * 8, "bad active-tile count");
   act_t* Xs = lds;                       // [2][BM][64]
   act_t* Ws = lds + 2 * XS;              // [2][128][64]
   const int lane = threadIdx.x & 63;
@@ -61,10 +67,10 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 
   // 32x32x16 MFMA tiles (variant): the wave's 64 x (128*WM/8) output as (MTW/2) x (NTW/2) 32x32
   // accumulators; blocks with a single 16-row weight tile per wave keep 16x16x32
-  constexpr bool M32 = NLS_GEMM_MFMA32 && NTW >= 2;
+  constexpr bool M32 = NLS_GEMM_MFMA32 && NTW >= 2 && NA == MTW;
   constexpr int MT2 = M32 ? MTW / 2 : 1, NT2 = M32 ? NTW / 2 : 1;
   f32x16 acc32[MT2][NT2];
-  f32x4 acc[M32 ? 1 : MTW][M32 ? 1 : NTW];
+  f32x4 acc[M32 ? 1 : NA][M32 ? 1 : NTW];
   if constexpr (M32) {
 #pragma unroll
     for (int i = 0; i < MT2; ++i)
@@ -74,7 +80,7 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
         for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
   } else {
 #pragma unroll
-    for (int i = 0; i < MTW; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -144,9 +150,9 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 #endif
       }
       } else {
-      f16x8 A[MTW], B[NTW];
+      f16x8 A[NA], B[NTW];
 #pragma unroll
-      for (int i = 0; i < MTW; ++i) A[i] = *reinterpret_cast<const f16x8*>(xb + (wm * MTW * 16 + 16 * i + r) * 64 + co);
+      for (int i = 0; i < NA; ++i) A[i] = *reinterpret_cast<const f16x8*>(xb + ((i * WM + wm) * 16 + r) * 64 + co);
 #pragma unroll
       for (int j = 0; j < NTW; ++j) B[j] = *reinterpret_cast<const f16x8*>(wb + (wn * NTW * 16 + 16 * j + r) * 64 + co);
       *reinterpret_cast<f16x8*>(wn_ + co) = f[s];
@@ -154,7 +160,7 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
-      for (int i = 0; i < MTW; ++i)
+      for (int i = 0; i < NA; ++i)
 #pragma unroll
         for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(A[i], B[j], acc[i][j]);
 #if NLS_GEMM_SETPRIO
@@ -226,13 +232,15 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   if (sb < sb1) sb_step(rA, sA, rB, sB, sb);
 
   // ---- epilogue from the accumulators ------------------------------------------------------------
-  // 16x16 tiles: lane holds weight row rbase + 16j + r and activation rows mbase + 16i + 4g + e;
+  // 16x16 tiles: lane holds weight row rbase + 16j + r and activation rows 16(i*WM + wm) + 4g + e;
   // 32x32 tiles: weight row rbase + 32j + r32, activation rows mbase + 32i + (e&3) + 8(e>>2) + 4 h32
   const int rbase = row0 + wn * NTW * 16, mbase = wm * MTW * 16;
-  constexpr int NJ = M32 ? NT2 : NTW, NI = M32 ? MT2 : MTW, NE = M32 ? 16 : 4;
+  constexpr int NJ = M32 ? NT2 : NTW, NI = M32 ? MT2 : NA, NE = M32 ? 16 : 4;
   constexpr int RED_LANES = M32 ? 32 : 16;       // lanes sharing an activation row (argmax reduction)
   auto wrow = [&](int j) { return M32 ? rbase + 32 * j + r32 : rbase + 16 * j + r; };
-  auto arow = [&](int i, int e) { return M32 ? mbase + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h32 : mbase + 16 * i + 4 * g + e; };
+  auto arow = [&](int i, int e) {
+    return M32 ? mbase + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h32 : (i * WM + wm) * 16 + 4 * g + e;
+  };
   auto accv = [&](int i, int j, int e) -> float {
     if constexpr (M32) return acc32[i][j][e];
     else return acc[i][j][e];
@@ -317,6 +325,17 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
 }
 
+template <int T, int WM>
+DEVI void lds_tile_na(int na, const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds,
+                      const int* xm, const int* ym) {
+  switch (na) {
+    case 1: lds_tile<T, WM, 1>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+    case 2: lds_tile<T, WM, 2>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+    case 3: lds_tile<T, WM, 3>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+    default: lds_tile<T, WM, 4>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+  }
+}
+
 template <int WM, int KSET>
 __global__ __launch_bounds__(512) void qmm_lds_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                       int nmb) {
@@ -346,17 +365,19 @@ __global__ __launch_bounds__(512) void qmm_lds_kernel(SegList segs, GemvArgs a, 
   if (a.argmax) a.argmax += m0;
   a.M = min(BM, mrows - m0);
   const int row0 = (tile - S.tile_begin) * 128;
+  // active 16-row tiles per wave (block-uniform): ceil(ceil(M / 16) / WM)
+  const int na = NLS_GEMM_MFMA32 ? 4 : min(4, ((a.M + 15) / 16 + WM - 1) / WM);
   if constexpr (KSET == 0) {
     switch (S.type) {
-      case QT_Q4_K: lds_tile<QT_Q4_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
-      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q4_K: lds_tile_na<QT_Q4_K, WM>(na, S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q6_K: lds_tile_na<QT_Q6_K, WM>(na, S, row0, kslice, ks, a, ws, lds, xm, ym); break;
       default: break;
     }
   } else {
     switch (S.type) {
-      case QT_Q5_K: lds_tile<QT_Q5_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
-      case QT_Q6_K: lds_tile<QT_Q6_K, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
-      case QT_Q8_0: lds_tile<QT_Q8_0, WM>(S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q5_K: lds_tile_na<QT_Q5_K, WM>(na, S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q6_K: lds_tile_na<QT_Q6_K, WM>(na, S, row0, kslice, ks, a, ws, lds, xm, ym); break;
+      case QT_Q8_0: lds_tile_na<QT_Q8_0, WM>(na, S, row0, kslice, ks, a, ws, lds, xm, ym); break;
       default: break;
     }
   }

@@ -143,7 +143,9 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
       if (l[i] == mx) best = min(best, i);
     float b = (float)best;   // exact for V < 2^24
     b = -block_max(-b, red);
-    return (int)b;
+    // no logit equals the max only when the row is all NaN: never hand an out-of-range id to the
+    // next step's embedding gather (chained decode feeds next_ids straight back on the device)
+    return b < (float)V ? (int)b : 0;
   }
   const float it = 1.f / p.temperature;
   // 3) keep-threshold on the logit scale: top-k (k-th largest) and min-p (p >= min_p * p_max)
@@ -200,7 +202,8 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
       for (int i = V - 1; i >= 0; --i)
         if (l[i] >= lo) { tok = i; break; }
     }
-    *s_tok = tok;
+    // nothing kept happens only for a non-finite row (NaN / -inf logits): return a valid id anyway
+    *s_tok = tok < 0 ? 0 : tok;
   }
   __syncthreads();
   return *s_tok;

@@ -34,6 +34,9 @@ _SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgr
 # fewest keys per flash-decoding split (0: the kernel's context-adaptive policy, attention.hip
 # split_chunk: 64 keys below 1K of context, 128 above)
 _MIN_CHUNK = int(os.environ.get("NLS_ATTN_MIN_CHUNK", "0"))
+# MoE expert GEMMs on the experts' f16 copies: (mode, waves, rt[, ks]) of gate/up and down
+_MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2").split(","))
+_MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
 
 
 @dataclass
@@ -233,27 +236,38 @@ class LlamaModel:
         head = "token_embd.weight" if cfg.tied_embeddings else "output.weight"
         self.lm_head = self._matrix(head, (self.vocab_lo, self.vocab_hi))
 
-    def dense_matrices(self) -> List[QWeight]:
-        """The projection matrices that get an f16 copy for the large-M dense GEMM (mode 4):
-        attention, dense FFN and the LM head (MoE experts stay quantised: their grouped GEMM
-        gathers rows and runs the LDS-dequant kernel)."""
+    def dense_matrices(self, experts: bool = False) -> List[QWeight]:
+        """The projection matrices that get an f16 copy for the large-M dense GEMM (modes 4/5):
+        attention, dense FFN and the LM head; experts=True: the local MoE experts (their grouped GEMM
+        gathers rows through the same maps on the f16 copies)."""
         out = []
         for lw in self.layers:
+            if experts:
+                out += list(lw.exp_gateup) + list(lw.exp_down)
+                continue
             out += [s.w for s in lw.qkv] + [lw.wo]
             if lw.gateup is not None:
                 out += [lw.gateup, lw.down]
-        out.append(self.lm_head)
+        if not experts:
+            out.append(self.lm_head)
         return out
 
-    def expand_dense(self, budget_bytes: Optional[int] = None) -> int:
-        """Give every dense_matrices() entry its f16 copy (ops.QWeight.expand_dense) when the whole set
-        fits in `budget_bytes` (None: no limit). All or nothing, so every large-M step takes one path;
-        returns the bytes added (0 if skipped or already expanded)."""
-        ws = self.dense_matrices()
-        need = sum(w.dense_bytes for w in ws if w.d16 is None)
-        if self.device.type != "cuda" or need == 0 or (budget_bytes is not None and need > budget_bytes):
+    def expand_dense(self, budget_bytes: Optional[int] = None, experts: bool = False) -> int:
+        """Give the dense_matrices() their f16 copies (ops.QWeight.expand_dense) in all-or-nothing
+        tiers -- attention/dense FFN/LM head, then (experts=True) the MoE experts -- each only when it
+        fits in what is left of `budget_bytes` (None: no limit), so every large-M launch of one kind
+        takes one path. Returns the bytes added (0 if skipped or already expanded)."""
+        if self.device.type != "cuda":
             return 0
-        added = sum(w.expand_dense() for w in ws)
+        added = 0
+        for tier in ((False, True) if experts else (False,)):
+            ws = self.dense_matrices(experts=tier)
+            need = sum(w.dense_bytes for w in ws if w.d16 is None)
+            if need == 0:
+                continue
+            if budget_bytes is not None and need > budget_bytes - added:
+                break
+            added += sum(w.expand_dense() for w in ws)
         self.dense_bytes = getattr(self, "dense_bytes", 0) + added
         return added
 
@@ -464,20 +478,28 @@ class LlamaModel:
         # path-A chunks of <= 32 tokens: the mapped GEMV then runs with <= 2 activation tiles, whose
         # kernels keep every fragment in registers (3-4 tiles spill: -Rpass-analysis scratch > 0)
         step = T if gemm else 32
-        # m-block = 64*rt rows. Every m-block re-dequantises the expert's weights, so the largest
-        # block wins even at ~64 routed rows per expert (Mixtral B=256, tools/moe_ab.sh: gate/up
-        # rt 4 / down rt 2 = 32.0 ms/step, 2/2 = 34.3, 2/1 = 39.6, 1/1 = 50.8)
+        # m-block = 64*rt rows. Every m-block re-dequantises the expert's weights, so the largest block
+        # wins; the GEMM multiplies only the block's real 16-row tiles (qgemm_impl.h NA), so ~64 routed
+        # rows in a 256-row block cost 64 rows of MFMA (Mixtral B=256, scripts/gpu_moe_na.sh: gate/up
+        # rt 4 / down rt 4 = 19.6 ms/step, 4/2 = 20.7, 2/2 = 28.3, 1/1 = 43.0)
         gu = dn = {}
         dn_rows = T
-        if gemm:
+        if gemm and all(w.d16 is not None for w in lw.exp_gateup + lw.exp_down):
+            # f16 expert copies (expand_dense tier 2): the dense DMA GEMM, bandwidth- rather than
+            # dequant-bound at ~64 rows per expert (NLS_MOE_DENSE_GU/_DN = mode,waves,rt)
+            gu = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_GU[:3]), ks=1)
+            dn = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_DN[:3]), ks=1)
+            kdn = _MOE_DENSE_DN[3] if len(_MOE_DENSE_DN) > 3 else 1
+        elif gemm:
             gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", 4)), ks=1)
-            dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", 2)), ks=1)
+            dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", 4)), ks=1)
+            kdn = int(os.environ.get("NLS_MOE_KS_DN", "1"))
+        if gemm:
             # down projection (K = d_ff): split K over workgroups when ONE launch covers every routed row
             # (<= 8 local experts, no EP: every y row written by exactly one expert in every K slice);
             # the slabs are indexed by the y row, so that launch's M is the T*k output rows
-            # (Mixtral-8x7B: B=256 28.5 vs 30.9 ms/step at 4 slices, B=128 25.8 vs 25.1: from ~48 rows per
-            # expert on, profiles/moe_down_splitk.txt)
-            kdn = int(os.environ.get("NLS_MOE_KS_DN", "4"))
+            # (Mixtral-8x7B before the NA tiles: B=256 28.5 vs 30.9 ms/step at 4 slices; with them the
+            # unsplit rt-4 launch is faster, 19.6 vs 20.6: off by default, profiles/moe_down_splitk.txt)
             if kdn > 1 and len(self.experts) <= 8 and not self.ep and T * k >= 48 * len(self.experts):
                 dn["ks"] = kdn
                 dn_rows = T * k

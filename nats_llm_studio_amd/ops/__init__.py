@@ -228,13 +228,15 @@ def gemv_config(segs: Sequence[Seg], M: int):
 
 
 def _seg_arr(segs: Sequence[Seg], mode: int):
-    """ctypes segment list of a launch: modes 4/5 point at the row-major f16 copies."""
+    """ctypes segment list of a launch: modes 4/5 point at the row-major f16 copies (MoE row maps
+    included: the dense GEMM gathers/scatters mapped rows like mode 2)."""
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
         if mode in (4, 5, 6):
             if s.w.d16 is None:
                 raise ValueError(f"{s.w.name}: mode 4 needs QWeight.expand_dense()")
-            arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), None, None, None, 1, s.w.rows, s.w.K, s.ycol)
+            arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, s.w.rows, s.w.K,
+                                 s.ycol)
         else:
             arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
                                  s.w.K, s.ycol)

@@ -189,9 +189,11 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
             srv.stop()
             if started:
                 engine.shutdown()
-    comp, good, rtts, ttft, gen = 0, 0, [], [], []
+    comp, good, rtts, ttft, gen, errors = 0, 0, [], [], [], []
     for i, b in bodies.items():
         r = json.loads(b)
+        if not (r.get("ok") and r["data"].get("http_status") == 200) and len(errors) < 3:
+            errors.append(b[:300].decode("utf-8", "replace"))
         if r.get("ok") and r["data"].get("http_status") == 200:
             good += 1
             resp = r["data"]["response"]
@@ -207,7 +209,7 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
             "rtt_p50_ms": round(_pct(rtts, 50), 1) if rtts else None,
             "rtt_p99_ms": round(_pct(rtts, 99), 1) if rtts else None,
             "ttft_p50_ms": round(_pct(ttft, 50), 1) if ttft else None,
-            "generation_p50_ms": round(_pct(gen, 50), 1) if gen else None}
+            "generation_p50_ms": round(_pct(gen, 50), 1) if gen else None, "errors": errors}
 
 
 if __name__ == "__main__":

@@ -125,10 +125,13 @@ def test_qgemv_mapped_rows(gpu):
     assert (y[1].cpu() == 7.0).all()
 
 
-@pytest.mark.parametrize("T,rt,qt", [(200, 2, GGMLType.Q4_K), (300, 4, GGMLType.Q5_K), (150, 1, GGMLType.Q6_K)])
-def test_qgemm_mapped_moe(gpu, T, rt, qt):
-    """Grouped MoE GEMM (mode 2, mapped rows): one route over T tokens, SwiGLU gate/up and f32 down
-    over every expert in one launch each, against the per-row fp32 reference."""
+@pytest.mark.parametrize("T,rt,qt,mode,waves", [(200, 2, GGMLType.Q4_K, 2, 8), (300, 4, GGMLType.Q5_K, 2, 8),
+                                                (150, 1, GGMLType.Q6_K, 2, 8), (200, 2, GGMLType.Q4_K, 5, 8),
+                                                (300, 4, GGMLType.Q5_K, 4, 16), (150, 2, GGMLType.Q6_K, 4, 8)])
+def test_qgemm_mapped_moe(gpu, T, rt, qt, mode, waves):
+    """Grouped MoE GEMM (mapped rows; mode 2 = LDS dequant, modes 4/5 = dense DMA GEMM on the experts'
+    f16 copies): one route over T tokens, SwiGLU gate/up and f32 down over every expert in one launch
+    each, against the per-row fp32 reference."""
     E, k, K, F = 4, 2, 512, 256
     logits = torch.randn(T, E, device=gpu)
     cap = T
@@ -146,17 +149,20 @@ def test_qgemm_mapped_moe(gpu, T, rt, qt):
         G.append(ops.QWeight(g_raw, qt, F, K, "cpu").dense())
         U.append(ops.QWeight(u_raw, qt, F, K, "cpu").dense())
     dns = [_qw(K, F, qt, gpu, 40 + e) for e in range(E)]
+    if mode >= 4:
+        for w in gus + [d[0] for d in dns]:
+            w.expand_dense()
     x = _x(T, K, gpu)
     act = torch.zeros(T * k, F, dtype=ops.ACT_DTYPE, device=gpu)
     yexp = torch.full((T * k, K), 5.0, device=gpu)
-    cfg = dict(mode=2, waves=8, rt=rt, ks=1)
+    cfg = dict(mode=mode, waves=waves, rt=rt, ks=1)
     segs = [ops.Seg(gus[e], 0, xrows[e * cap:], yrows[e * cap:], counts[e:e + 1]) for e in range(E)]
     ops.qgemv(segs, x, act, T, epi="swiglu", **cfg)
     segs = [ops.Seg(dns[e][0], 0, yrows[e * cap:], yrows[e * cap:], counts[e:e + 1]) for e in range(E)]
     ops.qgemv(segs, act, yexp, T, epi="f32", **cfg)
     # mapped split-K (the MoE down projection at many tokens): slabs by y row, launch M = T*k rows
     yks = torch.full((T * k, K), 7.0, device=gpu)
-    ops.qgemv(segs, act, yks, T * k, epi="f32", mode=2, waves=8, rt=rt, ks=3)
+    ops.qgemv(segs, act, yks, T * k, epi="f32", mode=mode, waves=waves, rt=rt, ks=3)
     torch.cuda.synchronize()
     _close(yks, yexp, 1e-3)
     cnt, xr, yr = counts.cpu(), xrows.cpu(), yrows.cpu()
@@ -453,6 +459,27 @@ def test_sample_kernel(gpu):
     g2 = [torch.Generator().manual_seed(7) for _ in range(8)]
     pp = [SamplingParams(temperature=1.5)] * 8
     assert sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g1) == sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g2)
+
+
+def test_sample_and_embed_never_emit_wild_ids(gpu):
+    """A non-finite logit row (all NaN / -inf) still yields an id inside the vocabulary from both the
+    greedy and the sampling branch, and the embedding gather clamps ids: chained decode feeds sampled
+    ids back on the device, so neither may turn into an out-of-range address."""
+    from nats_llm_studio_amd.engine.sampling import SamplingParams, sample_rows_gpu
+    V = 3000
+    lg = torch.full((4, V), float("nan"), device=gpu)
+    lg[2:] = float("-inf")
+    ps = [SamplingParams(), SamplingParams(temperature=0.7, top_p=0.95, top_k=40)] * 2
+    toks = sample_rows_gpu(lg, ps, [[]] * 4, [None] * 4)
+    assert all(0 <= t < V for t in toks), toks
+    raw = Q.random_blocks(GGMLType.Q4_K, 50 * 512, 0.05, np.random.default_rng(11))
+    qw = ops.QWeight(raw, GGMLType.Q4_K, 50, 512, gpu, layout="rows")
+    Wd = ops.QWeight(raw, GGMLType.Q4_K, 50, 512, "cpu").dense()
+    ids = torch.tensor([-1, 50, 1 << 30, 3], dtype=torch.int32, device=gpu)
+    e = torch.zeros(4, 512, device=gpu)
+    ops.embed(ids, qw, e, 4)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(e.cpu(), Wd[[0, 49, 49, 3]], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("M,cfg", [(5, (1, 8, 1, 4)), (64, (1, 4, 1, 2)), (200, (1, 8, 1, 3)), (200, (1, 8, 1, 1)),
