@@ -86,7 +86,12 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
   const int r32 = lane & 31, h32 = lane >> 5;
 
-  u32x4 xr[NXU];
+  // activation register ring: the quarter stored into LDS at step j was loaded XR steps earlier. vmcnt
+  // retires loads in issue order, so the first x load issued after a raw-weight load bounds how long
+  // that HBM load may take: XR = 4 gives it 5 quarter steps (XR = 1: 2). Four stages where registers
+  // allow (<= 2 chunks per thread: every block of <= 128 rows, i.e. MoE experts and small batches).
+  constexpr int XR = NXU <= 2 ? 4 : 1;
+  u32x4 xr[XR][NXU];
   // the activation row each thread stages (fixed for the whole K loop); rows >= M only feed
   // outputs that are never stored: clamp, never branch. xm: MoE gather (block-local row -> x row)
   int xrow[NXU];
@@ -95,18 +100,18 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     const int row = min((int)((threadIdx.x + 512 * u) >> 3), M - 1);
     xrow[u] = xm ? xm[row] : row;
   }
-  auto load_x = [&](int sb, int q) __attribute__((always_inline)) {
+  auto load_x = [&](int st, int sb, int q) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NXU; ++u) {
       const int ch = (threadIdx.x + 512 * u) & 7;
-      xr[u] = ld16(a.x + (size_t)xrow[u] * a.ldx + sb * 256 + q * 64 + ch * 8);
+      xr[st][u] = ld16(a.x + (size_t)xrow[u] * a.ldx + sb * 256 + q * 64 + ch * 8);
     }
   };
-  auto store_x = [&](int buf) __attribute__((always_inline)) {
+  auto store_x = [&](int st, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NXU; ++u) {
       const int idx = threadIdx.x + 512 * u, row = idx >> 3, ch = idx & 7;
-      *reinterpret_cast<u32x4*>(Xs + buf * XS + row * 64 + ((ch ^ (row & 7)) << 3)) = xr[u];
+      *reinterpret_cast<u32x4*>(Xs + buf * XS + row * 64 + ((ch ^ (row & 7)) << 3)) = xr[st][u];
     }
   };
   typedef typename RawOf<T>::type Raw;
@@ -183,53 +188,53 @@ DEVI void lds_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   if (sb0 < sb1) {
     rA = load_raw<T, true>(W, drow, sb0, g);
     rB = load_raw<T, true>(W, drow, min(sb0 + 1, sbl), g);
-    load_x(sb0, 0);
+    load_x(0, sb0, 0);
+#pragma unroll
+    for (int t = 1; t < XR; ++t) load_x(t, min(sb0 + t / 4, sbl), t % 4);   // quarters 1 .. XR-1
     prep_sc<T>(rA, g, sA);
-    store_x(0);
+    store_x(0, 0);
     deq_w(rA, sA, 0, 0);
-    load_x(sb0, 1);
+    load_x(0, min(sb0 + XR / 4, sbl), XR % 4);                                // quarter XR
   }
   __syncthreads();
-  // one super-block = 4 quarter steps; buffer parity = quarter & 1. Every load is unconditional
-  // (indices clamped): a conditional load breaks hipcc's vmcnt bookkeeping (qgemv_impl.h).
-  auto sb_step = [&](Raw& rc, Sc& sc, Raw& rn, Sc& sn, int sb) __attribute__((always_inline)) {
-    const int nx = min(sb + 1, sbl);
-    // Each step: write the x registers loaded one step ago into LDS, re-issue the next x loads
-    // at once (sched_barrier: hipcc would otherwise sink them to the end of the step, right
-    // before their use after the barrier), then dequant of the next W quarter + the MFMAs.
-    // q = 0
-    store_x(1);
-    load_x(sb, 2);
+  // One quarter step qq (0..3) of super-block sb; jj = quarter index within the unrolled pair of
+  // super-blocks (register stage (jj + 1) % XR holds quarter jj + 1). Buffer parity = quarter & 1.
+  // Every load is unconditional (indices clamped): a conditional load breaks hipcc's vmcnt
+  // bookkeeping (qgemv_impl.h). Each step: write the x registers of the next quarter into LDS,
+  // re-issue that stage's load XR quarters ahead at once (sched_barrier: hipcc would otherwise sink
+  // it to the end of the step), then the dequant of the next W quarter + this quarter's MFMAs.
+  auto qstep = [&](Raw& rc, Sc& sc, Raw& rn, Sc& sn, int sb, int qq, int jj) __attribute__((always_inline)) {
+    const int st = (jj + 1) % XR;
+    store_x(st, (qq + 1) & 1);
+    const int lq = qq + 1 + XR;
+    load_x(st, min(sb + lq / 4, sbl), lq % 4);
     __builtin_amdgcn_sched_barrier(0);
-    step_mma(rc, sc, 1, 0);
-    __syncthreads();
-    // q = 1
-    store_x(0);
-    load_x(sb, 3);
-    __builtin_amdgcn_sched_barrier(0);
-    step_mma(rc, sc, 2, 1);
-    __syncthreads();
-    // q = 2: last use of rc -> reload it two super-blocks ahead
-    store_x(1);
-    load_x(nx, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    step_mma(rc, sc, 3, 0);
-    rc = load_raw<T, true>(W, drow, min(sb + 2, sbl), g);
-    __syncthreads();
-    // q = 3: stage quarter 0 of the next super-block
-    store_x(0);
-    load_x(nx, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    prep_sc<T>(rn, g, sn);
-    step_mma(rn, sn, 0, 1);
+    if (qq < 3) {
+      step_mma(rc, sc, qq + 1, qq & 1);
+      if (qq == 2) rc = load_raw<T, true>(W, drow, min(sb + 2, sbl), g);   // last use of rc: 2 super-blocks ahead
+    } else {                                                               // quarter 0 of the next super-block
+      prep_sc<T>(rn, g, sn);
+      step_mma(rn, sn, 0, 1);
+    }
     __syncthreads();
   };
   int sb = sb0;
   for (; sb + 1 < sb1; sb += 2) {
-    sb_step(rA, sA, rB, sB, sb);
-    sb_step(rB, sB, rA, sA, sb + 1);
+    qstep(rA, sA, rB, sB, sb, 0, 0);
+    qstep(rA, sA, rB, sB, sb, 1, 1);
+    qstep(rA, sA, rB, sB, sb, 2, 2);
+    qstep(rA, sA, rB, sB, sb, 3, 3);
+    qstep(rB, sB, rA, sA, sb + 1, 0, 4);
+    qstep(rB, sB, rA, sA, sb + 1, 1, 5);
+    qstep(rB, sB, rA, sA, sb + 1, 2, 6);
+    qstep(rB, sB, rA, sA, sb + 1, 3, 7);
   }
-  if (sb < sb1) sb_step(rA, sA, rB, sB, sb);
+  if (sb < sb1) {
+    qstep(rA, sA, rB, sB, sb, 0, 0);
+    qstep(rA, sA, rB, sB, sb, 1, 1);
+    qstep(rA, sA, rB, sB, sb, 2, 2);
+    qstep(rA, sA, rB, sB, sb, 3, 3);
+  }
 
   // ---- epilogue from the accumulators ------------------------------------------------------------
   // 16x16 tiles: lane holds weight row rbase + 16j + r and activation rows 16(i*WM + wm) + 4g + e;

@@ -93,7 +93,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0 && ks > 1 && !ws) return -1;
   if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
   // mapped split-K (MoE down projection at many tokens): slabs indexed by the y row, one reduce
-  bool mks = (mode == 2 || mode == 4 || mode == 5) && ks > 1 && epi == EPI_F32 && !argmax;
+  bool mks = (mode == 1 || mode == 2 || mode == 4 || mode == 5) && ks > 1 && epi == EPI_F32 && !argmax;
   for (int i = 0; i < nseg && mks; ++i)
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
@@ -102,11 +102,11 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
-    // mapped rows (MoE): path A, or the LDS-dequant / dense GEMMs (modes 2, 4, 5) without arg-max;
-    // split-K only as "mapped split-K" (every segment an expert writing the same output columns of
-    // its own y rows, f32 store)
+    // mapped rows (MoE): path A, or path B / the LDS-dequant / dense GEMMs (modes 1, 2, 4, 5) without
+    // arg-max; split-K only as "mapped split-K" (every segment an expert writing the same output
+    // columns of its own y rows, f32 store)
     if ((segs[i].xmap || segs[i].ymap || segs[i].mcount) && mode != 0 &&
-        (!(mode == 2 || mode == 4 || mode == 5) || argmax || epi == EPI_SLABS || (ks > 1 && !mks)))
+        (!(mode == 1 || mode == 2 || mode == 4 || mode == 5) || argmax || epi == EPI_SLABS || (ks > 1 && !mks)))
       return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;

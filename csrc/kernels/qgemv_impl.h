@@ -507,8 +507,13 @@ DEVI int lds_off(int row, int k) {            // element offset in a [rows][256]
 // XL (few rows, MT = 1): the workgroup's whole x slice [M][K/ks] is staged in LDS once, so the main
 // loop issues only weight loads -- no per-step global x load whose in-order vmcnt wait would drain the
 // DEPTH-deep weight prefetch, and no per-step barrier (batch-1 gate|up / down / lm_head streaming).
-template <int T, int WAVES, int RT, int MT, bool XL = false>
-DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds) {
+// NA: activation tiles actually multiplied (<= MT, the LDS allocation): MoE blocks carry a device-side
+// row count, so a 128-row block with ~64 routed rows runs 4 tiles, not 8. xm / ym: MoE row maps
+// (block-local row -> x row / y row; nullptr: plain rows).
+template <int T, int WAVES, int RT, int MT, bool XL = false, int NA = MT>
+DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds,
+                  const int* xm = nullptr, const int* ym = nullptr) {
+  static_assert(NA >= 1 && NA <= MT, "active tiles exceed the staged tile");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -522,11 +527,11 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   for (int rt = 0; rt < RT; ++rt) rowc[rt] = min(base + rt * 16 + r, S.rows - 1);
 
   constexpr int NT = WAVES * 64;
-  f32x4 acc[RT][MT];
+  f32x4 acc[RT][NA];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < NA; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if constexpr (XL) {
     static_assert(MT == 1, "XL stages one activation tile");
@@ -598,19 +603,30 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     for (int d = 0; d < DEPTH - 1; ++d)
       if (sb + d < sb1) step(wb[d], sb + d);
   } else {
-  constexpr int NCH = (MT * 16 * 32) / NT;               // 16-B chunks staged per thread
-  static_assert((MT * 16 * 32) % NT == 0, "staging must divide evenly");
+  constexpr int NCH = (NA * 16 * 32) / NT;               // 16-B chunks staged per thread (active rows)
+  static_assert((NA * 16 * 32) % NT == 0, "staging must divide evenly");
   // large tiles stage x in two halves (half the staging registers)
-  constexpr bool SPLITX = MT >= 4 && NCH % 2 == 0;
+  constexpr bool SPLITX = NA >= 4 && NCH % 2 == 0;
   constexpr int NCHR = SPLITX ? NCH / 2 : NCH;
   u32x4 xst[NCHR];
+  // source row of each staged chunk (fixed for the whole K loop): rows >= M only feed output rows that
+  // are never stored -- clamp, never branch; MoE blocks gather through xm
+  // (two 16-bit row indices per register: the 8-tile instance sits at the 256-VGPR limit)
+  uint32_t xsr[(NCH + 1) / 2];
+#pragma unroll
+  for (int c = 0; c < (NCH + 1) / 2; ++c) xsr[c] = 0u;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int row = min((int)((threadIdx.x + c * NT) >> 5), M - 1);
+    xsr[c >> 1] |= (uint32_t)(xm ? xm[row] : row) << (16 * (c & 1));
+  }
   auto load_xh = [&](int sb, int h) {
 #pragma unroll
     for (int c = 0; c < NCHR; ++c) {
       const int idx = threadIdx.x + (c + h * NCHR) * NT;
-      const int row = idx >> 5, ch = idx & 31;
-      // rows >= M only feed output rows that are never stored: clamp, never branch
-      xst[c] = ld16(a.x + (size_t)min(row, M - 1) * a.ldx + sb * 256 + ch * 8);
+      const int ch = idx & 31, cc = c + h * NCHR;
+      const uint32_t row = (xsr[cc >> 1] >> (16 * (cc & 1))) & 0xFFFFu;
+      xst[c] = ld16(a.x + (size_t)row * a.ldx + sb * 256 + ch * 8);
     }
   };
   auto store_xh = [&](int buf, int h) {
@@ -675,7 +691,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
         for (int rt = 0; rt < RT; ++rt) wt[rt] = frag_t<T>(w[rt], sc[rt], t);
         const int ko = xoff<T>(t, g);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int mt = 0; mt < NA; ++mt) {
           const f16x8 xa = *reinterpret_cast<const f16x8*>(xb + lds_off(mt * 16 + r, ko));
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
@@ -698,7 +714,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       for (int t = 0; t < 8; ++t) {
         const int ko = xoff<T>(t, g);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int mt = 0; mt < NA; ++mt) {
           const f16x8 xa = *reinterpret_cast<const f16x8*>(xb + lds_off(mt * 16 + r, ko));
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
@@ -738,11 +754,15 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       const int row = base + rt * 16 + r;
       if (row >= S.rows) continue;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < NA; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int b = mt * 16 + 4 * g + i;
-          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][i];
+          if (b >= M) continue;
+          if (ym)        // mapped split-K: slab row = the token's y row, columns shared by every expert
+            ws[((size_t)kslice * a.mtot + ym[b]) * ntot + S.ycol + row] = acc[rt][mt][i];
+          else
+            ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][i];
         }
     }
     return;
@@ -751,7 +771,7 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   for (int rt = 0; rt < RT; ++rt) {
     const int row = base + rt * 16 + r;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < NA; ++mt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int b = mt * 16 + 4 * g + i;
@@ -760,12 +780,12 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           const float u = __shfl_xor(v, 8, 64);
           if (r < 8 && b < M && row < S.rows) {
             const int n = S.ycol + ((base + rt * 16) >> 1) + r;
-            reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
+            reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
           }
           continue;
         }
         if (b < M && row < S.rows) {
-          const size_t off = (size_t)b * a.ldy + S.ycol + row;
+          const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
           if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
           else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
           else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
@@ -784,11 +804,27 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   }
 }
 
+// Active-tile dispatch: only the 8-wave, 2-row-tile, 8-tile instance (the MoE grouped launch) picks NA
+// per block -- {2, 4, 6, 8}, rounded up to even to bound the instantiations; the rest run NA = MT.
+template <int T, int WAVES, int RT, int MT, bool XL>
+DEVI void mm_tile_na(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, act_t* lds,
+                     const int* xm, const int* ym) {
+  if constexpr (MT == 8 && WAVES == 8 && RT == 2 && !XL) {
+    const int na = ((a.M + 15) / 16 + 1) & ~1;
+    if (na <= 2) mm_tile<T, WAVES, RT, MT, XL, 2>(S, row0, kslice, ks, a, ws, lds, xm, ym);
+    else if (na <= 4) mm_tile<T, WAVES, RT, MT, XL, 4>(S, row0, kslice, ks, a, ws, lds, xm, ym);
+    else if (na <= 6) mm_tile<T, WAVES, RT, MT, XL, 6>(S, row0, kslice, ks, a, ws, lds, xm, ym);
+    else mm_tile<T, WAVES, RT, MT, XL, 8>(S, row0, kslice, ks, a, ws, lds, xm, ym);
+  } else {
+    mm_tile<T, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, lds, xm, ym);
+  }
+}
+
 template <int WAVES, int RT, int MT, int KSET, bool XL = false>
 __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                          int nmb) {
   extern __shared__ __attribute__((aligned(16))) act_t xlds[];
-  int tile, kslice = 0;
+  int tile, kslice = 0, mb = 0;
   if (nmb > 1) {
     // Large M (prefill / big decode batches): blocks of MT*16 activation rows. The workgroups
     // sharing one weight tile are placed on ONE XCD (dispatch assigns workgroup i to XCD i % 8),
@@ -796,16 +832,9 @@ __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs 
     // With split-K (ks > 1) the K slices of a tile are also kept on its XCD.
     const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
     kslice = j % ks;
-    const int mb = (j / ks) % nmb;
+    mb = (j / ks) % nmb;
     tile = (j / ks / nmb) * 8 + xcd;
     if (tile >= ntiles) return;
-    const int m0 = mb * MT * 16;
-    a.m0 = m0;
-    a.x += (size_t)m0 * a.ldx;
-    const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-    a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-    if (a.argmax) a.argmax += m0;
-    a.M = min(MT * 16, a.M - m0);
   } else {
     tile = blockIdx.x / ks;
     kslice = blockIdx.x % ks;
@@ -814,25 +843,38 @@ __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs 
 #pragma unroll
   for (int i = 1; i < 8; ++i)
     if (i < segs.nseg && tile >= segs.s[i].tile_begin) S = segs.s[i];
+  // MoE grouped launch: the expert's routed-row count lives on the device; m-blocks past it exit
+  // before reading any weights (the grid is sized for every token on one expert)
+  const int m0 = mb * MT * 16;
+  const int mrows = S.mcount ? min(*S.mcount, a.M) : a.M;
+  if (m0 >= mrows) return;
+  const int* xm = S.xmap ? S.xmap + m0 : nullptr;
+  const int* ym = S.ymap ? S.ymap + m0 : nullptr;
+  a.m0 = m0;
+  if (!xm) a.x += (size_t)m0 * a.ldx;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+  if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (a.argmax) a.argmax += m0;
+  a.M = min(MT * 16, mrows - m0);
   const int row0 = (tile - S.tile_begin) * WAVES * RT * 16;
   if constexpr (KSET == 0) {
     switch (S.type) {
-      case QT_Q4_K: mm_tile<QT_Q4_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q4_K: mm_tile_na<QT_Q4_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_Q6_K: mm_tile_na<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
       default: break;
     }
   } else if constexpr (KSET == 1) {
     switch (S.type) {
-      case QT_Q5_K: mm_tile<QT_Q5_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q6_K: mm_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_Q8_0: mm_tile<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_Q5_K: mm_tile_na<QT_Q5_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_Q6_K: mm_tile_na<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_Q8_0: mm_tile_na<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
       default: break;
     }
   } else {
     switch (S.type) {
-      case QT_F16: mm_tile<QT_F16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_BF16: mm_tile<QT_BF16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
-      case QT_F32: mm_tile<QT_F32, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds); break;
+      case QT_F16: mm_tile<QT_F16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_BF16: mm_tile<QT_BF16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_F32: mm_tile<QT_F32, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
       default: break;
     }
   }

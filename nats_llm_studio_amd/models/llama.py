@@ -34,6 +34,10 @@ _SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgr
 # fewest keys per flash-decoding split (0: the kernel's context-adaptive policy, attention.hip
 # split_chunk: 64 keys below 1K of context, 128 above)
 _MIN_CHUNK = int(os.environ.get("NLS_ATTN_MIN_CHUNK", "0"))
+# MoE: tokens per step above which the experts run as ONE grouped LDS-dequant GEMM launch (below: path-A
+# GEMVs over each expert's gathered rows)
+# (Mixtral-8x7B: B=64 15.2 vs 28.9 ms/step, B=32 15.2 vs 15.6, B=16 14.8 vs 9.7; scripts/gpu_moe_thresh.sh)
+_MOE_GEMM_T = int(os.environ.get("NLS_MOE_GEMM_T", "16"))
 # MoE expert GEMMs on the experts' f16 copies: (mode, waves, rt[, ks]) of gate/up and down
 _MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2").split(","))
 _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
@@ -474,7 +478,7 @@ class LlamaModel:
         # few tokens: path-A GEMV over each expert's gathered rows; many tokens: ONE route and the
         # LDS-dequant GEMM (mode 2) over all experts, each m-block of an expert gathering its rows
         # through xrows and exiting when it lies past the expert's device-side count
-        gemm = T > 64 and self.device.type == "cuda"
+        gemm = T > _MOE_GEMM_T and self.device.type == "cuda"
         # path-A chunks of <= 32 tokens: the mapped GEMV then runs with <= 2 activation tiles, whose
         # kernels keep every fragment in registers (3-4 tiles spill: -Rpass-analysis scratch > 0)
         step = T if gemm else 32
@@ -491,8 +495,15 @@ class LlamaModel:
             dn = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_DN[:3]), ks=1)
             kdn = _MOE_DENSE_DN[3] if len(_MOE_DENSE_DN) > 3 else 1
         elif gemm:
-            gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", 4)), ks=1)
-            dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", 4)), ks=1)
+            # few routed rows per expert: 128-row blocks (64 KiB of LDS, two workgroups per CU hide each
+            # other's dequant/barrier waits; Mixtral B=64: 13.8 vs 15.2 ms/step), else 256-row blocks
+            rt = 2 if T * k < 32 * E else 4
+            gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", rt)), ks=1)
+            dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", rt)), ks=1)
+            if os.environ.get("NLS_MOE_QCFG_GU"):      # explicit (mode, waves, rt) overrides
+                gu = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_GU"].split(","))), ks=1)
+            if os.environ.get("NLS_MOE_QCFG_DN"):
+                dn = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_DN"].split(","))), ks=1)
             kdn = int(os.environ.get("NLS_MOE_KS_DN", "1"))
         if gemm:
             # down projection (K = d_ff): split K over workgroups when ONE launch covers every routed row
