@@ -409,6 +409,26 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
   }
 }
 
+// SwiGLU pass after a library GEMM on the gate/up weights (ops "mode 7"): the GEMM's f16 output h keeps
+// the weights' [g0..g7, u0..u7] interleave per 16 columns, so out[m, 8j + i] = silu(alpha * h[m, 16j + i]) *
+// alpha * h[m, 16j + 8 + i]. One thread per 8 outputs: two 16-B loads, one 16-B store (HBM-bound).
+__global__ __launch_bounds__(256) void swiglu16_kernel(const act_t* __restrict__ h, long ldh, int ng, float alpha,
+                                                       act_t* __restrict__ out, long ldo) {
+  const int m = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= ng) return;
+  const act_t* src = h + (size_t)m * ldh + 16 * j;
+  const f16x8 g = *reinterpret_cast<const f16x8*>(src);
+  const f16x8 u = *reinterpret_cast<const f16x8*>(src + 8);
+  f16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float gv = alpha * (float)g[i];
+    o[i] = (act_t)(gv / (1.f + __expf(-gv)) * (alpha * (float)u[i]));
+  }
+  *reinterpret_cast<f16x8*>(out + (size_t)m * ldo + 8 * j) = o;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -469,6 +489,15 @@ int nls_dequant(const void* w, int type, int rows, int K, void* out, long ldo, v
     case QT_F32: hipLaunchKernelGGL(dequant_kernel<QT_F32>, grid, dim3(256), 0, st, W, o, ldo); break;
     default: return -1;
   }
+  return (int)hipGetLastError();
+}
+
+// h: f16 [M, ncol] (interleaved gate/up GEMM output, row stride ldh); out: f16 [M, ncol / 2] (stride ldo)
+int nls_swiglu16(const void* h, long ldh, int M, int ncol, float alpha, void* out, long ldo, void* stream) {
+  if (M < 1 || ncol % 16 || ldh % 8 || ldo % 8 || ((uintptr_t)h & 15) || ((uintptr_t)out & 15)) return -1;
+  const int ng = ncol / 16;
+  hipLaunchKernelGGL(swiglu16_kernel, dim3((ng + 255) / 256, M), dim3(256), 0, (hipStream_t)stream,
+                     (const act_t*)h, ldh, ng, alpha, (act_t*)out, ldo);
   return (int)hipGetLastError();
 }
 

@@ -92,6 +92,17 @@ def select_dense(segs, M: int):
     return hit if hit is not None else dense_heuristic(segs, M)
 
 
+def lib_key(segs, M: int) -> str:
+    return f"L:{sum(s.w.rows for s in segs)}:{segs[0].w.K}:{_mb(M)}"
+
+
+def select_lib(segs, M: int) -> bool:
+    """Did the library GEMM (hipBLASLt on the f16 copies + a separate epilogue pass, ops "mode 7")
+    measure faster than the hand-written large-M kernels for this shape and batch bucket
+    (tools/blaslt_ab.py)? Only shapes with an entry take it."""
+    return bool(table().get(lib_key(segs, M), (0,))[0])
+
+
 def select(segs, M: int):
     hit = table().get(key(segs, M))
     return hit if hit is not None else heuristic(segs, M)

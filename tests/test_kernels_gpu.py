@@ -758,6 +758,73 @@ def test_hgemm_dense_swiglu_multiseg_auto(gpu, mode, ks, wv):
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
 
 
+@pytest.mark.parametrize("M", [65, 300, 512])
+def test_lib_gemm_mode7(gpu, M):
+    """Mode 7: hipBLASLt GEMM on the f16 copies + the HIP SwiGLU pass (interleaved gate/up) / plain f32
+    store of a concatenated Q|K|V launch; vs the fp32 oracle. Then the automatic selection: mode 7
+    only for shapes with an "L:" tuning entry, never with an arg-max or a non-contiguous output."""
+    K, F = 512, 256
+    rng = np.random.default_rng(11)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    w.expand_dense()
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    x = _x(M, K, gpu)
+    xf = x[:M].float().cpu()
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=7)
+    _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
+    assert float(y[M:].abs().max().cpu()) == 0.0 if M < x.shape[0] else True
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(128, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(128, K, GGMLType.Q6_K, gpu, 3)
+    for q in (a, b, c):
+        q.expand_dense()
+    segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)]
+    yq = torch.zeros(x.shape[0], 512, device=gpu)
+    ops.qgemv(segs, x, yq, M, mode=7)                 # unfused: a separate concatenated copy
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+    d16 = [s.w.d16 for s in segs]
+    ops.fuse_dense(segs)                              # after a launch: a no-op (copies never move)
+    assert all(s.w.d16.data_ptr() == p.data_ptr() for s, p in zip(segs, d16))
+    fresh = [_qw(256, K, GGMLType.Q4_K, gpu, 1)[0], _qw(128, K, GGMLType.Q4_K, gpu, 2)[0],
+             _qw(128, K, GGMLType.Q6_K, gpu, 3)[0]]
+    for q in fresh:
+        q.expand_dense()
+    segs = [ops.Seg(fresh[0], 0), ops.Seg(fresh[1], 256), ops.Seg(fresh[2], 384)]
+    ops.fuse_dense(segs)                              # at load: the copies become views of one matrix
+    base = segs[0].w.d16.data_ptr()
+    assert [s.w.d16.data_ptr() - base for s in segs] == [0, 256 * K * 2, 384 * K * 2]
+    yq.zero_()
+    ops.qgemv(segs, x, yq, M, mode=7)
+    ref = xf @ torch.cat([Ad, Bd, Cd]).t()
+    _close(yq[:M], ref)
+    # the segments' f16 copies are now views into the concatenation: the fused kernels still agree
+    y4 = torch.zeros_like(yq)
+    ops.qgemv(segs, x, y4, M, mode=4, waves=8, rt=4, ks=1)
+    _close(y4[:M], yq[:M], 1e-3)
+    from nats_llm_studio_amd.ops import tuning
+    tab = tuning.table()
+    key = tuning.lib_key(segs, M)
+    try:
+        tab[key] = (1,)
+        if M < ops.DENSE_MIN_M:              # below the dense-GEMM threshold: never mode 7
+            assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
+            return
+        assert ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
+        assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, torch.zeros(4, dtype=torch.int64, device=gpu), yq)
+        assert not ops.lib_gemm_ok(segs, M, "add", 1.0, None, yq)
+        assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, torch.zeros(x.shape[0], 520, device=gpu))
+        yq.zero_()
+        ops.qgemv(segs, x, yq, M)            # auto: mode 7
+        _close(yq[:M], ref)
+    finally:
+        tab.pop(key, None)
+    assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
+
+
 def test_hgemm_dense_add_rmsnorm_slabs(gpu):
     """Mode 4 split-K slabs feeding the fused reduce + residual + RMSNorm kernel (o / down projections)."""
     D, K, M = 512, 1024, 200

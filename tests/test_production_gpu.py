@@ -24,8 +24,9 @@ from nats_llm_studio_amd.ops import tuning
 pytestmark = pytest.mark.gpu
 
 _TABLE = json.load(open(tuning._PATH))
-_SHAPES = sorted({k.rsplit(":", 1)[0] for k in _TABLE if not k.startswith("d:")})
+_SHAPES = sorted({k.rsplit(":", 1)[0] for k in _TABLE if not k.startswith(("d:", "L:"))})
 _DENSE = sorted({k.rsplit(":", 1)[0] for k in _TABLE if k.startswith("d:")})
+_LIB = sorted({k.rsplit(":", 1)[0] for k in _TABLE if k.startswith("L:")})
 
 
 def _weights(types, rows, K, dev, rng):
@@ -97,6 +98,48 @@ def test_dense_tuning_entries_at_real_shapes(gpu, shape):
         err = (got - ref).abs().max().item()
         assert err <= 2e-2 * ref.abs().max().item(), f"{k} cfg={cfg}: err {err:.4g}"
         assert not torch.isnan(y).any(), f"{k} cfg={cfg}: unwritten outputs"
+        del x, y
+    del segs, Wd
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("shape", _LIB)
+def test_lib_gemm_entries_at_real_shapes(gpu, shape):
+    """Every mode-7 entry ("L:<rows>:<K>:<M>": hipBLASLt on the f16 copies + epilogue pass) at its real
+    shape and M bucket, selected automatically: f32 store for every shape, SwiGLU for the gate/up shape."""
+    _, rows_s, K_s = shape.split(":")
+    rows, K = int(rows_s), int(K_s)
+    rng = np.random.default_rng(abs(hash(shape)) % (1 << 31))
+    types = [12, 12, 14] if rows == 6144 else [14 if rows > 100000 else 12]
+    segs, Wd = _weights(types, rows, K, gpu, rng)
+    for s in segs:
+        s.w.expand_dense()
+    sample = torch.from_numpy(np.sort(rng.choice(rows // 16, size=min(rows // 16, 256), replace=False))).to(gpu)
+    rsel = (sample[:, None] * 16 + torch.arange(16, device=gpu)[None, :]).reshape(-1)   # whole 16-row groups
+    Ws = Wd.index_select(0, rsel).float()
+    g = torch.Generator(device="cpu").manual_seed(13)
+    for k, cfg in sorted(_TABLE.items()):
+        if not k.startswith(shape + ":") or not cfg[0]:
+            continue
+        M = int(k.rsplit(":", 1)[1])
+        x = (torch.randn(M, K, generator=g) * 0.5).to(ops.ACT_DTYPE).to(gpu)
+        y = torch.full((M, rows), float("nan"), device=gpu)
+        assert ops.lib_gemm_ok(segs, M, "f32", 1.0, None, y), k
+        ops.qgemv(segs, x, y, M)
+        ref = x.float() @ Ws.t()
+        got = y.index_select(1, rsel)
+        err = (got - ref).abs().max().item()
+        assert err <= 2e-2 * ref.abs().max().item(), f"{k}: err {err:.4g}"
+        assert not torch.isnan(y).any(), f"{k}: unwritten outputs"
+        if rows == 28672:     # gate/up: interleaved [g0..g7, u0..u7] rows -> SwiGLU pass
+            a = torch.full((M, rows // 2), float("nan"), dtype=ops.ACT_DTYPE, device=gpu)
+            ops.qgemv(segs, x, a, M, epi="swiglu")
+            r4 = ref.view(M, -1, 2, 8)
+            want = (torch.nn.functional.silu(r4[:, :, 0]) * r4[:, :, 1]).reshape(M, -1)
+            cols = (sample[:, None] * 8 + torch.arange(8, device=gpu)[None, :]).reshape(-1)
+            got = a.index_select(1, cols).float()
+            assert (got - want).abs().max().item() <= 3e-2 * want.abs().max().item(), f"{k} swiglu"
+            del a
         del x, y
     del segs, Wd
     torch.cuda.empty_cache()
