@@ -223,9 +223,10 @@ def _contiguous_cols(segs: Sequence[Seg]) -> bool:
 
 
 def lib_gemm_ok(segs: Sequence[Seg], M: int, epi: str, alpha: float = 1.0, argmax=None, y=None) -> bool:
-    """May this launch run as mode 7 (library GEMM + epilogue pass)? Epilogues: SwiGLU (f16 out) and a
-    plain f32 store into a row-contiguous output; no arg-max, no row maps, no split-K slabs."""
-    if not LIB_GEMM or argmax is not None or epi not in ("swiglu", "f32") or not dense_ok(segs, M):
+    """May this launch run as mode 7 (library GEMM + epilogue pass)? Epilogues: SwiGLU (f16 out), a
+    plain f32 store into a row-contiguous output, and "addnorm" (one f32 slab for the fused residual add +
+    RMSNorm pass); no arg-max, no row maps."""
+    if not LIB_GEMM or argmax is not None or epi not in ("swiglu", "f32", "addnorm") or not dense_ok(segs, M):
         return False
     if not _contiguous_cols(segs):
         return False
@@ -490,6 +491,16 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
     launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel; a few-row
     path-A launch (M <= ADDNORM_MAX_M, `counter`: a zeroed int32 device word) normalises in its last
     workgroup, so the norm costs no launch at all."""
+    if (x.is_cuda and cfg is None and seg.ycol == 0 and seg.w.rows == x.shape[1]
+            and lib_gemm_ok([seg], M, "addnorm")):
+        # mode 7: the library GEMM writes ONE f32 slab, the split-K reduce kernel (ks = 1) adds it to the
+        # residual and normalises
+        ws = _workspace(x.device, M * seg.w.rows)
+        torch.mm(xin[:M], seg.w.d16.t(), out_dtype=torch.float32, out=ws[:M * seg.w.rows].view(M, seg.w.rows))
+        _lib.check(_lib.lib().nls_splitk_add_rmsnorm(ws.data_ptr(), 1, M, float(alpha), x.data_ptr(), x.stride(0),
+                                                     norm_w.data_ptr(), h.data_ptr(), h.stride(0), x.shape[1],
+                                                     float(eps), _stream_ptr(x)), "nls_splitk_add_rmsnorm")
+        return h
     if x.is_cuda and seg.xmap is None:
         mode, waves, rt, ks = cfg or gemv_config([seg], M)
         if (mode == 0 and counter is not None and M <= ADDNORM_MAX_M and seg.ycol == 0

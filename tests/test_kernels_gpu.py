@@ -820,8 +820,22 @@ def test_lib_gemm_mode7(gpu, M):
         yq.zero_()
         ops.qgemv(segs, x, yq, M)            # auto: mode 7
         _close(yq[:M], ref)
+        # residual add + RMSNorm: the library GEMM's single f32 slab through the fused reduce/norm kernel
+        o, Od = _qw(512, K, GGMLType.Q4_K, gpu, 5)
+        o.expand_dense()
+        tab[tuning.lib_key([ops.Seg(o)], M)] = (1,)
+        assert ops.lib_gemm_ok([ops.Seg(o)], M, "addnorm")
+        r = torch.randn(x.shape[0], 512, device=gpu)
+        r0 = r[:M].cpu().clone()
+        nw = torch.rand(512, device=gpu) + 0.5
+        hn = torch.zeros(x.shape[0], 512, dtype=ops.ACT_DTYPE, device=gpu)
+        ops.qgemv_add_rmsnorm(ops.Seg(o), x, r, nw, hn, M, 0.5, 1e-5)
+        want = r0 + 0.5 * xf @ Od.t()
+        _close(r[:M], want)
+        _close(hn[:M], want * torch.rsqrt(want.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu(), 2e-2)
     finally:
         tab.pop(key, None)
+        tab.pop(tuning.lib_key([ops.Seg(o)], M), None) if "o" in locals() else None
     assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
 
 

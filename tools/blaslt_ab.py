@@ -19,6 +19,7 @@ import torch
 from nats_llm_studio_amd import ops
 from nats_llm_studio_amd.gguf import quants as Q
 from nats_llm_studio_amd.gguf.synth import SPECS
+from nats_llm_studio_amd.ops import tuning
 
 REPS = 10
 
@@ -80,29 +81,41 @@ def main():
             y = torch.zeros(max(M, 64), ncol, dtype=ops.ACT_DTYPE if epi == "swiglu" else torch.float32,
                             device=dev)
             kw = dict(mode=cfg[0], waves=cfg[1], rt=cfg[2], ks=cfg[3])
-            ops.qgemv(segs, x, y, M, epi=epi, **kw)
+            if epi == "add":       # o / down: residual add + next RMSNorm, as the decode step runs them
+                nw = torch.rand(ncol, device=dev) + 0.5
+                hn = torch.zeros(max(M, 64), ncol, dtype=ops.ACT_DTYPE, device=dev)
+
+                def ours(i):
+                    ops.qgemv_add_rmsnorm(copies[i % ncopy][0], x, y, nw, hn, M, 1.0, 1e-5, cfg=cfg)
+
+                def lib(i):
+                    ops.LIB_GEMM, tab = True, tuning.table()
+                    key = tuning.lib_key(copies[i % ncopy], M)
+                    old = tab.get(key)
+                    tab[key] = (1,)
+                    ops.qgemv_add_rmsnorm(copies[i % ncopy][0], x, y, nw, hn, M, 1.0, 1e-5)
+                    tab.pop(key) if old is None else tab.__setitem__(key, old)
+            else:
+                def ours(i):
+                    ops.qgemv(copies[i % ncopy], x, y, M, epi=epi, **kw)
+
+                def lib(i):           # the production mode-7 path (HIP SwiGLU pass / f32 store)
+                    ops.lib_gemm(copies[i % ncopy], x, y, M, 1.0, epi)
+            ours(0)
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 for i in range(REPS):
-                    ops.qgemv(copies[i % ncopy], x, y, M, epi=epi, **kw)
-
-            def lib(i):
-                if epi in ("swiglu", "f32"):   # the production mode-7 path (HIP SwiGLU pass)
-                    ops.lib_gemm(copies[i % ncopy], x, y, M, 1.0, epi)
-                elif epi == "add":
-                    y[:M].add_(torch.mm(x[:M], wcat[i % ncopy].t(), out_dtype=torch.float32))
-                else:
-                    torch.mm(x[:M], wcat[i % ncopy].t(), out_dtype=torch.float32, out=y[:M])
+                    ours(i)
 
             def lib_gemm_only(i):
                 torch.mm(x[:M], wcat[i % ncopy].t())
 
             outs = []
-            for fn in (lambda: ops.qgemv(segs, x, y, M, epi=epi, **kw), lambda: lib(0)):
+            for fn in (lambda: ours(0), lambda: lib(0)):
                 y.zero_()
                 fn()
                 torch.cuda.synchronize()
-                outs.append(y[:M].float().clone())
+                outs.append((hn if epi == "add" else y)[:M].float().clone())
             err = (outs[1] - outs[0]).abs().max().item() / (outs[0].abs().max().item() + 1e-9)
             graphs = [g1]
             for f in (lib, lib_gemm_only):
