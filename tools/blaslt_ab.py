@@ -41,8 +41,9 @@ def main():
     ap.add_argument("--M", default="256,512,1024")
     ap.add_argument("--shapes", default="qkv,o,gateup,down,lm_head")
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--model", default="llama-3-8b", help="projection shapes of this synthetic spec")
     a = ap.parse_args()
-    spec = SPECS["llama-3-8b"]
+    spec = SPECS[a.model]
     d, hd = spec.d_model, spec.head_dim
     nq, nkv = spec.n_head * hd, spec.n_kv_head * hd
     defs = {"qkv": ([(12, nq), (12, nkv), (12, nkv)], d, "f32"), "o": ([(12, d)], nq, "add"),
