@@ -202,13 +202,14 @@ class Engine:
         self.max_blocks = math.ceil(self.ctx / block_size)
         # f16 copies of the projection weights for the large-M dense GEMM (prefill chunks, decode
         # batches >= ops.DENSE_MIN_M): NLS_DENSE_WEIGHTS=auto (default: when the copies take at most
-        # 45 % of free HBM -- Llama-3-8B: 15 GB of 288; the rest stays for the KV pool), 1 (always),
+        # 60 % of free HBM -- Llama-3-8B: 15 GB of 288, Llama-3-70B: 140 GB of ~245 (B=512 86.3 vs
+        # 96.8 ms/step with mode 7, profiles/bench_70b_mode7.txt); the rest stays for the KV pool), 1 (always),
         # 0 (never). NLS_DENSE_EXPERTS=1 adds the MoE experts (Mixtral-8x7B: 90 GB) as a second tier
         dense = os.environ.get("NLS_DENSE_WEIGHTS", "auto")
         self.dense_bytes = 0
         if self.dev.type == "cuda" and dense != "0" and hasattr(model, "expand_dense"):
             free, _ = torch.cuda.mem_get_info(self.dev)
-            self.dense_bytes = model.expand_dense(None if dense == "1" else int(0.45 * free),
+            self.dense_bytes = model.expand_dense(None if dense == "1" else int(0.60 * free),
                                                   experts=os.environ.get("NLS_DENSE_EXPERTS", "0") == "1")
         if num_blocks is None:
             num_blocks = self.max_batch * self.max_blocks
