@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--shapes", default="qkv,o,gateup,down,lm_head")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--model", default="llama-3-8b", help="projection shapes of this synthetic spec")
+    ap.add_argument("--lib-ks", type=int, default=1, help="add shapes: the 'gemm only' column runs K-split "
+                    "library GEMMs into slabs + the fused reduce/add/RMSNorm pass")
     a = ap.parse_args()
     spec = SPECS[a.model]
     d, hd = spec.d_model, spec.head_dim
@@ -109,6 +111,17 @@ def main():
                     ours(i)
 
             def lib_gemm_only(i):
+                if epi == "add" and a.lib_ks > 1:   # K split over slabs, then the fused reduce/norm pass
+                    Wc, n = wcat[i % ncopy], ncol
+                    ws = ops._workspace(dev, a.lib_ks * M * n)
+                    kk = K // a.lib_ks
+                    for j in range(a.lib_ks):
+                        torch.mm(x[:M, j * kk:(j + 1) * kk], Wc[:, j * kk:(j + 1) * kk].t(), out_dtype=torch.float32,
+                                 out=ws[j * M * n:(j + 1) * M * n].view(M, n))
+                    ops._lib.check(ops._lib.lib().nls_splitk_add_rmsnorm(
+                        ws.data_ptr(), a.lib_ks, M, 1.0, y.data_ptr(), y.stride(0), nw.data_ptr(), hn.data_ptr(),
+                        hn.stride(0), n, 1e-5, ops._stream_ptr(x)), "splitk")
+                    return
                 torch.mm(x[:M], wcat[i % ncopy].t())
 
             outs = []
