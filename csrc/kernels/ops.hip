@@ -356,19 +356,12 @@ __global__ __launch_bounds__(256) void moe_combine_norm_kernel(const float* __re
 // reductions, so nothing is indexed at run time (no scratch). NaN / inf logits: a NaN never wins a
 // comparison, ties and NaNs resolve to the lowest unused expert, so k distinct valid experts are
 // always chosen.
-__global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k,
-                                                        int renorm, float* __restrict__ topw,
-                                                        int* __restrict__ counts, int* __restrict__ xrows,
-                                                        int* __restrict__ yrows, int cap, int* __restrict__ sel) {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gridDim.x == 1) {      // one workgroup (<= 4 tokens): zero the counts here (no host memset launch)
-    for (int e = threadIdx.x; e < E; e += 256) counts[e] = 0;
-    __syncthreads();
-  }
-  if (t >= T || E > 64 || k > 8 || k > E) return;    // host checks these too
+// One wave routes token t from its E logits `lt` (global or LDS).
+DEVI void route_one(const float* __restrict__ lt, int t, int lane, int E, int k, int renorm, float* __restrict__ topw,
+                    int* __restrict__ counts, int* __restrict__ xrows, int* __restrict__ yrows, int cap,
+                    int* __restrict__ sel) {
   const bool live = lane < E;
-  const float l = live ? logits[(size_t)t * E + lane] : -INFINITY;
+  const float l = live ? lt[lane] : -INFINITY;
   float mx = l;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -407,6 +400,87 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
     xrows[lane * cap + pos] = t;
     yrows[lane * cap + pos] = t * k + myj;
   }
+}
+
+__global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k,
+                                                        int renorm, float* __restrict__ topw,
+                                                        int* __restrict__ counts, int* __restrict__ xrows,
+                                                        int* __restrict__ yrows, int cap, int* __restrict__ sel) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gridDim.x == 1) {      // one workgroup (<= 4 tokens): zero the counts here (no host memset launch)
+    for (int e = threadIdx.x; e < E; e += 256) counts[e] = 0;
+    __syncthreads();
+  }
+  if (t >= T || E > 64 || k > 8 || k > E) return;    // host checks these too
+  route_one(logits + (size_t)t * E, t, lane, E, k, renorm, topw, counts, xrows, yrows, cap, sel);
+}
+
+// MoE decode at <= 4 tokens: the post-attention RMSNorm (h = f16(x * rsqrt(mean(x^2) + eps) * nw), as
+// rmsnorm_kernel), the router logits h . Wr[e] (Wr: the router's f16 copy, [E][D] row-major -- the
+// router GEMV also multiplies f16 weights) and the top-k route (route_one) in ONE launch, where batch-1
+// Mixtral ran three latency-bound ones (rmsnorm 4.5 + router GEMV 7.2 + route 4.5 us per layer,
+// profiles/moe_selected_experts.txt).
+template <int E>
+__global__ __launch_bounds__(512) void moe_norm_route_kernel(
+    const float* __restrict__ x, long ldx, const float* __restrict__ nw, float eps, int D,
+    const act_t* __restrict__ wr, act_t* __restrict__ h, long ldh, float* __restrict__ logits, int T, int k,
+    int renorm, float* __restrict__ topw, int* __restrict__ counts, int* __restrict__ xrows, int* __restrict__ yrows,
+    int cap, int* __restrict__ sel) {
+  __shared__ float sh[8];
+  __shared__ float red[8][E];
+  __shared__ float lg[4][E];
+  for (int e = threadIdx.x; e < E; e += 512) counts[e] = 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  typedef act_t act4 __attribute__((ext_vector_type(4)));
+  for (int t = 0; t < T; ++t) {
+    const float* xr = x + (size_t)t * ldx;
+    float4 v[4], wv[4];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = (threadIdx.x + j * 512) * 4;
+      v[j] = i < D ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[j] = i < D ? *reinterpret_cast<const float4*>(nw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ss += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+    }
+    ss = block_sum<512>(ss, sh);
+    const float inv = rsqrtf(ss / (float)D + eps);
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = (threadIdx.x + j * 512) * 4;
+      if (i < D) {
+        const float4 ww = wv[j];
+        const act4 r = {(act_t)(v[j].x * inv * ww.x), (act_t)(v[j].y * inv * ww.y), (act_t)(v[j].z * inv * ww.z),
+                        (act_t)(v[j].w * inv * ww.w)};
+        *reinterpret_cast<act4*>(h + (size_t)t * ldh + i) = r;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const act4 w4 = *reinterpret_cast<const act4*>(wr + (size_t)e * D + i);
+          acc[e] += (float)r.x * (float)w4.x + (float)r.y * (float)w4.y + (float)r.z * (float)w4.z +
+                    (float)r.w * (float)w4.w;
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float a = wave_sum(acc[e]);
+      if (lane == 0) red[wave][e] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < E) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s2 += red[w][threadIdx.x];
+      lg[t][threadIdx.x] = s2;
+      logits[(size_t)t * E + threadIdx.x] = s2;
+    }
+    __syncthreads();
+  }
+  if (wave < T) route_one(lg[wave], wave, lane, E, k, renorm, topw, counts, xrows, yrows, cap, sel);
 }
 
 // SwiGLU pass after a library GEMM on the gate/up weights (ops "mode 7"): the GEMM's f16 output h keeps
@@ -520,6 +594,23 @@ int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* t
   hipLaunchKernelGGL(moe_route_kernel, dim3((T + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits, T, E, k,
                      renorm, topw, counts, xrows, yrows, cap, sel);
   return (int)hipGetLastError();
+}
+
+// x f32 [T][ldx] residual rows, nw f32 [D], wr f16 [E][D], h f16 [T][ldh] (out), logits f32 [T][E] (out)
+int nls_moe_norm_route(const float* x, long ldx, const float* nw, float eps, int D, const void* wr, void* h, long ldh,
+                       float* logits, int T, int E, int k, int renorm, float* topw, int* counts, int* xrows, int* yrows,
+                       int cap, int* sel, void* stream) {
+  if (T < 1 || T > 4 || D % 4 || D > 8192 || k < 1 || k > E || ldx % 4 || ldh % 4) return -1;
+  hipStream_t st = (hipStream_t)stream;
+#define NLS_MNR(EE)                                                                                              \
+  if (E == EE) {                                                                                               \
+    hipLaunchKernelGGL(moe_norm_route_kernel<EE>, dim3(1), dim3(512), 0, st, x, ldx, nw, eps, D, (const act_t*)wr, \
+                       (act_t*)h, ldh, logits, T, k, renorm, topw, counts, xrows, yrows, cap, sel);             \
+    return (int)hipGetLastError();                                                                             \
+  }
+  NLS_MNR(2) NLS_MNR(4) NLS_MNR(8)
+#undef NLS_MNR
+  return -1;
 }
 
 int nls_moe_combine(const float* y, const float* w, int T, int topk, float* resid, long ldr, int D, float alpha,

@@ -38,6 +38,9 @@ _MIN_CHUNK = int(os.environ.get("NLS_ATTN_MIN_CHUNK", "0"))
 # GEMVs over each expert's gathered rows)
 # (Mixtral-8x7B: B=64 15.2 vs 28.9 ms/step, B=32 15.2 vs 15.6, B=16 14.8 vs 9.7; scripts/gpu_moe_thresh.sh)
 _MOE_GEMM_T = int(os.environ.get("NLS_MOE_GEMM_T", "16"))
+# MoE decode at up to this many tokens (<= 4) fuses the FFN input RMSNorm, the router and the route
+# into one launch (ops.moe_norm_route); 0 disables
+_MOE_NORM_ROUTE_T = min(4, int(os.environ.get("NLS_MOE_NORM_ROUTE", "4")))
 # MoE expert GEMMs on the experts' f16 copies: (mode, waves, rt[, ks]) of gate/up and down
 _MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2").split(","))
 _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
@@ -79,6 +82,7 @@ class LayerWeights:
     qkv_bias: Optional[torch.Tensor] = None     # Qwen2: f32 [(Hq + 2*Hkv) * D] (this shard)
     # MoE
     router: Optional[QWeight] = None
+    router16: Optional[torch.Tensor] = None     # f16 [E, d] row-major copy for the fused norm + route kernel
     exp_gateup: List[QWeight] = field(default_factory=list)
     exp_down: List[QWeight] = field(default_factory=list)
 
@@ -227,6 +231,8 @@ class LlamaModel:
                 lw.qkv_bias = torch.from_numpy(np.concatenate([bq, bk, bv]).astype(np.float32)).to(self.device)
             if cfg.n_expert:
                 lw.router = self._matrix(p + "ffn_gate_inp.weight")
+                if self.device.type == "cuda" and cfg.n_expert in (2, 4, 8):
+                    lw.router16 = lw.router.dense(torch.float16).contiguous()
                 F = self.exp_ffn
                 ksl = None if self.ep else (r * F, (r + 1) * F)
                 for e in self.experts:          # local experts (all of them unless EP)
@@ -382,7 +388,11 @@ class LlamaModel:
                 ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
                               block_size, cfg.attn_softmax_scale, chunk=-_MIN_CHUNK, n_split=n_split, workspace=b.attn_ws,
                               counters=b.attn_cnt)
-            if fused:
+            moe_norm = fused and lw.router16 is not None and T <= _MOE_NORM_ROUTE_T
+            if moe_norm:
+                # the FFN input norm runs inside the MoE router/route launch (ops.moe_norm_route)
+                ops.qgemv([Seg(lw.wo)], b.ao, x, T, alpha=cfg.residual_scale, epi="add")
+            elif fused:
                 ops.qgemv_add_rmsnorm(Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps,
                                       counter=b.cnt)
             elif not self.comm.row_parallel_add_norm(lw.wo, b.ao, b.part, x, lw.ffn_norm, b.h, T,
@@ -392,7 +402,7 @@ class LlamaModel:
             nxt = self.layers[L + 1].attn_norm if L + 1 < len(self.layers) else self.out_norm
             fused_prev = False
             if cfg.n_expert:
-                fused_prev = self._moe(lw, b, T, nxt if fused else None)
+                fused_prev = self._moe(lw, b, T, nxt if fused else None, lw.ffn_norm if moe_norm else None)
             else:
                 ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
                 if fused:
@@ -468,16 +478,26 @@ class LlamaModel:
         else:
             self.comm.row_parallel_add(w, xin, resid, T, alpha)
 
-    def _moe(self, lw: LayerWeights, b: StepBuffers, T: int, next_norm: Optional[torch.Tensor] = None) -> bool:
+    def _moe(self, lw: LayerWeights, b: StepBuffers, T: int, next_norm: Optional[torch.Tensor] = None,
+             in_norm: Optional[torch.Tensor] = None) -> bool:
         """Top-k routed experts: router GEMV -> route kernel (per-expert row lists on device)
         -> grouped expert GEMVs (tiles of experts with no routed rows exit before reading
-        weights) -> deterministic weighted combine into the residual."""
+        weights) -> deterministic weighted combine into the residual. `in_norm` (<= 4 tokens): b.h is
+        not normalised yet; the FFN input RMSNorm, the router and the route run as ONE launch."""
         cfg = self.cfg
         normed = False
         m = b.moe
         k, E = cfg.n_expert_used, cfg.n_expert
         cap = b.x.shape[0]
-        ops.qgemv([Seg(lw.router)], b.h, m["rlogits"], T)
+        routed = False
+        if in_norm is not None:
+            use_sel = self.device.type == "cuda" and T * k < len(self.experts)
+            routed = ops.moe_norm_route(b.x, in_norm, cfg.eps, lw.router16, b.h, m["rlogits"], T, k, m["topw"],
+                                        m["counts"], m["xrows"], m["yrows"], cap, sel=m["sel"] if use_sel else None)
+            if not routed:
+                ops.rmsnorm(b.x, in_norm, b.h, T, cfg.eps)
+        if not routed:
+            ops.qgemv([Seg(lw.router)], b.h, m["rlogits"], T)
         # few tokens: path-A GEMV over each expert's gathered rows; many tokens: ONE route and the
         # LDS-dequant GEMM (mode 2) over all experts, each m-block of an expert gathering its rows
         # through xrows and exiting when it lies past the expert's device-side count
@@ -522,8 +542,9 @@ class LlamaModel:
             # few tokens: the route kernel also lists each (token, slot)'s expert and the expert GEMVs
             # launch only those experts' tiles (k of E; the rest would be launched just to exit)
             use_sel = not gemm and self.device.type == "cuda" and n * k < len(self.experts)
-            ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap,
-                          sel=m["sel"] if use_sel else None)
+            if not (routed and c0 == 0 and n == T):
+                ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap,
+                              sel=m["sel"] if use_sel else None)
             loc = list(zip(self.experts, lw.exp_gateup, lw.exp_down))
             segs = [Seg(gu, 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, gu, _ in loc]
 

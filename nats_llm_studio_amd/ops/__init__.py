@@ -798,6 +798,28 @@ def sample_decode(logits: torch.Tensor, n: int, params: torch.Tensor, seeds: tor
                "nls_sample_decode")
 
 
+def moe_norm_route(x: torch.Tensor, nw: torch.Tensor, eps: float, wr: torch.Tensor, h: torch.Tensor,
+                   logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
+                   yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None) -> bool:
+    """h[:T] = rmsnorm(x[:T]) * nw (f16), router logits h @ wr^T (wr: the router's f16 copy [E, D]) and the
+    top-k route, in one launch on the GPU (T <= 4, E in {2, 4, 8}). Returns False, having done nothing,
+    when the fused kernel does not take the shape."""
+    E = wr.shape[0]
+    if x.is_cuda:
+        rc = _lib.lib().nls_moe_norm_route(x.data_ptr(), x.stride(0), nw.data_ptr(), float(eps), x.shape[1],
+                                           wr.data_ptr(), h.data_ptr(), h.stride(0), logits.data_ptr(), T, E, k,
+                                           int(renorm), topw.data_ptr(), counts.data_ptr(), xrows.data_ptr(),
+                                           yrows.data_ptr(), cap, _p(sel), _stream_ptr(x))
+        if rc == -1:
+            return False
+        _lib.check(rc, "nls_moe_norm_route")
+        return True
+    rmsnorm(x, nw, h, T, eps)
+    logits[:T] = h[:T].float() @ wr.float().t()
+    moe_route(logits, T, k, topw, counts, xrows, yrows, cap, renorm, sel)
+    return True
+
+
 def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
               yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None):
     """Top-k routing: per-expert row lists (counts / xrows / yrows) and weights topw; `sel` (optional,

@@ -274,6 +274,49 @@ def test_moe_route(gpu):
         assert toks == sorted([t for t in range(T) if ex in e[t].tolist()])
 
 
+@pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (3, 8, 4096), (4, 4, 1024), (2, 2, 768)])
+def test_moe_norm_route_fused(gpu, T, E, D):
+    """One launch = RMSNorm -> f16 h, router logits h . Wr[e], top-2 route; vs the fp32 oracle of each part
+    and vs the unfused kernels' routing (the same experts, weights and row lists)."""
+    k, cap = 2, 16
+    g = torch.Generator().manual_seed(T * 100 + E)
+    x = (torch.randn(cap, D, generator=g) * 3).to(gpu)
+    nw = (torch.rand(D, generator=g) + 0.5).to(gpu)
+    wr = (torch.randn(E, D, generator=g) * 0.05).to(torch.float16).to(gpu)
+    outs = []
+    for fused in (True, False):
+        h = torch.zeros(cap, D, dtype=ops.ACT_DTYPE, device=gpu)
+        lg = torch.zeros(cap, E, device=gpu)
+        topw = torch.zeros(cap * k, device=gpu)
+        counts = torch.full((E,), 7, dtype=torch.int32, device=gpu)     # stale counts: zeroed in-kernel
+        xr = torch.full((E * cap,), -1, dtype=torch.int32, device=gpu)
+        yr = torch.full((E * cap,), -1, dtype=torch.int32, device=gpu)
+        sel = torch.full((cap * k,), -1, dtype=torch.int32, device=gpu)
+        if fused:
+            assert ops.moe_norm_route(x, nw, 1e-5, wr, h, lg, T, k, topw, counts, xr, yr, cap, sel=sel)
+        else:
+            ops.rmsnorm(x, nw, h, T, 1e-5)
+            lg[:T] = h[:T].float() @ wr.float().t()
+            ops.moe_route(lg, T, k, topw, counts, xr, yr, cap, sel=sel)
+        torch.cuda.synchronize()
+        outs.append((h.cpu(), lg.cpu(), topw.cpu(), counts.cpu(), xr.cpu(), yr.cpu(), sel.cpu()))
+    xs = x[:T].cpu()
+    href = xs * torch.rsqrt(xs.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu()
+    _close(outs[0][0][:T], href, 1e-2)
+    _close(outs[0][1][:T], outs[0][0][:T].float() @ wr.float().cpu().t(), 1e-3)
+    assert (outs[0][0][T:] == 0).all()
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-5, atol=1e-6)
+    assert torch.equal(outs[0][3], outs[1][3]) and int(outs[0][3].sum()) == T * k
+    assert torch.equal(outs[0][6], outs[1][6])
+    for ex in range(E):
+        c = int(outs[0][3][ex])
+        assert sorted(outs[0][4][ex * cap:ex * cap + c].tolist()) == sorted(outs[1][4][ex * cap:ex * cap + c].tolist())
+        assert sorted(outs[0][5][ex * cap:ex * cap + c].tolist()) == sorted(outs[1][5][ex * cap:ex * cap + c].tolist())
+    lgs = torch.zeros(cap, E)
+    assert not ops.moe_norm_route(x, nw, 1e-5, wr, torch.zeros(cap, D, dtype=ops.ACT_DTYPE, device=gpu),
+                                  lgs.to(gpu), 5, k, topw, counts, xr, yr, cap)      # > 4 tokens: not taken
+
+
 def test_moe_route_nan_rows_stay_in_bounds(gpu):
     """A router row of NaN / inf logits must still pick k distinct valid experts (no index -1)."""
     T, E, k, cap = 6, 8, 2, 64
