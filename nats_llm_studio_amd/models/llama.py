@@ -41,6 +41,9 @@ _MOE_GEMM_T = int(os.environ.get("NLS_MOE_GEMM_T", "16"))
 # MoE decode at up to this many tokens (<= 4) fuses the FFN input RMSNorm, the router and the route
 # into one launch (ops.moe_norm_route); 0 disables
 _MOE_NORM_ROUTE_T = min(4, int(os.environ.get("NLS_MOE_NORM_ROUTE", "4")))
+# MoE decode (path-A expert GEMVs): launch config (mode, waves, rt, ks) of the DOWN projection, whose
+# K (d_ff) is 3.5x the gate/up's; empty: ops.MOE_GEMV like gate/up
+_MOE_GEMV_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_GEMV_DN", "").split(",") if v)
 # MoE expert GEMMs on the experts' f16 copies: (mode, waves, rt[, ks]) of gate/up and down
 _MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2").split(","))
 _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
@@ -510,6 +513,8 @@ class LlamaModel:
         # rows in a 256-row block cost 64 rows of MFMA (Mixtral B=256, scripts/gpu_moe_na.sh: gate/up
         # rt 4 / down rt 4 = 19.6 ms/step, 4/2 = 20.7, 2/2 = 28.3, 1/1 = 43.0)
         gu = dn = {}
+        if not gemm and len(_MOE_GEMV_DN) == 4:
+            dn = dict(zip(("mode", "waves", "rt", "ks"), _MOE_GEMV_DN))
         dn_rows = T
         if gemm and all(w.d16 is not None for w in lw.exp_gateup + lw.exp_down):
             # f16 expert copies (expand_dense tier 2): the dense DMA GEMM, bandwidth- rather than
