@@ -33,9 +33,9 @@ __device__ __forceinline__ int split_chunk(int chunk, int ctx, int n_split, int 
   return max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
 }
 
-template <int D, int G>
+template <int D, int G, typename KV>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
-    const __bf16* __restrict__ q, long ldq, const __bf16* __restrict__ kc, const __bf16* __restrict__ vc,
+    const __bf16* __restrict__ q, long ldq, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
     const int* __restrict__ ctx_len, int Hkv, int bs, float scale, int chunk, int n_split,
     act_t* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -97,37 +97,39 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   auto kv_off = [&](int pos, int base) -> size_t { return ((size_t)slot_of(pos, base) * Hkv + kh) * D + 8 * dl; };
 
   // K/V rows PF steps ahead in flight (long contexts at small batch are latency-bound on this chain)
-  u32x4 kr = {0, 0, 0, 0}, vr = {0, 0, 0, 0}, k1 = kr, v1 = vr;
+  typedef KVRaw<KV> R;
+  typename R::raw kr{}, vr{}, k1{}, v1{};
   if (start < end) {
     const int p0 = min(start + stream, end - 1);
     const size_t off = kv_off(p0, start);
-    kr = ld16(kc + off);
-    vr = ld16(vc + off);
+    kr = R::ld(kc + off);
+    vr = R::ld(vc + off);
     if (NLS_ATTN_PREFETCH2 && start + NSTREAM < end) {
       const int p1 = min(start + NSTREAM + stream, end - 1);
       const size_t o1 = kv_off(p1, start + NSTREAM);
-      k1 = ld16(kc + o1);
-      v1 = ld16(vc + o1);
+      k1 = R::ld(kc + o1);
+      v1 = R::ld(vc + o1);
     }
   }
   for (int base = start; base < end; base += NSTREAM) {
     const int pos = base + stream;
     const bool valid = pos < end;
     constexpr int PF = NLS_ATTN_PREFETCH2 ? 2 : 1;
-    u32x4 kn = PF == 2 ? k1 : kr, vn = PF == 2 ? v1 : vr;
+    typename R::raw kn = PF == 2 ? k1 : kr, vn = PF == 2 ? v1 : vr;
     if (base + PF * NSTREAM < end) {
       const int pn = min(pos + PF * NSTREAM, end - 1);
       const size_t off = kv_off(pn, base + PF * NSTREAM);
-      kn = ld16(kc + off);
-      vn = ld16(vc + off);
+      kn = R::ld(kc + off);
+      vn = R::ld(vc + off);
     }
     float kf[8], vf[8];
+    const u32x4 kb = R::bf16(kr), vb = R::bf16(vr);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      kf[2 * i] = bf2f(kr[i] & 0xFFFF);
-      kf[2 * i + 1] = bf2f(kr[i] >> 16);
-      vf[2 * i] = bf2f(vr[i] & 0xFFFF);
-      vf[2 * i + 1] = bf2f(vr[i] >> 16);
+      kf[2 * i] = bf2f(kb[i] & 0xFFFF);
+      kf[2 * i + 1] = bf2f(kb[i] >> 16);
+      vf[2 * i] = bf2f(vb[i] & 0xFFFF);
+      vf[2 * i + 1] = bf2f(vb[i] >> 16);
     }
     float s[G];
 #pragma unroll
@@ -272,23 +274,27 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
 }
 
 template <int D, int G>
-void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const __bf16* kc, const __bf16* vc,
+void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const void* kc, const void* vc,
                  const int* bt, int bts, const int* ts, const int* cl, int Hkv, int bs, float scale, int chunk,
-                 int ns, act_t* out, long ldo, float* po, float* pml, int* cnt) {
-  hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, q, ldq, kc, vc, bt, bts, ts, cl, Hkv, bs,
-                     scale, chunk, ns, out, ldo, po, pml, cnt);
+                 int ns, act_t* out, long ldo, float* po, float* pml, int* cnt, bool kv8) {
+  if (kv8)
+    hipLaunchKernelGGL((attn_decode_kernel<D, G, uint8_t>), grid, dim3(256), 0, st, q, ldq, (const uint8_t*)kc,
+                       (const uint8_t*)vc, bt, bts, ts, cl, Hkv, bs, scale, chunk, ns, out, ldo, po, pml, cnt);
+  else
+    hipLaunchKernelGGL((attn_decode_kernel<D, G, __bf16>), grid, dim3(256), 0, st, q, ldq, (const __bf16*)kc,
+                       (const __bf16*)vc, bt, bts, ts, cl, Hkv, bs, scale, chunk, ns, out, ldo, po, pml, cnt);
 }
 
 }  // namespace
 
-extern "C" {
+namespace {
 
 // workspace: part_o [T*Hq*n_split*D] f32, part_ml [T*Hq*n_split*2] f32 (only if n_split > 1);
 // cnt: int32 [T*Hkv], zero (re-armed by every launch): the splits merge in-kernel; null: attn_combine
-int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
-                    int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
-                    int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
-                    float* part_ml, int* cnt, void* stream) {
+static int attn_decode_impl(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                            int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
+                            int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
+                            float* part_ml, int* cnt, void* stream, bool kv8) {
   if (Hq % Hkv || n_split < 1 || (chunk > 0 && chunk % block_size) || 64 % (64 / (D / 8)) ||
       (4 * 64 / (D / 8)) > 64 * block_size)
     return -1;
@@ -296,13 +302,11 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(T, Hkv, n_split);
   const __bf16* qq = (const __bf16*)q;
-  const __bf16* k = (const __bf16*)kc;
-  const __bf16* v = (const __bf16*)vc;
   act_t* o = (act_t*)out;
 #define NLS_ATTN_CASE(DD, GG)                                                                                 \
   if (D == DD && G == GG) {                                                                                  \
-    launch_attn<DD, GG>(grid, st, qq, ldq, k, v, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \
-                        scale, chunk, n_split, o, ldo, part_o, part_ml, cnt);                                \
+    launch_attn<DD, GG>(grid, st, qq, ldq, kc, vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \
+                        scale, chunk, n_split, o, ldo, part_o, part_ml, cnt, kv8);                                \
   } else
   // G = Hq/Hkv of the supported families: 1 (MHA), 2/4/8 (Llama/Mixtral), 3/5/6/7 (Qwen2 sizes, e.g. 28/4)
   NLS_ATTN_CASE(128, 1) NLS_ATTN_CASE(128, 2) NLS_ATTN_CASE(128, 3) NLS_ATTN_CASE(128, 4) NLS_ATTN_CASE(128, 5)
@@ -319,6 +323,27 @@ int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, con
                          n_split, chunk, block_size, o, ldo);
   }
   return (int)hipGetLastError();
+}
+
+}  // namespace (host)
+
+extern "C" {
+
+int nls_attn_decode(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                    int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
+                    int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
+                    float* part_ml, int* cnt, void* stream) {
+  return attn_decode_impl(q, ldq, kc, vc, block_tables, bt_stride, tok_seq, ctx_len, T, Hq, Hkv, D, block_size, scale,
+                          chunk, n_split, out, ldo, part_o, part_ml, cnt, stream, false);
+}
+
+// the same over an fp8 (OCP e4m3) K/V cache
+int nls_attn_decode8(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                     int bt_stride, const int* tok_seq, const int* ctx_len, int T, int Hq, int Hkv, int D,
+                     int block_size, float scale, int chunk, int n_split, void* out, long ldo, float* part_o,
+                     float* part_ml, int* cnt, void* stream) {
+  return attn_decode_impl(q, ldq, kc, vc, block_tables, bt_stride, tok_seq, ctx_len, T, Hq, Hkv, D, block_size, scale,
+                          chunk, n_split, out, ldo, part_o, part_ml, cnt, stream, true);
 }
 
 }  // extern "C"

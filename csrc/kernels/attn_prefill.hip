@@ -22,10 +22,10 @@ namespace {
 
 constexpr float LOG2E_P = 1.4426950408889634f;
 
-template <int D>
+template <int D, typename KV>
 __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restrict__ q, long ldq,
-                                                           const __bf16* __restrict__ kc,
-                                                           const __bf16* __restrict__ vc,
+                                                           const KV* __restrict__ kc,
+                                                           const KV* __restrict__ vc,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ qblocks, int Hkv, int G, int bs,
                                                            float scale, act_t* __restrict__ out, long ldo) {
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
       u32x4 v = u32x4{0u, 0u, 0u, 0u};
       if (p < nkeys) {
         const long slot = (long)bt[p / bs] * bs + p % bs;
-        v = ld16(kc + ((size_t)slot * Hkv + hk) * D + ch * 8);
+        v = KVRaw<KV>::bf16(KVRaw<KV>::ld(kc + ((size_t)slot * Hkv + hk) * D + ch * 8));
       }
       *reinterpret_cast<u32x4*>(Ks + key * KSTR + ch * 8) = v;
     }
@@ -79,11 +79,11 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
       u32x4 va = u32x4{0u, 0u, 0u, 0u}, vb = u32x4{0u, 0u, 0u, 0u};
       if (p < nkeys) {
         const long slot = (long)bt[p / bs] * bs + p % bs;
-        va = ld16(vc + ((size_t)slot * Hkv + hk) * D + ch * 8);
+        va = KVRaw<KV>::bf16(KVRaw<KV>::ld(vc + ((size_t)slot * Hkv + hk) * D + ch * 8));
       }
       if (p + 1 < nkeys) {
         const long slot = (long)bt[(p + 1) / bs] * bs + (p + 1) % bs;
-        vb = ld16(vc + ((size_t)slot * Hkv + hk) * D + ch * 8);
+        vb = KVRaw<KV>::bf16(KVRaw<KV>::ld(vc + ((size_t)slot * Hkv + hk) * D + ch * 8));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -178,20 +178,34 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
 
 }  // namespace
 
-extern "C" int nls_attn_prefill(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
-                                int bt_stride, const int* qblocks, int nqb, int Hq, int Hkv, int D, int block_size,
-                                float scale, void* out, long ldo, void* stream) {
+template <typename KV>
+int attn_prefill_impl(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables, int bt_stride,
+                      const int* qblocks, int nqb, int Hq, int Hkv, int D, int block_size, float scale, void* out,
+                      long ldo, void* stream) {
   if (Hq % Hkv || (Hq / Hkv) % 4 || (D != 64 && D != 128) || nqb < 1) return -1;
   const int G = Hq / Hkv;
   dim3 grid(nqb, Hkv, G / 4);
   hipStream_t st = (hipStream_t)stream;
   if (D == 128)
-    hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const __bf16*)kc,
-                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (act_t*)out,
-                       ldo);
+    hipLaunchKernelGGL((attn_prefill_kernel<128, KV>), grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const KV*)kc,
+                       (const KV*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (act_t*)out, ldo);
   else
-    hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const __bf16*)kc,
-                       (const __bf16*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (act_t*)out,
-                       ldo);
+    hipLaunchKernelGGL((attn_prefill_kernel<64, KV>), grid, dim3(256), 0, st, (const __bf16*)q, ldq, (const KV*)kc,
+                       (const KV*)vc, block_tables, bt_stride, qblocks, Hkv, G, block_size, scale, (act_t*)out, ldo);
   return (int)hipGetLastError();
+}
+
+extern "C" int nls_attn_prefill(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                                int bt_stride, const int* qblocks, int nqb, int Hq, int Hkv, int D, int block_size,
+                                float scale, void* out, long ldo, void* stream) {
+  return attn_prefill_impl<__bf16>(q, ldq, kc, vc, block_tables, bt_stride, qblocks, nqb, Hq, Hkv, D, block_size,
+                                   scale, out, ldo, stream);
+}
+
+// the same over an fp8 (OCP e4m3) K/V cache
+extern "C" int nls_attn_prefill8(const void* q, long ldq, const void* kc, const void* vc, const int* block_tables,
+                                 int bt_stride, const int* qblocks, int nqb, int Hq, int Hkv, int D, int block_size,
+                                 float scale, void* out, long ldo, void* stream) {
+  return attn_prefill_impl<uint8_t>(q, ldq, kc, vc, block_tables, bt_stride, qblocks, nqb, Hq, Hkv, D, block_size,
+                                    scale, out, ldo, stream);
 }

@@ -29,6 +29,7 @@
 // packed FMA with the sub-block scale (single rounding) give d*sc*q - dmin*m, two values
 // per instruction. The residual stream and all accumulators stay fp32.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -51,6 +52,45 @@ DEVI float bf2f(uint16_t b) { return __builtin_bit_cast(float, ((uint32_t)b) << 
 DEVI uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 DEVI u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
+
+// Paged KV cache element types: bf16 (default) or OCP fp8 e4m3 (NLS_KV_DTYPE=fp8: half the bytes per
+// decode step). raw = what one lane loads for 8 dims (kept in flight by the attention prefetch);
+// bf16() unpacks it to 8 bf16 (u32x4) -- exact for fp8 (3 mantissa bits fit bf16's 7).
+template <typename KV> struct KVRaw;
+template <> struct KVRaw<__bf16> {
+  typedef u32x4 raw;
+  static DEVI raw ld(const __bf16* p) { return ld16(p); }
+  static DEVI u32x4 bf16(const raw& r) { return r; }
+};
+template <> struct KVRaw<uint8_t> {
+  typedef uint2 raw;
+  static DEVI raw ld(const uint8_t* p) { return *reinterpret_cast<const uint2*>(p); }
+  static DEVI u32x4 bf16(const raw& r) {
+    // bytes 2i, 2i+1 -> dword i (bf16 pair). The scalar byte-select conversion: the packed form
+    // returned the selected word's first value in both lanes of its result on this toolchain
+    // (tools/kv8_probe.py).
+    auto b = [](uint32_t w, auto sel) {
+      return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_f32_fp8((int)w, decltype(sel)::value));
+    };
+    typedef std::integral_constant<int, 0> b0;
+    typedef std::integral_constant<int, 1> b1;
+    typedef std::integral_constant<int, 2> b2;
+    typedef std::integral_constant<int, 3> b3;
+    return u32x4{(b(r.x, b0{}) >> 16) | (b(r.x, b1{}) & 0xFFFF0000u), (b(r.x, b2{}) >> 16) | (b(r.x, b3{}) & 0xFFFF0000u),
+                 (b(r.y, b0{}) >> 16) | (b(r.y, b1{}) & 0xFFFF0000u), (b(r.y, b2{}) >> 16) | (b(r.y, b3{}) & 0xFFFF0000u)};
+  }
+};
+// 4 values -> the cache (fp8: saturated to +-448, the e4m3 range)
+DEVI void kv_st4(__bf16* d, float a, float b, float c, float e) {
+  typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<bf4*>(d) = bf4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)e};
+}
+DEVI void kv_st4(uint8_t* d, float a, float b, float c, float e) {
+  auto sat = [](float v) { return fminf(fmaxf(v, -448.f), 448.f); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(e), w, true);
+  *reinterpret_cast<int*>(d) = w;
+}
 DEVI u32x4 ld16_nt(const void* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }

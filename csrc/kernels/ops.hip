@@ -137,13 +137,14 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 // `ks` > 1: the QKV projection left split-K partial slabs (qkv = ks slabs of [T][ldqkv], stride
 // `slab` floats) and this kernel sums them in fixed order while rotating (fused reduce + RoPE).
+template <typename KV>
 __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, long ldqkv, int ks, long slab,
                                                       const float* __restrict__ bias,
                                                       const int* __restrict__ pos,
                                                       const int* __restrict__ slot,
                                                       const float* __restrict__ cs,
                                                       __bf16* __restrict__ q_out, long ldq,
-                                                      __bf16* __restrict__ kc, __bf16* __restrict__ vc,
+                                                      KV* __restrict__ kc, KV* __restrict__ vc,
                                                       int Hq, int Hkv, int D, int neox) {
   // Vectorised: every thread owns 4 consecutive columns (16-B slab loads, 8-B bf16 stores).
   const int t = blockIdx.x;
@@ -168,8 +169,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
   const long s = slot[t];  // int32 slot index, widened
   const int half = D >> 1;
   const float* c = cs + (size_t)p * D;   // [D/2][2] (cos, sin)
-  auto dst = [&](int h) -> __bf16* {
-    return h < Hq ? q_out + (size_t)t * ldq + h * D : kc + ((size_t)s * Hkv + (h - Hq)) * D;
+  // head h < Hq: q (bf16); else the K cache row of kv head h - Hq (KV type)
+  auto st = [&](int h, int col, float a, float b, float c2, float e) {
+    if (h < Hq) st4(q_out + (size_t)t * ldq + h * D + col, a, b, c2, e);
+    else kv_st4(kc + ((size_t)s * Hkv + (h - Hq)) * D + col, a, b, c2, e);
   };
   const int nh = s >= 0 ? Hq + Hkv : Hq;         // padded rows (slot -1) write no K/V
   if (!neox) {
@@ -178,8 +181,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
       const int h = idx / (D / 4), col = 4 * (idx - h * (D / 4));
       const float4 x = ld4(h * D + col);
       const float4 cw = *reinterpret_cast<const float4*>(c + col);   // (cos, sin) of pairs col/2, col/2+1
-      st4(dst(h) + col, x.x * cw.x - x.y * cw.y, x.x * cw.y + x.y * cw.x, x.z * cw.z - x.w * cw.w,
-          x.z * cw.w + x.w * cw.z);
+      st(h, col, x.x * cw.x - x.y * cw.y, x.x * cw.y + x.y * cw.x, x.z * cw.z - x.w * cw.w,
+         x.z * cw.w + x.w * cw.z);
     }
   } else {
     // NEOX halves: columns i..i+3 pair with i+half..i+half+3
@@ -195,17 +198,16 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
         y0[u] = av[u] * cc[u] - bv[u] * sn[u];
         y1[u] = av[u] * sn[u] + bv[u] * cc[u];
       }
-      __bf16* d = dst(h);
-      st4(d + i, y0[0], y0[1], y0[2], y0[3]);
-      st4(d + half + i, y1[0], y1[1], y1[2], y1[3]);
+      st(h, i, y0[0], y0[1], y0[2], y0[3]);
+      st(h, half + i, y1[0], y1[1], y1[2], y1[3]);
     }
   }
   if (s >= 0) {
     const int v0 = (Hq + Hkv) * D;
-    __bf16* vd = vc + (size_t)s * Hkv * D;
+    KV* vd = vc + (size_t)s * Hkv * D;
     for (int i = 4 * threadIdx.x; i < Hkv * D; i += 4 * blockDim.x) {
       const float4 v = ld4(v0 + i);
-      st4(vd + i, v.x, v.y, v.z, v.w);
+      kv_st4(vd + i, v.x, v.y, v.z, v.w);
     }
   }
 }
@@ -535,8 +537,18 @@ int nls_rope_kv(const float* qkv, long ldqkv, int ks, long slab, const float* bi
                 const float* cs, void* q_out, long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox,
                 void* stream) {
   if (ks < 1 || D % 8) return -1;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, bias, pos, slot, cs,
-                     (__bf16*)q_out, ldq, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, D, neox);
+  hipLaunchKernelGGL(rope_kv_kernel<__bf16>, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, bias, pos,
+                     slot, cs, (__bf16*)q_out, ldq, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, D, neox);
+  return (int)hipGetLastError();
+}
+
+// the same with an fp8 (OCP e4m3) K/V cache
+int nls_rope_kv8(const float* qkv, long ldqkv, int ks, long slab, const float* bias, const int* pos, const int* slot,
+                 const float* cs, void* q_out, long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox,
+                 void* stream) {
+  if (ks < 1 || D % 8) return -1;
+  hipLaunchKernelGGL(rope_kv_kernel<uint8_t>, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, bias,
+                     pos, slot, cs, (__bf16*)q_out, ldq, (uint8_t*)kc, (uint8_t*)vc, Hq, Hkv, D, neox);
   return (int)hipGetLastError();
 }
 

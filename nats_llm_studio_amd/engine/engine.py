@@ -214,7 +214,8 @@ class Engine:
         if num_blocks is None:
             num_blocks = self.max_batch * self.max_blocks
             if self.dev.type == "cuda":
-                per_block = 2 * self.cfg.n_layer * block_size * model.Hkv * model.D * 2
+                esz = torch.finfo(getattr(model, "kv_dtype", torch.bfloat16)).bits // 8
+                per_block = 2 * self.cfg.n_layer * block_size * model.Hkv * model.D * esz
                 free, _ = torch.cuda.mem_get_info(self.dev)
                 num_blocks = int(min(num_blocks, kv_mem_fraction * free // per_block))
         self.tp = model.comm if model.shard.size > 1 else None

@@ -288,9 +288,17 @@ class LlamaModel:
         return added
 
     # ------------------------------------------------------------------ buffers
+    @property
+    def kv_dtype(self) -> torch.dtype:
+        """Paged KV cache element type: NLS_KV_DTYPE=bf16 (default) | fp8 (OCP e4m3, half the bytes)."""
+        name = os.environ.get("NLS_KV_DTYPE", "bf16")
+        if name not in ops.KV_DTYPES:
+            raise ValueError(f"NLS_KV_DTYPE={name}: one of {sorted(ops.KV_DTYPES)}")
+        return ops.KV_DTYPES[name]
+
     def kv_cache(self, num_blocks: int, block_size: int = 16):
         L, slots = self.cfg.n_layer, num_blocks * block_size
-        k = torch.zeros(L, slots, self.Hkv, self.D, dtype=torch.bfloat16, device=self.device)
+        k = torch.zeros(L, slots, self.Hkv, self.D, dtype=self.kv_dtype, device=self.device)
         v = torch.zeros_like(k)
         return k, v
 

@@ -577,13 +577,27 @@ def rope_table(max_pos: int, head_dim: int, base: float, device, freq_factors=No
     return torch.from_numpy(cs).to(device)
 
 
+# K/V cache element types: bf16, or OCP fp8 e4m3 (half the attention bytes per decode step; opt-in,
+# NLS_KV_DTYPE=fp8 -- the kernels saturate to +-448 and convert exactly to bf16 on load)
+KV_DTYPES = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn}
+
+
+def _kv_fn(name: str, kc: torch.Tensor):
+    """The kernel entry point for this cache's element type (`<name>8`: fp8)."""
+    if kc.dtype == torch.float8_e4m3fn:
+        return getattr(_lib.lib(), name + "8")
+    if kc.dtype != torch.bfloat16:
+        raise TypeError(f"{name}: KV cache dtype {kc.dtype} (bf16 or float8_e4m3fn)")
+    return getattr(_lib.lib(), name)
+
+
 def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.Tensor, q_out: torch.Tensor,
             kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, neox: bool = False,
             bias: Optional[torch.Tensor] = None):
     """kc/vc: [slots, Hkv, D] bf16 for one layer. slot (int32) < 0 skips the cache write.
     `bias` (f32 [(Hq+2*Hkv)*D], Qwen2 QKV bias) is added before the rotation."""
     if qkv.is_cuda:
-        _lib.check(_lib.lib().nls_rope_kv(qkv.data_ptr(), qkv.stride(0), 1, 0, _p(bias), pos.data_ptr(),
+        _lib.check(_kv_fn("nls_rope_kv", kc)(qkv.data_ptr(), qkv.stride(0), 1, 0, _p(bias), pos.data_ptr(),
                                           slot.data_ptr(), cs.data_ptr(), q_out.data_ptr(), q_out.stride(0),
                                           kc.data_ptr(), vc.data_ptr(), T, Hq, Hkv, D, int(neox), _stream_ptr(qkv)),
                    "nls_rope_kv")
@@ -626,7 +640,8 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        if mode == 0 and T <= 64 and not neox and contiguous and ncol == (Hq + 2 * Hkv) * D and fuse_rope:
+        if (mode == 0 and T <= 64 and not neox and contiguous and ncol == (Hq + 2 * Hkv) * D and fuse_rope
+                and kc.dtype == torch.bfloat16):
             # path A: RoPE + KV append in the GEMV epilogue (no qkv round trip, no RoPE launch)
             fz = _lib.NlsFuse(pos=pos.data_ptr(), slot=slot.data_ptr(), cs=cs.data_ptr(), bias=_p(bias),
                               q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
@@ -658,7 +673,8 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
             st = _stream_ptr(h)
             _lib.check(L.nls_qgemv(arr, len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
                                    EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
-            _lib.check(L.nls_rope_kv(ws.data_ptr(), ncol, ks, T * ncol, _p(bias), pos.data_ptr(), slot.data_ptr(),
+            _lib.check(_kv_fn("nls_rope_kv", kc)(ws.data_ptr(), ncol, ks, T * ncol, _p(bias), pos.data_ptr(),
+                                                 slot.data_ptr(),
                                      cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(), vc.data_ptr(),
                                      T, Hq, Hkv, D, int(neox), st), "nls_rope_kv")
             return
@@ -692,7 +708,7 @@ def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables:
                 workspace = torch.empty(need, dtype=torch.float32, device=q.device)
             po = workspace.data_ptr()
             pml = po + T * Hq * n_split * D * 4
-        _lib.check(_lib.lib().nls_attn_decode(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
+        _lib.check(_kv_fn("nls_attn_decode", kc)(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
                                               block_tables.data_ptr(), block_tables.stride(0), tok_seq.data_ptr(),
                                               ctx_len.data_ptr(), T, Hq, Hkv, D, block_size, float(scale), chunk,
                                               n_split, out.data_ptr(), out.stride(0), po, pml,
@@ -744,7 +760,7 @@ def attention_prefill(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block
                       out: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, block_size: int, scale: float):
     """Causal MFMA flash attention over the paged cache for prompt chunks (query blocks of 16)."""
     if q.is_cuda:
-        _lib.check(_lib.lib().nls_attn_prefill(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
+        _lib.check(_kv_fn("nls_attn_prefill", kc)(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
                                                block_tables.data_ptr(), block_tables.stride(0), qblocks.data_ptr(),
                                                nqb, Hq, Hkv, D, block_size, float(scale), out.data_ptr(),
                                                out.stride(0), _stream_ptr(q)), "nls_attn_prefill")

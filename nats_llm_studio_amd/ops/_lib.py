@@ -49,6 +49,8 @@ _SIGS = {
                                c_float, c_void_p],
     "nls_rope_kv": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                     c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nls_rope_kv8": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
+                    c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nls_embed": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_float, c_void_p],
     "nls_dequant": [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p],
     "nls_swiglu16": [c_void_p, c_long, c_int, c_int, c_float, c_void_p, c_long, c_void_p],
@@ -64,7 +66,12 @@ _SIGS = {
     "nls_attn_decode": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                         c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p,
                         c_void_p, c_void_p],
+    "nls_attn_decode8": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
+                        c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p,
+                        c_void_p, c_void_p],
     "nls_attn_prefill": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                         c_int, c_int, c_float, c_void_p, c_long, c_void_p],
+    "nls_attn_prefill8": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_sample": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "nls_sample_params_size": [],

@@ -196,8 +196,10 @@ def test_rmsnorm_embed(gpu):
         torch.testing.assert_close(e.cpu(), 2.0 * Wd[[0, 49, 7]], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
 @pytest.mark.parametrize("neox", [False, True])
-def test_rope_kv(gpu, neox):
+def test_rope_kv(gpu, neox, kvt):
+    """RoPE + paged KV append (bf16 or fp8 e4m3 cache: the CPU path rounds the same values)."""
     T, Hq, Hkv, D = 3, 8, 2, 128
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=gpu)
     pos = torch.tensor([0, 5, 100], dtype=torch.int32, device=gpu)
@@ -206,20 +208,27 @@ def test_rope_kv(gpu, neox):
     outs = []
     for dev in (gpu, "cpu"):
         q = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=dev)
-        kc = torch.zeros(16, Hkv, D, dtype=torch.bfloat16, device=dev)
+        kc = torch.zeros(16, Hkv, D, dtype=kvt, device=dev)
         vc = torch.zeros_like(kc)
         ops.rope_kv(qkv.to(dev), pos.to(dev), slot.to(dev), cs.to(dev), q, kc, vc, T, Hq, Hkv, D, neox)
         outs.append((q.cpu().float(), kc.cpu().float(), vc.cpu().float()))
+    tol = 1e-2 if kvt == torch.bfloat16 else 7e-2      # e4m3: 3 mantissa bits (rounding may differ by 1 ulp)
     for a, b in zip(*outs):
-        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(a, b, rtol=tol, atol=tol)
+    if kvt != torch.bfloat16:
+        assert outs[0][1].abs().sum() > 0 and float(outs[0][1][[0, 1, 2, 4]].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8), (128, 1), (128, 7), (64, 6), (128, 5)])
 @pytest.mark.parametrize("n_split,chunk", [(1, 0), (4, 0), (32, 0), (8, -16), (3, 512)])
 @pytest.mark.parametrize("fused", [False, True])
-def test_attention_paged(gpu, D, G, n_split, chunk, fused):
+@pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
+def test_attention_paged(gpu, D, G, n_split, chunk, fused, kvt):
     """fused: flash-decoding splits merged in-kernel by the last split (ticket counters), called twice
-    to check the counters re-arm; else the separate combine kernel."""
+    to check the counters re-arm; else the separate combine kernel. kvt: bf16 or fp8 e4m3 cache (the
+    fp32 reference reads the same rounded values)."""
+    if kvt != torch.bfloat16 and (G not in (1, 4) or chunk == 512):
+        pytest.skip("fp8 cache: a representative subset")
     Hkv = 2
     Hq = Hkv * G
     bs = 16
@@ -227,8 +236,8 @@ def test_attention_paged(gpu, D, G, n_split, chunk, fused):
     T = len(ctx)
     nblk = 256
     g = torch.Generator().manual_seed(0)
-    kc = torch.randn(nblk * bs, Hkv, D, generator=g).to(torch.bfloat16)
-    vc = torch.randn(nblk * bs, Hkv, D, generator=g).to(torch.bfloat16)
+    kc = torch.randn(nblk * bs, Hkv, D, generator=g).to(kvt)
+    vc = torch.randn(nblk * bs, Hkv, D, generator=g).to(kvt)
     bt = torch.zeros(T, 100, dtype=torch.int32)
     for i in range(T):
         bt[i] = torch.randperm(nblk, generator=g)[:100].to(torch.int32)
@@ -440,8 +449,9 @@ def test_qgemm_large_m_swiglu(gpu):
     _close(y[:M], torch.nn.functional.silu(xf @ G.t()) * (xf @ U.t()), 3e-2)
 
 
+@pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
 @pytest.mark.parametrize("D,G", [(128, 4), (64, 4), (128, 8)])
-def test_attention_prefill_paged(gpu, D, G):
+def test_attention_prefill_paged(gpu, D, G, kvt):
     """MFMA flash-prefill vs the fp32 reference: 3 sequences, chunks that start mid-context
     (chunked prefill), partial 16-token blocks, scattered KV pages."""
     torch.manual_seed(0)
@@ -452,8 +462,8 @@ def test_attention_prefill_paged(gpu, D, G):
     nblk = 16
     perm = torch.randperm(3 * nblk).view(3, nblk).int()
     slots = 3 * nblk * bs
-    kc = (torch.randn(slots, Hkv, D) * 0.5).to(torch.bfloat16)
-    vc = torch.randn(slots, Hkv, D).to(torch.bfloat16)
+    kc = (torch.randn(slots, Hkv, D) * 0.5).to(kvt)
+    vc = torch.randn(slots, Hkv, D).to(kvt)
     T = sum(n for _, _, n in chunks)
     pos, tseq = [], []
     for s, p0, n in chunks:

@@ -80,6 +80,27 @@ def test_engine_greedy_matches_reference(gpu, tiny_models, name, graphs):
         assert eng.counters["graph_replays"] > 0
 
 
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
+def test_engine_fp8_kv_cache(gpu, tiny_models, name, monkeypatch):
+    """NLS_KV_DTYPE=fp8: an OCP e4m3 paged KV cache (half the attention bytes) through prefill (MFMA flash
+    prefill), the graph-captured decode and the fused RoPE/KV-append paths; greedy tokens stay close to
+    the fp32 reference (e4m3 rounds K/V to 3 mantissa bits, so exact agreement is not expected)."""
+    monkeypatch.setenv("NLS_KV_DTYPE", "fp8")
+    r = GGUFReader(tiny_models[name])
+    m = LlamaModel(r, gpu)
+    ref = ReferenceModel(r)
+    eng = Engine(m, None, max_batch=8, max_prefill_tokens=48, use_graphs=True)
+    assert eng.kc.dtype == torch.float8_e4m3fn
+    rng = np.random.default_rng(2)
+    prompts = [list(rng.integers(0, 900, n)) for n in (5, 17, 33, 50, 3)]
+    futs = [eng.submit(GenRequest(p, SamplingParams(max_tokens=8, ignore_eos=True))) for p in prompts]
+    while not all(f.done() for f in futs):
+        eng.step()
+    ok = sum(sum(int(a == b) for a, b in zip(f.result().token_ids, ref.greedy(p, 8))) for p, f in zip(prompts, futs))
+    assert ok >= 0.7 * 8 * len(prompts), ok
+    assert eng.counters["graph_replays"] > 0
+
+
 def test_graph_equals_eager(gpu, tiny_models):
     r = GGUFReader(tiny_models["tiny-llama"])
     m = LlamaModel(r, gpu)
