@@ -81,3 +81,67 @@ def test_stop_strings_incremental(tiny_models):
     assert res.finish_reason == "stop" and res.stop_reason == "stopStringFound"
     assert res.text == text[:first]
     assert len(res.token_ids) < len(full.token_ids)
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
+def test_cpu_fp8_kv_cache_engine(tiny_models, name, monkeypatch):
+    """NLS_KV_DTYPE=fp8: the paged KV cache is OCP e4m3 (the CPU reference paths round through the same
+    dtype); greedy decoding still tracks the fp32 reference closely."""
+    from nats_llm_studio_amd.engine.engine import Engine, GenRequest
+    from nats_llm_studio_amd.engine.sampling import SamplingParams
+    monkeypatch.setenv("NLS_KV_DTYPE", "fp8")
+    r = GGUFReader(tiny_models[name])
+    m = LlamaModel(r, "cpu")
+    ref = ReferenceModel(r)
+    eng = Engine(m, None, max_batch=4, max_prefill_tokens=32, use_graphs=False)
+    assert eng.kc.dtype == torch.float8_e4m3fn
+    prompts = [[5, 9, 200, 33], list(range(40, 60))]
+    futs = [eng.submit(GenRequest(p, SamplingParams(max_tokens=6, ignore_eos=True))) for p in prompts]
+    while not all(f.done() for f in futs):
+        eng.step()
+    ok = sum(sum(int(a == b) for a, b in zip(f.result().token_ids, ref.greedy(p, 6))) for p, f in zip(prompts, futs))
+    assert ok >= 0.6 * 12, ok
+    monkeypatch.setenv("NLS_KV_DTYPE", "fp16")
+    with pytest.raises(ValueError):
+        m.kv_cache(2, 16)
+
+
+def test_cpu_moe_norm_route_reference():
+    """ops.moe_norm_route on CPU == rmsnorm, then h @ Wr^T, then the top-k route."""
+    from nats_llm_studio_amd import ops
+    g = torch.Generator().manual_seed(3)
+    T, D, E, k, cap = 3, 256, 8, 2, 8
+    x = torch.randn(cap, D, generator=g)
+    nw = torch.rand(D, generator=g) + 0.5
+    wr = (torch.randn(E, D, generator=g) * 0.1).half()
+    bufs = [dict(h=torch.zeros(cap, D, dtype=ops.ACT_DTYPE), lg=torch.zeros(cap, E), topw=torch.zeros(cap * k),
+                 counts=torch.zeros(E, dtype=torch.int32), xr=torch.zeros(E * cap, dtype=torch.int32),
+                 yr=torch.zeros(E * cap, dtype=torch.int32)) for _ in range(2)]
+    a, b = bufs
+    assert ops.moe_norm_route(x, nw, 1e-5, wr, a["h"], a["lg"], T, k, a["topw"], a["counts"], a["xr"], a["yr"], cap)
+    ops.rmsnorm(x, nw, b["h"], T, 1e-5)
+    b["lg"][:T] = b["h"][:T].float() @ wr.float().t()
+    ops.moe_route(b["lg"], T, k, b["topw"], b["counts"], b["xr"], b["yr"], cap)
+    for key in a:
+        assert torch.equal(a[key], b[key]), key
+
+
+def test_lib_gemm_gating_cpu():
+    """Mode 7 is a GPU path for weights with f16 copies: never selected on CPU weights, for arg-max
+    launches, row maps or epilogues it lacks."""
+    from nats_llm_studio_amd import ops
+    from nats_llm_studio_amd.gguf import quants as Q
+    from nats_llm_studio_amd.gguf.constants import GGMLType
+    from nats_llm_studio_amd.ops import tuning
+    w = ops.QWeight(Q.random_blocks(GGMLType.Q4_K, 256 * 512, 0.05, np.random.default_rng(0)), 12, 256, 512, "cpu")
+    segs = [ops.Seg(w)]
+    tab = tuning.table()
+    key = tuning.lib_key(segs, 512)
+    assert key == "L:256:512:512"
+    try:
+        tab[key] = (1,)
+        assert tuning.select_lib(segs, 512)
+        assert not ops.lib_gemm_ok(segs, 512, "f32", 1.0, None, torch.zeros(512, 256))   # no f16 copy on CPU
+    finally:
+        tab.pop(key)
+    assert not tuning.select_lib(segs, 512)
