@@ -33,8 +33,8 @@ __device__ __forceinline__ int split_chunk(int chunk, int ctx, int n_split, int 
   return max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
 }
 
-template <int D, int G, typename KV>
-__global__ __launch_bounds__(256) void attn_decode_kernel(
+template <int D, int G, typename KV, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void attn_decode_kernel(
     const __bf16* __restrict__ q, long ldq, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
     const int* __restrict__ ctx_len, int Hkv, int bs, float scale, int chunk, int n_split,
@@ -42,7 +42,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     int* __restrict__ cnt) {
   constexpr int LPT = D / 8;          // lanes per key
   constexpr int TPW = 64 / LPT;       // keys per wave per step
-  constexpr int NSTREAM = 4 * TPW;    // independent softmax streams per workgroup
+  constexpr int NSTREAM = WAVES * TPW;  // independent softmax streams per workgroup (keys per step)
+  constexpr int NT = 64 * WAVES;
   const int t = blockIdx.x, kh = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int dl = lane % LPT, ts = lane / LPT;
@@ -163,30 +164,47 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
 
-  // ---- merge the NSTREAM streams through LDS ----------------------------------
-  __shared__ float sml[NSTREAM][G][2];
-  __shared__ float so[NSTREAM][G][D];
-  if (dl == 0) {
+  // ---- merge the TPW streams of each wave with shuffles (log-sum-exp, base 2), then the WAVES
+  // per-wave results through LDS
+#pragma unroll
+  for (int off = LPT; off < 64; off <<= 1) {
 #pragma unroll
     for (int h = 0; h < G; ++h) {
-      sml[stream][h][0] = m[h];
-      sml[stream][h][1] = l[h];
+      const float mo = __shfl_xor(m[h], off, 64), lo = __shfl_xor(l[h], off, 64);
+      const float mn = fmaxf(m[h], mo);
+      const float a = m[h] == -INFINITY ? 0.f : exp2f(m[h] - mn);
+      const float b = mo == -INFINITY ? 0.f : exp2f(mo - mn);
+      l[h] = l[h] * a + lo * b;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * a + __shfl_xor(o[h][i], off, 64) * b;
+      m[h] = mn;
     }
   }
+  __shared__ float sml[WAVES][G][2];
+  __shared__ float so[WAVES][G][D];
+  if (ts == 0) {
+    if (dl == 0) {
 #pragma unroll
-  for (int h = 0; h < G; ++h)
+      for (int h = 0; h < G; ++h) {
+        sml[wave][h][0] = m[h];
+        sml[wave][h][1] = l[h];
+      }
+    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) so[stream][h][8 * dl + i] = o[h][i];
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) so[wave][h][8 * dl + i] = o[h][i];
+  }
   __syncthreads();
-  for (int e = threadIdx.x; e < G * D; e += 256) {
+  for (int e = threadIdx.x; e < G * D; e += NT) {
     const int h = e / D, d = e - h * D;
     float M = -INFINITY;
 #pragma unroll
-    for (int s2 = 0; s2 < NSTREAM; ++s2) M = fmaxf(M, sml[s2][h][0]);
+    for (int s2 = 0; s2 < WAVES; ++s2) M = fmaxf(M, sml[s2][h][0]);
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int s2 = 0; s2 < NSTREAM; ++s2) {
+      for (int s2 = 0; s2 < WAVES; ++s2) {
         const float ms = sml[s2][h][0];
         if (ms == -INFINITY) continue;
         const float f = exp2f(ms - M);
@@ -227,7 +245,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   }
   __syncthreads();
   if (!last) return;
-  for (int e = threadIdx.x; e < G * D; e += 256) {
+  for (int e = threadIdx.x; e < G * D; e += NT) {
     const int h = e / D, d = e - h * D;
     const int qh = kh * G + h;
     const size_t pb = ((size_t)t * Hq + qh) * n_split;
@@ -276,13 +294,16 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
 template <int D, int G>
 void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const void* kc, const void* vc,
                  const int* bt, int bts, const int* ts, const int* cl, int Hkv, int bs, float scale, int chunk,
-                 int ns, act_t* out, long ldo, float* po, float* pml, int* cnt, bool kv8) {
-  if (kv8)
-    hipLaunchKernelGGL((attn_decode_kernel<D, G, uint8_t>), grid, dim3(256), 0, st, q, ldq, (const uint8_t*)kc,
-                       (const uint8_t*)vc, bt, bts, ts, cl, Hkv, bs, scale, chunk, ns, out, ldo, po, pml, cnt);
-  else
-    hipLaunchKernelGGL((attn_decode_kernel<D, G, __bf16>), grid, dim3(256), 0, st, q, ldq, (const __bf16*)kc,
-                       (const __bf16*)vc, bt, bts, ts, cl, Hkv, bs, scale, chunk, ns, out, ldo, po, pml, cnt);
+                 int ns, act_t* out, long ldo, float* po, float* pml, int* cnt, bool kv8, int waves) {
+#define NLS_ATTN_L(KVT, W)                                                                                      \
+  hipLaunchKernelGGL((attn_decode_kernel<D, G, KVT, W>), grid, dim3(64 * W), 0, st, q, ldq, (const KVT*)kc,      \
+                     (const KVT*)vc, bt, bts, ts, cl, Hkv, bs, scale, chunk, ns, out, ldo, po, pml, cnt)
+  if (kv8) {
+    if (waves == 8) NLS_ATTN_L(uint8_t, 8); else NLS_ATTN_L(uint8_t, 4);
+  } else {
+    if (waves == 8) NLS_ATTN_L(__bf16, 8); else NLS_ATTN_L(__bf16, 4);
+  }
+#undef NLS_ATTN_L
 }
 
 }  // namespace
@@ -301,12 +322,17 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(T, Hkv, n_split);
+  // waves per workgroup: 8 (twice the keys in flight per step) while the grid is small -- batch 1 / 16 at
+  // 4K context 2.93 -> 2.68 / 5.19 -> 4.76 ms/step, batch 1 at 128 2.24 -> 2.17 -- and 4 once the grid
+  // fills the chip (batch 512: 12.97 vs 13.74), profiles/attn_waves_ab.txt. NLS_ATTN_WAVES=4|8 forces.
+  static const int forced = [] { const char* e = getenv("NLS_ATTN_WAVES"); return e ? atoi(e) : 0; }();
+  const int waves = forced == 4 || forced == 8 ? forced : ((long)T * Hkv * n_split < 1024 ? 8 : 4);
   const __bf16* qq = (const __bf16*)q;
   act_t* o = (act_t*)out;
 #define NLS_ATTN_CASE(DD, GG)                                                                                 \
   if (D == DD && G == GG) {                                                                                  \
     launch_attn<DD, GG>(grid, st, qq, ldq, kc, vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, block_size, \
-                        scale, chunk, n_split, o, ldo, part_o, part_ml, cnt, kv8);                                \
+                        scale, chunk, n_split, o, ldo, part_o, part_ml, cnt, kv8, waves);                         \
   } else
   // G = Hq/Hkv of the supported families: 1 (MHA), 2/4/8 (Llama/Mixtral), 3/5/6/7 (Qwen2 sizes, e.g. 28/4)
   NLS_ATTN_CASE(128, 1) NLS_ATTN_CASE(128, 2) NLS_ATTN_CASE(128, 3) NLS_ATTN_CASE(128, 4) NLS_ATTN_CASE(128, 5)

@@ -51,6 +51,10 @@ _MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2"
 _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
 
 
+# device buffers superseded by larger ones; captured hipGraphs may still point at them
+_RETIRED: List[torch.Tensor] = []
+
+
 @dataclass
 class ShardSpec:
     """Model shard of this process (rank of size); size 1 = whole model.
@@ -331,7 +335,9 @@ class LlamaModel:
             logits=torch.zeros(min(pad, max(64, max_seqs)), Vs, **f),
             keys=torch.zeros(pad, dtype=torch.int64, device=dev),
             next_ids=torch.zeros(pad, dtype=torch.int32, device=dev),
-            attn_ws=torch.zeros(1, **f),
+            # flash-decoding partials for the split policy's largest T * n_split (attn_splits keeps
+            # T * Hkv * n_split <= _SPLIT_WG): allocated once, because captured decode graphs hold it
+            attn_ws=torch.zeros(max(1, (_SPLIT_WG // self.Hkv + 1) * self.Hq * (self.D + 2)), **f),
         )
         b.meta = meta
         b.pad = pad
@@ -380,6 +386,10 @@ class LlamaModel:
         ops.embed(b.ids, self.tok_embd, x, T, cfg.embedding_scale)
         need = T * Hq * n_split * (D + 2)
         if n_split > 1 and b.attn_ws.numel() < need:
+            # a larger explicit split than the policy's: grow, but keep the old buffer alive -- a graph
+            # captured earlier still writes its partials there (freeing it let a later allocation, e.g.
+            # prefill metadata, land under a replaying graph: the 256 x 1K-context fault of this round)
+            _RETIRED.append(b.attn_ws)
             b.attn_ws = torch.zeros(need, dtype=torch.float32, device=self.device)
         fused = self.shard.size == 1            # row-parallel GEMM + residual + next RMSNorm in one pass
         # few-row decode steps: every RMSNorm is folded into the GEMV that consumes it (no norm launches)
