@@ -164,10 +164,15 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_kernel(
     }
   }
 
-  // ---- merge the TPW streams of each wave with shuffles (log-sum-exp, base 2), then the WAVES
-  // per-wave results through LDS
+  // ---- merge the streams. 8 waves: first the TPW streams of each wave with shuffles (log-sum-exp,
+  // base 2), then the WAVES per-wave results through LDS (keeps the LDS area at 16 KiB); 4 waves: all
+  // NSTREAM streams through LDS directly (measured faster at batch 512, where the merge is a larger
+  // share of a short workgroup: profiles/attn_waves_ab.txt)
+  constexpr bool SHFL = WAVES == 8;
+  constexpr int NM = SHFL ? WAVES : NSTREAM;     // partials merged through LDS
+  const int slotm = SHFL ? wave : stream;
 #pragma unroll
-  for (int off = LPT; off < 64; off <<= 1) {
+  for (int off = LPT; SHFL && off < 64; off <<= 1) {
 #pragma unroll
     for (int h = 0; h < G; ++h) {
       const float mo = __shfl_xor(m[h], off, 64), lo = __shfl_xor(l[h], off, 64);
@@ -180,31 +185,31 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_kernel(
       m[h] = mn;
     }
   }
-  __shared__ float sml[WAVES][G][2];
-  __shared__ float so[WAVES][G][D];
-  if (ts == 0) {
+  __shared__ float sml[NM][G][2];
+  __shared__ float so[NM][G][D];
+  if (!SHFL || ts == 0) {
     if (dl == 0) {
 #pragma unroll
       for (int h = 0; h < G; ++h) {
-        sml[wave][h][0] = m[h];
-        sml[wave][h][1] = l[h];
+        sml[slotm][h][0] = m[h];
+        sml[slotm][h][1] = l[h];
       }
     }
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) so[wave][h][8 * dl + i] = o[h][i];
+      for (int i = 0; i < 8; ++i) so[slotm][h][8 * dl + i] = o[h][i];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < G * D; e += NT) {
     const int h = e / D, d = e - h * D;
     float M = -INFINITY;
 #pragma unroll
-    for (int s2 = 0; s2 < WAVES; ++s2) M = fmaxf(M, sml[s2][h][0]);
+    for (int s2 = 0; s2 < NM; ++s2) M = fmaxf(M, sml[s2][h][0]);
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int s2 = 0; s2 < WAVES; ++s2) {
+      for (int s2 = 0; s2 < NM; ++s2) {
         const float ms = sml[s2][h][0];
         if (ms == -INFINITY) continue;
         const float f = exp2f(ms - M);
