@@ -203,7 +203,8 @@ class Engine:
         # f16 copies of the projection weights for the large-M dense GEMM (prefill chunks, decode
         # batches >= ops.DENSE_MIN_M): NLS_DENSE_WEIGHTS=auto (default: when the copies take at most
         # 60 % of free HBM -- Llama-3-8B: 15 GB of 288, Llama-3-70B: 140 GB of ~245 (B=512 86.3 vs
-        # 96.8 ms/step with mode 7, profiles/bench_70b_mode7.txt); the rest stays for the KV pool), 1 (always),
+        # 96.8 ms/step with mode 7; at <= 256 rows its launches keep the quantised GEMMs, tuning "d:" -1
+        # entries: B=256 51.4 vs 58.4, profiles/bench_70b_mode7.txt); the rest stays for the KV pool), 1 (always),
         # 0 (never). NLS_DENSE_EXPERTS=1 adds the MoE experts (Mixtral-8x7B: 90 GB) as a second tier
         dense = os.environ.get("NLS_DENSE_WEIGHTS", "auto")
         self.dense_bytes = 0
