@@ -167,8 +167,13 @@ def run(args, world: int):
     prefill_steps = (B * args.prompt_len + max_prefill - 1) // max_prefill
     gen_tokens = args.warmup + args.steps + prefill_steps + 8
     need_tokens = args.prompt_len + gen_tokens
+    # the same engine later serves the --serve-load burst (prompts up to 1.5x --prompt-len + serve_tokens):
+    # its context covers those, and on GPUs the KV pool takes the engine's default share of free HBM
+    # (blocks are allocated as sequences grow, so pool size costs nothing in the timed decode steps)
+    serve_ctx = (3 * args.prompt_len // 2 + 16 + args.serve_tokens + 16) if args.serve_load > 0 else 0
+    ctx = max(need_tokens + 16, 512, serve_ctx)
     eng = Engine(model, None, max_batch=B, max_prefill_tokens=max_prefill, use_graphs=cuda and not args.no_graphs,
-                 ctx=max(need_tokens + 16, 512), num_blocks=B * ((need_tokens + 15) // 16 + 1))
+                 ctx=ctx, num_blocks=None if cuda else B * ((need_tokens + 15) // 16 + 1))
     marks = []
 
     def barrier_hook():                 # both sides of the timed region, on every rank
@@ -202,7 +207,7 @@ def run(args, world: int):
             for i in range(B)]
     # prefill every request (not timed), then warm up the decode loop
     t0 = time.time()
-    while any(s.n_prefilled < s.n_prompt for s in eng.running) or eng.waiting:
+    while any(s.n_prefilled < s.n_target for s in eng.running) or eng.waiting:
         eng.step()
     sync()
     t_prefill = time.time() - t0
@@ -284,7 +289,8 @@ def run(args, world: int):
             try:   # service-path throughput: concurrent chat_model burst through natscore
                 from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_load
                 extra["service_load"] = measure_engine_chat_load(eng, reader.metadata, n=args.serve_load,
-                                                                 max_tokens=args.serve_tokens)
+                                                                 max_tokens=args.serve_tokens,
+                                                                 prompt_tokens=args.prompt_len)
             except Exception as e:
                 extra["service_load_error"] = str(e)[:300]
     eng.stop_followers()

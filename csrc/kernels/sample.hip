@@ -60,7 +60,7 @@ DEVI float hist_threshold(const float* __restrict__ l, int V, float a, float b, 
     const float scale = (float)NB / (b - a);
     for (int i = threadIdx.x; i < V; i += NT) {
       const float v = l[i];
-      if (v >= a && v <= b && v >= keep_lo) {
+      if (v >= a && v <= b && v >= keep_lo && v > -INFINITY) {     // NaN / -inf never binned
         const int bin = min(NB - 1, (int)((b - v) * scale));
         atomicAdd(&hbin[bin], count ? 1.f : __expf((v - mx) * it));
       }
@@ -151,8 +151,13 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
   // 3) keep-threshold on the logit scale: top-k (k-th largest) and min-p (p >= min_p * p_max)
   float lo = -INFINITY;
   if (p.top_k > 0 && p.top_k < V) {
+    // lower search bound over FINITE logits only: a masked (-inf) entry would make the bin scale 0
+    // and its bin index NaN, and the threshold -inf would keep the whole vocabulary
     float mn = INFINITY;
-    for (int i = threadIdx.x; i < V; i += NT) mn = fminf(mn, l[i]);
+    for (int i = threadIdx.x; i < V; i += NT) {
+      const float v = l[i];
+      if (v > -INFINITY) mn = fminf(mn, v);
+    }
     mn = -block_max(-mn, red);
     lo = hist_threshold(l, V, mn, mx, -INFINITY, true, mx, it, (float)p.top_k, hbin, red);
   }

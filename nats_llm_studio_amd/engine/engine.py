@@ -5,7 +5,9 @@ Replaces LM Studio's request path behind `lmstudio.chat_model`
 serialises one generation per subscription. Here every in-flight request shares
 each decode step:
 
-  admission (KV blocks reserved for prompt + max_tokens)
+  admission (KV blocks for the prompt only; decode grows a sequence one block at a time and, when
+  the pool runs dry, preempts the most recently admitted sequences -- their blocks are freed and
+  they are re-prefilled from prompt + generated tokens when room returns: recompute preemption)
    -> chunked prefill (eager; quantised GEMVs in 64-row chunks + paged attention)
    -> decode loop: one hipGraph replay per step for the padded batch bucket
       + ONE host<-device copy of the next-token ids
@@ -30,7 +32,7 @@ import torch
 
 from .. import ops
 from ..models.llama import LlamaModel
-from .sampling import HIST, SamplingParams, sample_rows, sample_rows_gpu
+from .sampling import HIST, SamplingParams, sample_rows, sample_rows_gpu, uniform01
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 640, 768, 1024)
 
@@ -160,13 +162,16 @@ class BlockAllocator:
 
 class _Seq:
     __slots__ = ("req", "fut", "tokens", "n_prompt", "n_prefilled", "blocks", "t_submit", "t_admit", "t_first",
-                 "t_done", "gen", "max_new", "done", "text_cache", "row", "n_fed", "keys", "n_cached")
+                 "t_done", "gen", "max_new", "done", "text_cache", "row", "n_fed", "keys", "n_cached", "n_target",
+                 "preempted")
 
     def __init__(self, req: GenRequest, fut: Future):
         self.req = req
         self.fut = fut
         self.tokens = list(req.prompt_ids)
         self.n_prompt = len(req.prompt_ids)
+        self.n_target = self.n_prompt   # tokens to prefill before decoding (prompt + generated after a preemption)
+        self.preempted = 0
         self.n_prefilled = 0
         self.blocks: List[int] = []
         self.t_submit = time.monotonic()
@@ -226,6 +231,11 @@ class Engine:
         self.num_blocks = num_blocks
         self.kc, self.vc = model.kv_cache(num_blocks, block_size)
         self.alloc = BlockAllocator(num_blocks, cache=prefix_cache)
+        # admission keeps this many blocks free for the running sequences to grow into (fewer
+        # preemptions right after a burst of admissions); NLS_KV_RESERVE=full restores worst-case
+        # reservation of prompt + max_tokens at admission (no growth, no preemption)
+        self.watermark = max(1, num_blocks // 100)
+        self.reserve_full = os.environ.get("NLS_KV_RESERVE", "ondemand") == "full"
         self.max_prefill = max_prefill_tokens
         self.prefill_attn = prefill_attn      # MFMA flash-prefill attention (else per-token decode kernel)
         self.db = model.step_buffers(self.max_batch, self.max_batch, self.max_blocks)
@@ -260,7 +270,7 @@ class Engine:
         self.stop_flag = False
         self._ids = itertools.count()
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0,
-                             device_sampled_steps=0)
+                             device_sampled_steps=0, preemptions=0, recompute_tokens=0)
         self.full_logits: Optional[torch.Tensor] = None
         self._ctrl_hdr = torch.zeros(_HDR + self.max_batch, dtype=torch.int32)
         # In-graph sampling (single GPU): per-row sampling params / seeds / penalty-history rings live on
@@ -286,9 +296,16 @@ class Engine:
         if s.n_prompt >= self.ctx:
             fut.set_exception(ValueError(f"prompt ({s.n_prompt} tokens) exceeds the context length ({self.ctx})"))
             return fut
-        s.max_new = max(1, min(req.params.max_tokens, self.ctx - s.n_prompt))
-        if req.params.seed is not None and not req.params.greedy:
-            s.gen = torch.Generator(device="cpu").manual_seed(int(req.params.seed))
+        # a sequence must fit the context and, alone, the whole KV pool (it can always finish once every
+        # other sequence has been preempted)
+        cap = min(self.ctx, self.num_blocks * self.bs)
+        if s.n_prompt >= cap:
+            fut.set_exception(ValueError(f"prompt ({s.n_prompt} tokens) exceeds the KV cache ({cap} tokens)"))
+            return fut
+        s.max_new = max(1, min(req.params.max_tokens, cap - s.n_prompt))
+        if not req.params.greedy:             # one seed per request: u = uniform01(seed, position)
+            sd = req.params.seed
+            s.gen = (int(sd) if sd is not None else int.from_bytes(os.urandom(8), "little") >> 1) & 0x7FFFFFFFFFFFFFFF
         with self.lock:
             if self.stop_flag or self.model is None:    # unloaded / shut down: never park a request
                 fut.set_exception(RuntimeError("engine is not running (model unloaded)"))
@@ -369,10 +386,11 @@ class Engine:
     def step(self):
         self._expire()
         self._admit()
-        if any(s.n_prefilled < s.n_prompt for s in self.running):
-            self._drain()
+        if any(s.n_prefilled < s.n_target for s in self.running):
+            # the prefill chunk is queued behind the in-flight decode step (separate step buffers) and
+            # the next decode step still chains on that step's device-side tokens: no pipeline drain
             self._prefill()
-        dec = [s for s in self.running if s.n_prefilled >= s.n_prompt and not s.done]
+        dec = [s for s in self.running if s.n_prefilled >= s.n_target and not s.done]
         if dec:
             self._decode(dec)
         else:
@@ -399,11 +417,17 @@ class Engine:
         with self.lock:
             while self.waiting and len(self.running) < self.max_batch:
                 s = self.waiting[0]
-                need = math.ceil((s.n_prompt + s.max_new) / self.bs)
+                if self.reserve_full:
+                    need = math.ceil((s.n_prompt + s.max_new) / self.bs)
+                else:                          # the prompt now, decode blocks on demand (_ensure_blocks)
+                    need = math.ceil(s.n_target / self.bs)
                 # full prompt blocks, leaving >= 1 prompt token to prefill (its logits pick token 1)
-                s.keys = BlockAllocator.chain_keys(s.tokens, self.bs, (s.n_prompt - 1) // self.bs)
+                s.keys = BlockAllocator.chain_keys(s.tokens, self.bs, (s.n_target - 1) // self.bs)
                 hit = self.alloc.match(s.keys)
-                blocks = self.alloc.alloc(need - len(hit))
+                reserve = self.watermark if (self.running and not self.reserve_full) else 0
+                blocks = None
+                if need - len(hit) + reserve <= self.alloc.n_free:
+                    blocks = self.alloc.alloc(need - len(hit))
                 if blocks is None:
                     self.alloc.release(hit)
                     break
@@ -426,11 +450,11 @@ class Engine:
         budget = self.max_prefill
         T = 0
         rows, finishing = [], []
-        batch = [s for s in self.running if s.n_prefilled < s.n_prompt]
+        batch = [s for s in self.running if s.n_prefilled < s.n_target]
         for si, s in enumerate(batch):
             if budget <= 0:
                 break
-            n = min(budget, s.n_prompt - s.n_prefilled)
+            n = min(budget, s.n_target - s.n_prefilled)
             p0 = s.n_prefilled
             ids[T:T + n] = s.tokens[p0:p0 + n]
             pr = np.arange(p0, p0 + n)
@@ -443,7 +467,7 @@ class Engine:
             s.n_prefilled += n
             T += n
             budget -= n
-            if s.n_prefilled >= s.n_prompt:
+            if s.n_prefilled >= s.n_target:
                 rows.append(T - 1)
                 finishing.append(s)
                 self.alloc.register(s.blocks[:len(s.keys)], s.keys)
@@ -456,7 +480,8 @@ class Engine:
             toks = self._pick(finishing, b, list(range(len(finishing))))
             now = time.monotonic()
             for s, t in zip(finishing, toks):
-                s.t_first = now
+                if s.t_first is None:
+                    s.t_first = now
                 self._append(s, t)
 
     def _exec_prefill(self, T: int, rows: List[int], need_logits: bool):
@@ -546,10 +571,16 @@ class Engine:
             lg = self.full_logits if self.full_logits is not None else b.logits
             fn = sample_rows_gpu if lg.is_cuda else sample_rows
             toks = fn(lg[[rows[i] for i in sampled]], [seqs[i].req.params for i in sampled],
-                               [seqs[i].tokens for i in sampled], [seqs[i].gen for i in sampled])
+                      [seqs[i].tokens for i in sampled], [self._u(seqs[i]) for i in sampled])
             for i, t in zip(sampled, toks):
                 out[i] = t
         return out
+
+    @staticmethod
+    def _u(s: _Seq) -> float:
+        """The variate of s's next draw: uniform01(seed, position of its last token) -- what the in-graph
+        sampler uses for the same row and step."""
+        return uniform01(s.gen, len(s.tokens) - 1)
 
     def _bucket(self, B: int) -> int:
         for k in BUCKETS:
@@ -593,7 +624,7 @@ class Engine:
             seed = 0
         else:
             raw = ops.sample_params_bytes(p)
-            seed = int(p.seed) if p.seed is not None else int.from_bytes(os.urandom(8), "little") >> 1
+            seed = s.gen
         hist = np.full(HIST, -1, dtype=np.int32)
         n = len(s.tokens)
         for q in range(max(0, n - HIST), n):
@@ -680,10 +711,66 @@ class Engine:
             self._process(infl)
             self._release_rows()
 
+    def _ensure_blocks(self, seqs: List[_Seq]) -> List[_Seq]:
+        """Give every sequence about to decode the KV block its next position falls in. When the pool
+        cannot cover them, finish the in-flight step first (its finished sequences free blocks), then
+        preempt the most recently submitted sequences until it can. Returns the sequences still running."""
+        if self.reserve_full:
+            return seqs
+        bs = self.bs
+
+        def needers():
+            return [s for s in seqs if not s.done and s.n_fed < self.ctx and s.n_fed // bs >= len(s.blocks)
+                    and len(s.tokens) - s.n_prompt < s.max_new]
+        need = needers()
+        if len(need) > self.alloc.n_free:
+            self._drain()
+            seqs = [s for s in seqs if not s.done]
+            need = needers()
+            # priority is arrival order: the most recently submitted sequences give their blocks up first
+            victims = sorted((s for s in self.running if not s.done), key=lambda x: x.t_submit)
+            while len(need) > self.alloc.n_free and len(victims) > 1:
+                v = victims.pop()
+                self._preempt(v)
+                seqs = [s for s in seqs if s is not v]
+                need = [s for s in need if s is not v]
+        for s in need:
+            b = self.alloc.alloc(1)
+            if b is None:                      # cannot happen: one sequence always fits the pool
+                raise RuntimeError("KV pool exhausted by a single sequence")
+            s.blocks.append(b[0])
+            if s.row >= 0:
+                for hm in self.h_meta_d2:
+                    hm.numpy()[_NSEG * self.db.pad:].reshape(self.max_batch, self.max_blocks)[s.row, len(s.blocks) - 1] = b[0]
+        return seqs
+
+    def _preempt(self, s: _Seq):
+        """Recompute preemption (no step in flight): free the sequence's blocks and decode row and put it
+        back at the head of the queue; it is re-prefilled from prompt + generated tokens (the prefix cache
+        usually still holds its prompt blocks) and its stream continues where it stopped."""
+        self.alloc.release(s.blocks)
+        s.blocks = []
+        if s.row >= 0:
+            self.rows[s.row] = None
+            s.row = -1
+        s.n_target = len(s.tokens)
+        s.n_prefilled = s.n_cached = 0
+        s.n_fed = 0
+        s.preempted += 1
+        self.counters["preemptions"] += 1
+        self.counters["recompute_tokens"] += s.n_target
+        self.running = [x for x in self.running if x is not s]
+        with self.lock:
+            self.waiting.appendleft(s)
+
     def _decode(self, seqs: List[_Seq]):
         for s in seqs:
             if s.row < 0:
                 self._assign_row(s)
+        seqs = self._ensure_blocks(seqs)
+        if not seqs:
+            self._drain()
+            return
         greedy = all(s.req.params.greedy for s in seqs)
         dsamp = not greedy and self.device_sampling    # sampled rows drawn inside the decode graph
         chain = self.async_decode and (greedy or dsamp)
@@ -730,7 +817,7 @@ class Engine:
             lg = self.full_logits if self.full_logits is not None else b.logits
             fn = sample_rows_gpu if lg.is_cuda else sample_rows
             toks = fn(lg[[rows[i] for i in sampled]], [launch[i].req.params for i in sampled],
-                      [launch[i].tokens for i in sampled], [launch[i].gen for i in sampled])
+                      [launch[i].tokens for i in sampled], [self._u(launch[i]) for i in sampled])
             for i, t in zip(sampled, toks):
                 out[i] = t
         for s, t in zip(launch, out):
@@ -858,5 +945,6 @@ class Engine:
     def stats(self) -> dict:
         return dict(self.counters, running=len(self.running), waiting=len(self.waiting),
                     kv_blocks_free=self.alloc.n_free, kv_blocks_total=self.num_blocks,
+                    kv_reserve="full" if self.reserve_full else "ondemand",
                     prefix_cache_hit_tokens=self.alloc.hits, prefix_cache_blocks=len(self.alloc.block_of),
                     graphs=sorted(self.graphs))

@@ -2,10 +2,18 @@
 
 Greedy rows never leave the device: the lm-head GEMV fuses the arg-max. Only
 rows that ask for temperature / top-k / top-p / min-p / penalties go through
-this torch sampler on their logits rows.
+a sampler on their logits rows.
+
+Every sampling path draws the SAME way: the kept tokens (penalties -> temperature -> top-k ->
+min-p -> top-p) are walked in index order and the token where the cumulative mass passes u * Z
+is taken, with u = uniform01(seed, position) -- the counter-based splitmix64 variate of
+csrc/kernels/sample.hip. A seeded request therefore yields the same tokens whether it is sampled
+in the decode hipGraph, by the batched GPU sampler on the host-driven path (tensor parallel,
+logits requested) or by this module's CPU reference.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -56,9 +64,22 @@ class SamplingParams:
         )
 
 
+_M64 = (1 << 64) - 1
+
+
+def uniform01(seed: int, pos: int) -> float:
+    """Counter-based uniform in [0, 1) of (seed, position): bit-exact twin of sample.hip uniform01."""
+    z = (int(seed) + 0x9E3779B97F4A7C15 * (int(pos) + 1)) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    z ^= z >> 31
+    return (z >> 40) * (1.0 / 16777216.0)
+
+
 def sample_rows(logits: torch.Tensor, params: Sequence[SamplingParams], histories: Sequence[Sequence[int]],
-                generators: Sequence[Optional[torch.Generator]]) -> List[int]:
-    """logits [n, V] (device) -> one token per row."""
+                uniforms: Sequence) -> List[int]:
+    """logits [n, V] -> one token per row (CPU reference of the GPU sampler; `uniforms`: one variate per
+    row -- a float in [0, 1), a torch.Generator, or None for a fresh random one)."""
     out = []
     for i, p in enumerate(params):
         l = logits[i].float()
@@ -75,27 +96,26 @@ def sample_rows(logits: torch.Tensor, params: Sequence[SamplingParams], historie
         if p.temperature <= 0.0:
             out.append(int(l.argmax()))
             continue
-        l = l / p.temperature
-        if p.top_k and p.top_k > 0:
-            kth = torch.topk(l, min(p.top_k, l.numel())).values[-1]
-            l = torch.where(l < kth, torch.full_like(l, float("-inf")), l)
-        probs = torch.softmax(l, dim=-1)
+        l = l.double()
+        mx = l.max()
+        lo = torch.tensor(float("-inf"), dtype=l.dtype)
+        if p.top_k and 0 < p.top_k < l.numel():
+            lo = torch.topk(l, p.top_k).values[-1]          # k-th largest logit (ties kept)
         if p.min_p > 0.0:
-            probs = torch.where(probs < p.min_p * probs.max(), torch.zeros_like(probs), probs)
-        if p.top_p < 1.0:
-            sp, si = torch.sort(probs, descending=True)
-            cum = torch.cumsum(sp, 0)
-            keep = cum - sp < p.top_p
-            keep[0] = True
-            mask = torch.zeros_like(probs, dtype=torch.bool)
-            mask[si[keep]] = True
-            probs = torch.where(mask, probs, torch.zeros_like(probs))
-        probs = probs / probs.sum()
-        g = generators[i]
-        if g is not None and g.device != probs.device:
-            tok = int(torch.multinomial(probs.cpu(), 1, generator=g))
-        else:
-            tok = int(torch.multinomial(probs, 1, generator=g))
+            lo = torch.maximum(lo, mx + p.temperature * math.log(p.min_p))
+        w = torch.where(l >= lo, torch.exp((l - mx) / p.temperature), torch.zeros_like(l))
+        if p.top_p < 1.0:                                   # smallest top set whose mass reaches top_p
+            sw, si = torch.sort(w, descending=True)
+            cum = torch.cumsum(sw, 0)
+            n_keep = int(torch.searchsorted(cum, p.top_p * cum[-1]).item()) + 1
+            thr = sw[min(n_keep, sw.numel()) - 1]
+            w = torch.where(w >= thr, w, torch.zeros_like(w))
+        cdf = torch.cumsum(w, 0)
+        target = uniform(uniforms[i]) * float(cdf[-1])
+        tok = int(torch.searchsorted(cdf, torch.tensor(target, dtype=cdf.dtype), right=True).item())
+        kept = torch.nonzero(w > 0).flatten()
+        if tok >= l.numel() or w[tok] <= 0:                  # rounding at the very end: last kept token
+            tok = int(kept[-1]) if kept.numel() else 0
         out.append(tok)
     return out
 
@@ -103,15 +123,18 @@ def sample_rows(logits: torch.Tensor, params: Sequence[SamplingParams], historie
 HIST = 64      # penalty window (last tokens)
 
 
-def uniform(gen: Optional[torch.Generator]) -> float:
-    if gen is not None:
-        return float(torch.rand(1, generator=gen).item())
+def uniform(u) -> float:
+    """A row's variate: a float as given, a draw from a torch.Generator, or a fresh random one (None)."""
+    if isinstance(u, float):
+        return u
+    if u is not None:
+        return float(torch.rand(1, generator=u).item())
     import random
     return random.random()
 
 
 def sample_rows_gpu(logits: torch.Tensor, params: Sequence[SamplingParams], histories: Sequence[Sequence[int]],
-                    generators: Sequence[Optional[torch.Generator]]) -> List[int]:
+                    uniforms: Sequence) -> List[int]:
     """All sampled rows of a step in ONE kernel launch (csrc/kernels/sample.hip).
     `logits` [n, V] fp32 on the GPU is used as scratch (penalties are applied in place)."""
     import ctypes
@@ -128,7 +151,7 @@ def sample_rows_gpu(logits: torch.Tensor, params: Sequence[SamplingParams], hist
         h = list(histories[i])[-HIST:]
         hist[i, :len(h)] = h
         P[i] = _lib.SampleParams(p.temperature, p.top_p, p.min_p, p.repeat_penalty, p.presence_penalty,
-                                 p.frequency_penalty, uniform(generators[i]), int(p.top_k or 0), len(h), 0)
+                                 p.frequency_penalty, uniform(uniforms[i]), int(p.top_k or 0), len(h), 0)
     dev = lg.device
     pbytes = torch.frombuffer(bytearray(bytes(P)), dtype=torch.uint8).to(dev)
     hd = torch.from_numpy(hist).to(dev)

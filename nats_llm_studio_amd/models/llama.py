@@ -38,7 +38,7 @@ _SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgr
 _MIN_CHUNK = int(os.environ.get("NLS_ATTN_MIN_CHUNK", "0"))
 # MoE: tokens per step above which the experts run as ONE grouped LDS-dequant GEMM launch (below: path-A
 # GEMVs over each expert's gathered rows)
-# (Mixtral-8x7B: B=64 15.2 vs 28.9 ms/step, B=32 15.2 vs 15.6, B=16 14.8 vs 9.7; scripts/gpu_moe_thresh.sh)
+# (Mixtral-8x7B: B=64 15.2 vs 28.9 ms/step, B=32 15.2 vs 15.6, B=16 14.8 vs 9.7; round-2 sweep)
 _MOE_GEMM_T = int(os.environ.get("NLS_MOE_GEMM_T", "16"))
 # MoE decode at up to this many tokens (<= 4) fuses the FFN input RMSNorm, the router and the route
 # into one launch (ops.moe_norm_route); 0 disables
@@ -530,7 +530,7 @@ class LlamaModel:
         step = T if gemm else 32
         # m-block = 64*rt rows. Every m-block re-dequantises the expert's weights, so the largest block
         # wins; the GEMM multiplies only the block's real 16-row tiles (qgemm_impl.h NA), so ~64 routed
-        # rows in a 256-row block cost 64 rows of MFMA (Mixtral B=256, scripts/gpu_moe_na.sh: gate/up
+        # rows in a 256-row block cost 64 rows of MFMA (Mixtral B=256, round-2 sweep: gate/up
         # rt 4 / down rt 4 = 19.6 ms/step, 4/2 = 20.7, 2/2 = 28.3, 1/1 = 43.0)
         gu = dn = {}
         if not gemm and len(_MOE_GEMV_DN) == 4:

@@ -106,14 +106,18 @@ class EngineBackend:
 
     Loading never holds the registry lock: a model is built outside it (concurrent chats for the
     same model wait on one per-model future), so `list_models` / `health` / chats of loaded models
-    keep answering during a tens-of-seconds load. Every chat pins its model state (`inflight`);
-    an evicted or deleted model is unloaded only when its last in-flight chat has finished."""
+    keep answering during a tens-of-seconds load. Loads of DIFFERENT models are serialised by a
+    separate build mutex, and each evicts before it builds: two first requests for two models never
+    size their weights / KV pools against each other's half-finished allocations, and a model being
+    built counts toward `max_loaded_models`. Every chat pins its model state (`inflight`); an evicted
+    or deleted model is unloaded only when its last in-flight chat has finished."""
 
     name = "engine"
 
     def __init__(self, cfg):
         self.cfg = cfg
         self._lock = threading.RLock()
+        self._build_lock = threading.Lock()   # one model build at a time (device memory is sized at build)
         self._loaded: "collections.OrderedDict[str, dict]" = collections.OrderedDict()
         self._loading: Dict[str, "Future"] = {}
         self._ids: tuple = ()          # lock-free snapshot of the loaded model ids
@@ -194,14 +198,16 @@ class EngineBackend:
                 owner = fut is None
                 if owner:
                     fut = self._loading[entry.id] = Future()
-                    idle = self._evict_locked(max(1, self.cfg.max_loaded_models) - 1)
             if not owner:
                 fut.result()            # another chat is loading this model; then pin it (loop)
                 continue
-            for old in idle:
-                old["engine"].unload()
             try:
-                st = self.build_state(entry)
+                with self._build_lock:
+                    with self._lock:    # evict under the build mutex: the slot this build takes is free
+                        idle = self._evict_locked(max(1, self.cfg.max_loaded_models) - 1)
+                    for old in idle:
+                        old["engine"].unload()
+                    st = self.build_state(entry)
             except BaseException as e:
                 with self._lock:
                     self._loading.pop(entry.id, None)

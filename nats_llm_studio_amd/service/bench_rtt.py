@@ -102,14 +102,18 @@ def measure_engine_chat_rtt(engine, metadata: dict, model_id: str = "llama-3-8b"
 
 def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b", n: int = 512,
                              max_tokens: int = 64, sampled_frac: float = 0.5, timeout_s: float = 600.0,
-                             seed: int = 0) -> dict:
+                             seed: int = 0, prompt_tokens: int = 128) -> dict:
     """Service-path throughput: `n` concurrent `lmstudio.chat_model` requests published at once through
     the embedded NATS server (natscore) -> Python handlers -> chat template / tokenizer -> the REAL
     continuous-batching engine -> JSON replies to per-request inboxes. A fraction `sampled_frac` of the
     requests carries the reference README's sampling payload (`temperature: 0.7`,
     /root/reference/README.md:200-203); the rest are greedy. Reports output tok/s over the whole
     burst (first publish -> last reply, from the replies' usage.completion_tokens) and per-request
-    RTT p50/p99."""
+    RTT p50/p99. Prompts are random word sequences cut to a rendered length drawn uniformly from
+    [prompt_tokens/2, 3*prompt_tokens/2] tokens (mean = the headline config's seq_len). The result
+    carries the per-phase breakdown of the service tracer (recv -> validate -> tokenize -> queue ->
+    prefill -> decode -> respond, p50/p99 over all requests), the client-side dispatch share (RTT minus
+    the traced span) and the engine's counters over the burst."""
     import random
     import threading
     import time
@@ -149,7 +153,7 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
         cli = Client().connect(srv.url)
 
         def on_reply(m):
-            now = time.perf_counter()
+            now = time.monotonic()
             i = int(m.subject.rsplit(".", 1)[1])
             with lock:
                 t_recv[i] = now
@@ -160,11 +164,20 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
         sub = cli.subscribe("_INBOX.load.>", "", on_reply, 4)
         cli.flush()
         payloads = []
+        plens = []
+        tmpl_o = ChatTemplate(tmpl, bos, eos)
         for i in range(n):
-            text = " ".join(rnd.choice(words) for _ in range(rnd.randint(40, 90)))
-            req = {"model": model_id, "messages": [{"role": "system", "content": "You are a helpful assistant."},
-                                                   {"role": "user", "content": text}],
-                   "max_tokens": max_tokens, "ignore_eos": True}
+            target = rnd.randint(max(8, prompt_tokens // 2), max(9, 3 * prompt_tokens // 2))
+            ws = []
+            while True:
+                ws.append(rnd.choice(words))
+                msgs = [{"role": "system", "content": "You are a helpful assistant."},
+                        {"role": "user", "content": " ".join(ws)}]
+                nt = len(tok.encode(tmpl_o.render(msgs, add_generation_prompt=True), add_bos=False))
+                if nt >= target:
+                    break
+            plens.append(nt)
+            req = {"model": model_id, "messages": msgs, "max_tokens": max_tokens, "ignore_eos": True}
             if i < int(round(sampled_frac * n)):
                 req.update(temperature=0.7, top_p=0.95, seed=i)
             else:
@@ -172,14 +185,17 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
             payloads.append(json.dumps(req).encode())
         order = list(range(n))
         rnd.shuffle(order)                  # sampled and greedy requests interleave in the batch
+        c0 = dict(engine.counters)
         try:
-            t0 = time.perf_counter()
+            t0 = time.monotonic()
             for i in order:
-                t_send[i] = time.perf_counter()
+                t_send[i] = time.monotonic()
                 cli.publish("lmstudio.chat_model", payloads[i], reply=f"_INBOX.load.{i}")
             cli.flush()
             ok = done.wait(timeout_s)
-            t1 = max(t_recv.values()) if t_recv else time.perf_counter()
+            t1 = max(t_recv.values()) if t_recv else time.monotonic()
+            phases = svc.tracer.summary(last=0)["phases_ms"]
+            eng_d = {k: engine.counters[k] - c0.get(k, 0) for k in engine.counters}
         finally:
             sub.unsubscribe()
             cli.close()
@@ -204,12 +220,19 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
                 gen.append(st["generation_time"] * 1e3)
         rtts.append((t_recv[i] - t_send[i]) * 1e3)
     wall = t1 - t0
+    totals = [ph for ph in (phases.get("total") or {},)]
     return {"requests": n, "ok": good, "complete": bool(ok), "sampled_frac": sampled_frac, "max_tokens": max_tokens,
-            "completion_tokens": comp, "wall_s": round(wall, 3), "tok_s": round(comp / wall, 1) if wall > 0 else None,
+            "prompt_tokens_mean": round(sum(plens) / len(plens), 1), "prompt_tokens_max": max(plens),
+            "completion_tokens": comp, "completion_tokens_requested": n * max_tokens,
+            "wall_s": round(wall, 3), "tok_s": round(comp / wall, 1) if wall > 0 else None,
             "rtt_p50_ms": round(_pct(rtts, 50), 1) if rtts else None,
             "rtt_p99_ms": round(_pct(rtts, 99), 1) if rtts else None,
             "ttft_p50_ms": round(_pct(ttft, 50), 1) if ttft else None,
-            "generation_p50_ms": round(_pct(gen, 50), 1) if gen else None, "errors": errors}
+            "generation_p50_ms": round(_pct(gen, 50), 1) if gen else None,
+            "phases_ms": phases, "engine": {k: v for k, v in eng_d.items() if v},
+            "client_dispatch_p50_ms": (round(_pct(rtts, 50) - totals[0]["p50"], 2)
+                                       if rtts and totals and "p50" in totals[0] else None),
+            "errors": errors}
 
 
 if __name__ == "__main__":

@@ -2,7 +2,8 @@
 log.Printf calls, `nats_llm_studio.go:95, 210, 215`).
 
 A chat request is traced as monotonic spans
-    recv -> validate -> queue (engine admission wait) -> prefill -> decode -> respond
+    recv -> validate -> tokenize (chat template + BPE, model pin) -> queue (engine admission wait)
+         -> prefill (admission -> first token) -> decode -> respond (reply JSON + publish)
 kept in a bounded ring (exposed by `lmstudio.metrics`, phase percentiles + the last traces)
 and, with NLS_TRACE=1, written as one JSON log line per request.
 """
@@ -15,7 +16,7 @@ from typing import Dict, List, Optional
 
 from .metrics import LatencyHistogram, log
 
-PHASES = ("validate", "queue", "prefill", "decode", "respond", "total")
+PHASES = ("validate", "tokenize", "queue", "prefill", "decode", "respond", "total")
 
 
 class Tracer:
@@ -35,6 +36,7 @@ class Tracer:
                 spans[name] = marks[b] - marks[a]
 
         span("validate", "recv", "validated")
+        span("tokenize", "validated", "queued")
         span("queue", "queued", "admitted")
         span("prefill", "admitted", "first_token")
         span("decode", "first_token", "done")
@@ -55,6 +57,6 @@ class Tracer:
 
     def summary(self, last: int = 10) -> dict:
         with self._lock:
-            tail: List[dict] = list(self.recent)[-last:]
+            tail: List[dict] = list(self.recent)[-last:] if last > 0 else []
         return {"phases_ms": {k: h.summary_ms() for k, h in self.phase.items() if h.count},
                 "recent": tail}

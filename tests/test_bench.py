@@ -53,6 +53,11 @@ def test_service_load_generator_cpu(tiny_models):
     from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_load
     r = GGUFReader(tiny_models["tiny-llama"])
     eng = Engine(LlamaModel(r, "cpu"), None, max_batch=8, use_graphs=False, ctx=512)
-    out = measure_engine_chat_load(eng, r.metadata, n=8, max_tokens=3)
-    assert out["complete"] and out["ok"] == 8 and out["completion_tokens"] == 24
+    out = measure_engine_chat_load(eng, r.metadata, n=8, max_tokens=3, prompt_tokens=32)
+    assert out["complete"] and out["ok"] == 8 and out["completion_tokens"] == 24 == out["completion_tokens_requested"]
     assert out["tok_s"] > 0 and out["rtt_p99_ms"] >= out["rtt_p50_ms"]
+    assert 16 <= out["prompt_tokens_mean"] <= 64
+    ph = out["phases_ms"]
+    for k in ("validate", "tokenize", "queue", "prefill", "decode", "respond", "total"):
+        assert ph[k]["count"] == 8, (k, ph)
+    assert out["engine"]["prefill_tokens"] >= 8 * 16

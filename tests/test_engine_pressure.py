@@ -60,3 +60,40 @@ def test_pool_pressure_matches_roomy_engine(tiny_models):
             assert _margin(m, list(t) + b[:k]) < 1e-3, (a, b)
     assert tight.alloc.n_free == tight.num_blocks and all(r == 0 for r in tight.alloc.ref)
     assert tight._inflight is None and all(r is None for r in tight.rows)
+
+
+def test_preemption_completes_requests_larger_than_pool(tiny_models):
+    """KV blocks are allocated as sequences grow: requests whose prompt + max_tokens together need
+    ~2.5x the pool all run, the pool runs dry mid-decode, the most recently submitted sequences are
+    preempted (blocks freed) and re-prefilled from prompt + generated tokens later, and every request
+    still returns exactly max_tokens tokens -- the same tokens as on an engine with room to spare."""
+    m = LlamaModel(GGUFReader(tiny_models["tiny-llama"]), "cpu")
+    rng = np.random.default_rng(11)
+    reqs = [([int(v) for v in rng.integers(20, 200, int(rng.integers(4, 14)))],
+             SamplingParams(max_tokens=int(rng.integers(60, 100)), ignore_eos=True)) for _ in range(6)]
+    roomy = Engine(m, None, max_batch=8, max_prefill_tokens=64, num_blocks=256, use_graphs=False, ctx=256,
+                   async_decode=False)
+    ref = _run_all(roomy, reqs)
+    assert roomy.counters["preemptions"] == 0
+    # 16 blocks x 16 = 256 token slots for ~6 x 95 tokens of KV
+    tight = Engine(m, None, max_batch=8, max_prefill_tokens=32, num_blocks=16, use_graphs=False, ctx=256,
+                   async_decode=True)
+    got = _run_all(tight, reqs)
+    assert tight.counters["preemptions"] > 0, tight.stats()
+    for (t, p), a, b in zip(reqs, got, ref):
+        assert len(a) == len(b) == p.max_tokens
+        k = next((i for i in range(len(a)) if a[i] != b[i]), None)
+        if k is not None:
+            assert _margin(m, list(t) + b[:k]) < 1e-3, (a, b)
+    assert tight.alloc.n_free == tight.num_blocks and all(r == 0 for r in tight.alloc.ref)
+    assert tight._inflight is None and all(r is None for r in tight.rows)
+
+
+def test_full_reservation_mode_never_preempts(tiny_models, monkeypatch):
+    monkeypatch.setenv("NLS_KV_RESERVE", "full")
+    m = LlamaModel(GGUFReader(tiny_models["tiny-llama"]), "cpu")
+    reqs = _reqs(n=10, seed=5)
+    eng = Engine(m, None, max_batch=8, max_prefill_tokens=24, num_blocks=12, use_graphs=False, ctx=128)
+    got = _run_all(eng, reqs)
+    assert eng.counters["preemptions"] == 0 and eng.stats()["kv_reserve"] == "full"
+    assert [len(g) for g in got] == [p.max_tokens for _, p in reqs]

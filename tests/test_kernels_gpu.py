@@ -516,6 +516,23 @@ def test_sample_kernel(gpu):
     assert sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g1) == sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g2)
 
 
+def test_sample_top_k_with_masked_logits(gpu):
+    """-inf entries (a logit-bias / grammar mask) do not widen top-k: the histogram search spans the
+    finite logits only, so every draw stays inside the k largest finite logits."""
+    from nats_llm_studio_amd.engine.sampling import SamplingParams, sample_rows_gpu
+    torch.manual_seed(1)
+    V = 6000
+    base = torch.randn(1, V)
+    base[0, ::2] = float("-inf")
+    base[0, 101] = 7.0
+    base[0, 303] = 6.8
+    base[0, 505] = 6.6
+    n = 512
+    lg = base.repeat(n, 1).to(gpu)
+    toks = sample_rows_gpu(lg, [SamplingParams(temperature=1.0, top_k=3)] * n, [[]] * n, [None] * n)
+    assert set(toks) <= {101, 303, 505} and len(set(toks)) == 3, sorted(set(toks))
+
+
 def test_sample_and_embed_never_emit_wild_ids(gpu):
     """A non-finite logit row (all NaN / -inf) still yields an id inside the vocabulary from both the
     greedy and the sampling branch, and the embedding gather clamps ids: chained decode feeds sampled

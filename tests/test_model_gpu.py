@@ -165,3 +165,27 @@ def test_split_rmsnorm_decode_matches_plain(gpu, tiny_models, graphs):
         eng.shutdown()
     agree = sum(int(a == b) for r0, r1 in zip(*outs) for a, b in zip(r0, r1))
     assert outs[0][0][:4] == outs[1][0][:4] and agree >= 30, outs
+
+
+def test_seeded_sampling_same_on_device_and_host_paths(gpu, tiny_models, monkeypatch):
+    """A seeded request draws u = uniform01(seed, position) on every path: the in-graph sampler
+    (chained decode) and the host-driven batched GPU sampler (NLS_DEVICE_SAMPLING=0, the path tensor
+    parallel and logits requests take) produce the same tokens for the same seeds."""
+    r = GGUFReader(tiny_models["tiny-llama"])
+    m = LlamaModel(r, gpu)
+    prompt = [5, 17, 99, 3, 250, 7, 81, 12]
+    ps = [SamplingParams(max_tokens=16, ignore_eos=True, temperature=1.3, top_p=0.95, top_k=40, seed=s)
+          for s in (3, 4, 5)]
+
+    def run(dev):
+        monkeypatch.setenv("NLS_DEVICE_SAMPLING", "1" if dev else "0")
+        eng = Engine(m, None, max_batch=4, use_graphs=True)
+        assert eng.device_sampling == dev
+        futs = [eng.submit(GenRequest(list(prompt), p)) for p in ps]
+        while not all(f.done() for f in futs):
+            eng.step()
+        return [f.result().token_ids for f in futs], eng.counters["device_sampled_steps"]
+    a, na = run(True)
+    b, nb = run(False)
+    assert na > 0 and nb == 0
+    assert a == b, (a, b)

@@ -2,7 +2,7 @@
 # One GPU-box validation pass (used through gpurun): GPU tests, smoke, headline bench.
 # Every GPU step has its own time limit; a crash / abort / timeout stops the script (test
 # failures, exit 1, do not: the bench still runs so a single failing case does not hide perf).
-#   scripts/gpu_check.sh [tests|smoke|bench|all] [extra bench args...]
+#   tools/gpu_check.sh [tests|smoke|bench|all] [extra bench args...]
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out

@@ -4,7 +4,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD
-scripts/gpu_check.sh all || exit $?
+tools/gpu_check.sh all || exit $?
 timeout -k 10 300 python -u bench.py --concurrency 1 --steps 64 --warmup 8 --no-rtt > gpurun_out/bench_b1.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_b1.log
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
