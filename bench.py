@@ -59,6 +59,13 @@ def parse(argv=None):
                     help="after the timed region: N concurrent lmstudio.chat_model requests through NATS (half "
                          "sampled at temperature 0.7) against the same engine; 0 disables")
     ap.add_argument("--serve-tokens", type=int, default=256, help="max_tokens of each --serve-load request")
+    ap.add_argument("--tp-leg", type=int, default=1,
+                    help="with --gpus N > 1 and --tp 1: also measure Llama-3-70B over all N ranks (tensor parallel; "
+                         "reported as tp_leg); 0 disables")
+    ap.add_argument("--tp-leg-model", default=None,
+                    help="model of the TP leg (default llama-3-70b; on --device cpu llama-3-70b-1layer)")
+    ap.add_argument("--tp-leg-concurrency", type=int, default=64)
+    ap.add_argument("--tp-leg-timeout", type=float, default=900.0, help="seconds before the TP leg is abandoned")
     ap.add_argument("--step-breakdown", action="store_true",
                     help="report host time vs time blocked on the previous step's tokens (diagnostic)")
     a = ap.parse_args(argv)
@@ -98,11 +105,9 @@ def main(argv=None):
     return run(args, world)
 
 
-def run(args, world: int):
-    import numpy as np
+def _setup(args, world: int):
     import torch
     import torch.distributed as dist
-
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = args.device == "cuda"
@@ -112,29 +117,118 @@ def run(args, world: int):
     else:
         dev = torch.device("cpu")
         torch.set_num_threads(max(1, min(4, (os.cpu_count() or 2) // max(1, world))))
-    sync = torch.cuda.synchronize if cuda else (lambda *a: None)
-    tp = args.tp
-    replica, tp_rank = rank // tp, rank % tp
-    comm = None
     if world > 1:
         import datetime
         kw = dict(backend="nccl" if cuda else "gloo", timeout=datetime.timedelta(seconds=1800))
         if cuda:
             kw["device_id"] = dev
         dist.init_process_group(**kw)
-    if tp > 1:
-        from nats_llm_studio_amd.parallel.comm import Comm
-        mine = None
-        for g in range(world // tp):     # every rank creates every group, in the same order
-            ranks = list(range(g * tp, (g + 1) * tp))
-            pg = dist.new_group(ranks) if world > tp else dist.group.WORLD
-            cg = dist.new_group(ranks, backend="gloo") if cuda else pg
-            if g == replica:
-                mine = (pg, cg)
-        comm = Comm(mine[0], mine[1], dev)
-        if cuda and os.environ.get("NLS_ONESHOT_AR", "1") == "1":
-            from nats_llm_studio_amd.parallel.oneshot import try_oneshot
-            comm.oneshot = try_oneshot(comm)
+    return rank, local, cuda, dev
+
+
+def _tp_comm(world: int, tp: int, rank: int, cuda: bool, dev):
+    """This rank's tensor-parallel communicator (RCCL data plane + gloo/shm control, one-shot IPC AR)."""
+    import torch.distributed as dist
+    from nats_llm_studio_amd.parallel.comm import Comm
+    mine = None
+    for g in range(world // tp):     # every rank creates every group, in the same order
+        ranks = list(range(g * tp, (g + 1) * tp))
+        pg = dist.new_group(ranks) if world > tp else dist.group.WORLD
+        cg = dist.new_group(ranks, backend="gloo") if cuda else pg
+        if g == rank // tp:
+            mine = (pg, cg)
+    comm = Comm(mine[0], mine[1], dev)
+    if cuda and os.environ.get("NLS_ONESHOT_AR", "1") == "1":
+        from nats_llm_studio_amd.parallel.oneshot import try_oneshot
+        comm.oneshot = try_oneshot(comm)
+    return comm
+
+
+def run(args, world: int):
+    import torch
+    import torch.distributed as dist
+    rank, local, cuda, dev = _setup(args, world)
+    leg = _leg(args, world, rank, local, cuda, dev, args.model, args.ftype, args.tp, args.ep, args.concurrency,
+               args.steps, args.warmup, headline=True)
+    if world > 1 and args.tp == 1 and args.tp_leg > 0:
+        # dp runs on N > 1 GPUs also measure the tensor-parallel data plane: the 70B model over all N GPUs
+        # (BASELINE config 3), reported next to the headline as "tp_leg". It runs as a CHILD job (its own
+        # torch.distributed.run, started by rank 0 once every rank has freed its headline model) under a
+        # time limit, so a TP problem costs the leg, never the headline measurement.
+        leg["info"].pop("model", None)
+        leg.pop("eng", None)
+        import gc
+        gc.collect()
+        if cuda:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        ctrl = dist.new_group(backend="gloo") if cuda else None
+        dist.barrier(group=ctrl)
+        if rank == 0:
+            leg["extra"]["tp_leg"] = _run_tp_leg(args, world, cuda)
+        dist.barrier(group=ctrl)
+    _reduce_and_report(args, world, dist, torch, dev, leg["elapsed"], leg["tokens"], leg["info"], rank)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def _run_tp_leg(args, world: int, cuda: bool) -> dict:
+    tmodel = args.tp_leg_model or ("llama-3-70b" if cuda else "llama-3-70b-1layer")
+    if cuda and _skip_tp_leg(args, tmodel):
+        import shutil
+        free = shutil.disk_usage(args.model_dir).free
+        return {"skipped": f"{free / 1e9:.0f} GB free in {args.model_dir}; the {tmodel} GGUF needs ~43 GB"}
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--tp", str(world), "--model", tmodel,
+           "--ftype", "Q4_K_M", "--steps", str(args.steps), "--warmup", str(args.warmup), "--concurrency",
+           str(args.tp_leg_concurrency), "--prompt-len", str(args.prompt_len), "--no-rtt", "--serve-load", "0",
+           "--tp-leg", "0", "--device", args.device, "--model-dir", args.model_dir]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+                        "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE",
+                        "ROLE_NAME", "TORCH_NCCL_ASYNC_ERROR_HANDLING")}
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.tp_leg_timeout, env=env,
+                           start_new_session=True)
+    except subprocess.TimeoutExpired:
+        return {"model": f"{tmodel} Q4_K_M", "parallelism": f"tp{world}",
+                "error": f"no result within {args.tp_leg_timeout} s (killed)"}
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"model": f"{tmodel} Q4_K_M", "parallelism": f"tp{world}", "error": f"rc {r.returncode}",
+                "stderr_tail": r.stderr[-600:]}
+    d = json.loads(lines[-1])
+    return {"model": d["config"]["model"], "parallelism": d["config"]["parallelism"],
+            "concurrency": args.tp_leg_concurrency, "value": d["value"], "unit": d["unit"],
+            "ms_per_step": d["ms_per_step"], "steps": d["steps"], "weights_gb_per_rank": d["weights_gb_per_rank"],
+            "comm": d["comm"], "timings_s": d["timings_s"], "wall_s": round(time.time() - t0, 1)}
+
+
+    _reduce_and_report(args, world, dist, torch, dev, leg["elapsed"], leg["tokens"], leg["info"], rank)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def _skip_tp_leg(args, tmodel: str) -> bool:
+    """The 70B GGUF needs ~43 GB of disk next to the 8B one: skip (and say so) where there is no room."""
+    import shutil
+    os.makedirs(args.model_dir, exist_ok=True)
+    have = os.path.exists(os.path.join(args.model_dir, f"{tmodel}-Q4_K_M.gguf"))
+    return not have and shutil.disk_usage(args.model_dir).free < 50e9
+
+
+def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, steps, warmup, headline):
+    """One measured configuration: N/tp replicas of `model_name`, B in-flight requests per replica,
+    `warmup` untimed then `steps` timed decode steps bracketed by a world barrier + device sync."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sync = torch.cuda.synchronize if cuda else (lambda *a: None)
+    tp_rank = rank % tp
+    comm = _tp_comm(world, tp, rank, cuda, dev) if tp > 1 else None
 
     from nats_llm_studio_amd import build as nbuild
     from nats_llm_studio_amd.gguf.reader import GGUFReader
@@ -143,34 +237,34 @@ def run(args, world: int):
     from nats_llm_studio_amd.engine.engine import Engine, GenRequest
     from nats_llm_studio_amd.engine.sampling import SamplingParams
 
-    path = os.path.join(args.model_dir, f"{args.model}-{args.ftype}.gguf")
+    path = os.path.join(args.model_dir, f"{model_name}-{ftype}.gguf")
     t0 = time.time()
     if local == 0:
         if cuda:
             nbuild.build_kernels()
         if not os.path.exists(path):
             os.makedirs(args.model_dir, exist_ok=True)
-            write_synthetic_gguf(path, args.model, args.ftype, seed=0)
+            write_synthetic_gguf(path, model_name, ftype, seed=0)
     if world > 1:
         dist.barrier()
     t_gen = time.time() - t0
 
     t0 = time.time()
     reader = GGUFReader(path)
-    model = LlamaModel(reader, dev, ShardSpec(tp_rank, tp, args.ep), comm)
+    model = LlamaModel(reader, dev, ShardSpec(tp_rank, tp, ep), comm)
     sync()
     t_load = time.time() - t0
 
-    B = args.concurrency
     max_prefill = 2048
     # sequences prefilled early already decode while later ones prefill: budget those steps too
     prefill_steps = (B * args.prompt_len + max_prefill - 1) // max_prefill
-    gen_tokens = args.warmup + args.steps + prefill_steps + 8
+    gen_tokens = warmup + steps + prefill_steps + 8
     need_tokens = args.prompt_len + gen_tokens
-    # the same engine later serves the --serve-load burst (prompts up to 1.5x --prompt-len + serve_tokens):
+    serve = headline and args.serve_load > 0
+    # the headline engine later serves the --serve-load burst (prompts up to 1.5x --prompt-len + serve_tokens):
     # its context covers those, and on GPUs the KV pool takes the engine's default share of free HBM
     # (blocks are allocated as sequences grow, so pool size costs nothing in the timed decode steps)
-    serve_ctx = (3 * args.prompt_len // 2 + 16 + args.serve_tokens + 16) if args.serve_load > 0 else 0
+    serve_ctx = (3 * args.prompt_len // 2 + 16 + args.serve_tokens + 16) if serve else 0
     ctx = max(need_tokens + 16, 512, serve_ctx)
     eng = Engine(model, None, max_batch=B, max_prefill_tokens=max_prefill, use_graphs=cuda and not args.no_graphs,
                  ctx=ctx, num_blocks=None if cuda else B * ((need_tokens + 15) // 16 + 1))
@@ -183,15 +277,16 @@ def run(args, world: int):
         sync()
         marks.append(time.perf_counter())
 
+    info = dict(B=B, tp=tp, weights_gb=round(model.weight_bytes / 1e9, 3), n_expert=model.cfg.n_expert,
+                timings={"gguf_write": round(t_gen, 1), "load": round(t_load, 1)})
+    out = dict(elapsed=0.0, tokens=0.0, info=info, extra={})
     leader = tp_rank == 0
     if not leader:                      # follower: replay the leader's steps until STOP
         eng.sync_hook = barrier_hook
         eng.follow()
-        elapsed = marks[1] - marks[0] if len(marks) >= 2 else 0.0
-        _reduce_and_report(args, world, dist, torch, dev, elapsed, 0.0, None, rank)
-        if world > 1:
-            dist.destroy_process_group()
-        return 0
+        out["elapsed"] = marks[1] - marks[0] if len(marks) >= 2 else 0.0
+        info.update(model=model, comm_stats=None, rtt=None, chat_rtt=None, t_prefill=0.0, extra=out["extra"])
+        return out
 
     eng.capture_all()
     rng = np.random.default_rng(rank)
@@ -211,13 +306,15 @@ def run(args, world: int):
         eng.step()
     sync()
     t_prefill = time.time() - t0
-    for _ in range(args.warmup):
+    info["timings"]["prefill_all"] = round(t_prefill, 3)
+    for _ in range(warmup):
         eng.step()
     assert len(eng.running) == B, "all requests must still be decoding in the timed region"
 
     wait = [0.0]
     orig = eng._process
-    if args.step_breakdown and cuda:    # time the host spends blocked on step N's event (GPU-bound share)
+    extra = out["extra"]
+    if args.step_breakdown and cuda and headline:    # time the host spends blocked on step N's event
         def timed_outer(infl):
             t = time.perf_counter()
             eng._ev[infl[1]].synchronize()
@@ -226,24 +323,22 @@ def run(args, world: int):
         eng._process = timed_outer
     st0 = dict(comm.stats) if comm is not None else None
     eng.sync(barrier_hook) if tp > 1 else barrier_hook()
-    for _ in range(args.steps):
+    for _ in range(steps):
         eng.step()
     eng.sync(barrier_hook) if tp > 1 else barrier_hook()
     elapsed = marks[1] - marks[0]
-    tokens = B * args.steps
     eng._process = orig
     comm_stats = None
     if comm is not None:
         d = {k: comm.stats[k] - st0.get(k, 0) for k in comm.stats}
-        comm_stats = {"all_reduce_per_step": round(d["all_reduce"] / args.steps, 2),
-                      "all_reduce_bytes_per_step": int(d["all_reduce_bytes"] / args.steps),
-                      "ctrl_msgs_per_step": round(d["ctrl"] / args.steps, 2),
-                      "ctrl_us_per_step": round(d["ctrl_s"] / args.steps * 1e6, 1),
+        comm_stats = {"all_reduce_per_step": round(d["all_reduce"] / steps, 2),
+                      "all_reduce_bytes_per_step": int(d["all_reduce_bytes"] / steps),
+                      "ctrl_msgs_per_step": round(d["ctrl"] / steps, 2),
+                      "ctrl_us_per_step": round(d["ctrl_s"] / steps * 1e6, 1),
                       "ctrl_transport": "shm-ring" if comm.ring is not None else "gloo",
                       "oneshot": comm.oneshot is not None}
 
-    extra = {}
-    if args.step_breakdown and cuda:
+    if args.step_breakdown and cuda and headline:
         eng._drain()
         g = eng.graphs.get((eng._bucket(B), False))
         replay = None
@@ -256,8 +351,8 @@ def run(args, world: int):
             e1.record()
             sync()
             replay = round(e0.elapsed_time(e1) / 10, 3)
-        extra["step_breakdown_ms"] = {"gpu_wait": round(wait[0] / args.steps * 1e3, 3),
-                                      "host_other": round((elapsed - wait[0]) / args.steps * 1e3, 3),
+        extra["step_breakdown_ms"] = {"gpu_wait": round(wait[0] / steps * 1e3, 3),
+                                      "host_other": round((elapsed - wait[0]) / steps * 1e3, 3),
                                       "graph_replay_only": replay}
     moe = getattr(eng.db, "moe", None)
     if cuda and moe and "counts" in moe:   # routed rows per local expert, last MoE layer of the last step
@@ -268,13 +363,13 @@ def run(args, world: int):
         eng.step()
     for f in futs:
         f.result()
-    if args.single_stream:
+    if args.single_stream and headline:
         r = eng.generate(list(rng.integers(0, 1000, args.prompt_len)), SamplingParams(max_tokens=64, ignore_eos=True))
         extra["single_stream_tok_s"] = round(r.tokens_per_second, 1)
         extra["single_stream_ttft_ms"] = round(r.time_to_first_token * 1e3, 2)
 
     rtt = chat_rtt = None
-    if not args.no_rtt and rank == 0:
+    if headline and not args.no_rtt and rank == 0:
         try:
             from nats_llm_studio_amd.service.bench_rtt import measure_rtt
             rtt = measure_rtt(n=500)
@@ -285,7 +380,7 @@ def run(args, world: int):
             chat_rtt = measure_engine_chat_rtt(eng, reader.metadata, n=30)
         except Exception as e:
             extra["chat_rtt_error"] = str(e)[:300]
-        if args.serve_load > 0 and tp == 1:
+        if serve and tp == 1:
             try:   # service-path throughput: concurrent chat_model burst through natscore
                 from nats_llm_studio_amd.service.bench_rtt import measure_engine_chat_load
                 extra["service_load"] = measure_engine_chat_load(eng, reader.metadata, n=args.serve_load,
@@ -294,13 +389,9 @@ def run(args, world: int):
             except Exception as e:
                 extra["service_load_error"] = str(e)[:300]
     eng.stop_followers()
-
-    info = dict(model=model, B=B, tp=tp, t_gen=t_gen, t_load=t_load, t_prefill=t_prefill, rtt=rtt,
-                chat_rtt=chat_rtt, comm_stats=comm_stats, extra=extra)
-    _reduce_and_report(args, world, dist, torch, dev, elapsed, float(tokens), info, rank)
-    if world > 1:
-        dist.destroy_process_group()
-    return 0
+    info.update(model=model, rtt=rtt, chat_rtt=chat_rtt, comm_stats=comm_stats, t_prefill=t_prefill, extra=extra)
+    out.update(elapsed=elapsed, tokens=float(B * steps), eng=eng)
+    return out
 
 
 def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, rank):
@@ -313,10 +404,10 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
         t_max, tok_sum = float(mx[0]), float(tt[1])
     if rank != 0:
         return
-    model, B, tp = info["model"], info["B"], info["tp"]
+    B, tp = info["B"], info["tp"]
     dp = world // tp
     par = f"dp{dp}" if tp == 1 else (f"tp{tp}" if dp == 1 else f"dp{dp}xtp{tp}")
-    if args.ep and model.cfg.n_expert:
+    if args.ep and info["n_expert"]:
         par += "+ep"
     rtt, chat_rtt = info["rtt"], info["chat_rtt"]
     out = {
@@ -345,10 +436,9 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
         "p50_rtt_ms": (chat_rtt or {}).get("p50_ms", None if rtt is None else rtt.get("p50_ms")),
         "rtt_chat_model_engine": chat_rtt,
         "rtt": rtt,
-        "weights_gb_per_rank": round(model.weight_bytes / 1e9, 3),
+        "weights_gb_per_rank": info["weights_gb"],
         "comm": info["comm_stats"],
-        "timings_s": {"gguf_write": round(info["t_gen"], 1), "load": round(info["t_load"], 1),
-                      "prefill_all": round(info["t_prefill"], 3)},
+        "timings_s": info["timings"],
         **info["extra"],
     }
     print(json.dumps(out), flush=True)

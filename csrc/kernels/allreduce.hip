@@ -6,36 +6,93 @@
 // slices locally in RANK ORDER, so every rank gets a bit-identical result (the replicated residual
 // stream never drifts between shards).
 //
-// Synchronisation is carried by the data itself: each fp32 value travels as one 8-byte granule
-// {epoch:32 | bits:32} written with ONE system-scope atomic store; the consumer polls its granules
-// with system-scope atomic loads until every tag equals the current epoch. No flags, no fences,
-// no ordering between payload and signal to get wrong. Receive buffers are uncached device memory
-// (hipDeviceMallocUncached), so polls always observe HBM.
+// Synchronisation is carried by the data itself, 4 bytes per value: each fp32 travels with its two
+// low mantissa bits replaced by a 2-bit epoch tag (value rounded to 30 bits: relative error <= 2^-22)
+// and the consumer polls until every dword of a 16-byte load carries the current tag. A naturally
+// aligned dword is written and read atomically, so a 16-byte store that reaches the peer in pieces
+// is still checked dword by dword: no flags, no fences, no payload/signal ordering to get wrong.
+// Receive buffers are uncached device memory (hipDeviceMallocUncached): polls always observe HBM.
 //
-// Double-buffered by epoch parity: a rank can be at most one call ahead of any peer (it cannot
-// finish call c+1 without every peer's call-c+1 data, which a peer writes only after finishing c).
-// The grid is FIXED (AR_BLOCKS x AR_THREADS, grid-stride), so element -> block is the same on every
-// call and per-block epoch counters (local memory, advanced by the block itself) stay in lock-step
+// Why a 2-bit tag suffices: slots are double-buffered by epoch parity and a rank can be at most one
+// call ahead of any peer (it cannot finish call c+1 without every peer's call-c+1 data, which a peer
+// writes only after finishing c). A consumer overwrites every granule it has read with the tag of
+// the OTHER parity, and the buffers start out that way (parity-0 slots tag 1, parity-1 slots tag 0),
+// so a slot that a later epoch of its parity finds was either just written by that epoch or carries
+// a tag no epoch of that parity ever has -- also when calls of different sizes skip some slots.
+// Every rank uses the ROUNDED value of its own partial too, so the sums stay bit-identical.
+//
+// Element -> workgroup maps are fixed (the plain all-reduce runs a FIXED grid, grid-stride; the
+// fused add+norm maps row b, 256-column slice c to workgroup (b, c) for a given D), so the per-
+// workgroup epoch counters (device memory, advanced by the workgroup itself) stay in lock-step
 // across ranks and across hipGraph replays (no per-launch argument is frozen into a graph).
-// Spins are bounded: on timeout the block records an error code and exits (never hangs the GPU).
+// Spins are bounded: on timeout a workgroup raises the error word of EVERY rank (an extra 256-byte
+// area after the receive slots, written over xGMI) and its own, then exits -- never hangs the GPU;
+// the engine reads its error word after each decode step and fails the step's requests.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #define AR_MAX_RANKS 8
 #define AR_BLOCKS 32
 #define AR_THREADS 512
+#define ARN_THREADS 64          // fused add+norm: one wave per 256-column slice
+#define ARN_VPB (ARN_THREADS * 4)
+#define AR_ERR_BYTES 256
 
 struct ArPeers {
-  unsigned long long* buf[AR_MAX_RANKS];
+  uint32_t* buf[AR_MAX_RANKS];
 };
 
-__device__ __forceinline__ void st_sys(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint32_t ar_pack(float v, uint32_t tag) {
+  return ((__float_as_uint(v) + 2u) & ~3u) | tag;     // round to 30 bits, tag in the low 2
 }
-__device__ __forceinline__ unsigned long long ld_sys(unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ float ar_val(uint32_t g) { return __uint_as_float(g & ~3u); }
+__device__ __forceinline__ bool ar_tagged(uint4 g, uint32_t tag) {
+  return ((g.x & 3u) == tag) & ((g.y & 3u) == tag) & ((g.z & 3u) == tag) & ((g.w & 3u) == tag);
+}
+typedef uint32_t ar_u4 __attribute__((ext_vector_type(4)));
+// 16-byte volatile (cache-bypassing, never merged or hoisted) store / load of four tagged dwords
+__device__ __forceinline__ void ar_store(uint32_t* p, uint4 g) {
+  *reinterpret_cast<volatile ar_u4*>(p) = ar_u4{g.x, g.y, g.z, g.w};
+}
+__device__ __forceinline__ uint4 ar_load(const uint32_t* p) {
+  const ar_u4 r = *reinterpret_cast<const volatile ar_u4*>(p);
+  return make_uint4(r[0], r[1], r[2], r[3]);
+}
+__device__ __forceinline__ uint4 ar_pack4(float4 v, uint32_t tag) {
+  return make_uint4(ar_pack(v.x, tag), ar_pack(v.y, tag), ar_pack(v.z, tag), ar_pack(v.w, tag));
+}
+__device__ __forceinline__ float4 ar_val4(uint4 g) {
+  return make_float4(ar_val(g.x), ar_val(g.y), ar_val(g.z), ar_val(g.w));
 }
 
+// this rank's error word and the peers' (after the 2 x world x cap receive slots)
+__device__ __forceinline__ uint32_t* ar_err_word(uint32_t* buf, int world, long cap) {
+  return buf + 2L * world * cap;
+}
+__device__ void ar_raise(const ArPeers& P, int world, long cap, int* err) {
+  atomicExch(err, 1);
+  for (int p = 0; p < world; ++p)
+    __hip_atomic_store(ar_err_word(P.buf[p], world, cap), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// poll one 16-byte granule of peer data until every dword carries `tag` (bounded)
+__device__ __forceinline__ uint4 ar_poll(const uint32_t* src, uint32_t tag, long max_spins, bool& failed) {
+  uint4 g = ar_load(src);
+  long spins = 0;
+  while (!failed && !ar_tagged(g, tag)) {
+    if (++spins > max_spins) {
+      failed = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    g = ar_load(src);
+  }
+  return g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// plain all-reduce (MoE expert outputs, generic decode-size sums): fixed grid, grid-stride over
+// 16-byte granules (n % 4 == 0), data reduced in place
 __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restrict__ data, long n, ArPeers P,
                                                                  int world, int rank, long cap,
                                                                  unsigned* __restrict__ epochs,
@@ -44,161 +101,184 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
   __shared__ int s_fail;
   if (threadIdx.x == 0) {
     s_ep = epochs[blockIdx.x] + 1u;
-    if (s_ep == 0u) s_ep = 1u;  // epoch 0 is the zero-initialised (never written) tag
     s_fail = 0;
   }
   __syncthreads();
   const unsigned ep = s_ep;
+  const uint32_t tag = ep & 3u;
   const int par = (int)(ep & 1u);
   const long stride = (long)AR_BLOCKS * AR_THREADS;
-  // 1) push: my value -> slot [par][rank] of every peer (one 8-byte atomic granule per value)
-  for (long i = (long)blockIdx.x * AR_THREADS + threadIdx.x; i < n; i += stride) {
-    const unsigned long long g = ((unsigned long long)ep << 32) | __float_as_uint(data[i]);
+  const long n4 = n >> 2;
+  // 1) push: my (rounded, tagged) values -> slot [par][rank] of every peer, 16 B per lane
+  for (long i = (long)blockIdx.x * AR_THREADS + threadIdx.x; i < n4; i += stride) {
+    const uint4 g = ar_pack4(reinterpret_cast<const float4*>(data)[i], tag);
     for (int p = 0; p < world; ++p)
-      if (p != rank) st_sys(P.buf[p] + ((long)(par * world + rank)) * cap + i, g);
+      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + 4 * i, g);
   }
-  // 2) gather + reduce in rank order (bit-identical on every rank)
-  unsigned long long* mine = P.buf[rank];
-  bool failed = false;  // after one timeout, stop waiting (the error code is already recorded)
-  for (long i = (long)blockIdx.x * AR_THREADS + threadIdx.x; i < n; i += stride) {
-    float acc = 0.f;
+  // 2) gather + reduce in rank order (bit-identical on every rank); consumed granules get the
+  //    other parity's tag
+  uint32_t* mine = P.buf[rank];
+  const uint32_t ct = (ep + 1u) & 3u;
+  const uint4 clr = make_uint4(ct, ct, ct, ct);
+  bool failed = false;   // after one timeout, stop waiting (the error word is raised below)
+  for (long i = (long)blockIdx.x * AR_THREADS + threadIdx.x; i < n4; i += stride) {
+    const float4 own = ar_val4(ar_pack4(reinterpret_cast<const float4*>(data)[i], tag));
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = 0; p < world; ++p) {
-      float v;
-      if (p == rank) {
-        v = data[i];
-      } else {
-        unsigned long long* src = mine + ((long)(par * world + p)) * cap + i;
-        unsigned long long x = ld_sys(src);
-        long spins = 0;
-        while (!failed && (unsigned)(x >> 32) != ep) {
-          if (++spins > max_spins) {
-            failed = true;
-            s_fail = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-          x = ld_sys(src);
-        }
-        v = __uint_as_float((unsigned)(x & 0xFFFFFFFFull));
+      float4 v = own;
+      if (p != rank) {
+        uint32_t* src = mine + ((long)(par * world + p)) * cap + 4 * i;
+        v = ar_val4(ar_poll(src, tag, max_spins, failed));
+        ar_store(src, clr);
       }
-      acc += v;
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
     }
-    data[i] = acc;
+    reinterpret_cast<float4*>(data)[i] = acc;
   }
+  if (failed) s_fail = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
     epochs[blockIdx.x] = ep;
-    if (s_fail) atomicExch(err, 1);
+    if (s_fail) ar_raise(P, world, cap, err);
   }
 }
 
+// ---------------------------------------------------------------------------------------------
 // Fused row-parallel epilogue for tensor-parallel decode: x[b] += sum_r part_r[b] (rank order, one-shot
 // over the same IPC buffers), then h[b] = f16(rmsnorm(x[b]) * w) -- the all-reduce, the residual add and
-// the NEXT layer's input RMSNorm in one launch (vs all-reduce + norm launches; the residual row is read
-// and written once). One block per activation row; each block keeps its own epoch (all TP ranks replay
-// the same launches with the same row count, so block b's epoch advances in lock-step on every rank).
-// Receive slots: [parity][rank][row < rowcap][D] granules inside the same peer buffers.
-#define ARN_MAXV 16     // D <= ARN_MAXV * AR_THREADS elements per row kept in registers
-__global__ __launch_bounds__(AR_THREADS) void oneshot_ar_addnorm_kernel(
+// the NEXT layer's input RMSNorm in one launch. Workgroup (b, c) moves row b's 256-column slice c
+// (a 70B row of 8192 columns is spread over 32 workgroups, so at batch 1 the 7 x 32 KiB of pushes and
+// polls run on 32 CUs), adds it into the residual and leaves its share of sum(x^2); the slice that
+// arrives last at the row's ticket (agent-scope release / acquire, cdna_hip_programming.md Guideline
+// 16) sums the shares and normalises the whole row. Receive slots: [parity][rank][cap], row b at b * D.
+__global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     const float* __restrict__ part, long ldp, float* __restrict__ x, long ldx, const float* __restrict__ nw,
-    _Float16* __restrict__ h, long ldh, int D, float eps, ArPeers P, int world, int rank, long rowcap,
-    unsigned* __restrict__ epochs, int* __restrict__ err, long max_spins, long sp, long sx, long sh, long se) {
+    _Float16* __restrict__ h, long ldh, int D, float eps, ArPeers P, int world, int rank, long cap,
+    unsigned* __restrict__ epochs, int* __restrict__ tickets, float* __restrict__ ssq, int* __restrict__ err,
+    long max_spins, int sim, long sp, long sx, long sh, long se, long st, long sq) {
   __shared__ unsigned s_ep;
-  __shared__ int s_fail;
-  __shared__ float s_red[AR_THREADS / 64];
-  const int b = blockIdx.x;
-  if (gridDim.y > 1) {
-    // single-GPU simulation: ALL ranks in one grid (blockIdx.y = rank, per-rank operand strides), so
-    // the ranks' blocks are co-scheduled by construction (separate streams may share a hardware queue)
-    rank = blockIdx.y;
+  __shared__ int s_last;
+  int b = blockIdx.x;
+  const int c = blockIdx.y, nblk = gridDim.y;
+  if (sim > 1) {
+    // single-GPU simulation: ALL ranks in one grid, rank fastest (blockIdx.x = row * sim + rank, per-rank
+    // operand strides), so the ranks' workgroups of one slice are dispatched together and no slice
+    // waits on a workgroup the dispatcher has not placed yet
+    rank = blockIdx.x % sim;
+    b = blockIdx.x / sim;
     part += rank * sp;
     x += rank * sx;
     h += rank * sh;
     epochs += rank * se;
+    tickets += rank * st;
+    ssq += rank * sq;
   }
-  if (threadIdx.x == 0) {
-    s_ep = epochs[b] + 1u;
-    if (s_ep == 0u) s_ep = 1u;
-    s_fail = 0;
-  }
+  const int eidx = b * nblk + c;
+  if (threadIdx.x == 0) s_ep = epochs[eidx] + 1u;
   __syncthreads();
   const unsigned ep = s_ep;
+  const uint32_t tag = ep & 3u;
   const int par = (int)(ep & 1u);
-  const float* pr = part + (size_t)b * ldp;
-  // 1) push this rank's partial row to every peer
-  for (int i = threadIdx.x; i < D; i += AR_THREADS) {
-    const unsigned long long g = ((unsigned long long)ep << 32) | __float_as_uint(pr[i]);
-    for (int p = 0; p < world; ++p)
-      if (p != rank) st_sys(P.buf[p] + (((long)(par * world + rank)) * rowcap + b) * D + i, g);
-  }
-  // 2) rank-ordered sum + residual add (bit-identical on every rank), sum of squares in registers
-  unsigned long long* mine = P.buf[rank];
-  float xr[ARN_MAXV];
-  float ss = 0.f;
+  const int col = c * ARN_VPB + 4 * threadIdx.x;
+  const bool act = col < D;
   bool failed = false;
-#pragma unroll
-  for (int j = 0; j < ARN_MAXV; ++j) {
-    const int i = threadIdx.x + j * AR_THREADS;
-    xr[j] = 0.f;
-    if (i >= D) continue;
-    float acc = 0.f;
+  float ss = 0.f;
+  if (act) {
+    const float4 pv = *reinterpret_cast<const float4*>(part + (size_t)b * ldp + col);
+    const uint4 g = ar_pack4(pv, tag);
+    // 1) push this rank's partial slice to every peer
+    for (int p = 0; p < world; ++p)
+      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + (long)b * D + col, g);
+    // 2) rank-ordered sum + residual add (bit-identical on every rank); consumed granules get the
+    //    other parity's tag
+    uint32_t* mine = P.buf[rank];
+    const uint32_t ct = (ep + 1u) & 3u;
+    const float4 own = ar_val4(g);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = 0; p < world; ++p) {
-      float v;
-      if (p == rank) {
-        v = pr[i];
-      } else {
-        unsigned long long* src = mine + (((long)(par * world + p)) * rowcap + b) * D + i;
-        unsigned long long g = ld_sys(src);
-        long spins = 0;
-        while (!failed && (unsigned)(g >> 32) != ep) {
-          if (++spins > max_spins) {
-            failed = true;
-            s_fail = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-          g = ld_sys(src);
-        }
-        v = __uint_as_float((unsigned)(g & 0xFFFFFFFFull));
+      float4 v = own;
+      if (p != rank) {
+        uint32_t* src = mine + ((long)(par * world + p)) * cap + (long)b * D + col;
+        v = ar_val4(ar_poll(src, tag, max_spins, failed));
+        ar_store(src, make_uint4(ct, ct, ct, ct));
       }
-      acc += v;
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
     }
-    const float xi = x[(size_t)b * ldx + i] + acc;
-    x[(size_t)b * ldx + i] = xi;
-    xr[j] = xi;
-    ss += xi * xi;
+    float4* xp = reinterpret_cast<float4*>(x + (size_t)b * ldx + col);
+    float4 xv = *xp;
+    xv.x += acc.x;
+    xv.y += acc.y;
+    xv.z += acc.z;
+    xv.w += acc.w;
+    *xp = xv;
+    ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
   }
-  // 3) RMSNorm of the updated row
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = ss;
+  const unsigned long long fm = __ballot(failed);
+  // 3) publish the slice (x stores + share), then the row ticket: the last slice normalises the row
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) {
+    ssq[eidx] = ss;
+    epochs[eidx] = ep;
+    if (fm) ar_raise(P, world, cap, err);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(tickets + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tickets[b] = 0;          // stream order makes the reset visible to the next launch
+  }
   __syncthreads();
   float tot = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += ARN_THREADS) tot += ssq[(size_t)b * nblk + i];
 #pragma unroll
-  for (int w = 0; w < AR_THREADS / 64; ++w) tot += s_red[w];
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
   const float inv = rsqrtf(tot / (float)D + eps);
-#pragma unroll
-  for (int j = 0; j < ARN_MAXV; ++j) {
-    const int i = threadIdx.x + j * AR_THREADS;
-    if (i < D) h[(size_t)b * ldh + i] = (_Float16)(xr[j] * inv * nw[i]);
-  }
-  if (threadIdx.x == 0) {
-    epochs[b] = ep;
-    if (s_fail) atomicExch(err, 1);
+  const float* xr = x + (size_t)b * ldx;
+  _Float16* hr = h + (size_t)b * ldh;
+#pragma unroll 4
+  for (int i = 4 * threadIdx.x; i < D; i += 4 * ARN_THREADS) {
+    const float4 xv = *reinterpret_cast<const float4*>(xr + i);
+    const float4 wv = *reinterpret_cast<const float4*>(nw + i);
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    h4 o;
+    o[0] = (_Float16)(xv.x * inv * wv.x);
+    o[1] = (_Float16)(xv.y * inv * wv.y);
+    o[2] = (_Float16)(xv.z * inv * wv.z);
+    o[3] = (_Float16)(xv.w * inv * wv.w);
+    *reinterpret_cast<h4*>(hr + i) = o;
   }
 }
 
+__global__ void ar_err_clear_kernel(uint32_t* w) { *w = 0u; }
+
 extern "C" {
 
-// bytes of one rank's receive buffer for messages of up to `cap` floats
-long nls_ar_buffer_bytes(long cap, int world) { return 2L * world * cap * 8L; }
+// bytes of one rank's receive buffer for messages of up to `cap` floats (+ its error word area)
+long nls_ar_buffer_bytes(long cap, int world) { return 2L * world * cap * 4L + AR_ERR_BYTES; }
 
 int nls_ar_alloc(long cap, int world, void** buf, void* ipc_handle /* hipIpcMemHandle_t, 64 B */) {
-  if (world < 1 || world > AR_MAX_RANKS) return -1;
+  if (world < 1 || world > AR_MAX_RANKS || cap % 4) return -1;
   size_t bytes = (size_t)nls_ar_buffer_bytes(cap, world);
   hipError_t e = hipExtMallocWithFlags(buf, bytes, hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
+  // parity-0 slots start with tag 1, parity-1 slots (and the error word) with tag 0: no epoch of a
+  // slot's parity ever carries its initial tag
   e = hipMemset(*buf, 0, bytes);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*buf, 0x01, (size_t)world * cap * 4);
   if (e != hipSuccess) return (int)e;
   if (ipc_handle) {
     e = hipIpcGetMemHandle((hipIpcMemHandle_t*)ipc_handle, *buf);
@@ -221,41 +301,56 @@ int nls_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
 int nls_ar_blocks() { return AR_BLOCKS; }
 
-int nls_ar_addnorm_sim(const float*, long, float*, long, const float*, void*, long, int, int, float, void* const*, int,
-                       int, long, unsigned*, int*, long, void*, int, long, long, long, long);
+// workgroups per row of the fused add+norm (its epoch / share / ticket layout: [rows][nls_ar_row_blocks])
+int nls_ar_row_blocks(int D) { return (D + ARN_VPB - 1) / ARN_VPB; }
 
-// rows x D fused all-reduce + residual + RMSNorm; rows * D <= cap / 1 (the same buffers), `epochs` holds
-// one counter per row block (>= rowcap entries)
+// this rank's error word (raised by any rank whose poll timed out): async copy to `host` (pinned), clear
+int nls_ar_err_fetch(void* buf, long cap, int world, void* host, void* stream) {
+  return (int)hipMemcpyAsync(host, (char*)buf + 2L * world * cap * 4L, 4, hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+int nls_ar_err_clear(void* buf, long cap, int world, void* stream) {
+  hipLaunchKernelGGL(ar_err_clear_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
+                     (uint32_t*)((char*)buf + 2L * world * cap * 4L));
+  return (int)hipGetLastError();
+}
+
+int nls_ar_addnorm_sim(const float*, long, float*, long, const float*, void*, long, int, int, float, void* const*, int,
+                       int, long, unsigned*, int*, float*, int*, long, void*, int, long, long, long, long, long, long);
+
+// rows x D fused all-reduce + residual + RMSNorm; rows * D <= cap (the same buffers). `epochs`, `ssq`:
+// rowcap * nls_ar_row_blocks(D) entries; `tickets`: rowcap zero-initialised ints (left zeroed)
 int nls_ar_addnorm(const float* part, long ldp, float* x, long ldx, const float* nw, void* h, long ldh, int rows,
-                   int D, float eps, void* const* peers, int world, int rank, long cap, unsigned* epochs, int* err,
-                   long max_spins, void* stream) {
-  return nls_ar_addnorm_sim(part, ldp, x, ldx, nw, h, ldh, rows, D, eps, peers, world, rank, cap, epochs, err,
-                            max_spins, stream, 0, 0, 0, 0, 0);
+                   int D, float eps, void* const* peers, int world, int rank, long cap, unsigned* epochs, int* tickets,
+                   float* ssq, int* err, long max_spins, void* stream) {
+  return nls_ar_addnorm_sim(part, ldp, x, ldx, nw, h, ldh, rows, D, eps, peers, world, rank, cap, epochs, tickets,
+                            ssq, err, max_spins, stream, 0, 0, 0, 0, 0, 0, 0);
 }
 
 // sim_ranks > 1: every rank in one launch (rank r's operands at base + r * stride) -- SimulatedGroup
 int nls_ar_addnorm_sim(const float* part, long ldp, float* x, long ldx, const float* nw, void* h, long ldh, int rows,
-                       int D, float eps, void* const* peers, int world, int rank, long cap, unsigned* epochs, int* err,
-                       long max_spins, void* stream, int sim_ranks, long sp, long sx, long sh, long se) {
-  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || rows < 1 || D < 1 ||
-      D > ARN_MAXV * AR_THREADS)
+                       int D, float eps, void* const* peers, int world, int rank, long cap, unsigned* epochs,
+                       int* tickets, float* ssq, int* err, long max_spins, void* stream, int sim_ranks, long sp,
+                       long sx, long sh, long se, long st, long sq) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || rows < 1 || D < 4 || D % 4 || ldp % 4 ||
+      ldx % 4 || ldh % 4)
     return -1;
   const long rowcap = cap / D;
   if (rows > rowcap) return -1;
   ArPeers P;
-  for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (unsigned long long*)peers[i] : nullptr;
+  for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   if (sim_ranks > 1 && sim_ranks != world) return -1;
-  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(rows, sim_ranks > 1 ? sim_ranks : 1), dim3(AR_THREADS), 0,
-                     (hipStream_t)stream, part, ldp, x, ldx, nw, (_Float16*)h, ldh, D, eps, P, world, rank, rowcap,
-                     epochs, err, max_spins, sp, sx, sh, se);
+  const int sim = sim_ranks > 1 ? sim_ranks : 1;
+  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(rows * sim, nls_ar_row_blocks(D)), dim3(ARN_THREADS), 0,
+                     (hipStream_t)stream, part, ldp, x, ldx, nw, (_Float16*)h, ldh, D, eps, P, world, rank, cap, epochs,
+                     tickets, ssq, err, max_spins, sim, sp, sx, sh, se, st, sq);
   return (int)hipGetLastError();
 }
 
 int nls_ar_run(float* data, long n, void* const* peers, int world, int rank, long cap, unsigned* epochs,
                int* err, long max_spins, void* stream) {
-  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n > cap) return -1;
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n > cap || n % 4) return -1;
   ArPeers P;
-  for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (unsigned long long*)peers[i] : nullptr;
+  for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   hipLaunchKernelGGL(oneshot_ar_kernel, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, data, n, P,
                      world, rank, cap, epochs, err, max_spins);
   return (int)hipGetLastError();

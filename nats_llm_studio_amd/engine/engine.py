@@ -283,6 +283,11 @@ class Engine:
             self.d_seeds = torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev)
             self.d_hist = torch.full((self.max_batch, HIST), -1, dtype=torch.int32, device=self.dev)
         self.sync_hook: Optional[Callable[[], None]] = None   # follower side of Engine.sync()
+        # tensor parallel with the IPC one-shot all-reduce: its error words (raised on every rank when any
+        # rank's poll timed out) travel to the host with each step's tokens; a raised word fails the step
+        self._oneshot = getattr(model.comm, "oneshot", None) if self.tp is not None else None
+        self.h_err2 = ([torch.zeros(2, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+                       if self._oneshot is not None else None)
 
     # ------------------------------------------------------------------ API
     def submit(self, req: GenRequest) -> Future:
@@ -381,6 +386,8 @@ class Engine:
                 for s in list(self.running):
                     self._finish(s, "error", "engineError", error=str(e))
                 self.running.clear()
+                self._inflight = None          # the failed step's tokens are discarded with its requests
+                self._release_rows()
 
     # ------------------------------------------------------------------ scheduling
     def step(self):
@@ -690,16 +697,27 @@ class Engine:
             s.n_fed += 1
         if self.dev.type == "cuda":
             self.h_next2[k][:Bp].copy_(b.next_ids[:Bp], non_blocking=True)
+            if self._oneshot is not None:
+                self._oneshot.err_fetch(self.h_err2[k])
             self._ev[k].record()
         else:
             self.h_next2[k][:Bp].copy_(b.next_ids[:Bp])
         self.counters["decode_tokens"] += len(launch)
         return ([(s.row, s) for s in launch], k)
 
+    def _check_comm(self, k: int):
+        """Raise (failing the step's requests in _loop) when a tensor-parallel all-reduce of step buffer k
+        timed out on any rank: its sums -- and so its tokens -- are not trustworthy."""
+        if self.h_err2 is not None and int(self.h_err2[k].max()):
+            self.h_err2[k].zero_()
+            self._oneshot.err_clear()
+            raise RuntimeError("tensor-parallel all-reduce timed out waiting for a peer rank")
+
     def _process(self, infl):
         snap, k = infl
         if self.dev.type == "cuda":
             self._ev[k].synchronize()
+            self._check_comm(k)
         toks = self.h_next2[k].numpy()
         for row, s in snap:
             if not s.done:
@@ -808,6 +826,7 @@ class Engine:
         rows = [r for r, _ in snap]
         if self.dev.type == "cuda":
             self._ev[k].synchronize()
+            self._check_comm(k)
         greedy = self.h_next2[k].numpy()
         out = [int(greedy[r]) for r in rows]
         sampled = [i for i, s in enumerate(launch) if not s.req.params.greedy]

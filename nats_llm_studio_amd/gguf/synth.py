@@ -61,6 +61,9 @@ SPECS: Dict[str, ModelSpec] = {
     "tiny-llama": ModelSpec("tiny-llama", "llama", 2, 512, 4, 2, 768, 1024, 512, 10000.0),
     # TP-shardable tiny shape (TP=2: per-rank FFN 512, one kv head each) for CPU multi-rank benches
     "tiny-llama-tp": ModelSpec("tiny-llama-tp", "llama", 2, 512, 4, 2, 1024, 1024, 512, 10000.0),
+    # Llama-3-70B per-layer shapes (d 8192, 64 q / 8 kv heads, FFN 28672) with ONE layer and a 4K vocab: the
+    # CPU rehearsal of the TP=4/8 data plane (bench.py TP leg on --device cpu, tests/test_parallel_shapes.py)
+    "llama-3-70b-1layer": ModelSpec("llama-3-70b-1layer", "llama", 1, 8192, 64, 8, 28672, 4096, 512, 500000.0),
     "tiny-mixtral-tp": ModelSpec("tiny-mixtral-tp", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,
                                  n_expert=4, n_expert_used=2, tokenizer="llama"),
     "tiny-mixtral": ModelSpec("tiny-mixtral", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,

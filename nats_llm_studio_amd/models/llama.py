@@ -154,7 +154,7 @@ class LlamaModel:
         self.exp_ffn = cfg.d_ff if self.ep else self.ffn
         per = cfg.n_expert // n if self.ep else cfg.n_expert
         self.experts = list(range(shard.rank * per, (shard.rank + 1) * per)) if self.ep else list(range(cfg.n_expert))
-        if (self.Hq * self.D) % 256 or self.ffn % 256:
+        if (self.Hq * self.D) % 256 or self.exp_ffn % 256 or (not cfg.n_expert and self.ffn % 256):
             raise ValueError("TP shard widths must be multiples of 256 (K-quant super-blocks)")
         self.vocab_lo, self.vocab_hi = self._vocab_range()
         self.weight_bytes = 0

@@ -84,10 +84,13 @@ _SIGS = {
     "nls_ar_handle_size": [],
     "nls_ar_blocks": [],
     "nls_ar_addnorm": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float,
-                       c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_long, c_void_p],
+                       c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p],
     "nls_ar_addnorm_sim": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float,
-                           c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_long, c_void_p, c_int, c_long,
-                           c_long, c_long, c_long],
+                           c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
+                           c_int, c_long, c_long, c_long, c_long, c_long, c_long],
+    "nls_ar_row_blocks": [c_int],
+    "nls_ar_err_fetch": [c_void_p, c_long, c_int, c_void_p, c_void_p],
+    "nls_ar_err_clear": [c_void_p, c_long, c_int, c_void_p],
     "nls_ar_run": [c_void_p, c_long, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_long, c_void_p],
 }
 

@@ -8,9 +8,11 @@ the decode hipGraph. Messages above `cap` floats fall back to RCCL (Comm.all_red
 
 On by default for TP on GPUs (NLS_ONESHOT_AR=0 disables; an IPC setup failure falls back to RCCL).
 Row-parallel decode projections use the FUSED variant (`add_norm`): the ranks' partial sums, the
-residual add and the next RMSNorm in one launch. `SimulatedGroup` runs the same kernels for W
-"ranks" inside one process on one GPU (one stream per rank) -- the protocol test used on
-single-GPU boxes, where cross-device IPC cannot be exercised.
+residual add and the next RMSNorm in one launch, each row spread over D/256 workgroups. A poll that
+times out raises the error word of every rank; the engine fetches its word with each decode step's
+tokens (`err_fetch`) and fails the step instead of returning wrong sums. `SimulatedGroup` runs the
+same kernels for W "ranks" inside one process on one GPU -- the protocol test used on single-GPU
+boxes, where cross-device IPC cannot be exercised.
 """
 from __future__ import annotations
 
@@ -49,9 +51,10 @@ class OneShotAllReduce:
             self.close()
             raise RuntimeError("one-shot all-reduce: IPC buffer setup failed on some rank")
         dev = comm.device
+        self.device = dev
         self.epochs = torch.zeros(L.nls_ar_blocks(), dtype=torch.int32, device=dev)
-        self.nepochs = torch.zeros(max(1, self.cap // 1024), dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._norm = {}               # D -> (epochs, tickets, ssq) of the fused add+norm
         comm.barrier()
 
     def _exchange(self, L, hs, comm):
@@ -79,22 +82,46 @@ class OneShotAllReduce:
                 ptrs.append(None)
         return buf.value, (ctypes.c_void_p * self.world)(*ptrs)
 
+    def _norm_state(self, D: int):
+        st = self._norm.get(D)
+        if st is None:
+            st = _norm_buffers(self.cap, D, self.device)
+            self._norm[D] = st
+        return st
+
     def addnorm_ok(self, rows: int, D: int) -> bool:
-        return rows * D <= self.cap and rows <= self.nepochs.numel() and D <= 16 * 512
+        return D % 4 == 0 and rows * D <= self.cap
 
     def add_norm(self, part: torch.Tensor, x: torch.Tensor, nw: torch.Tensor, h: torch.Tensor, rows: int,
                  eps: float):
         """x[:rows] += sum over ranks of part[:rows] (rank order), h = f16(rmsnorm(x) * nw): one launch."""
         D = x.shape[1]
+        ep, tk, sq = self._norm_state(D)
         rc = _lib.lib().nls_ar_addnorm(part.data_ptr(), part.stride(0), x.data_ptr(), x.stride(0), nw.data_ptr(),
                                        h.data_ptr(), h.stride(0), rows, D, float(eps), self.npeers, self.world,
-                                       self.rank, self.cap, self.nepochs.data_ptr(), self.err.data_ptr(),
-                                       self.max_spins, _stream(x))
+                                       self.rank, self.cap, ep.data_ptr(), tk.data_ptr(), sq.data_ptr(),
+                                       self.err.data_ptr(), self.max_spins, _stream(x))
         _lib.check(rc, "nls_ar_addnorm")
         return h
 
     def eligible(self, t: torch.Tensor) -> bool:
-        return t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= self.cap
+        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= self.cap
+                and t.numel() % 4 == 0)
+
+    def err_fetch(self, host: torch.Tensor):
+        """Enqueue the copy of this rank's error word (raised by ANY rank's timed-out poll, in either buffer
+        set) into pinned int32 host[0:2] on the current stream; read it after the stream has passed."""
+        L = _lib.lib()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(L.nls_ar_err_fetch(self.buf, self.cap, self.world, host.data_ptr(), st), "nls_ar_err_fetch")
+        _lib.check(L.nls_ar_err_fetch(self.nbuf, self.cap, self.world, host.data_ptr() + 4, st), "nls_ar_err_fetch")
+
+    def err_clear(self):
+        L = _lib.lib()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        for b in (self.buf, self.nbuf):
+            _lib.check(L.nls_ar_err_clear(b, self.cap, self.world, st), "nls_ar_err_clear")
+        self.err.zero_()
 
     def all_reduce(self, t: torch.Tensor):
         rc = _lib.lib().nls_ar_run(t.data_ptr(), t.numel(), self.peers, self.world, self.rank, self.cap,
@@ -103,8 +130,11 @@ class OneShotAllReduce:
         return t
 
     def check(self):
-        """Raise if any call timed out waiting for a peer (call outside graph capture)."""
-        if int(self.err.item()):
+        """Raise if any rank's call timed out waiting for a peer (call outside graph capture)."""
+        host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        self.err_fetch(host)
+        torch.cuda.current_stream(self.device).synchronize()
+        if int(self.err.item()) or int(host[0]) or int(host[1]):
             raise RuntimeError("one-shot all-reduce timed out waiting for a peer")
 
     def close(self):
@@ -116,6 +146,17 @@ class OneShotAllReduce:
             L.nls_ar_free(ctypes.c_void_p(b))
         self._owned = []
         self.buf = None
+
+
+def _norm_buffers(cap: int, D: int, device, world_sim: int = 0):
+    """Per-workgroup epochs, per-row tickets and per-workgroup sum-of-squares shares of the fused
+    add+norm for rows of D columns (rows <= cap // D); world_sim > 0: one set per simulated rank."""
+    nblk = _lib.lib().nls_ar_row_blocks(D)
+    rowcap = max(1, cap // D)
+    lead = (world_sim,) if world_sim else ()
+    return (torch.zeros(*lead, rowcap * nblk, dtype=torch.int32, device=device),
+            torch.zeros(*lead, rowcap, dtype=torch.int32, device=device),
+            torch.zeros(*lead, rowcap * nblk, dtype=torch.float32, device=device))
 
 
 def try_oneshot(comm) -> Optional["OneShotAllReduce"]:
@@ -149,20 +190,50 @@ class SimulatedGroup:
             _lib.check(L.nls_ar_alloc(cap, world, ctypes.byref(b), None), "nls_ar_alloc")
             self.nbufs.append(b.value)
         self.npeers = (ctypes.c_void_p * world)(*self.nbufs)
-        self.nepochs_all = torch.zeros(world, max(1, cap // 1024), dtype=torch.int32, device=device)
+        self.device = device
+        self._norm = {}
 
     def add_norm(self, parts: torch.Tensor, xs: torch.Tensor, nw: torch.Tensor, hs: torch.Tensor, rows: int,
                  eps: float):
         """parts / xs (f32) and hs (f16): [world, rows, D]; every rank runs in ONE launch (blockIdx.y = rank),
         so the ranks are co-scheduled however streams map onto hardware queues."""
         D = xs.shape[2]
-        ep = self.nepochs_all
+        if D not in self._norm:
+            self._norm[D] = _norm_buffers(self.cap, D, self.device, self.world)
+        ep, tk, sq = self._norm[D]
         rc = _lib.lib().nls_ar_addnorm_sim(parts.data_ptr(), parts.stride(1), xs.data_ptr(), xs.stride(1),
                                            nw.data_ptr(), hs.data_ptr(), hs.stride(1), rows, D, float(eps),
-                                           self.npeers, self.world, 0, self.cap, ep.data_ptr(), self.err.data_ptr(),
-                                           self.max_spins, torch.cuda.current_stream().cuda_stream, self.world,
-                                           parts.stride(0), xs.stride(0), hs.stride(0), ep.stride(0))
+                                           self.npeers, self.world, 0, self.cap, ep.data_ptr(), tk.data_ptr(),
+                                           sq.data_ptr(), self.err.data_ptr(), self.max_spins,
+                                           torch.cuda.current_stream().cuda_stream, self.world,
+                                           parts.stride(0), xs.stride(0), hs.stride(0), ep.stride(0), tk.stride(0),
+                                           sq.stride(0))
         _lib.check(rc, "nls_ar_addnorm_sim")
+
+    def add_norm_rank(self, rank: int, part: torch.Tensor, x: torch.Tensor, nw: torch.Tensor, h: torch.Tensor,
+                      rows: int, eps: float, max_spins: int):
+        """ONE rank's fused add+norm alone (the production launch; the other ranks never arrive): the
+        fault-injection path of the bounded spin."""
+        D = x.shape[1]
+        if D not in self._norm:
+            self._norm[D] = _norm_buffers(self.cap, D, self.device, self.world)
+        ep, tk, sq = self._norm[D]
+        rc = _lib.lib().nls_ar_addnorm(part.data_ptr(), part.stride(0), x.data_ptr(), x.stride(0), nw.data_ptr(),
+                                       h.data_ptr(), h.stride(0), rows, D, float(eps), self.npeers, self.world, rank,
+                                       self.cap, ep[rank].data_ptr(), tk[rank].data_ptr(), sq[rank].data_ptr(),
+                                       self.err.data_ptr(), int(max_spins), torch.cuda.current_stream().cuda_stream)
+        _lib.check(rc, "nls_ar_addnorm")
+
+    def err_words(self) -> List[int]:
+        """Every simulated rank's error words (both buffer sets), synchronously."""
+        L = _lib.lib()
+        host = torch.zeros(2 * self.world, dtype=torch.int32, pin_memory=True)
+        st = torch.cuda.current_stream().cuda_stream
+        for r in range(self.world):
+            L.nls_ar_err_fetch(self.bufs[r], self.cap, self.world, host.data_ptr() + 8 * r, st)
+            L.nls_ar_err_fetch(self.nbufs[r], self.cap, self.world, host.data_ptr() + 8 * r + 4, st)
+        torch.cuda.current_stream().synchronize()
+        return host.tolist()
 
     def all_reduce(self, tensors: List[torch.Tensor]):
         L = _lib.lib()

@@ -49,6 +49,8 @@ class ShmCtrlRing:
             self.acks[:] = 0
             np.frombuffer(buf, dtype=np.int64, count=1, offset=0)[0] = 0
         dist.barrier(group=group)
+        import atexit
+        atexit.register(self.close)        # drop the numpy views before the segment is unmapped
 
     def _slot(self, seq: int):
         off = self.hdr + (seq % SLOTS) * self.slot_bytes
@@ -99,10 +101,15 @@ class ShmCtrlRing:
         return t
 
     def close(self):
+        if getattr(self, "shm", None) is None:
+            return
         try:
             self.mem = self.acks = None
+            import gc
+            gc.collect()
             self.shm.close()
             if self.rank == 0:
                 self.shm.unlink()
         except Exception:
             pass
+        self.shm = None

@@ -23,7 +23,7 @@ def _bench(tmp_path, *args):
 
 @pytest.mark.parametrize("extra,par,scaling", [
     (["--gpus", "2", "--tp", "2", "--model", "tiny-llama-tp"], "tp2", "strong"),
-    (["--gpus", "2", "--model", "tiny-llama-tp"], "dp2", "weak"),
+    (["--gpus", "2", "--model", "tiny-llama-tp", "--tp-leg", "0"], "dp2", "weak"),
     (["--gpus", "2", "--tp", "2", "--ep", "--model", "tiny-mixtral-tp"], "tp2+ep", "strong"),
 ])
 def test_bench_spawns_ranks(tmp_path, extra, par, scaling):
@@ -35,6 +35,19 @@ def test_bench_spawns_ranks(tmp_path, extra, par, scaling):
     if "tp" in par:
         assert out["comm"]["all_reduce_per_step"] > 0
     assert out["config"]["global_batch"] == (4 if "tp" in par else 8)
+
+
+def test_bench_dp_run_adds_tp_leg(tmp_path):
+    """--gpus N (dp, the driver's scaling run) also reports a tensor-parallel leg over all N ranks on the
+    70B per-layer shapes (CPU: one layer) with its all-reduce accounting: 2 row-parallel sums of 8192
+    fp32 per layer and token, plus the vocab-parallel argmax."""
+    out = _bench(tmp_path, "--gpus", "4", "--model", "tiny-llama-tp", "--tp-leg-concurrency", "2")
+    assert out["config"]["parallelism"] == "dp4" and out["value"] > 0
+    tl = out["tp_leg"]
+    assert tl["parallelism"] == "tp4" and tl["model"].startswith("llama-3-70b-1layer") and tl["value"] > 0
+    c = tl["comm"]
+    assert c["all_reduce_per_step"] >= 3 and c["all_reduce_bytes_per_step"] >= 2 * 2 * 8192 * 4
+    assert c["oneshot"] is False and c["ctrl_transport"] == "shm-ring"
 
 
 def test_bench_rejects_mismatched_world(tmp_path):

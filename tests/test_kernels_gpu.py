@@ -356,13 +356,14 @@ def test_oneshot_allreduce_simulated(gpu, world):
     """The one-shot IPC all-reduce protocol with W ranks as W concurrent streams on one GPU
     (W=2: with GPU_MAX_HW_QUEUES=4 more simulated ranks can share a hardware queue and then
     serialise, which the bounded spin reports as a timeout rather than a hang):
-    every rank must get the rank-ordered fp32 sum, bit-identical across ranks, over several
-    calls of varying size (epoch parity / slot reuse)."""
+    every rank must get the rank-ordered fp32 sum (of values rounded to 30 bits: 2-bit epoch tags),
+    bit-identical across ranks, over calls of varying size -- small calls skip most slots, so a
+    later call of the same parity must not take a stale granule (consumed slots are re-tagged)."""
     from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
     cap = 1 << 16
     g = SimulatedGroup(world, cap, gpu)
     try:
-        for it, n in enumerate([4096, 100, 65536, 7, 4096 * 3, 4096]):
+        for it, n in enumerate([4096, 100, 65536, 8, 4096 * 3, 4096, 64, 65536, 8, 65536, 4096]):
             xs = [torch.randn(n, device=gpu) for _ in range(world)]
             ref = xs[0].clone()
             for r in range(1, world):
@@ -373,33 +374,57 @@ def test_oneshot_allreduce_simulated(gpu, world):
             for r in range(world):
                 assert torch.equal(xs[r], xs[0])
             torch.testing.assert_close(xs[0], ref, rtol=1e-6, atol=1e-5)
+        assert not any(g.err_words())
     finally:
         g.close()
 
 
-@pytest.mark.parametrize("rows,D", [(1, 4096), (3, 8192), (16, 4096), (5, 2048)])
-def test_oneshot_allreduce_addnorm_simulated(gpu, rows, D):
-    """Fused TP decode epilogue (one launch): x += sum of the ranks' partials in rank order, then
-    h = f16(rmsnorm(x) * w) -- vs the fp32 reference, bit-identical x across ranks, repeated to
-    exercise both epoch parities."""
+@pytest.mark.parametrize("world,rows,D", [(2, 1, 4096), (2, 3, 8192), (2, 16, 4096), (2, 5, 2048),
+                                          (8, 1, 8192), (8, 16, 8192), (8, 64, 8192), (4, 7, 5120)])
+def test_oneshot_allreduce_addnorm_simulated(gpu, world, rows, D):
+    """Fused TP decode epilogue (one launch, each row over D/256 workgroups, the last to arrive at the
+    row ticket normalises): x += sum of the ranks' partials in rank order, then h = f16(rmsnorm(x) * w)
+    -- vs the fp32 reference, bit-identical x and h across ranks; repeated with a varying row count to
+    exercise both epoch parities, slot re-tagging and the per-row ticket reset. World 8, D 8192, rows
+    1/16/64 is the Llama-3-70B TP=8 decode regime."""
     from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
-    world = 2
-    g = SimulatedGroup(world, 1 << 16, gpu)
+    g = SimulatedGroup(world, 1 << 20, gpu)
     try:
         nw = (1 + 0.1 * torch.randn(D, device=gpu)).float()
-        for it in range(3):
-            base = torch.randn(rows, D, device=gpu)
-            parts = torch.randn(world, rows, D, device=gpu)
+        for it, rr in enumerate([rows, max(1, rows // 2), rows, rows]):
+            base = torch.randn(rr, D, device=gpu)
+            parts = torch.randn(world, rr, D, device=gpu)
             xs = base.unsqueeze(0).repeat(world, 1, 1).contiguous()
-            hs = torch.zeros(world, rows, D, dtype=ops.ACT_DTYPE, device=gpu)
-            g.add_norm(parts, xs, nw, hs, rows, 1e-5)
+            hs = torch.zeros(world, rr, D, dtype=ops.ACT_DTYPE, device=gpu)
+            g.add_norm(parts, xs, nw, hs, rr, 1e-5)
             torch.cuda.synchronize()
             assert int(g.err.item()) == 0, f"timeout at call {it}"
-            ref = base + parts[0] + parts[1]
+            ref = base + parts.sum(0)
             href = ref * torch.rsqrt(ref.pow(2).mean(1, keepdim=True) + 1e-5) * nw
-            assert torch.equal(xs[0], xs[1]) and torch.equal(hs[0], hs[1])
-            torch.testing.assert_close(xs[0], ref, rtol=1e-6, atol=1e-5)
+            for r in range(1, world):
+                assert torch.equal(xs[0], xs[r]) and torch.equal(hs[0], hs[r])
+            torch.testing.assert_close(xs[0], ref, rtol=1e-5, atol=1e-5)
             _close(hs[0], href, 1e-2)
+        assert not any(g.err_words())
+    finally:
+        g.close()
+
+
+def test_oneshot_timeout_raises_every_rank(gpu):
+    """Fault injection: rank 0 runs its fused add+norm while its peer never arrives. The bounded spin
+    gives up, the kernel returns (no GPU hang) and raises the error word of EVERY rank -- which the
+    engine reads with each decode step's tokens -- and OneShot's local flag."""
+    from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
+    g = SimulatedGroup(2, 1 << 16, gpu)
+    try:
+        D = 4096
+        x = torch.randn(2, D, device=gpu)
+        h = torch.zeros(2, D, dtype=ops.ACT_DTYPE, device=gpu)
+        g.add_norm_rank(0, torch.randn(2, D, device=gpu), x, torch.ones(D, device=gpu), h, 2, 1e-5, max_spins=2000)
+        torch.cuda.synchronize()
+        assert int(g.err.item()) == 1
+        w = g.err_words()                   # [rank0 buf, rank0 nbuf, rank1 buf, rank1 nbuf]
+        assert w[1] == 1 and w[3] == 1, w
     finally:
         g.close()
 

@@ -33,7 +33,7 @@ def _worker(rank, world, port, q):
         ar = OneShotAllReduce(comm, cap=1 << 16, max_spins=1 << 22)
         g = torch.Generator(device="cpu")
         out = {}
-        for it, n in enumerate([4096, 7, 65536]):
+        for it, n in enumerate([4096, 8, 65536]):
             xs = [torch.randn(n, generator=g.manual_seed(100 * it + r)) for r in range(world)]
             t = xs[rank].to(dev)
             ar.all_reduce(t)
