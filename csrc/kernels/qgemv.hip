@@ -9,6 +9,9 @@ namespace nls_hgemm {
 int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
                  const GemvArgs& a, hipStream_t st);
 }
+namespace nls_hg8 {
+int launch_dense8(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
+}
 
 
 extern "C" {
@@ -44,6 +47,9 @@ struct NlsFuse {
 //         blocks, 2: 128-row), optional split-K as mode 1.
 // mode 5: mode 4 with 256-row weight tiles (twice the MFMA work per fetched activation byte).
 // mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
+// mode 8: dense f16 GEMM with a 5-deep 32-k stage ring and register-double-buffered fragments
+//         (hgemm8.hip): 256-row activation blocks x 32*rt weight rows (rt 8: 256, 7: 224, 4: 128),
+//         plain rows only (no row maps), optional split-K as mode 1.
 // Returns 0 on success, a hipError_t, or -1 on bad arguments.
 static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, void* y, long ldy, int M,
                       float alpha, int epi, void* argmax, int waves, int rt, int mode, int ks, void* ws,
@@ -79,8 +85,14 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       if (segs[i].rows != segs[0].rows || segs[i].K != segs[0].K) return -1;
   }
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
-  if (mode < 0 || mode > 6 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
-  if (mode >= 4 && mode <= 6) {
+  if (mode < 0 || mode > 8 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode == 8) {
+    if (waves != 8 || (rt != 8 && rt != 7 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE || ldx % 8 ||
+        ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
+      return -1;
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
+  } else if (mode >= 4 && mode <= 6) {
     if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16) return -1;
@@ -98,7 +110,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16);
+  const int tile_rows = mode == 8 ? 32 * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -183,7 +195,9 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0) {
     if (ks < 1) ks = 1;
     int rc;
-    if (mode >= 4)
+    if (mode == 8)
+      rc = nls_hg8::launch_dense8(32 * rt, sl, tiles, ks, (float*)ws, a, st);
+    else if (mode >= 4)
       rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : 3, sl, tiles, ks, (float*)ws, a,
                                    st);
     else if (mode == 3)

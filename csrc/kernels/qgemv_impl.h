@@ -141,7 +141,9 @@ DEVI unsigned long long argmax_key(float v, int idx) {
   return ((unsigned long long)u << 32) | (0xFFFFFFFFu - (uint32_t)idx);
 }
 
-DEVI float silu(float g) { return g / (1.f + __expf(-g)); }
+// x * sigmoid(x) with the hardware reciprocal (1 ulp; an IEEE divide is ~10 instructions per value in
+// the GEMM epilogues). exp(-g) = inf for g << 0 gives g * 0 = -0.
+DEVI float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 // XL: the activation rows are first staged into LDS (batch <= a few rows, no row maps), so the
 // main loop's x reads are ds_reads and the VMEM queue holds only the weight stream: its in-order

@@ -319,9 +319,9 @@ def _seg_arr(segs: Sequence[Seg], mode: int):
     included: the dense GEMM gathers/scatters mapped rows like mode 2)."""
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
-        if mode in (4, 5, 6):
+        if mode in (4, 5, 6, 8):
             if s.w.d16 is None:
-                raise ValueError(f"{s.w.name}: mode 4 needs QWeight.expand_dense()")
+                raise ValueError(f"{s.w.name}: dense modes (4-6, 8) need QWeight.expand_dense()")
             arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, s.w.rows, s.w.K,
                                  s.ycol)
         else:
@@ -522,7 +522,11 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
                                                 norm_w.data_ptr(), h.data_ptr(), h.stride(0), x.shape[1], float(eps),
                                                 st), "nls_splitk_add_rmsnorm")
             return h
-    qgemv([seg], xin, x, M, alpha=alpha, epi="add")
+    if cfg is not None and x.is_cuda:
+        mode, waves, rt, ks = cfg
+        qgemv([seg], xin, x, M, alpha=alpha, epi="add", mode=mode, waves=waves, rt=rt, ks=ks)
+    else:
+        qgemv([seg], xin, x, M, alpha=alpha, epi="add")
     return rmsnorm(x, norm_w, h, M, eps)
 
 
