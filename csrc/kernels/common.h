@@ -42,7 +42,10 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 act_t;   // activation dtype of GEMM operands (torch.float16 on the host)
 
 enum QType : int {
-  QT_F32 = 0, QT_F16 = 1, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14, QT_BF16 = 30
+  QT_F32 = 0, QT_F16 = 1, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14, QT_BF16 = 30,
+  // device-only: the 32-value affine blocks of ggml Q4_0 / Q4_1 / Q5_0 / Q5_1 (x = d*q + m, q 5-bit; the
+  // symmetric types with m = -8d / -16d, exact) in the Q5_K tile layout with per-block f16 (d, m)
+  QT_Q51 = 101
 };
 
 #define DEVI __device__ __forceinline__
@@ -134,6 +137,7 @@ DEVI void bytes_to_h(uint32_t w, f16x2 off, f16x2& lo, f16x2& hi) {
 
 struct RawQ4K { u32x4 hdr, p0, p1; };
 struct RawQ5K { u32x4 hdr, p0, p1; u32x2 qh; };
+struct RawQ51 { u32x4 dd, mm, p0, p1; u32x2 qh; };
 struct RawQ6K { u32x4 qa, qb, qh; u32x4 sc; uint32_t d; };
 struct RawQ8 { u32x4 q[4]; u32x4 d; };
 struct RawF16 { u32x4 v[8]; };
@@ -142,6 +146,7 @@ struct RawF32 { u32x4 v[16]; };
 template <int T> struct RawOf;
 template <> struct RawOf<QT_Q4_K> { typedef RawQ4K type; };
 template <> struct RawOf<QT_Q5_K> { typedef RawQ5K type; };
+template <> struct RawOf<QT_Q51> { typedef RawQ51 type; };
 template <> struct RawOf<QT_Q6_K> { typedef RawQ6K type; };
 template <> struct RawOf<QT_Q8_0> { typedef RawQ8 type; };
 template <> struct RawOf<QT_F16> { typedef RawF16 type; };
@@ -163,6 +168,7 @@ DEVI f16x2 bcast(const f16x2* a2, int s) {
 template <int T> struct ScOf { typedef ScNone type; };
 template <> struct ScOf<QT_Q4_K> { typedef ScK type; };
 template <> struct ScOf<QT_Q5_K> { typedef ScK type; };
+template <> struct ScOf<QT_Q51> { typedef ScK type; };
 template <> struct ScOf<QT_Q6_K> { typedef ScQ6K type; };
 template <> struct ScOf<QT_Q8_0> { typedef ScQ8 type; };
 
@@ -176,6 +182,7 @@ struct WDesc {
 template <int T> struct TileBytes;
 template <> struct TileBytes<QT_Q4_K> { static constexpr int v = 2304; };
 template <> struct TileBytes<QT_Q5_K> { static constexpr int v = 2816; };
+template <> struct TileBytes<QT_Q51> { static constexpr int v = 3072; };
 template <> struct TileBytes<QT_Q6_K> { static constexpr int v = 3360; };
 template <> struct TileBytes<QT_Q8_0> { static constexpr int v = 4352; };
 template <> struct TileBytes<QT_F16> { static constexpr int v = 8192; };
@@ -212,6 +219,36 @@ DEVI RawQ5K load_raw_q5k(const WDesc& W, int row, int sb, int g) {
   x.p0 = NT ? ld16_nt(b + 768 + 16 * l) : ld16(b + 768 + 16 * l);
   x.p1 = NT ? ld16_nt(b + 1792 + 16 * l) : ld16(b + 1792 + 16 * l);
   return x;
+}
+
+// Q51 tile-block: [16 rows x (8 f16 d | 8 f16 m)] 512 B | QH as Q5_K 512 B | P as Q5_K 2048 B
+template <bool NT>
+DEVI RawQ51 load_raw_q51(const WDesc& W, int row, int sb, int g) {
+  const uint8_t* b = tile_block<QT_Q51>(W, row, sb);
+  const int r = row & 15, l = 16 * g + r;
+  RawQ51 x;
+  x.dd = ld16(b + 32 * r);
+  x.mm = ld16(b + 32 * r + 16);
+  x.qh = NT ? ld8_nt(b + 512 + 8 * l) : ld8(b + 512 + 8 * l);
+  x.p0 = NT ? ld16_nt(b + 1024 + 16 * l) : ld16(b + 1024 + 16 * l);
+  x.p1 = NT ? ld16_nt(b + 2048 + 16 * l) : ld16(b + 2048 + 16 * l);
+  return x;
+}
+// block t's (d, m) are the scale pair of K-step t: no unpacking
+DEVI void prep_q51(const RawQ51& r, ScK& s) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s.a2[i] = as_h2(r.dd[i]);
+    s.c2[i] = as_h2(r.mm[i]);
+  }
+}
+// the Q5_K nibble / high-bit arrangement (the loader re-packs the 32-blocks that way)
+DEVI f16x8 frag_q51(const RawQ51& r, const ScK& s, int t) {
+  const u32x4 p = t < 4 ? r.p0 : r.p1;
+  const int wi = 2 * ((t >> 1) & 1), sh = 4 * (t & 1);
+  const uint32_t n0 = ((p[wi] >> sh) & 0x0F0F0F0Fu) | (((r.qh[0] >> t) & 0x01010101u) << 4);
+  const uint32_t n1 = ((p[wi + 1] >> sh) & 0x0F0F0F0Fu) | (((r.qh[1] >> t) & 0x01010101u) << 4);
+  return frag8(n0, n1, h2((_Float16)1024.f), bcast(s.a2, t), bcast(s.c2, t));
 }
 
 // ggml get_scale_min_k4 for all 8 sub-blocks at once (bytes of 3 dwords), then f16:
@@ -356,6 +393,7 @@ template <int T, bool NT>
 DEVI typename RawOf<T>::type load_raw(const WDesc& W, int row, int sb, int g) {
   if constexpr (T == QT_Q4_K) return load_raw_q4k<NT>(W, row, sb, g);
   else if constexpr (T == QT_Q5_K) return load_raw_q5k<NT>(W, row, sb, g);
+  else if constexpr (T == QT_Q51) return load_raw_q51<NT>(W, row, sb, g);
   else if constexpr (T == QT_Q6_K) return load_raw_q6k<NT>(W, row, sb, g);
   else if constexpr (T == QT_Q8_0) return load_raw_q8<NT>(W, row, sb, g);
   else if constexpr (T == QT_F16 || T == QT_BF16) return load_raw_f16<NT>(W, row, sb, g);
@@ -366,6 +404,7 @@ DEVI typename RawOf<T>::type load_raw(const WDesc& W, int row, int sb, int g) {
 template <int T>
 DEVI void prep_sc(const typename RawOf<T>::type& r, int g, typename ScOf<T>::type& s) {
   if constexpr (T == QT_Q4_K || T == QT_Q5_K) prep_kquant(r.hdr, s);
+  else if constexpr (T == QT_Q51) prep_q51(r, s);
   else if constexpr (T == QT_Q6_K) prep_q6k(r, g, s);
   else if constexpr (T == QT_Q8_0) prep_q8(r, s);
 }
@@ -373,6 +412,7 @@ template <int T>
 DEVI f16x8 frag_t(const typename RawOf<T>::type& r, const typename ScOf<T>::type& s, int t) {
   if constexpr (T == QT_Q4_K) return frag_q4k(r, s, t);
   else if constexpr (T == QT_Q5_K) return frag_q5k(r, s, t);
+  else if constexpr (T == QT_Q51) return frag_q51(r, s, t);
   else if constexpr (T == QT_Q6_K) return frag_q6k(r, s, t);
   else if constexpr (T == QT_Q8_0) return frag_q8(r, s, t);
   else if constexpr (T == QT_F16) return frag_f16(r, t);

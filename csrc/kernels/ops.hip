@@ -570,6 +570,7 @@ int nls_dequant(const void* w, int type, int rows, int K, void* out, long ldo, v
     case QT_Q5_K: hipLaunchKernelGGL(dequant_kernel<QT_Q5_K>, grid, dim3(256), 0, st, W, o, ldo); break;
     case QT_Q6_K: hipLaunchKernelGGL(dequant_kernel<QT_Q6_K>, grid, dim3(256), 0, st, W, o, ldo); break;
     case QT_Q8_0: hipLaunchKernelGGL(dequant_kernel<QT_Q8_0>, grid, dim3(256), 0, st, W, o, ldo); break;
+    case QT_Q51: hipLaunchKernelGGL(dequant_kernel<QT_Q51>, grid, dim3(256), 0, st, W, o, ldo); break;
     case QT_F16: hipLaunchKernelGGL(dequant_kernel<QT_F16>, grid, dim3(256), 0, st, W, o, ldo); break;
     case QT_BF16: hipLaunchKernelGGL(dequant_kernel<QT_BF16>, grid, dim3(256), 0, st, W, o, ldo); break;
     case QT_F32: hipLaunchKernelGGL(dequant_kernel<QT_F32>, grid, dim3(256), 0, st, W, o, ldo); break;

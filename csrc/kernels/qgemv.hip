@@ -134,17 +134,19 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     cols += segs[i].rows;
   }
   sl.nseg = nseg;
-  // pick the smallest kernel type-set that covers every segment (Q6_K is in sets 0 and 1)
-  bool has[3] = {false, false, false}, bad = false;
+  // pick the kernel type-set that covers every segment (Q6_K is in sets 0, 1 and 3; Q8_0 in 1 and 3)
+  bool q4k = false, q5k = false, q8 = false, q51 = false, flt = false, bad = false;
   for (int i = 0; i < nseg; ++i) {
     const int t = segs[i].type;
-    if (t == QT_Q4_K) has[0] = true;
-    else if (t == QT_Q5_K || t == QT_Q8_0) has[1] = true;
-    else if (t == QT_F16 || t == QT_BF16 || t == QT_F32) has[2] = true;
+    if (t == QT_Q4_K) q4k = true;
+    else if (t == QT_Q5_K) q5k = true;
+    else if (t == QT_Q8_0) q8 = true;
+    else if (t == QT_Q51) q51 = true;
+    else if (t == QT_F16 || t == QT_BF16 || t == QT_F32) flt = true;
     else if (t != QT_Q6_K) bad = true;
   }
-  if (bad || (has[0] + has[1] + has[2]) > 1) return -1;
-  const int kset = has[2] ? 2 : (has[1] ? 1 : 0);
+  if (bad || (flt && (q4k || q5k || q8 || q51)) || (q4k && (q5k || q8 || q51)) || (q51 && q5k)) return -1;
+  const int kset = flt ? 2 : (q51 ? 3 : (q4k ? 0 : ((q5k || q8) ? 1 : 0)));
   GemvArgs a{};
   a.x = (const act_t*)x;
   a.ldx = ldx;
@@ -187,8 +189,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   const int mt = M > 64 ? 8 : (M + 15) / 16;
   const int nmb = M > 64 ? (M + 127) / 128 : 1;
   hipStream_t st = (hipStream_t)stream;
-  auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : launch_k2);
-  if (mode >= 2 && mode <= 3 && kset == 2) return -1;   // tiled float weights: path B only
+  auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : (kset == 2 ? launch_k2 : launch_k3));
+  if (mode >= 2 && mode <= 3 && kset >= 2) return -1;   // tiled float / Q51 weights: paths A and B only
   if (mode == 3)
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type == QT_Q8_0) return -1;   // raw Q8_0 tiles do not fit the DMA LDS budget

@@ -477,6 +477,13 @@ __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArg
       case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, a, lds); break;
       default: break;
     }
+  } else if constexpr (KSET == 3) {
+    switch (S.type) {
+      case QT_Q51: gemv_tile<QT_Q51, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_Q6_K: gemv_tile<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      case QT_Q8_0: gemv_tile<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, a, lds); break;
+      default: break;
+    }
   } else {
     switch (S.type) {
       case QT_F16: gemv_tile<QT_F16, WAVES, RT, MT, XL>(S, row0, a, lds); break;
@@ -872,6 +879,13 @@ __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs 
       case QT_Q8_0: mm_tile_na<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
       default: break;
     }
+  } else if constexpr (KSET == 3) {
+    switch (S.type) {
+      case QT_Q51: mm_tile_na<QT_Q51, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_Q6_K: mm_tile_na<QT_Q6_K, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      case QT_Q8_0: mm_tile_na<QT_Q8_0, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
+      default: break;
+    }
   } else {
     switch (S.type) {
       case QT_F16: mm_tile<QT_F16, WAVES, RT, MT, XL>(S, row0, kslice, ks, a, ws, xlds, xm, ym); break;
@@ -1023,5 +1037,6 @@ int launch_kset(int mode, int waves, int rt, int mt, const SegList& sl, int tile
 int launch_k0(int, int, int, int, const SegList&, int, int, float*, const GemvArgs&, hipStream_t, int);
 int launch_k1(int, int, int, int, const SegList&, int, int, float*, const GemvArgs&, hipStream_t, int);
 int launch_k2(int, int, int, int, const SegList&, int, int, float*, const GemvArgs&, hipStream_t, int);
+int launch_k3(int, int, int, int, const SegList&, int, int, float*, const GemvArgs&, hipStream_t, int);
 
 }  // namespace nls_gemv

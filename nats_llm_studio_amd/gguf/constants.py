@@ -53,7 +53,13 @@ GGML_BLOCK = {
     GGMLType.F32: (1, 4),
     GGMLType.F16: (1, 2),
     GGMLType.BF16: (1, 2),
+    GGMLType.Q4_0: (32, 18),
+    GGMLType.Q4_1: (32, 20),
+    GGMLType.Q5_0: (32, 22),
+    GGMLType.Q5_1: (32, 24),
     GGMLType.Q8_0: (32, 34),
+    GGMLType.Q2_K: (256, 84),
+    GGMLType.Q3_K: (256, 110),
     GGMLType.Q4_K: (256, 144),
     GGMLType.Q5_K: (256, 176),
     GGMLType.Q6_K: (256, 210),
@@ -63,7 +69,15 @@ GGML_BLOCK = {
 FILE_TYPE_NAMES = {
     0: "F32",
     1: "F16",
+    2: "Q4_0",
+    3: "Q4_1",
     7: "Q8_0",
+    8: "Q5_0",
+    9: "Q5_1",
+    10: "Q2_K",
+    11: "Q3_K_S",
+    12: "Q3_K_M",
+    13: "Q3_K_L",
     15: "Q4_K_M",
     14: "Q4_K_S",
     17: "Q5_K_M",

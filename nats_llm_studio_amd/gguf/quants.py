@@ -8,6 +8,18 @@ Block layouts follow ggml's on-disk contract (QK_K = 256):
 * Q4_K  {f16 d; f16 dmin; u8 scales[12]; u8 qs[128]}        144 B / 256
 * Q5_K  {f16 d; f16 dmin; u8 scales[12]; u8 qh[32]; u8 qs[128]} 176 B / 256
 * Q6_K  {u8 ql[128]; u8 qh[64]; i8 scales[16]; f16 d}       210 B / 256
+* Q4_0  {f16 d; u8 qs[16]}                      18 B / 32: x = d*(q - 8)
+* Q4_1  {f16 d; f16 m; u8 qs[16]}               20 B / 32: x = d*q + m
+* Q5_0  {f16 d; u8 qh[4]; u8 qs[16]}            22 B / 32: x = d*(q - 16)
+* Q5_1  {f16 d; f16 m; u8 qh[4]; u8 qs[16]}     24 B / 32: x = d*q + m
+  (32-blocks: element j < 16 is the low nibble of qs[j], j >= 16 the high nibble of qs[j-16];
+  the 5th bit of element j is bit j of the little-endian u32 qh)
+* Q2_K  {u8 scales[16]; u8 qs[64]; f16 d; f16 dmin}          84 B / 256: 16 sub-blocks of 16,
+  x = d*(sc & 15)*q - dmin*(sc >> 4), q 2-bit
+* Q3_K  {u8 hmask[32]; u8 qs[64]; u8 scales[12]; f16 d}      110 B / 256: 16 sub-blocks of 16,
+  x = d*(sc - 32)*(q - 4), q = 2 low bits from qs + 4 * hmask bit, sc 6-bit
+  (For both K types, value v of the 128-half n, shift group j, half u, lane l -- v = 128n + 32j + 16u + l
+  -- takes bits 2j.. of qs[32n + 16u + l] and, for Q3_K, hmask bit (4n + j) of byte 16u + l.)
 
 The quantisers are simple min/max fits (not llama.cpp's iterative search);
 only the *decode* side has to be bit-exact with ggml, because that is what a
@@ -120,6 +132,99 @@ def dequant_q6_k(raw: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
+def _q_32(qs: np.ndarray) -> np.ndarray:
+    """32-block nibbles: uint8[nb, 16] -> 4-bit values uint8[nb, 32] (j < 16 low nibbles, j >= 16 high)."""
+    return np.concatenate([qs & 0xF, qs >> 4], axis=1)
+
+
+def _qh_32(qh: np.ndarray) -> np.ndarray:
+    """uint8[nb, 4] little-endian bit field -> uint8[nb, 32] (bit j of element j)."""
+    bits = qh.astype(np.uint32)
+    w = bits[:, 0] | (bits[:, 1] << 8) | (bits[:, 2] << 16) | (bits[:, 3] << 24)
+    return ((w[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).astype(np.uint8)
+
+
+def unpack_q5_1_family(raw: np.ndarray, ggml_type: int):
+    """Q4_0 / Q4_1 / Q5_0 / Q5_1 blocks -> (d f32[nb], m f32[nb], q uint8[nb, 32]) with x = d*q + m EXACTLY
+    (m = -8d / -16d for the symmetric types: a power-of-two multiple of an f16, exact in f16 too)."""
+    t = GGMLType(ggml_type)
+    nbytes = GGML_BLOCK[t][1]
+    b = np.ascontiguousarray(raw).view(np.uint8).reshape(-1, nbytes)
+    d = _f16(b[:, 0:2])
+    if t == GGMLType.Q4_0:
+        return d, -8.0 * d, _q_32(b[:, 2:18])
+    if t == GGMLType.Q4_1:
+        return d, _f16(b[:, 2:4]), _q_32(b[:, 4:20])
+    if t == GGMLType.Q5_0:
+        return d, -16.0 * d, _q_32(b[:, 6:22]) | (_qh_32(b[:, 2:6]) << 4)
+    if t == GGMLType.Q5_1:
+        return d, _f16(b[:, 2:4]), _q_32(b[:, 8:24]) | (_qh_32(b[:, 4:8]) << 4)
+    raise ValueError(t.name)
+
+
+def _k_lowbit_index():
+    """For the 2-bit K layouts: value v -> (qs byte, shift); v = 128n + 32j + 16u + l."""
+    v = np.arange(256)
+    n, j, u, l = v // 128, (v // 32) % 4, (v // 16) % 2, v % 16
+    return 32 * n + 16 * u + l, 2 * j, 4 * n + j, 16 * u + l
+
+
+_KIDX = _k_lowbit_index()
+
+
+def unpack_q2_k(raw: np.ndarray):
+    """-> (a f32[nb, 16], c f32[nb, 16], q uint8[nb, 256]): x = a[v // 16] * q[v] + c[v // 16]."""
+    b = np.ascontiguousarray(raw).view(np.uint8).reshape(-1, 84)
+    sc = b[:, 0:16]
+    qs = b[:, 16:80]
+    d = _f16(b[:, 80:82])
+    dmin = _f16(b[:, 82:84])
+    byte, shift, _, _ = _KIDX
+    q = (qs[:, byte] >> shift[None, :]) & 3
+    return d[:, None] * (sc & 0xF).astype(np.float32), -dmin[:, None] * (sc >> 4).astype(np.float32), q
+
+
+def _unpack_q3_scales(sc12: np.ndarray) -> np.ndarray:
+    """ggml Q3_K 6-bit scales (kmask1/kmask2 shuffle): uint8[nb, 12] -> int[nb, 16] in [0, 63]."""
+    a = sc12.astype(np.uint32)
+    aux = [a[:, 4 * i] | (a[:, 4 * i + 1] << 8) | (a[:, 4 * i + 2] << 16) | (a[:, 4 * i + 3] << 24) for i in range(3)]
+    k1, k2 = 0x03030303, 0x0F0F0F0F
+    tmp = aux[2]
+    w = [(aux[0] & k2) | (((tmp >> 0) & k1) << 4), (aux[1] & k2) | (((tmp >> 2) & k1) << 4),
+         ((aux[0] >> 4) & k2) | (((tmp >> 4) & k1) << 4), ((aux[1] >> 4) & k2) | (((tmp >> 6) & k1) << 4)]
+    out = np.empty((sc12.shape[0], 16), np.int32)
+    for i in range(4):
+        for k in range(4):
+            out[:, 4 * i + k] = (w[i] >> (8 * k)) & 0xFF
+    return out
+
+
+def _pack_q3_scales(s: np.ndarray) -> np.ndarray:
+    """Inverse of _unpack_q3_scales: int[nb, 16] in [0, 63] -> uint8[nb, 12]."""
+    s = s.astype(np.uint32)
+    out = np.zeros((s.shape[0], 12), np.uint8)
+    for i in range(16):
+        lo, hi = s[:, i] & 0xF, s[:, i] >> 4
+        if i < 8:
+            out[:, i] |= lo.astype(np.uint8)
+        else:
+            out[:, i - 8] |= (lo << 4).astype(np.uint8)
+        out[:, 8 + (i % 4)] |= (hi << (2 * (i // 4))).astype(np.uint8)
+    return out
+
+
+def unpack_q3_k(raw: np.ndarray):
+    """-> (d f32[nb], s int[nb, 16] (signed, sc - 32), q3 uint8[nb, 256] in [0, 7]): x = d*s*(q3 - 4)."""
+    b = np.ascontiguousarray(raw).view(np.uint8).reshape(-1, 110)
+    hm = b[:, 0:32]
+    qs = b[:, 32:96]
+    s = _unpack_q3_scales(b[:, 96:108]) - 32
+    d = _f16(b[:, 108:110])
+    byte, shift, hbit, hbyte = _KIDX
+    q = ((qs[:, byte] >> shift[None, :]) & 3) | (((hm[:, hbyte] >> hbit[None, :]) & 1) << 2)
+    return d, s, q.astype(np.uint8)
+
+
 def dequantize(raw: np.ndarray, ggml_type: int, shape) -> np.ndarray:
     """Dequantise raw tensor bytes to float32 with numpy shape `shape` (row-major, innermost last)."""
     t = GGMLType(ggml_type)
@@ -138,6 +243,15 @@ def dequantize(raw: np.ndarray, ggml_type: int, shape) -> np.ndarray:
         out = dequant_q5_k(raw)
     elif t == GGMLType.Q6_K:
         out = dequant_q6_k(raw)
+    elif t in (GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1):
+        d, m, q = unpack_q5_1_family(raw, t)
+        out = (d[:, None] * q.astype(np.float32) + m[:, None]).reshape(-1)
+    elif t == GGMLType.Q2_K:
+        a, c, q = unpack_q2_k(raw)
+        out = (np.repeat(a, 16, axis=1) * q.astype(np.float32) + np.repeat(c, 16, axis=1)).reshape(-1)
+    elif t == GGMLType.Q3_K:
+        d, sc, q = unpack_q3_k(raw)
+        out = (d[:, None] * np.repeat(sc.astype(np.float32), 16, axis=1) * (q.astype(np.float32) - 4)).reshape(-1)
     else:
         raise NotImplementedError(f"dequantize: {t.name}")
     return out.reshape(shape)
@@ -237,6 +351,92 @@ def quant_q6_k(x: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
+def _pack_32(q: np.ndarray) -> np.ndarray:
+    """4-bit values uint8[nb, 32] -> 32-block nibbles uint8[nb, 16]."""
+    return ((q[:, :16] & 0xF) | ((q[:, 16:] & 0xF) << 4)).astype(np.uint8)
+
+
+def _pack_qh_32(q: np.ndarray) -> np.ndarray:
+    w = (((q.astype(np.uint32) >> 4) & 1) << np.arange(32, dtype=np.uint32)[None, :]).sum(axis=1).astype(np.uint32)
+    return w.view(np.uint8).reshape(-1, 4)
+
+
+def quant_q5_1_family(x: np.ndarray, ggml_type: int) -> np.ndarray:
+    """Q4_0 / Q4_1 / Q5_0 / Q5_1 by per-block min/max (symmetric types: amax)."""
+    t = GGMLType(ggml_type)
+    x = x.reshape(-1, 32).astype(np.float32)
+    nb = x.shape[0]
+    bits = 5 if t in (GGMLType.Q5_0, GGMLType.Q5_1) else 4
+    qmax = (1 << bits) - 1
+    if t in (GGMLType.Q4_0, GGMLType.Q5_0):
+        half = 1 << (bits - 1)
+        amax_i = np.abs(x).argmax(axis=1)
+        mx = x[np.arange(nb), amax_i]
+        d = (mx / -half).astype(np.float16).astype(np.float32)
+        inv = np.where(d != 0, 1.0 / np.where(d != 0, d, 1), 0)
+        q = np.clip(np.rint(x * inv[:, None]) + half, 0, qmax).astype(np.uint8)
+        m = None
+    else:
+        mn, mxv = x.min(axis=1), x.max(axis=1)
+        d = ((mxv - mn) / qmax).astype(np.float16).astype(np.float32)
+        m = mn.astype(np.float16).astype(np.float32)
+        inv = np.where(d > 0, 1.0 / np.where(d > 0, d, 1), 0)
+        q = np.clip(np.rint((x - m[:, None]) * inv[:, None]), 0, qmax).astype(np.uint8)
+    out = [_to_f16_bytes(d)]
+    if m is not None:
+        out.append(_to_f16_bytes(m))
+    if bits == 5:
+        out.append(_pack_qh_32(q))
+    out.append(_pack_32(q))
+    return np.concatenate(out, axis=1).reshape(-1)
+
+
+def quant_q2_k(x: np.ndarray) -> np.ndarray:
+    x = x.reshape(-1, 16, 16).astype(np.float32)
+    nb = x.shape[0]
+    mn = np.minimum(x.min(axis=2), 0.0)
+    scale = (x.max(axis=2) - mn) / 3.0
+    d = (scale.max(axis=1) / 15.0).astype(np.float16).astype(np.float32)
+    dmin = ((-mn).max(axis=1) / 15.0).astype(np.float16).astype(np.float32)
+    sc = np.clip(np.rint(scale / np.where(d > 0, d, 1)[:, None]), 0, 15).astype(np.uint8)
+    m = np.clip(np.rint(-mn / np.where(dmin > 0, dmin, 1)[:, None]), 0, 15).astype(np.uint8)
+    a = d[:, None] * sc
+    q = np.clip(np.rint((x + (dmin[:, None] * m)[:, :, None]) / np.where(a > 0, a, 1)[:, :, None]), 0, 3)
+    q = q.reshape(nb, 256).astype(np.uint8)
+    byte, shift, _, _ = _KIDX
+    qs = np.zeros((nb, 64), np.uint8)
+    for v in range(256):
+        qs[:, byte[v]] |= (q[:, v] << shift[v]).astype(np.uint8)
+    out = np.empty((nb, 84), np.uint8)
+    out[:, 0:16] = sc | (m << 4)
+    out[:, 16:80] = qs
+    out[:, 80:82] = _to_f16_bytes(d)
+    out[:, 82:84] = _to_f16_bytes(dmin)
+    return out.reshape(-1)
+
+
+def quant_q3_k(x: np.ndarray) -> np.ndarray:
+    x = x.reshape(-1, 16, 16).astype(np.float32)
+    nb = x.shape[0]
+    scale = np.abs(x).max(axis=2) / 4.0
+    d = (scale.max(axis=1) / 31.0).astype(np.float16).astype(np.float32)
+    s = np.clip(np.rint(scale / np.where(d > 0, d, 1)[:, None]), -32, 31).astype(np.int32)
+    a = d[:, None] * s
+    q = np.clip(np.rint(x / np.where(a != 0, a, 1)[:, :, None]) + 4, 0, 7).astype(np.uint8).reshape(nb, 256)
+    byte, shift, hbit, hbyte = _KIDX
+    qs = np.zeros((nb, 64), np.uint8)
+    hm = np.zeros((nb, 32), np.uint8)
+    for v in range(256):
+        qs[:, byte[v]] |= ((q[:, v] & 3) << shift[v]).astype(np.uint8)
+        hm[:, hbyte[v]] |= (((q[:, v] >> 2) & 1) << hbit[v]).astype(np.uint8)
+    out = np.empty((nb, 110), np.uint8)
+    out[:, 0:32] = hm
+    out[:, 32:96] = qs
+    out[:, 96:108] = _pack_q3_scales(s + 32)
+    out[:, 108:110] = _to_f16_bytes(d)
+    return out.reshape(-1)
+
+
 def quantize(x: np.ndarray, ggml_type: int) -> np.ndarray:
     """float array -> raw uint8 bytes in the given ggml type (row-major)."""
     t = GGMLType(ggml_type)
@@ -257,6 +457,12 @@ def quantize(x: np.ndarray, ggml_type: int) -> np.ndarray:
         return quant_q5_k(x)
     if t == GGMLType.Q6_K:
         return quant_q6_k(x)
+    if t in (GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1):
+        return quant_q5_1_family(x, t)
+    if t == GGMLType.Q2_K:
+        return quant_q2_k(x)
+    if t == GGMLType.Q3_K:
+        return quant_q3_k(x)
     raise NotImplementedError(f"quantize: {t.name}")
 
 
@@ -299,6 +505,31 @@ def random_blocks(ggml_type: int, n_elements: int, std: float, rng: np.random.Ge
         d = np.full(nb, std / (32.0 * q_std), np.float32)
         raw[:, 192:208] = sc.view(np.uint8)
         raw[:, 208:210] = _to_f16_bytes(d)
+        return raw.reshape(-1)
+    if t in (GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1):
+        qmax = 31 if t in (GGMLType.Q5_0, GGMLType.Q5_1) else 15
+        q_std = np.sqrt((qmax + 1) ** 2 - 1) / np.sqrt(12.0)
+        d = np.full(nb, std / q_std, np.float32) * rng.uniform(0.8, 1.2, nb).astype(np.float32)
+        raw[:, 0:2] = _to_f16_bytes(d)
+        if t in (GGMLType.Q4_1, GGMLType.Q5_1):      # zero-mean: m = -d * qmax / 2
+            raw[:, 2:4] = _to_f16_bytes(-d * qmax / 2.0)
+        return raw.reshape(-1)
+    if t == GGMLType.Q2_K:
+        sc = rng.integers(6, 12, size=(nb, 16)).astype(np.uint8)
+        q_std = np.sqrt(4 ** 2 - 1) / np.sqrt(12.0)
+        d = np.full(nb, std / (9.0 * q_std), np.float32)
+        dmin = d * 1.5 * 9.0 / 8.0
+        m = np.clip(np.rint(d[:, None] * sc * 1.5 / dmin[:, None]), 0, 15).astype(np.uint8)
+        raw[:, 0:16] = sc | (m << 4)
+        raw[:, 80:82] = _to_f16_bytes(d)
+        raw[:, 82:84] = _to_f16_bytes(dmin)
+        return raw.reshape(-1)
+    if t == GGMLType.Q3_K:
+        s = rng.integers(40, 56, size=(nb, 16))                  # sc - 32 in [8, 24)
+        q_std = np.sqrt(8 ** 2 - 1) / np.sqrt(12.0)
+        d = np.full(nb, std / (16.0 * q_std), np.float32)
+        raw[:, 96:108] = _pack_q3_scales(s)
+        raw[:, 108:110] = _to_f16_bytes(d)
         return raw.reshape(-1)
     raise NotImplementedError(f"random_blocks: {t.name}")
 

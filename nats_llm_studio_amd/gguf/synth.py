@@ -82,6 +82,13 @@ QUANT_MIX = {
     "Q5_K_M": (GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q6_K, GGMLType.Q5_K),
     "Q6_K": (GGMLType.Q6_K, GGMLType.Q6_K, GGMLType.Q6_K, GGMLType.Q6_K),
     "Q8_0": (GGMLType.Q8_0, GGMLType.Q8_0, GGMLType.Q8_0, GGMLType.Q8_0),
+    # the legacy 32-block types and the low-bit K mixes (llama.cpp keeps output.weight at Q6_K)
+    "Q4_0": (GGMLType.Q4_0, GGMLType.Q4_0, GGMLType.Q6_K, GGMLType.Q4_0),
+    "Q4_1": (GGMLType.Q4_1, GGMLType.Q4_1, GGMLType.Q6_K, GGMLType.Q4_1),
+    "Q5_0": (GGMLType.Q5_0, GGMLType.Q5_0, GGMLType.Q6_K, GGMLType.Q5_0),
+    "Q5_1": (GGMLType.Q5_1, GGMLType.Q5_1, GGMLType.Q6_K, GGMLType.Q5_1),
+    "Q3_K_M": (GGMLType.Q3_K, GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q3_K),
+    "Q2_K": (GGMLType.Q2_K, GGMLType.Q3_K, GGMLType.Q6_K, GGMLType.Q2_K),
     "F16": (GGMLType.F16, GGMLType.F16, GGMLType.F16, GGMLType.F16),
     "F32": (GGMLType.F32, GGMLType.F32, GGMLType.F32, GGMLType.F32),
 }

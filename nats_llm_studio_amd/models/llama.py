@@ -230,6 +230,8 @@ class LlamaModel:
             wq = self._matrix(p + "attn_q.weight", (r * Hq * D, (r + 1) * Hq * D))
             wk = self._matrix(p + "attn_k.weight", (r * Hkv * D, (r + 1) * Hkv * D))
             wv = self._matrix(p + "attn_v.weight", (r * Hkv * D, (r + 1) * Hkv * D))
+            if ops.kernel_set([wq.type, wk.type, wv.type]) is None:   # e.g. Q2_K (-> F16) with a Q3_K V
+                wq, wk, wv = wq.to_f16(), wk.to_f16(), wv.to_f16()
             qkv = [Seg(wq, 0), Seg(wk, Hq * D), Seg(wv, (Hq + Hkv) * D)]
             wo = self._matrix(p + "attn_output.weight", None, (r * Hq * D, (r + 1) * Hq * D))
             lw = LayerWeights(self._vec(p + "attn_norm.weight"), self._vec(p + "ffn_norm.weight"), qkv, wo)

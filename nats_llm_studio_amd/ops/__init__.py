@@ -18,6 +18,7 @@ import torch
 from ..gguf.constants import GGMLType, GGML_BLOCK
 from ..gguf.quants import dequantize
 from . import _lib
+from . import transcode
 
 EPI = {"f32": 0, "act": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5, "rope": 6}
 import os as _os
@@ -125,10 +126,13 @@ def row_bytes(ggml_type: int, K: int) -> int:
 class QWeight:
     """A [rows, K] weight matrix resident on `device` in its quantised form.
 
-    layout="tiled" (GEMV/GEMM operands) or "rows" (embedding tables, row gathers)."""
+    layout="tiled" (GEMV/GEMM operands) or "rows" (embedding tables, row gathers). `gtype` is the GGUF
+    block type of the file; `type` the format the kernels execute (the same, except for the formats
+    ops/transcode.py re-encodes at load: Q4_0/Q4_1/Q5_0/Q5_1 -> Q51, Q3_K -> Q6_K, Q2_K -> F16)."""
 
     def __init__(self, raw: np.ndarray, ggml_type: int, rows: int, K: int, device, name: str = "",
                  layout: str = "tiled"):
+        self.gtype = int(ggml_type)
         self.type = int(ggml_type)
         self.rows = int(rows)
         self.K = int(K)
@@ -139,7 +143,18 @@ class QWeight:
             raise ValueError(f"{name}: K={K} is not a multiple of 256")
         with warnings.catch_warnings():     # read-only mmap views: copied below
             warnings.simplefilter("ignore", UserWarning)
-            if layout == "rows":
+            if GGMLType(ggml_type) in transcode.TRANSCODED:
+                t = torch.from_numpy(np.ascontiguousarray(np.asarray(raw).view(np.uint8).reshape(-1)))
+                t = t.to(self.device) if self.device.type != "cpu" else t
+                t, self.type = transcode.device_form(t, ggml_type, rows, K, layout)
+                if layout == "rows":
+                    t = torch.from_numpy(np.ascontiguousarray(to_device_layout(t.cpu().numpy(), self.type, rows, K)))
+                    self.data = t.to(self.device) if self.device.type != "cpu" else t.clone()
+                elif self.type == transcode.QT_Q51:
+                    self.data = t
+                else:
+                    self.data = tile_layout(t, self.type, rows, K)
+            elif layout == "rows":
                 t = torch.from_numpy(np.ascontiguousarray(to_device_layout(raw, ggml_type, rows, K)))
                 self.data = t.to(self.device) if self.device.type != "cpu" else t.clone()
             else:
@@ -149,6 +164,19 @@ class QWeight:
         self._raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1) if self.device.type == "cpu" else None
         self._dense = None
         self.d16: Optional[torch.Tensor] = None    # row-major f16 copy for the large-M GEMM (mode 4)
+
+    def to_f16(self) -> "QWeight":
+        """This matrix re-encoded as tiled F16 (its dequantised values): for a fused launch whose segments
+        would otherwise need two kernel type-sets (e.g. a Q2_K model's Q|K|V with a Q3_K V)."""
+        if self.device.type == "cpu" or self.type == int(GGMLType.F16):
+            return self
+        w = QWeight.__new__(QWeight)
+        w.__dict__.update(self.__dict__)
+        w.type = int(GGMLType.F16)
+        w.data = tile_layout(self.dense(torch.float16).contiguous().view(torch.uint8).reshape(-1), GGMLType.F16,
+                             self.rows, self.K)
+        w.d16 = None
+        return w
 
     def expand_dense(self) -> int:
         """Keep a dequantised row-major f16 copy next to the quantised tiles (GPU; idempotent).
@@ -171,12 +199,25 @@ class QWeight:
         """Dequantised [rows, K] (CPU: numpy ggml codec; GPU: HIP dequant kernel, f16)."""
         if self.device.type == "cpu":
             if self._dense is None:
-                self._dense = torch.from_numpy(dequantize(self._raw, self.type, (self.rows, self.K)).copy())
+                self._dense = torch.from_numpy(dequantize(self._raw, self.gtype, (self.rows, self.K)).copy())
             return self._dense.to(dtype)
         out = torch.empty(self.rows, self.K, dtype=ACT_DTYPE, device=self.device)
         _lib.check(_lib.lib().nls_dequant(self.data.data_ptr(), self.type, self.rows, self.K, out.data_ptr(),
                                           self.K, _stream_ptr(out)), "nls_dequant")
         return out.to(dtype)
+
+
+def kernel_set(types) -> Optional[int]:
+    """The HIP kernel type-set that runs one launch over segments of these device types, None if no single
+    set covers them (csrc/kernels/qgemv.hip: Q6_K joins any quantised set, Q8_0 sets 1 and 3)."""
+    ts = set(int(t) for t in types)
+    flt = ts & {0, 1, 30}
+    q4k, q5k, q8, q51 = 12 in ts, 13 in ts, 8 in ts, transcode.QT_Q51 in ts
+    if ts - {0, 1, 30, 8, 12, 13, 14, transcode.QT_Q51}:
+        return None
+    if (flt and ts - flt) or (q4k and (q5k or q8 or q51)) or (q51 and q5k):
+        return None
+    return 2 if flt else (3 if q51 else (0 if q4k else (1 if (q5k or q8) else 0)))
 
 
 def interleave_gate_up(gate_raw: np.ndarray, up_raw: np.ndarray, ggml_type: int, rows: int, K: int,

@@ -26,6 +26,22 @@ def tiny_models(tmp_path_factory):
     return out
 
 
+NEW_FTYPES = ("Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q3_K_M", "Q2_K")
+
+
+@pytest.fixture(scope="session")
+def tiny_ftypes(tmp_path_factory):
+    """tiny-llama written in every GGUF mix that is re-encoded at load (ops/transcode.py)."""
+    from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
+    d = tmp_path_factory.mktemp("ftypes")
+    out = {}
+    for ft in NEW_FTYPES:
+        p = str(d / f"tiny-llama-{ft}.gguf")
+        write_synthetic_gguf(p, "tiny-llama", ft, seed=0)
+        out[ft] = p
+    return out
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

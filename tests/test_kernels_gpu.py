@@ -12,7 +12,10 @@ from nats_llm_studio_amd.gguf.constants import GGMLType
 
 pytestmark = pytest.mark.gpu
 
-TYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16, GGMLType.BF16, GGMLType.F32]
+TYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16, GGMLType.BF16, GGMLType.F32,
+         # re-encoded at load (ops/transcode.py): Q51 device blocks, Q3_K -> Q6_K, Q2_K -> F16
+         GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1, GGMLType.Q3_K, GGMLType.Q2_K]
+NEW_TYPES = [GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1, GGMLType.Q3_K, GGMLType.Q2_K]
 
 
 def _qw(rows, K, t, dev, seed=0):
@@ -60,6 +63,44 @@ def test_dequant_kernel_exact(gpu):
         w, Wd = _qw(48, 512, t, gpu, seed=3)
         d = w.dense().float().cpu()
         torch.testing.assert_close(d, Wd, rtol=2e-3, atol=2e-3 * Wd.abs().max().item())
+
+
+@pytest.mark.parametrize("t", NEW_TYPES)
+@pytest.mark.parametrize("M", [65, 300])
+def test_new_types_large_m_and_dense(gpu, t, M):
+    """The load-time re-encoded formats at prefill sizes: path-B GEMM (mode 1, split-K), and the dense
+    f16 copy (the dequant kernel of the device format) through mode 8 -- vs the fp32 product of the
+    numpy ggml decode of the ORIGINAL bytes."""
+    rows, K = 200, 1024
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    ref = x[:M].float().cpu() @ Wd.t()
+    y = torch.zeros(x.shape[0], rows, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=1, waves=8, rt=1, ks=2)
+    _close(y[:M], ref)
+    y.zero_()
+    ops.qgemv([ops.Seg(w)], x, y, M)                      # automatic launch config
+    _close(y[:M], ref)
+    w.expand_dense()
+    y.zero_()
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=8, waves=8, rt=8, ks=1)
+    _close(y[:M], ref)
+
+
+def test_q51_mixed_with_q6k_q8_segments(gpu):
+    """A Q4_0 model's fused launch: Q51 (re-encoded Q4_0 / Q5_1) segments next to Q6_K and Q8_0 ones in
+    ONE launch (kernel type-set 3)."""
+    K = 512
+    a, Ad = _qw(64, K, GGMLType.Q4_0, gpu, 1)
+    b, Bd = _qw(48, K, GGMLType.Q6_K, gpu, 2)
+    c, Cd = _qw(32, K, GGMLType.Q5_1, gpu, 3)
+    d, Dd = _qw(16, K, GGMLType.Q8_0, gpu, 4)
+    assert ops.kernel_set([a.type, b.type, c.type, d.type]) == 3
+    for M in (3, 40):
+        x = _x(M, K, gpu)
+        y = torch.zeros(64, 160, device=gpu)
+        ops.qgemv([ops.Seg(a, 0), ops.Seg(b, 64), ops.Seg(c, 112), ops.Seg(d, 144)], x, y, M)
+        _close(y[:M], x[:M].float().cpu() @ torch.cat([Ad, Bd, Cd, Dd]).t())
 
 
 @pytest.mark.parametrize("cfg", CFGS)

@@ -30,6 +30,32 @@ def test_cpu_prefill_matches_reference(tiny_models, name):
     assert err < 0.02 * rl.abs().max().item(), err
 
 
+@pytest.mark.parametrize("ft", ["Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q3_K_M", "Q2_K"])
+def test_cpu_prefill_new_quant_mixes(tiny_ftypes, ft):
+    """GGUF mixes of the legacy 32-block types and the low-bit K types load (the weights re-encoded for
+    the device, ops/transcode.py; the CPU path decodes the original bytes) and match the oracle; the
+    registry-facing file_type round-trips."""
+    from nats_llm_studio_amd.gguf.constants import FILE_TYPE_NAMES
+    r = GGUFReader(tiny_ftypes[ft])
+    assert FILE_TYPE_NAMES[int(r.metadata["general.file_type"])] == ft
+    m = LlamaModel(r, "cpu")
+    ref = ReferenceModel(r)
+    S = 20
+    ids = list(np.random.default_rng(1).integers(0, 900, S))
+    b = m.step_buffers(64, 4, 8)
+    kc, vc = m.kv_cache(8, 16)
+    b.ids[:S] = torch.tensor(ids, dtype=torch.int32)
+    b.pos[:S] = torch.arange(S)
+    b.slot[:S] = torch.arange(S)
+    b.tok_seq[:S] = 0
+    b.ctx_len[:S] = torch.arange(S) + 1
+    b.block_tables[0] = torch.arange(8)
+    m.forward(b, kc, vc, S, 16)
+    rl = ref.logits(ids)
+    err = (b.logits[:S] - rl).abs().max().item()
+    assert err < 0.02 * rl.abs().max().item(), err
+
+
 def test_rope_freqs_change_the_rotation(tiny_models):
     """The Llama-3.1 factors are applied (a model that ignored them would differ from the oracle)."""
     from nats_llm_studio_amd import ops

@@ -35,6 +35,38 @@ def test_prefill_logits_match_reference(gpu, tiny_models, name):
     assert agree > 0.9
 
 
+@pytest.mark.parametrize("ft", ["Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q3_K_M", "Q2_K"])
+def test_new_quant_mixes_match_reference(gpu, tiny_ftypes, ft):
+    """Whole models in the re-encoded mixes on the GPU kernels: prefill logits vs the fp32 oracle of the
+    original GGUF bytes, then hipGraph decode == eager decode."""
+    r = GGUFReader(tiny_ftypes[ft])
+    m = LlamaModel(r, gpu)
+    ref = ReferenceModel(r)
+    S = 40
+    ids = list(np.random.default_rng(0).integers(0, 900, S))
+    b = m.step_buffers(64, 4, 8)
+    kc, vc = m.kv_cache(8, 16)
+    b.ids[:S] = torch.tensor(ids, dtype=torch.int32)
+    b.pos[:S] = torch.arange(S)
+    b.slot[:S] = torch.arange(S)
+    b.tok_seq[:S] = 0
+    b.ctx_len[:S] = torch.arange(S) + 1
+    b.block_tables[0] = torch.arange(8)
+    m.forward(b, kc, vc, S, 16, n_split=2)
+    rl = ref.logits(ids)
+    err = (b.logits[:S].cpu() - rl).abs().max().item()
+    assert err < 0.05 * rl.abs().max().item(), err
+    outs = []
+    for graphs in (False, True):
+        eng = Engine(m, None, max_batch=4, use_graphs=graphs)
+        futs = [eng.submit(GenRequest([1, 2, 3, 4 + i], SamplingParams(max_tokens=8, ignore_eos=True)))
+                for i in range(3)]
+        while not all(f.done() for f in futs):
+            eng.step()
+        outs.append([f.result().token_ids for f in futs])
+    assert outs[0] == outs[1]
+
+
 def test_moe_grouped_gemm_prefill(gpu, tiny_models):
     """T > 64 routes every token at once and runs the experts as mapped-row LDS GEMMs (mode 2)."""
     r = GGUFReader(tiny_models["tiny-mixtral"])

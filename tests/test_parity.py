@@ -78,8 +78,78 @@ def spec_q8_0(b):
     return [d * (v - 256 if v > 127 else v) for v in b[2:34]]
 
 
+def _nib32(qs, j):
+    """ggml 32-blocks: element j < 16 is the low nibble of qs[j], j >= 16 the high nibble of qs[j - 16]."""
+    return (qs[j] & 0xF) if j < 16 else (qs[j - 16] >> 4)
+
+
+def spec_q4_0(b):
+    d = _h(b, 0)
+    return [d * (_nib32(b[2:18], j) - 8) for j in range(32)]
+
+
+def spec_q4_1(b):
+    d, m = _h(b, 0), _h(b, 2)
+    return [d * _nib32(b[4:20], j) + m for j in range(32)]
+
+
+def spec_q5_0(b):
+    d = _h(b, 0)
+    qh = struct.unpack_from("<I", bytes(b[2:6]))[0]
+    return [d * ((_nib32(b[6:22], j) | (((qh >> j) & 1) << 4)) - 16) for j in range(32)]
+
+
+def spec_q5_1(b):
+    d, m = _h(b, 0), _h(b, 2)
+    qh = struct.unpack_from("<I", bytes(b[4:8]))[0]
+    return [d * (_nib32(b[8:24], j) | (((qh >> j) & 1) << 4)) + m for j in range(32)]
+
+
+def spec_q2_k(b):
+    """ggml dequantize_row_q2_K: per 128-half, four 2-bit planes (shift 0, 2, 4, 6) of 32 bytes, each split
+    into two 16-value sub-blocks with their own (scale, min) nibbles."""
+    sc, qs = list(b[0:16]), list(b[16:80])
+    d, dmin = _h(b, 80), _h(b, 82)
+    y, k = [], 0
+    for n in range(2):
+        q = qs[32 * n:32 * n + 32]
+        for j in range(4):
+            for half in range(2):
+                s = sc[k]
+                k += 1
+                y += [d * (s & 0xF) * ((q[16 * half + l] >> (2 * j)) & 3) - dmin * (s >> 4) for l in range(16)]
+    return y
+
+
+def spec_q3_k(b):
+    """ggml dequantize_row_q3_K with the scale bytes decoded the way quantize_row_q3_K_reference packs
+    them (low nibbles in bytes 0..7, top 2 bits in bytes 8..11) -- not the kmask word shuffle."""
+    hm, qs, scb = list(b[0:32]), list(b[32:96]), list(b[96:108])
+    d = _h(b, 108)
+    scales = []
+    for j in range(16):
+        lo = (scb[j] & 0xF) if j < 8 else (scb[j - 8] >> 4)
+        hi = (scb[8 + j % 4] >> (2 * (j // 4))) & 3
+        scales.append((lo | (hi << 4)) - 32)
+    y, k, m = [], 0, 1
+    for n in range(2):
+        q = qs[32 * n:32 * n + 32]
+        for j in range(4):
+            for half in range(2):
+                dl = d * scales[k]
+                k += 1
+                for l in range(16):
+                    v = (q[16 * half + l] >> (2 * j)) & 3
+                    y.append(dl * (v - (0 if hm[16 * half + l] & m else 4)))
+            m <<= 1
+    return y
+
+
 SPEC = {GGMLType.Q4_K: (144, 256, spec_q4_k), GGMLType.Q5_K: (176, 256, spec_q5_k),
-        GGMLType.Q6_K: (210, 256, spec_q6_k), GGMLType.Q8_0: (34, 32, spec_q8_0)}
+        GGMLType.Q6_K: (210, 256, spec_q6_k), GGMLType.Q8_0: (34, 32, spec_q8_0),
+        GGMLType.Q4_0: (18, 32, spec_q4_0), GGMLType.Q4_1: (20, 32, spec_q4_1),
+        GGMLType.Q5_0: (22, 32, spec_q5_0), GGMLType.Q5_1: (24, 32, spec_q5_1),
+        GGMLType.Q2_K: (84, 256, spec_q2_k), GGMLType.Q3_K: (110, 256, spec_q3_k)}
 
 
 def _random_blocks(t, n, rng):
@@ -88,13 +158,32 @@ def _random_blocks(t, n, rng):
     # finite f16 scale fields (random bytes could be NaN / inf): small normal values
     f16 = lambda: np.frombuffer(np.float16(rng.uniform(-0.05, 0.05)).tobytes(), np.uint8)
     for blk in raw:
-        if t in (GGMLType.Q4_K, GGMLType.Q5_K):
+        if t in (GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q4_1, GGMLType.Q5_1):
             blk[0:2], blk[2:4] = f16(), f16()
         elif t == GGMLType.Q6_K:
             blk[208:210] = f16()
+        elif t == GGMLType.Q2_K:
+            blk[80:82], blk[82:84] = f16(), f16()
+        elif t == GGMLType.Q3_K:
+            blk[108:110] = f16()
         else:
             blk[0:2] = f16()
     return raw
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1, GGMLType.Q2_K,
+                               GGMLType.Q3_K])
+def test_quantizer_roundtrip_new_types(t):
+    """The simple fits of gguf/quants.py produce blocks that decode (through the independent spec
+    decoder) back to the input within the format's resolution."""
+    rng = np.random.default_rng(100 + int(t))
+    x = (rng.standard_normal(256 * 8) * 0.05).astype(np.float32)
+    raw = Q.quantize(x, t)
+    size, per, spec = SPEC[t]
+    blocks = raw.reshape(-1, size)
+    y = np.concatenate([np.array(spec([int(v) for v in b])) for b in blocks])
+    tol = {GGMLType.Q2_K: 0.35, GGMLType.Q3_K: 0.3}.get(t, 0.12)
+    assert np.abs(y - x).max() <= tol * np.abs(x).max(), np.abs(y - x).max()
 
 
 @pytest.mark.parametrize("t", list(SPEC))
