@@ -28,6 +28,12 @@
 // tile on ONE XCD (the tile is fetched from HBM once per XCD L2).
 #include "qgemm_dma.h"
 
+// tools/hg8_probe.hip builds speed-of-light variants: bit 0 = no MFMA (fragments still read),
+// bit 1 = no DMA, bit 2 = no vmcnt waits (results wrong; timing only). 0 in the library.
+#ifndef H8_PROBE
+#define H8_PROBE 0
+#endif
+
 namespace nls_hg8 {
 using namespace nls_gemv;
 using nls_dma::glds16;
@@ -54,6 +60,7 @@ DEVI int swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }
 
 template <int N>
 DEVI void wait_vm() {
+  if constexpr (H8_PROBE & 4) return;
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
@@ -91,6 +98,7 @@ DEVI void h8_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   const uint32_t xdst = base + (uint32_t)(C::XI * wave) * 1024u;
   const uint32_t wdst = base + C::XB + (uint32_t)wave * 1024u;
   auto dma = [&](int j) __attribute__((always_inline)) {      // stage j (clamped) -> ring slot j % NS
+    if constexpr (H8_PROBE & 2) return;
     const int jj = min(j, nst - 1);
     const uint32_t so = (uint32_t)(j % NS) * C::SB;
 #pragma unroll
@@ -121,7 +129,10 @@ DEVI void h8_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
-      for (int j = 0; j < MT; ++j) acc[i][j] = mfma16(FA[i], FB[j], acc[i][j]);
+      for (int j = 0; j < MT; ++j) {
+        if constexpr (H8_PROBE & 1) asm volatile("" ::"v"(FA[i]), "v"(FB[j]));
+        else acc[i][j] = mfma16(FA[i], FB[j], acc[i][j]);
+      }
   };
 
   if (nst > 0) {

@@ -955,6 +955,68 @@ def test_hgemm8_swiglu_multiseg(gpu, rt, ks):
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
 
 
+Q9_TYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.Q4_0, GGMLType.Q5_1, GGMLType.Q3_K]
+
+
+@pytest.mark.parametrize("t", Q9_TYPES)
+@pytest.mark.parametrize("M,waves,rt,ks", [(256, 8, 2, 1), (300, 8, 1, 2), (100, 8, 2, 3), (512, 8, 1, 1), (512, 8, 2, 2),
+                                           (300, 4, 2, 1), (512, 4, 2, 3)])
+def test_qgemm9_types(gpu, t, M, waves, rt, ks):
+    """Mode 9 (qgemm9.hip: raw tile-blocks DMA'd per super-block and dequantised in registers, activations
+    through an NS-deep 32-k stage ring, weights as the MFMA A operand): every device format, a partial last
+    weight tile (264 rows over 128 / 256-row tiles), partial activation blocks, k-slices of 1..3
+    super-blocks (split-K through the slab reduce); f32 store with arg-max keys, residual add with alpha."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=9, waves=waves, rt=rt, ks=ks, argmax=keys if ks == 1 else None)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    if M < pad:
+        assert float(y[M:].abs().max().cpu()) == 0.0
+    if ks == 1:
+        ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+        ops.argmax_unpack(keys, M, ids)
+        assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=9, waves=waves, rt=rt, ks=ks)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+
+
+@pytest.mark.parametrize("waves,rt,ks", [(8, 2, 1), (8, 1, 1), (8, 2, 2), (4, 2, 1)])
+def test_qgemm9_swiglu_multiseg(gpu, waves, rt, ks):
+    """Mode 9 SwiGLU epilogue on interleaved gate/up tile-blocks and a Q|K|V-style launch mixing Q4_K and
+    Q6_K segments (each workgroup picks its segment's format) at column offsets; the mode-2 LDS-dequant
+    GEMM agrees to accumulation order."""
+    K, F = 512, 256
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 333
+    x = _x(M, K, gpu)
+    xf = x[:M].float().cpu()
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=9, waves=waves, rt=rt, ks=ks)
+    _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(256, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(256, K, GGMLType.Q6_K, gpu, 3)
+    segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 512)]
+    yq = torch.zeros(x.shape[0], 768, device=gpu)
+    ops.qgemv(segs, x, yq, M, mode=9, waves=waves, rt=rt, ks=ks)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+    y2 = torch.zeros(x.shape[0], 768, device=gpu)
+    ops.qgemv(segs, x, y2, M, mode=2, waves=8, rt=4, ks=1)
+    _close(yq[:M], y2[:M], 1e-3)
+
+
 @pytest.mark.parametrize("M", [65, 300, 512])
 def test_lib_gemm_mode7(gpu, M):
     """Mode 7: hipBLASLt GEMM on the f16 copies + the HIP SwiGLU pass (interleaved gate/up) / plain f32

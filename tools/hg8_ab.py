@@ -7,6 +7,7 @@ at the Llama-3-8B projection shapes: every launch is captured in a hipGraph over
   * prod:  ops.gemv_config's launch with the shape's fused epilogue (what the engine runs today)
   * m8:    every mode-8 (rt, ks) candidate with the same fused epilogue; the best is reported and, with
            --emit, written as "d8:" tuning entries (JSON on stdout, tools/README.md)
+  * m9:    every mode-9 (rt, ks) candidate (qgemm9.hip: the quantised tile-blocks, no f16 copy)
 
     python tools/hg8_ab.py --M 256,512,1024,2048 [--shapes qkv,o,gateup,down,lm_head] [--emit]
 """
@@ -57,6 +58,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--cands", default="8:1,8:2,8:4,7:1,7:2,4:1,4:2,4:4,8:8,4:8")
+    ap.add_argument("--cands9", default="8:2:1,8:2:2,8:2:4,8:2:8,8:1:1,8:1:2,8:1:4,4:2:1,4:2:2,4:2:4")
+    ap.add_argument("--types", default="", help="override the weight format of every shape (e.g. 14 = Q6_K)")
     ap.add_argument("--emit", action="store_true")
     a = ap.parse_args()
     spec = SPECS[a.model]
@@ -65,7 +68,10 @@ def main():
     defs = {"qkv": ([(12, nq), (12, nkv), (12, nkv)], d, "f32"), "o": ([(12, d)], nq, "add"),
             "gateup": ([(12, 2 * spec.d_ff)], d, "swiglu"), "down": ([(12, d)], spec.d_ff, "add"),
             "lm_head": ([(14, spec.vocab)], d, "argmax")}
-    cands = [tuple(int(v) for v in c.split(":")) for c in a.cands.split(",")]
+    cands = [tuple(int(v) for v in c.split(":")) for c in a.cands.split(",") if c]
+    cands9 = [tuple(int(v) for v in c.split(":")) for c in a.cands9.split(",") if c]
+    if a.types:
+        defs = {k: ([(int(a.types), r) for _, r in sd], K, e) for k, (sd, K, e) in defs.items()}
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(0)
     emit = {}
@@ -87,6 +93,7 @@ def main():
                 w = ops.QWeight.__new__(ops.QWeight)
                 w.__dict__.update(s.w.__dict__)
                 w.d16 = s.w.d16.clone()
+                w.data = s.w.data.clone()
                 cp.append(ops.Seg(w, s.ycol))
             copies.append(cp)
         wcat = [torch.cat([s.w.d16 for s in cp], 0) for cp in copies]
@@ -138,17 +145,37 @@ def main():
                     continue
                 if best is None or t < best[0]:
                     best = (t, cfg)
+            best9 = None
+            for wv, rt, ks in cands9:
+                if epi == "argmax" and ks > 1:
+                    continue
+                cfg = (9, wv, rt, ks)
+                try:
+                    t = timed(graph_of(launch(cfg)), a.rounds)
+                except Exception as e:
+                    print(f"  m9 {cfg} failed: {e}")
+                    continue
+                if best9 is None or t < best9[0]:
+                    best9 = (t, cfg)
             # correctness of the winner (plain f32 output vs the library's product)
             t8, cfg8 = best
             yy = torch.zeros(max(M, 64), col, device=dev)
             ops.qgemv(segs, x, yy, M, mode=8, waves=8, rt=cfg8[2], ks=cfg8[3])
             torch.mm(x[:M], wcat[0].t(), out=lib_out[:M])
             rel = float((yy[:M] - lib_out[:M].float()).abs().max() / (lib_out[:M].float().abs().max() + 1e-6))
+            t9, cfg9, rel9 = float("nan"), None, float("nan")
+            if best9 is not None:
+                t9, cfg9 = best9
+                yy.zero_()
+                ops.qgemv(segs, x, yy, M, mode=9, waves=cfg9[1], rt=cfg9[2], ks=cfg9[3])
+                rel9 = float((yy[:M] - lib_out[:M].float()).abs().max() / (lib_out[:M].float().abs().max() + 1e-6))
             print(f"{name:8s} M={M:5d} lib {t_lib:8.2f}us {flop / t_lib / 1e6:7.1f}TF | prod{prod} {t_prod:8.2f}us | "
                   f"m8{cfg8} {t8:8.2f}us {flop / t8 / 1e6:7.1f}TF | m8/lib {t8 / t_lib:5.2f} m8/prod {t8 / t_prod:5.2f} "
-                  f"| maxrel {rel:.1e}", flush=True)
+                  f"| maxrel {rel:.1e} | m9{cfg9} {t9:8.2f}us {flop / t9 / 1e6:7.1f}TF m9/lib {t9 / t_lib:5.2f} "
+                  f"maxrel {rel9:.1e}", flush=True)
             emit[f"{name}:{M}"] = dict(cfg=list(cfg8), us=round(t8, 2), lib_us=round(t_lib, 2), prod=list(prod),
-                                       prod_us=round(t_prod, 2))
+                                       prod_us=round(t_prod, 2), cfg9=list(cfg9) if cfg9 else None,
+                                       us9=round(t9, 2))
     if a.emit:
         print(json.dumps(emit))
 
