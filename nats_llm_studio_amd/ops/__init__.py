@@ -443,6 +443,9 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
             raise TypeError(f"qgemv: activations must be {ACT_DTYPE}, got {x.dtype}")
         L = _lib.lib()
         mapped = any(s.xmap is not None for s in segs)
+        if not mapped and (x.shape[0] < M or (epi != "argmax" and y.shape[0] < M)):
+            # the kernels index rows 0..M-1 unchecked: fail here, not with a device fault
+            raise ValueError(f"qgemv: M={M} rows but x has {x.shape[0]}, y {y.shape[0]}")
         if mode == 7 or ((mode < 0 or waves == 0) and lib_gemm_ok(segs, M, epi, alpha, argmax, y)):
             return lib_gemm(segs, x, y, M, alpha, epi)
         if mode < 0 or waves == 0:

@@ -171,3 +171,16 @@ def test_lib_gemm_gating_cpu():
     finally:
         tab.pop(key)
     assert not tuning.select_lib(segs, 512)
+
+
+def test_reference_streaming_decode_matches_cached(tiny_models):
+    """The oracle's streaming mode (cache=False, parallel row-range decoding, gathered embedding rows)
+    computes exactly what the cached whole-tensor mode does."""
+    from nats_llm_studio_amd.gguf.reader import GGUFReader
+    from nats_llm_studio_amd.models.reference import ReferenceModel
+    for name in ("tiny-llama", "tiny-mixtral"):
+        r = GGUFReader(tiny_models[name])
+        ids = [1, 5, 9, 200, 33, 7]
+        a = ReferenceModel(r).logits(ids)
+        b = ReferenceModel(r, cache=False, workers=4).logits(ids)
+        assert torch.equal(a, b)
