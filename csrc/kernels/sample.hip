@@ -107,6 +107,122 @@ DEVI float hist_threshold(const float* __restrict__ l, int V, float a, float b, 
   return a;
 }
 
+// Max and sum exp((l - max) * it) of a row in ONE pass (online rescaling), non-finite entries skipped.
+DEVI void block_max_z(const float* __restrict__ l, int V, float it, float& mx, float& z, float* red) {
+  float m = -INFINITY, s = 0.f;
+#pragma unroll 8
+  for (int i = threadIdx.x; i < V; i += NT) {
+    const float v = l[i];
+    if (!(v > -INFINITY)) continue;                  // -inf and NaN
+    if (v > m) {
+      s = s * __expf((m - v) * it) + 1.f;
+      m = v;
+    } else {
+      s += __expf((v - m) * it);
+    }
+  }
+  mx = block_max(m, red);
+  z = block_sum(m > -INFINITY ? s * __expf((m - mx) * it) : 0.f, red);
+}
+
+// The draw: inverse CDF in index order over the kept logits (l >= lo), u in [0, 1). Weights are summed
+// per 64-token tile (a wave per tile, coalesced), the tile sums are scanned block-wide, and one wave scans
+// the tile that holds the target -- no serial walk over chunks or tokens. Returns the token in every thread.
+constexpr int MAXT = 4096;                            // 64-token tiles: V <= 262144
+DEVI int draw_index_order(const float* __restrict__ l, int V, float lo, float mx, float it, float u, float* tile,
+                          float* red, int* s_tok) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nt = (V + 63) >> 6;
+#pragma unroll 4
+  for (int t = w; t < nt; t += NT / 64) {
+    const int i = (t << 6) + lane;
+    float x = 0.f;
+    if (i < V) {
+      const float v = l[i];
+      if (v >= lo && v > -INFINITY) x = __expf((v - mx) * it);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane == 0) tile[t] = x;
+  }
+  __shared__ int s_tile;
+  __shared__ float s_before;
+  if (threadIdx.x == 0) s_tile = -1;
+  __syncthreads();
+  // exclusive scan of per-thread tile runs [per * tid, per * tid + per)
+  const int per = (nt + NT - 1) / NT;
+  const int t0 = threadIdx.x * per;
+  float loc = 0.f;
+  for (int j = 0; j < per; ++j)
+    if (t0 + j < nt) loc += tile[t0 + j];
+  float incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) red[w] = incl;
+  __syncthreads();
+  float off = 0.f, Z = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    const float r = red[i];
+    off += i < w ? r : 0.f;
+    Z += r;
+  }
+  const float target = u * Z;
+  const float excl = off + incl - loc;
+  if (loc > 0.f && excl <= target && target < excl + loc) {
+    float acc = excl;
+    for (int j = 0; j < per && t0 + j < nt; ++j) {
+      const float x = tile[t0 + j];
+      if (x > 0.f && acc + x > target) {
+        s_tile = t0 + j;
+        s_before = acc;
+        break;
+      }
+      acc += x;
+    }
+  }
+  __syncthreads();
+  int t = s_tile;
+  float before = s_before;
+  bool last = false;
+  if (t < 0) {                                        // rounding at the very end: the last kept token
+    int mine = -1;
+    for (int j = per - 1; j >= 0; --j)
+      if (t0 + j < nt && tile[t0 + j] > 0.f) { mine = t0 + j; break; }
+    t = (int)block_max((float)mine, red);             // exact for tile ids < 2^24
+    last = true;
+  }
+  if (w == 0) {
+    int tok = -1;
+    if (t >= 0) {
+      const int i = (t << 6) + lane;
+      float x = 0.f;
+      if (i < V) {
+        const float v = l[i];
+        if (v >= lo && v > -INFINITY) x = __expf((v - mx) * it);
+      }
+      const unsigned long long kept = __ballot(x > 0.f);
+      if (!last) {
+        float c = x;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const float y = __shfl_up(c, o, 64);
+          if (lane >= o) c += y;
+        }
+        const unsigned long long hit = __ballot(x > 0.f && before + c > target);
+        if (hit) tok = (t << 6) + __ffsll((long long)hit) - 1;
+      }
+      if (tok < 0 && kept) tok = (t << 6) + 63 - __clzll((long long)kept);
+    }
+    if (lane == 0) *s_tok = tok < 0 ? 0 : tok;       // nothing kept: a non-finite row -> a valid id anyway
+  }
+  __syncthreads();
+  return *s_tok;
+}
+
 // One row: penalties over the history window h[0, n_hist) (any order), then greedy / temperature /
 // top-k / min-p / top-p and the draw with uniform u. The token is returned in EVERY thread.
 DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u, const int* __restrict__ h,
@@ -134,9 +250,15 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
     __syncthreads();
   }
   // 2) greedy: plain arg-max (lowest index on ties)
-  float mx = -INFINITY;
-  for (int i = threadIdx.x; i < V; i += NT) mx = fmaxf(mx, l[i]);
-  mx = block_max(mx, red);
+  const bool trunc = (p.top_k > 0 && p.top_k < V) || p.min_p > 0.f;
+  const float it = p.temperature > 0.f ? 1.f / p.temperature : 0.f;
+  float mx = -INFINITY, Z = 0.f;
+  if (p.temperature > 0.f && !trunc) {
+    block_max_z(l, V, it, mx, Z, red);               // max and the untruncated mass in one pass
+  } else {
+    for (int i = threadIdx.x; i < V; i += NT) mx = fmaxf(mx, l[i]);
+    mx = block_max(mx, red);
+  }
   if (p.temperature <= 0.f) {
     int best = 0x7FFFFFFF;
     for (int i = threadIdx.x; i < V; i += NT)
@@ -147,7 +269,6 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
     // next step's embedding gather (chained decode feeds next_ids straight back on the device)
     return b < (float)V ? (int)b : 0;
   }
-  const float it = 1.f / p.temperature;
   // 3) keep-threshold on the logit scale: top-k (k-th largest) and min-p (p >= min_p * p_max)
   float lo = -INFINITY;
   if (p.top_k > 0 && p.top_k < V) {
@@ -163,55 +284,19 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
   }
   if (p.min_p > 0.f) lo = fmaxf(lo, mx + p.temperature * __logf(p.min_p));
   // 4) top-p: logit threshold above which the kept mass reaches top_p of the kept total
-  float Z = 0.f;
-  for (int i = threadIdx.x; i < V; i += NT)
-    if (l[i] >= lo) Z += __expf((l[i] - mx) * it);
-  Z = block_sum(Z, red);
   if (p.top_p < 1.f) {
+    if (trunc) {
+      Z = 0.f;
+      for (int i = threadIdx.x; i < V; i += NT)
+        if (l[i] >= lo) Z += __expf((l[i] - mx) * it);
+      Z = block_sum(Z, red);
+    }
     // tokens more than 30 temperatures below the max carry < e^-30 of the mass each: search above them
     const float a = fmaxf(lo, mx - 30.f * p.temperature);
     lo = fmaxf(lo, hist_threshold(l, V, a, mx, lo, false, mx, it, p.top_p * Z, hbin, red));
-    Z = 0.f;
-    for (int i = threadIdx.x; i < V; i += NT)
-      if (l[i] >= lo) Z += __expf((l[i] - mx) * it);
-    Z = block_sum(Z, red);
   }
-  // 5) inverse CDF in index order: contiguous chunk per thread, scan of chunk sums
-  const int per = (V + NT - 1) / NT;
-  const int i0 = threadIdx.x * per, i1 = min(V, i0 + per);
-  float cs = 0.f;
-  for (int i = i0; i < i1; ++i)
-    if (l[i] >= lo) cs += __expf((l[i] - mx) * it);
-  s_chunk[threadIdx.x] = cs;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float target = u * Z;
-    float acc = 0.f;
-    int owner = -1;
-    for (int t = 0; t < NT; ++t) {
-      if (acc + s_chunk[t] > target && s_chunk[t] > 0.f) { owner = t; break; }
-      acc += s_chunk[t];
-    }
-    int tok = -1, last = -1;
-    if (owner >= 0) {
-      const int a0 = owner * per, a1 = min(V, a0 + per);
-      for (int i = a0; i < a1; ++i) {
-        if (l[i] < lo) continue;
-        last = i;
-        acc += __expf((l[i] - mx) * it);
-        if (acc > target) { tok = i; break; }
-      }
-      if (tok < 0) tok = last;
-    }
-    if (tok < 0) {            // rounding at the very end: the last kept token
-      for (int i = V - 1; i >= 0; --i)
-        if (l[i] >= lo) { tok = i; break; }
-    }
-    // nothing kept happens only for a non-finite row (NaN / -inf logits): return a valid id anyway
-    *s_tok = tok < 0 ? 0 : tok;
-  }
-  __syncthreads();
-  return *s_tok;
+  // 5) inverse CDF in index order over the kept tokens
+  return draw_index_order(l, V, lo, mx, it, u, s_chunk, red, s_tok);
 }
 
 __global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, long ld, int V,
@@ -219,7 +304,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(float* __restrict__ logits, 
                                                     const int* __restrict__ hist, int hist_stride,
                                                     int* __restrict__ out) {
   __shared__ float red[NT / 64];
-  __shared__ float s_chunk[NT];
+  __shared__ float s_chunk[MAXT];
   __shared__ int s_tok;
   __shared__ float hbin[NB];
   const int row = blockIdx.x;
@@ -250,7 +335,7 @@ __global__ __launch_bounds__(NT) void sample_decode_kernel(float* __restrict__ l
                                                            int* __restrict__ hist, int hist_stride,
                                                            int* __restrict__ next_ids) {
   __shared__ float red[NT / 64];
-  __shared__ float s_chunk[NT];
+  __shared__ float s_chunk[MAXT];
   __shared__ int s_tok;
   __shared__ float hbin[NB];
   const int row = blockIdx.x;
@@ -272,7 +357,7 @@ __global__ __launch_bounds__(NT) void sample_decode_kernel(float* __restrict__ l
 
 extern "C" int nls_sample(void* logits, long ld, int n, int V, const void* params, const int* hist, int hist_stride,
                           int* out, void* stream) {
-  if (n < 1 || V < 1) return -1;
+  if (n < 1 || V < 1 || V > 64 * MAXT) return -1;
   hipLaunchKernelGGL(sample_kernel, dim3(n), dim3(NT), 0, (hipStream_t)stream, (float*)logits, ld, V,
                      (const SampleParams*)params, hist, hist_stride, out);
   return (int)hipGetLastError();
@@ -283,7 +368,7 @@ extern "C" int nls_sample_params_size() { return (int)sizeof(SampleParams); }
 extern "C" int nls_sample_decode(void* logits, long ld, int n, int V, const void* params, const void* seeds,
                                  const int* pos, const int* ctx_len, int* hist, int hist_stride, int* next_ids,
                                  void* stream) {
-  if (n < 1 || V < 1 || hist_stride < 1 || hist_stride > NT) return -1;
+  if (n < 1 || V < 1 || V > 64 * MAXT || hist_stride < 1 || hist_stride > NT) return -1;
   hipLaunchKernelGGL(sample_decode_kernel, dim3(n), dim3(NT), 0, (hipStream_t)stream, (float*)logits, ld, V,
                      (const SampleParams*)params, (const unsigned long long*)seeds, pos, ctx_len, hist, hist_stride,
                      next_ids);

@@ -22,7 +22,7 @@ import os
 import math
 import threading
 import time
-from collections import deque
+from collections import defaultdict, deque
 from concurrent.futures import Future
 from dataclasses import dataclass, field
 from typing import Callable, Deque, Dict, List, Optional, Sequence as Seq
@@ -269,6 +269,7 @@ class Engine:
         self.thread: Optional[threading.Thread] = None
         self.stop_flag = False
         self._ids = itertools.count()
+        self.host_ms = defaultdict(float)
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0,
                              device_sampled_steps=0, preemptions=0, recompute_tokens=0)
         self.full_logits: Optional[torch.Tensor] = None
@@ -282,6 +283,21 @@ class Engine:
             self.d_sparams = torch.zeros(self.max_batch, ops.SAMPLE_PARAMS_BYTES, dtype=torch.uint8, device=self.dev)
             self.d_seeds = torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev)
             self.d_hist = torch.full((self.max_batch, HIST), -1, dtype=torch.int32, device=self.dev)
+            # rows taking a decode slot are staged in pinned memory (double-buffered like the step
+            # metadata) and go up as ONE async copy + device scatter before the next launch: per-row
+            # pageable copies stall the host and serialise behind the step in flight (a 512-request
+            # burst paid ~1.5K of them)
+            nb_ = ops.SAMPLE_PARAMS_BYTES
+            self._srow_pin = [dict(idx=torch.zeros(self.max_batch, dtype=torch.int64, pin_memory=True),
+                                   par=torch.zeros(self.max_batch, nb_, dtype=torch.uint8, pin_memory=True),
+                                   seed=torch.zeros(self.max_batch, dtype=torch.int64, pin_memory=True),
+                                   hist=torch.zeros(self.max_batch, HIST, dtype=torch.int32, pin_memory=True))
+                              for _ in range(2)]
+            self._srow_dev = dict(idx=torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev),
+                                  par=torch.zeros(self.max_batch, nb_, dtype=torch.uint8, device=self.dev),
+                                  seed=torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev),
+                                  hist=torch.zeros(self.max_batch, HIST, dtype=torch.int32, device=self.dev))
+            self._srow_dirty: Dict[int, tuple] = {}
         self.sync_hook: Optional[Callable[[], None]] = None   # follower side of Engine.sync()
         # tensor parallel with the IPC one-shot all-reduce: its error words (raised on every rank when any
         # rank's poll timed out) travel to the host with each step's tokens; a raised word fails the step
@@ -391,12 +407,21 @@ class Engine:
 
     # ------------------------------------------------------------------ scheduling
     def step(self):
+        # host-time accounting (ms, cumulative; stats()["host_ms"]): where the engine thread spends a step
+        # -- "wait" is blocked on the GPU (the step in flight), everything else is host work that the
+        # async decode pipeline has to hide behind the GPU step
+        hm, clk = self.host_ms, time.perf_counter
+        t0 = clk()
         self._expire()
         self._admit()
+        t1 = clk()
+        hm["schedule"] += (t1 - t0) * 1e3
         if any(s.n_prefilled < s.n_target for s in self.running):
             # the prefill chunk is queued behind the in-flight decode step (separate step buffers) and
             # the next decode step still chains on that step's device-side tokens: no pipeline drain
             self._prefill()
+        t2 = clk()
+        hm["prefill"] += (t2 - t1) * 1e3
         dec = [s for s in self.running if s.n_prefilled >= s.n_target and not s.done]
         if dec:
             self._decode(dec)
@@ -404,6 +429,7 @@ class Engine:
             self._drain()
         self.running = [s for s in self.running if not s.done]
         self.counters["steps"] += 1
+        hm["decode"] += (clk() - t2) * 1e3
 
     def _expire(self):
         now = time.monotonic()
@@ -493,12 +519,33 @@ class Engine:
 
     def _exec_prefill(self, T: int, rows: List[int], need_logits: bool):
         b = self.pb
-        b.meta.copy_(self.h_meta_p, non_blocking=self.dev.type == "cuda" and self.rank == 0)
-        lr = torch.tensor(rows, dtype=torch.int32, device=self.dev)
+        cuda = self.dev.type == "cuda"
+        b.meta.copy_(self.h_meta_p, non_blocking=cuda and self.rank == 0)
         pad = b.pad
         h = self.h_meta_p.numpy()
         qb = ops.prefill_blocks(h[3 * pad:4 * pad], h[pad:2 * pad], T) if self.prefill_attn else None
-        qbt = torch.from_numpy(qb).to(self.dev) if qb is not None and len(qb) else None
+        # logit rows and query blocks through pinned staging (async, stream-ordered): pageable uploads
+        # block the host until the decode step in flight has drained
+        if not hasattr(self, "_pf_pin"):
+            nq = (self.max_prefill + 15) // 16 + self.max_batch
+            self._pf_pin = (torch.zeros(self.max_batch, dtype=torch.int32, pin_memory=cuda),
+                            torch.zeros(nq, 4, dtype=torch.int32, pin_memory=cuda))
+            self._pf_dev = (torch.zeros(self.max_batch, dtype=torch.int32, device=self.dev),
+                            torch.zeros(nq, 4, dtype=torch.int32, device=self.dev))
+        # (the previous prefill's uploads have executed: its tokens were read back before this one)
+        lp, qp = self._pf_pin
+        ld, qd = self._pf_dev
+        lp.numpy()[:len(rows)] = rows
+        lr = ld[:len(rows)]
+        lr.copy_(lp[:len(rows)], non_blocking=cuda)
+        qbt = None
+        if qb is not None and len(qb):
+            if len(qb) > qp.shape[0]:
+                qbt = torch.from_numpy(qb).to(self.dev)
+            else:
+                qp.numpy()[:len(qb)] = qb
+                qbt = qd[:len(qb)]
+                qbt.copy_(qp[:len(qb)], non_blocking=cuda)
         n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
                                logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb),
                                need_logits=need_logits)
@@ -636,9 +683,30 @@ class Engine:
         n = len(s.tokens)
         for q in range(max(0, n - HIST), n):
             hist[q % HIST] = s.tokens[q]
-        self.d_sparams[r].copy_(torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()))
-        self.d_seeds[r] = seed & 0x7FFFFFFFFFFFFFFF
-        self.d_hist[r].copy_(torch.from_numpy(hist))
+        self._srow_dirty[r] = (raw, seed & 0x7FFFFFFFFFFFFFFF, hist)
+
+    def _flush_sampling_rows(self, k: int):
+        """Upload the staged rows (pinned buffer k) before the launch that first samples them: one async
+        copy per table into device staging, then an index_copy_ scatter -- all ordered on the stream."""
+        if not self._srow_dirty:
+            return
+        rows = sorted(self._srow_dirty)
+        n = len(rows)
+        hp, dv = self._srow_pin[k], self._srow_dev
+        ip, pp, sp, hh = hp["idx"].numpy(), hp["par"].numpy(), hp["seed"].numpy(), hp["hist"].numpy()
+        for j, r in enumerate(rows):
+            raw, seed, hist = self._srow_dirty[r]
+            ip[j] = r
+            pp[j] = np.frombuffer(raw, dtype=np.uint8)
+            sp[j] = seed
+            hh[j] = hist
+        self._srow_dirty.clear()
+        for key in ("idx", "par", "seed", "hist"):
+            dv[key][:n].copy_(hp[key][:n], non_blocking=True)
+        idx = dv["idx"][:n]
+        self.d_sparams.index_copy_(0, idx, dv["par"][:n])
+        self.d_seeds.index_copy_(0, idx, dv["seed"][:n])
+        self.d_hist.index_copy_(0, idx, dv["hist"][:n])
 
     def _release_rows(self, keep=()):
         keep = set(id(x) for x in keep)
@@ -681,7 +749,16 @@ class Engine:
         return Bp
 
     def _launch(self, launch: List[_Seq], prev: set, need: bool = False, dsamp: bool = False):
+        t0 = time.perf_counter()
+        try:
+            return self._launch_inner(launch, prev, need, dsamp)
+        finally:
+            self.host_ms["launch"] += (time.perf_counter() - t0) * 1e3
+
+    def _launch_inner(self, launch: List[_Seq], prev: set, need: bool, dsamp: bool):
         k = self._kbuf = self._kbuf ^ 1
+        if self.device_sampling:
+            self._flush_sampling_rows(k)
         Bp = self._build_meta(k, launch, prev)
         pad = self.db.pad
         self._ctrl(_OP_DECODE, Bp, 0, need, [], Bp, self.h_meta_d2[k], pad)
@@ -716,12 +793,16 @@ class Engine:
     def _process(self, infl):
         snap, k = infl
         if self.dev.type == "cuda":
+            t0 = time.perf_counter()
             self._ev[k].synchronize()
+            self.host_ms["wait"] += (time.perf_counter() - t0) * 1e3
             self._check_comm(k)
+        t0 = time.perf_counter()
         toks = self.h_next2[k].numpy()
         for row, s in snap:
             if not s.done:
                 self._append(s, int(toks[row]))
+        self.host_ms["tokens"] += (time.perf_counter() - t0) * 1e3
 
     def _drain(self):
         if self._inflight is not None:
@@ -966,4 +1047,4 @@ class Engine:
                     kv_blocks_free=self.alloc.n_free, kv_blocks_total=self.num_blocks,
                     kv_reserve="full" if self.reserve_full else "ondemand",
                     prefix_cache_hit_tokens=self.alloc.hits, prefix_cache_blocks=len(self.alloc.block_of),
-                    graphs=sorted(self.graphs))
+                    graphs=sorted(self.graphs), host_ms={k: round(v, 1) for k, v in self.host_ms.items()})

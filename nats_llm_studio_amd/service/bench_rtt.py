@@ -186,6 +186,7 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
         order = list(range(n))
         rnd.shuffle(order)                  # sampled and greedy requests interleave in the batch
         c0 = dict(engine.counters)
+        h0 = dict(engine.host_ms) if hasattr(engine, "host_ms") else {}
         try:
             t0 = time.monotonic()
             for i in order:
@@ -196,6 +197,8 @@ def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b
             t1 = max(t_recv.values()) if t_recv else time.monotonic()
             phases = svc.tracer.summary(last=0)["phases_ms"]
             eng_d = {k: engine.counters[k] - c0.get(k, 0) for k in engine.counters}
+            if h0 or hasattr(engine, "host_ms"):
+                eng_d["host_ms"] = {k: round(v - h0.get(k, 0.0), 1) for k, v in engine.host_ms.items()}
         finally:
             sub.unsubscribe()
             cli.close()
