@@ -296,6 +296,217 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
   out[(size_t)t * ldo + (size_t)h * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Decode attention on MFMA (large grids: batch x kv heads >= 1K workgroups). The VALU kernel above
+// spends ~170 vector instructions per 4 keys of a wave (dot products, cross-lane sums, the online
+// softmax and 32 FMAs of P.V per lane): at batch 512 it runs at ~3.5 TB/s of K/V, bound by issue, not
+// HBM (tools/attn_layout_probe.py: time linear in the context at every length). Here the G query heads
+// of a kv head are the 16 COLUMNS of the MFMA tiles (G <= 16, the rest zero), so per 32 keys a wave
+// issues 16 v_mfma_f32_16x16x32_bf16 and softmaxes 8 values per lane:
+//   S^T = K Q^T   A = K rows straight from HBM into registers (lane (g, r): key r, dims 8g..8g+7 of
+//                 each 32-dim k-step), B = Q^T (lane column r = head r, loaded once)
+//   O^T += V^T P^T  A = V^T through LDS: the 32-key V tile is stored row-major with a 16-byte chunk XOR
+//                 swizzle and read back transposed by ds_read_b64_tr_b16 (cdna_hip_programming.md T10);
+//                 B = P^T straight from the S^T accumulators (lane (g, r) holds keys 4g..4g+3 of each
+//                 16-key n-tile for head r: the MFMA's k order is free, so V^T's transposed reads take
+//                 rows {4g..4g+3} and {16+4g..16+4g+3} to match)
+// The O^T accumulators keep head r in lane column r -- exactly where the softmax state of head r lives,
+// so the rescale needs no cross-lane traffic. One wave per workgroup; the next 32 keys' K/V loads are
+// in flight while the current ones are computed. Splits and the fused combine as the VALU kernel.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+template <typename KV>
+__global__ __launch_bounds__(64) void attn_decode_mfma_kernel(
+    const __bf16* __restrict__ q, long ldq, const KV* __restrict__ kc, const KV* __restrict__ vc,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
+    const int* __restrict__ ctx_len, int Hkv, int G, int bs, float scale, int chunk, int n_split,
+    act_t* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int* __restrict__ cnt) {
+  constexpr int D = 128, NKK = D / 32, NDT = D / 16, KG = 32;
+  typedef KVRaw<KV> R;
+  __shared__ __attribute__((aligned(16))) uint8_t Vs[2][KG * D * 2];          // 2 x 8 KiB
+  const int t = blockIdx.x, kh = blockIdx.y, split = blockIdx.z;
+  const int lane = threadIdx.x, g = lane >> 4, r = lane & 15;
+  const int Hq = Hkv * G;
+  const int ctx = ctx_len[t];
+  chunk = split_chunk(chunk, ctx, n_split, bs);
+  const int start = split * chunk;
+  if (n_split > 1 && start >= ctx && ctx > 0) return;       // inactive split: combine skips it
+  const int end = min(ctx, start + chunk);
+  const int* bt = block_tables + (size_t)tok_seq[t] * bt_stride;
+  const float sl2 = scale * LOG2E;
+
+  bf16x8 qf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    qf[kk] = bf16x8{};
+    if (r < G) qf[kk] = *reinterpret_cast<const bf16x8*>(q + (size_t)t * ldq + (size_t)(kh * G + r) * D + kk * 32 + 8 * g);
+  }
+  f32x4 o[NDT];
+#pragma unroll
+  for (int c = 0; c < NDT; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  auto kv_row = [&](int p) -> size_t {       // element offset of key p's row for this kv head
+    const int pc = min(p, end - 1);
+    return ((size_t)((long)bt[pc / bs] * bs + pc % bs) * Hkv + kh) * D;
+  };
+  // swizzled byte offset of 16-byte chunk ch of V row `row` (256-byte rows): conflict-free for the
+  // transposed reads and the row writes (cdna_hip_programming.md T10, layout (b))
+  auto voff = [](int row, int ch) { return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); };
+  // K of 32 keys: [n-tile][k-step]; V of 32 keys: 8 rows-of-4 per lane (row = 4i + lane / 16, chunk lane % 16)
+  typename R::raw kr[2][NKK], vr[8];
+  auto load = [&](int base, typename R::raw (&K)[2][NKK], typename R::raw (&V)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const size_t o0 = kv_row(base + 16 * nt + r);
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) K[nt][kk] = R::ld(kc + o0 + kk * 32 + 8 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) V[i] = R::ld(vc + kv_row(base + 4 * i + (lane >> 4)) + 8 * (lane & 15));
+  };
+  auto store_v = [&](int buf, typename R::raw (&V)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      *reinterpret_cast<u32x4*>(Vs[buf] + voff(4 * i + (lane >> 4), lane & 15)) = R::bf16(V[i]);
+  };
+  const int ngrp = end > start ? (end - start + KG - 1) / KG : 0;
+  if (ngrp > 0) {
+    load(start, kr, vr);
+    store_v(0, vr);
+  }
+  for (int j = 0; j < ngrp; ++j) {
+    const int base = start + j * KG;
+    typename R::raw kn[2][NKK], vn[8];
+    const bool more = j + 1 < ngrp;
+    if (more) load(base + KG, kn, vn);
+    // ---- S^T = K Q^T: s[nt][i] = S[head r][key base + 16 nt + 4 g + i]
+    f32x4 s[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+        s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, R::bf16(kr[nt][kk])), qf[kk],
+                                                        s[nt], 0, 0, 0);
+    }
+    // ---- online softmax of head r (base 2), keys past `end` masked
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = base + 16 * nt + 4 * g + i < end ? s[nt][i] * sl2 : -INFINITY;
+        s[nt][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = m == -INFINITY ? 0.f : exp2f(m - mn);
+    float ps = 0.f;
+    bf16x8 pb;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pv = s[nt][i] == -INFINITY ? 0.f : exp2f(s[nt][i] - mn);
+        ps += pv;
+        pb[4 * nt + i] = (__bf16)pv;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = mn;
+    // ---- O^T = O^T * alpha + V^T P^T over the 32 keys; V^T fragment of dim tile c: transposed reads of
+    // rows {4g+q} and {16+4g+q}, columns 16c + 4p .. +3 (lane 4q + p of the group supplies the address)
+    const uint8_t* vb = Vs[j & 1];
+    const int qq = r >> 2, pp = r & 3;
+#pragma unroll
+    for (int c = 0; c < NDT; ++c) {
+      const int ch = 2 * c + (pp >> 1);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(vb + voff(4 * g + qq, ch) + 8 * (pp & 1)));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(vb + voff(16 + 4 * g + qq, ch) + 8 * (pp & 1)));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 a8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a8), pb, o[c] * alpha, 0, 0, 0);
+    }
+    if (more) {
+      store_v((j + 1) & 1, vn);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) kr[nt][kk] = kn[nt][kk];
+    }
+  }
+
+  // ---- output: lane (g, r) holds dims 16c + 4g + i of head r
+  const int qh = kh * G + r;
+  if (n_split == 1) {
+    if (r < G) {
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+      for (int c = 0; c < NDT; ++c) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<h4*>(out + (size_t)t * ldo + (size_t)qh * D + 16 * c + 4 * g) =
+            h4{(_Float16)(o[c][0] * inv), (_Float16)(o[c][1] * inv), (_Float16)(o[c][2] * inv),
+               (_Float16)(o[c][3] * inv)};
+      }
+    }
+    return;
+  }
+  if (r < G) {
+    const size_t pi = ((size_t)t * Hq + qh) * n_split + split;
+#pragma unroll
+    for (int c = 0; c < NDT; ++c) *reinterpret_cast<f32x4*>(part_o + pi * D + 16 * c + 4 * g) = o[c];
+    if (g == 0) {
+      part_ml[2 * pi] = m;
+      part_ml[2 * pi + 1] = l;
+    }
+  }
+  if (!cnt) return;
+  // fused combine: the last active split of (token, kv head) to arrive merges them (as the VALU kernel)
+  const int na = ctx > 0 ? min(n_split, (ctx + chunk - 1) / chunk) : n_split;
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* cp = cnt + (size_t)t * Hkv + kh;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == na - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int e = threadIdx.x; e < G * D; e += 64) {
+    const int h = e / D, d = e - h * D;
+    const int qh2 = kh * G + h;
+    const size_t pb0 = ((size_t)t * Hq + qh2) * n_split;
+    float M = -INFINITY;
+    for (int s2 = 0; s2 < na; ++s2) M = fmaxf(M, part_ml[2 * (pb0 + s2)]);
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+      for (int s2 = 0; s2 < na; ++s2) {
+        const float ms = part_ml[2 * (pb0 + s2)];
+        if (ms == -INFINITY) continue;
+        const float f = exp2f(ms - M);
+        L += part_ml[2 * (pb0 + s2) + 1] * f;
+        O += part_o[(pb0 + s2) * D + d] * f;
+      }
+    }
+    out[(size_t)t * ldo + (size_t)qh2 * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
+  }
+}
+
 template <int D, int G>
 void launch_attn(dim3 grid, hipStream_t st, const __bf16* q, long ldq, const void* kc, const void* vc,
                  const int* bt, int bts, const int* ts, const int* cl, int Hkv, int bs, float scale, int chunk,
@@ -327,6 +538,22 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(T, Hkv, n_split);
+  // MFMA kernel once the grid fills the chip (NLS_ATTN_MFMA=0 disables it, =1 forces it for D = 128)
+  static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
+  if (D == 128 && G <= 16 && mf != 0 && (mf == 1 || (long)T * Hkv * n_split >= 1024)) {
+    if (kv8)
+      hipLaunchKernelGGL(attn_decode_mfma_kernel<uint8_t>, grid, dim3(64), 0, st, (const __bf16*)q, ldq,
+                         (const uint8_t*)kc, (const uint8_t*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G,
+                         block_size, scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt);
+    else
+      hipLaunchKernelGGL(attn_decode_mfma_kernel<__bf16>, grid, dim3(64), 0, st, (const __bf16*)q, ldq,
+                         (const __bf16*)kc, (const __bf16*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G,
+                         block_size, scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt);
+    if (n_split > 1 && !cnt)
+      hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
+                         n_split, chunk, block_size, (act_t*)out, ldo);
+    return (int)hipGetLastError();
+  }
   // waves per workgroup: 8 (twice the keys in flight per step) while the grid is small -- batch 1 / 16 at
   // 4K context 2.93 -> 2.68 / 5.19 -> 4.76 ms/step, batch 1 at 128 2.24 -> 2.17 -- and 4 once the grid
   // fills the chip (batch 512: 12.97 vs 13.74), profiles/attn_waves_ab.txt. NLS_ATTN_WAVES=4|8 forces.

@@ -297,6 +297,38 @@ def test_attention_paged(gpu, D, G, n_split, chunk, fused, kvt):
         assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("G", [4, 8, 1, 7])
+@pytest.mark.parametrize("n_split,fused", [(1, False), (4, True), (3, False)])
+@pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
+def test_attention_decode_mfma(gpu, G, n_split, fused, kvt):
+    """The MFMA decode kernel (taken once batch x kv heads x splits >= 1K workgroups, D = 128): G query
+    heads as MFMA columns, V^T through transposed LDS reads; contexts around the 32-key groups (0, 1, 31,
+    32, 33, ...), flash-decoding splits with the fused or the separate combine, bf16 and fp8 caches."""
+    if kvt != torch.bfloat16 and G not in (4, 1):
+        pytest.skip("fp8 cache: a representative subset")
+    D, Hkv, bs, nblk = 128, 8, 16, 512
+    Hq = Hkv * G
+    ctx = [0, 1, 31, 32, 33, 100, 300, 777] * 16
+    T = len(ctx)
+    g = torch.Generator().manual_seed(1)
+    kc = torch.randn(nblk * bs, Hkv, D, generator=g).to(kvt)
+    vc = torch.randn(nblk * bs, Hkv, D, generator=g).to(kvt)
+    bt = torch.stack([torch.randperm(nblk, generator=g)[:64] for _ in range(T)]).to(torch.int32)
+    q = torch.randn(T, Hq * D, generator=g).to(torch.bfloat16)
+    ts = torch.arange(T, dtype=torch.int32)
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    ref = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE)
+    ops.attention(q, kc, vc, bt, ts, cl, ref, T, Hq, Hkv, D, bs, D ** -0.5)
+    cnt = torch.zeros(T * Hkv, dtype=torch.int32, device=gpu) if fused else None
+    for _ in range(2 if fused else 1):
+        out = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE, device=gpu)
+        ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), ts.to(gpu), cl.to(gpu), out, T, Hq, Hkv, D, bs,
+                      D ** -0.5, chunk=0, n_split=n_split, counters=cnt)
+        torch.testing.assert_close(out.cpu().float(), ref.float(), rtol=2e-2, atol=2e-2)
+    if fused:
+        assert int(cnt.abs().sum()) == 0
+
+
 def test_argmax_kernel(gpu):
     lg = torch.randn(3, 128256, device=gpu)
     lg[1, 777] = 100.0
