@@ -51,6 +51,9 @@ class ModelSpec:
 
 SPECS: Dict[str, ModelSpec] = {
     "llama-3-8b": ModelSpec("llama-3-8b", "llama", 32, 4096, 32, 8, 14336, 128256, 8192, 500000.0),
+    # Llama-3.1-8B: the same shapes with the 128K context and rope_freqs scaling (long-context sweeps)
+    "llama-3.1-8b": ModelSpec("llama-3.1-8b", "llama", 32, 4096, 32, 8, 14336, 128256, 131072, 500000.0,
+                              rope_freqs=True),
     "llama-3-70b": ModelSpec("llama-3-70b", "llama", 80, 8192, 64, 8, 28672, 128256, 8192, 500000.0),
     "mixtral-8x7b": ModelSpec("mixtral-8x7b", "llama", 32, 4096, 32, 8, 14336, 32000, 32768, 1e6,
                               n_expert=8, n_expert_used=2, tokenizer="llama"),
