@@ -315,8 +315,8 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
 // in flight while the current ones are computed. Splits and the fused combine as the VALU kernel.
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-template <typename KV>
-__global__ __launch_bounds__(64) void attn_decode_mfma_kernel(
+template <typename KV, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
     const __bf16* __restrict__ q, long ldq, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
     const int* __restrict__ ctx_len, int Hkv, int G, int bs, float scale, int chunk, int n_split,
@@ -324,9 +324,12 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(
     int* __restrict__ cnt) {
   constexpr int D = 128, NKK = D / 32, NDT = D / 16, KG = 32;
   typedef KVRaw<KV> R;
-  __shared__ __attribute__((aligned(16))) uint8_t Vs[2][KG * D * 2];          // 2 x 8 KiB
+  // per wave: a double-buffered 32-key V tile (2 x 8 KiB); reused for the cross-wave merge at the end
+  __shared__ __attribute__((aligned(16))) uint8_t Vsm[WAVES][2][KG * D * 2];
   const int t = blockIdx.x, kh = blockIdx.y, split = blockIdx.z;
-  const int lane = threadIdx.x, g = lane >> 4, r = lane & 15;
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t (*Vs)[KG * D * 2] = Vsm[wave];
   const int Hq = Hkv * G;
   const int ctx = ctx_len[t];
   chunk = split_chunk(chunk, ctx, n_split, bs);
@@ -371,16 +374,18 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(
     for (int i = 0; i < 8; ++i)
       *reinterpret_cast<u32x4*>(Vs[buf] + voff(4 * i + (lane >> 4), lane & 15)) = R::bf16(V[i]);
   };
-  const int ngrp = end > start ? (end - start + KG - 1) / KG : 0;
+  // wave w takes the 32-key groups w, w + WAVES, ... of the workgroup's range
+  const int ngrp_all = end > start ? (end - start + KG - 1) / KG : 0;
+  const int ngrp = ngrp_all > wave ? (ngrp_all - wave + WAVES - 1) / WAVES : 0;
   if (ngrp > 0) {
-    load(start, kr, vr);
+    load(start + wave * KG, kr, vr);
     store_v(0, vr);
   }
   for (int j = 0; j < ngrp; ++j) {
-    const int base = start + j * KG;
+    const int base = start + (j * WAVES + wave) * KG;
     typename R::raw kn[2][NKK], vn[8];
     const bool more = j + 1 < ngrp;
-    if (more) load(base + KG, kn, vn);
+    if (more) load(base + WAVES * KG, kn, vn);
     // ---- S^T = K Q^T: s[nt][i] = S[head r][key base + 16 nt + 4 g + i]
     f32x4 s[2];
 #pragma unroll
@@ -443,28 +448,70 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(
     }
   }
 
-  // ---- output: lane (g, r) holds dims 16c + 4g + i of head r
-  const int qh = kh * G + r;
-  if (n_split == 1) {
-    if (r < G) {
-      const float inv = l > 0.f ? 1.f / l : 0.f;
+  // ---- output. WAVES > 1: merge the waves' partial (m, l, O) of each head through LDS (the V tiles'
+  // space), every thread finishing (head, dim) elements; WAVES == 1: lane (g, r) holds dims 16c + 4g + i of
+  // head r in registers
+  if constexpr (WAVES > 1) {
+    float* mb = reinterpret_cast<float*>(&Vsm[0][0][0]);            // [WAVES][16] m, [WAVES][16] l
+    float* ob = mb + 2 * WAVES * 16;                                  // [WAVES][16 heads][D]
+    __syncthreads();                                                  // every wave is done with its V tiles
+    if (g == 0) {
+      mb[wave * 16 + r] = m;
+      mb[(WAVES + wave) * 16 + r] = l;
+    }
 #pragma unroll
-      for (int c = 0; c < NDT; ++c) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<h4*>(out + (size_t)t * ldo + (size_t)qh * D + 16 * c + 4 * g) =
-            h4{(_Float16)(o[c][0] * inv), (_Float16)(o[c][1] * inv), (_Float16)(o[c][2] * inv),
-               (_Float16)(o[c][3] * inv)};
+    for (int c = 0; c < NDT; ++c)
+      *reinterpret_cast<f32x4*>(ob + ((size_t)wave * 16 + r) * D + 16 * c + 4 * g) = o[c];
+    __syncthreads();
+    for (int e = threadIdx.x; e < G * D; e += 64 * WAVES) {
+      const int h = e / D, d = e - h * D;
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) M = fmaxf(M, mb[w * 16 + h]);
+      float L = 0.f, O = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) {
+        const float mw = mb[w * 16 + h];
+        const float f = mw == -INFINITY ? 0.f : exp2f(mw - M);
+        L += mb[(WAVES + w) * 16 + h] * f;
+        O += ob[((size_t)w * 16 + h) * D + d] * f;
+      }
+      const int qh2 = kh * G + h;
+      if (n_split == 1) {
+        out[(size_t)t * ldo + (size_t)qh2 * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
+      } else {
+        const size_t pi = ((size_t)t * Hq + qh2) * n_split + split;
+        part_o[pi * D + d] = O;
+        if (d == 0) {
+          part_ml[2 * pi] = M;
+          part_ml[2 * pi + 1] = L;
+        }
       }
     }
-    return;
-  }
-  if (r < G) {
-    const size_t pi = ((size_t)t * Hq + qh) * n_split + split;
+    if (n_split == 1) return;
+  } else {
+    const int qh = kh * G + r;
+    if (n_split == 1) {
+      if (r < G) {
+        const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-    for (int c = 0; c < NDT; ++c) *reinterpret_cast<f32x4*>(part_o + pi * D + 16 * c + 4 * g) = o[c];
-    if (g == 0) {
-      part_ml[2 * pi] = m;
-      part_ml[2 * pi + 1] = l;
+        for (int c = 0; c < NDT; ++c) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<h4*>(out + (size_t)t * ldo + (size_t)qh * D + 16 * c + 4 * g) =
+              h4{(_Float16)(o[c][0] * inv), (_Float16)(o[c][1] * inv), (_Float16)(o[c][2] * inv),
+                 (_Float16)(o[c][3] * inv)};
+        }
+      }
+      return;
+    }
+    if (r < G) {
+      const size_t pi = ((size_t)t * Hq + qh) * n_split + split;
+#pragma unroll
+      for (int c = 0; c < NDT; ++c) *reinterpret_cast<f32x4*>(part_o + pi * D + 16 * c + 4 * g) = o[c];
+      if (g == 0) {
+        part_ml[2 * pi] = m;
+        part_ml[2 * pi + 1] = l;
+      }
     }
   }
   if (!cnt) return;
@@ -487,7 +534,7 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(
   }
   __syncthreads();
   if (!last) return;
-  for (int e = threadIdx.x; e < G * D; e += 64) {
+  for (int e = threadIdx.x; e < G * D; e += 64 * WAVES) {
     const int h = e / D, d = e - h * D;
     const int qh2 = kh * G + h;
     const size_t pb0 = ((size_t)t * Hq + qh2) * n_split;
@@ -538,17 +585,22 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(T, Hkv, n_split);
-  // MFMA kernel once the grid fills the chip (NLS_ATTN_MFMA=0 disables it, =1 forces it for D = 128)
+  // D = 128: the MFMA kernel -- one wave per workgroup once the grid fills the chip (>= 1K workgroups),
+  // else four waves splitting the workgroup's keys (more K/V in flight per (token, kv head, split): long
+  // contexts at small batch). NLS_ATTN_MFMA=0 keeps the VALU kernel.
   static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
-  if (D == 128 && G <= 16 && mf != 0 && (mf == 1 || (long)T * Hkv * n_split >= 1024)) {
-    if (kv8)
-      hipLaunchKernelGGL(attn_decode_mfma_kernel<uint8_t>, grid, dim3(64), 0, st, (const __bf16*)q, ldq,
-                         (const uint8_t*)kc, (const uint8_t*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G,
-                         block_size, scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt);
-    else
-      hipLaunchKernelGGL(attn_decode_mfma_kernel<__bf16>, grid, dim3(64), 0, st, (const __bf16*)q, ldq,
-                         (const __bf16*)kc, (const __bf16*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G,
-                         block_size, scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt);
+  if (D == 128 && G <= 16 && mf != 0) {
+    const bool big = (long)T * Hkv * n_split >= 1024;
+#define NLS_ATTN_M(KVT, W)                                                                                     \
+  hipLaunchKernelGGL((attn_decode_mfma_kernel<KVT, W>), grid, dim3(64 * W), 0, st, (const __bf16*)q, ldq,       \
+                     (const KVT*)kc, (const KVT*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G, block_size, \
+                     scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt)
+    if (kv8) {
+      if (big) NLS_ATTN_M(uint8_t, 1); else NLS_ATTN_M(uint8_t, 4);
+    } else {
+      if (big) NLS_ATTN_M(__bf16, 1); else NLS_ATTN_M(__bf16, 4);
+    }
+#undef NLS_ATTN_M
     if (n_split > 1 && !cnt)
       hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
                          n_split, chunk, block_size, (act_t*)out, ldo);

@@ -69,18 +69,14 @@ template <> struct KVRaw<uint8_t> {
   typedef uint2 raw;
   static DEVI raw ld(const uint8_t* p) { return *reinterpret_cast<const uint2*>(p); }
   static DEVI u32x4 bf16(const raw& r) {
-    // bytes 2i, 2i+1 -> dword i (bf16 pair). The scalar byte-select conversion: the packed form
-    // returned the selected word's first value in both lanes of its result on this toolchain
-    // (tools/kv8_probe.py).
-    auto b = [](uint32_t w, auto sel) {
-      return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_f32_fp8((int)w, decltype(sel)::value));
+    // bytes 2i, 2i+1 -> dword i (bf16 pair): one packed scaled conversion (scale 1) per pair, exact (e4m3's
+    // 3 mantissa bits and its exponent range fit bf16)
+    auto cv = [](uint32_t w, auto hi) {
+      return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.f, decltype(hi)::value));
     };
-    typedef std::integral_constant<int, 0> b0;
-    typedef std::integral_constant<int, 1> b1;
-    typedef std::integral_constant<int, 2> b2;
-    typedef std::integral_constant<int, 3> b3;
-    return u32x4{(b(r.x, b0{}) >> 16) | (b(r.x, b1{}) & 0xFFFF0000u), (b(r.x, b2{}) >> 16) | (b(r.x, b3{}) & 0xFFFF0000u),
-                 (b(r.y, b0{}) >> 16) | (b(r.y, b1{}) & 0xFFFF0000u), (b(r.y, b2{}) >> 16) | (b(r.y, b3{}) & 0xFFFF0000u)};
+    typedef std::integral_constant<bool, false> lo_w;
+    typedef std::integral_constant<bool, true> hi_w;
+    return u32x4{cv(r.x, lo_w{}), cv(r.x, hi_w{}), cv(r.y, lo_w{}), cv(r.y, hi_w{})};
   }
 };
 // 4 values -> the cache (fp8: saturated to +-448, the e4m3 range)

@@ -218,7 +218,10 @@ class Engine:
             self.dense_bytes = model.expand_dense(None if dense == "1" else int(0.60 * free),
                                                   experts=os.environ.get("NLS_DENSE_EXPERTS", "0") == "1")
         if num_blocks is None:
+            # every row at full context, plus the admission watermark (below) on top: a pool sized to the
+            # worst case never preempts
             num_blocks = self.max_batch * self.max_blocks
+            num_blocks += num_blocks // 99 + 1
             if self.dev.type == "cuda":
                 esz = torch.finfo(getattr(model, "kv_dtype", torch.bfloat16)).bits // 8
                 per_block = 2 * self.cfg.n_layer * block_size * model.Hkv * model.D * esz
