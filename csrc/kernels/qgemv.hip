@@ -12,6 +12,9 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
 namespace nls_hg8 {
 int launch_dense8(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
 }
+namespace nls_hg10 {
+int launch_dense10(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
+}
 namespace nls_q9 {
 int launch_q9(int kset, int waves, int rt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
               hipStream_t st);
@@ -54,6 +57,8 @@ struct NlsFuse {
 // mode 8: dense f16 GEMM with a 5-deep 32-k stage ring and register-double-buffered fragments
 //         (hgemm8.hip): 256-row activation blocks x 32*rt weight rows (rt 8: 256, 7: 224, 4: 128),
 //         plain rows only (no row maps), optional split-K as mode 1.
+// mode 10: dense f16 GEMM, 256 x 256 tiles, 4 phases per 64-deep K-tile with the two wave groups staggered
+//         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
 // mode 9: quantised GEMM on the raw tile-blocks (qgemm9.hip; Q4_K/Q5_K/Q6_K/Q8_0/Q51): 256-row activation
 //         blocks x 16*waves*rt weight rows ((waves, rt) = (4, 2) | (8, 2) | (8, 1)), the mode-8
 //         epilogues, optional split-K.
@@ -92,8 +97,14 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       if (segs[i].rows != segs[0].rows || segs[i].K != segs[0].K) return -1;
   }
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
-  if (mode < 0 || mode > 9 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
-  if (mode == 9) {
+  if (mode < 0 || mode > 10 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode == 10) {
+    if (waves != 8 || fz->xf || fz->onw || epi == EPI_ROPE || ldx % 8 ||
+        ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
+      return -1;
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
+  } else if (mode == 9) {
     if (!((waves == 4 && rt == 2) || (waves == 8 && (rt == 2 || rt == 1))) || fz->xf || fz->onw || epi == EPI_ROPE || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
@@ -123,7 +134,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 9 ? 16 * waves * rt : mode == 8 ? 32 * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = mode == 10 ? 256 : mode == 9 ? 16 * waves * rt : mode == 8 ? 32 * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -211,7 +222,9 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0) {
     if (ks < 1) ks = 1;
     int rc;
-    if (mode == 9)
+    if (mode == 10)
+      rc = nls_hg10::launch_dense10(sl, tiles, ks, (float*)ws, a, st);
+    else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 8)
       rc = nls_hg8::launch_dense8(32 * rt, sl, tiles, ks, (float*)ws, a, st);

@@ -34,6 +34,11 @@ def table():
         if os.path.exists(_PATH):
             with open(_PATH) as f:
                 _TABLE = {k: tuple(v) for k, v in json.load(f).items()}
+        # A/B overrides without editing the table: NLS_TUNING_EXTRA='{"<key>": [..], ...}' (an entry of
+        # [0] under an "L:" key removes a library-GEMM selection)
+        extra = os.environ.get("NLS_TUNING_EXTRA")
+        if extra:
+            _TABLE.update({k: tuple(v) for k, v in json.loads(extra).items()})
     return _TABLE
 
 

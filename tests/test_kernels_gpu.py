@@ -987,6 +987,65 @@ def test_hgemm8_swiglu_multiseg(gpu, rt, ks):
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
 
 
+@pytest.mark.parametrize("M,ks", [(512, 1), (333, 1), (100, 2), (256, 3), (1024, 1), (64, 4)])
+def test_hgemm10_dense(gpu, M, ks):
+    """Mode 10 (hgemm10.hip: 256 x 256 tiles, 4 phases per 64-deep K-tile, the two wave groups staggered by
+    a barrier, one LDS-DMA unit per phase under a counted vmcnt): partial last weight tile (264 rows),
+    partial / multiple activation blocks, k-slices of 1..12 K-tiles (the clamped tail units), split-K
+    through the slab reduce; f32 store with arg-max keys, residual add with alpha."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, GGMLType.Q4_K, gpu)
+    w.expand_dense()
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=10, waves=8, rt=1, ks=ks, argmax=keys if ks == 1 else None)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    if M < pad:
+        assert float(y[M:].abs().max().cpu()) == 0.0
+    if ks == 1:
+        ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+        ops.argmax_unpack(keys, M, ids)
+        assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=10, waves=8, rt=1, ks=ks)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+    y3 = torch.zeros(pad, rows, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y3, M, mode=8, waves=8, rt=8, ks=1)
+    _close(y3[:M], y[:M], 1e-3)
+
+
+@pytest.mark.parametrize("ks", [1, 2])
+def test_hgemm10_swiglu_multiseg(gpu, ks):
+    """Mode 10 SwiGLU epilogue (interleaved gate/up rows: partner lane ^ 32) and a Q|K|V-style launch."""
+    K, F = 512, 256
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    w.expand_dense()
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 333
+    x = _x(M, K, gpu)
+    xf = x[:M].float().cpu()
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=10, waves=8, rt=1, ks=ks)
+    _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(256, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(256, K, GGMLType.Q6_K, gpu, 3)
+    for q in (a, b, c):
+        q.expand_dense()
+    segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 512)]
+    yq = torch.zeros(x.shape[0], 768, device=gpu)
+    ops.qgemv(segs, x, yq, M, mode=10, waves=8, rt=1, ks=ks)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+
+
 Q9_TYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.Q4_0, GGMLType.Q5_1, GGMLType.Q3_K]
 
 

@@ -3,10 +3,12 @@
 // Llama-3-8B gate|up shape over rotating weight copies (weights stream from HBM as in decode).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DH8_PROBE=1 tools/hg8_probe.hip -o /tmp/p1
 //   ./p1 [M=512] [bn=224] [rows=28672] [K=4096] [epi=3] [ks=1] [type=1]
-// type 1 = the f16 mode-8 kernel (bn 256/224/128); 12 / 14 = Q4_K / Q6_K tile-blocks through mode 9
+// type 1 = the f16 mode-8 kernel (bn 256/224/128), 10 = the f16 mode-10 kernel (256 x 256 tiles);
+// 12 / 14 = Q4_K / Q6_K tile-blocks through mode 9
 // (bn 256/128; -DH9_PROBE=<bits> selects its probe), any byte pattern (timing only)
 #include "../csrc/kernels/hgemm8.hip"
 #include "../csrc/kernels/qgemm9.hip"
+#include "../csrc/kernels/hgemm10.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -25,7 +27,7 @@ int main(int argc, char** argv) {
   const int qt = argc > 7 ? atoi(argv[7]) : 1;
   const int q9w = argc > 8 ? atoi(argv[8]) : 4;   // mode-9 waves (4 | 8)
   if (rows % bn || K % 32 || M <= 0) { printf("bad shape\n"); return 1; }
-  const size_t wbytes = qt == 1 ? (size_t)rows * K * 2
+  const size_t wbytes = (qt == 1 || qt == 10) ? (size_t)rows * K * 2
                                 : (size_t)(rows / 16) * (K / 256) * (qt == 12 ? 2304 : 3360);
   const int ncopy = (int)std::max<size_t>(1, ((size_t)1 << 30) / wbytes + 1);
   std::vector<void*> W(ncopy);
@@ -38,7 +40,7 @@ int main(int argc, char** argv) {
   if (ks > 1) CK(hipMalloc(&ws, (size_t)ks * M * rows * 4));
   nls_gemv::SegList sl{};
   sl.nseg = 1;
-  sl.s[0].type = qt;
+  sl.s[0].type = qt == 10 ? QT_F16 : qt;
   sl.s[0].rows = rows;
   sl.s[0].K = K;
   nls_gemv::GemvArgs a{};
@@ -55,7 +57,8 @@ int main(int argc, char** argv) {
   CK(hipStreamCreate(&st));
   auto run = [&](int i) {
     sl.s[0].w = (const uint8_t*)W[i % ncopy];
-    const int rc = qt == 1 ? nls_hg8::launch_dense8(bn, sl, rows / bn, ks, (float*)ws, a, st)
+    const int rc = qt == 10 ? nls_hg10::launch_dense10(sl, rows / 256, ks, (float*)ws, a, st)
+                 : qt == 1 ? nls_hg8::launch_dense8(bn, sl, rows / bn, ks, (float*)ws, a, st)
                            : nls_q9::launch_q9(0, q9w, bn / 16 / q9w, sl, rows / bn, ks, (float*)ws, a, st);
     if (rc) { printf("launch failed\n"); exit(1); }
   };
