@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--cands", default="8:1,8:2,8:4,7:1,7:2,4:1,4:2,4:4,8:8,4:8")
     ap.add_argument("--cands9", default="8:2:1,8:2:2,8:2:4,8:2:8,8:1:1,8:1:2,8:1:4,4:2:1,4:2:2,4:2:4")
+    ap.add_argument("--cands10", default="1,2,3,4,6,8", help="mode-10 split-K candidates")
     ap.add_argument("--types", default="", help="override the weight format of every shape (e.g. 14 = Q6_K)")
     ap.add_argument("--emit", action="store_true")
     a = ap.parse_args()
@@ -70,6 +71,7 @@ def main():
             "lm_head": ([(14, spec.vocab)], d, "argmax")}
     cands = [tuple(int(v) for v in c.split(":")) for c in a.cands.split(",") if c]
     cands9 = [tuple(int(v) for v in c.split(":")) for c in a.cands9.split(",") if c]
+    cands10 = [int(c) for c in a.cands10.split(",") if c]
     if a.types:
         defs = {k: ([(int(a.types), r) for _, r in sd], K, e) for k, (sd, K, e) in defs.items()}
     dev = torch.device("cuda:0")
@@ -157,12 +159,25 @@ def main():
                     continue
                 if best9 is None or t < best9[0]:
                     best9 = (t, cfg)
+            best10 = None
+            for ks in cands10:
+                if epi == "argmax" and ks > 1:
+                    continue
+                cfg = (10, 8, 1, ks)
+                try:
+                    t = timed(graph_of(launch(cfg)), a.rounds)
+                except Exception as e:
+                    print(f"  m10 {cfg} failed: {e}")
+                    continue
+                if best10 is None or t < best10[0]:
+                    best10 = (t, cfg)
             # correctness of the winner (plain f32 output vs the library's product)
             t8, cfg8 = best
             yy = torch.zeros(max(M, 64), col, device=dev)
             ops.qgemv(segs, x, yy, M, mode=8, waves=8, rt=cfg8[2], ks=cfg8[3])
             torch.mm(x[:M], wcat[0].t(), out=lib_out[:M])
             rel = float((yy[:M] - lib_out[:M].float()).abs().max() / (lib_out[:M].float().abs().max() + 1e-6))
+            t10, cfg10 = best10 if best10 is not None else (float("nan"), None)
             t9, cfg9, rel9 = float("nan"), None, float("nan")
             if best9 is not None:
                 t9, cfg9 = best9
@@ -172,10 +187,11 @@ def main():
             print(f"{name:8s} M={M:5d} lib {t_lib:8.2f}us {flop / t_lib / 1e6:7.1f}TF | prod{prod} {t_prod:8.2f}us | "
                   f"m8{cfg8} {t8:8.2f}us {flop / t8 / 1e6:7.1f}TF | m8/lib {t8 / t_lib:5.2f} m8/prod {t8 / t_prod:5.2f} "
                   f"| maxrel {rel:.1e} | m9{cfg9} {t9:8.2f}us {flop / t9 / 1e6:7.1f}TF m9/lib {t9 / t_lib:5.2f} "
-                  f"maxrel {rel9:.1e}", flush=True)
+                  f"maxrel {rel9:.1e} | m10{cfg10} {t10:8.2f}us {flop / t10 / 1e6:7.1f}TF m10/lib {t10 / t_lib:5.2f} "
+                  f"m10/prod {t10 / t_prod:5.2f}", flush=True)
             emit[f"{name}:{M}"] = dict(cfg=list(cfg8), us=round(t8, 2), lib_us=round(t_lib, 2), prod=list(prod),
                                        prod_us=round(t_prod, 2), cfg9=list(cfg9) if cfg9 else None,
-                                       us9=round(t9, 2))
+                                       us9=round(t9, 2), cfg10=list(cfg10) if cfg10 else None, us10=round(t10, 2))
     if a.emit:
         print(json.dumps(emit))
 
