@@ -978,6 +978,11 @@ class Engine:
             if (Bp, False) not in self.graphs:
                 self._ctrl(_OP_CAPTURE, Bp, 0, False, [], 0, None, 0)
                 self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv))
+            # the in-graph sampling variant too: captured lazily, it stalls the first sampled burst at
+            # every bucket (an eager step + capture + two device syncs each, ~0.2-0.4 s over a 512-request
+            # ramp). Padded rows have ctx 0 and every row's params are greedy here: no history writes.
+            if self.device_sampling and (Bp, False, True) not in self.graphs:
+                self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv), dsamp=True)
 
     # ------------------------------------------------------------------ completion
     def _append(self, s: _Seq, t: int):

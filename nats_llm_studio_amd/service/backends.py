@@ -11,6 +11,7 @@ under data.response, `/root/reference/nats_llm_studio.go:356-363`).
 from __future__ import annotations
 
 import collections
+import os
 import threading
 import time
 import uuid
@@ -157,6 +158,8 @@ class EngineBackend:
         eos = tok.tokens[tok.eos_id] if tok.eos_id is not None else ""
         eng = Engine(model, tok, max_batch=self.cfg.max_batch, ctx=self.cfg.max_ctx or None,
                      kv_mem_fraction=self.cfg.kv_mem_fraction, max_prefill_tokens=self.cfg.max_prefill_tokens)
+        if eng.use_graphs and os.environ.get("NLS_CAPTURE_AT_LOAD", "1") == "1":
+            eng.capture_all()      # every decode bucket's graphs now, not inside the first request burst
         if start:
             eng.start()
         return {"engine": eng, "tok": tok, "tmpl": ChatTemplate(tmpl, bos, eos), "entry": entry,
