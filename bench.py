@@ -439,9 +439,19 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
         "weights_gb_per_rank": info["weights_gb"],
         "comm": info["comm_stats"],
         "timings_s": info["timings"],
+        "kernels_built_from_sources": _kernels_current(),
         **info["extra"],
     }
     print(json.dumps(out), flush=True)
+
+
+def _kernels_current():
+    """Whether _kernels.so carries the content stamp of this tree's kernel sources (build.py)."""
+    try:
+        from nats_llm_studio_amd import build
+        return build.kernels_current()
+    except Exception:
+        return None
 
 
 if __name__ == "__main__":

@@ -24,12 +24,14 @@ namespace {
 constexpr float LOG2E = 1.4426950408889634f;
 
 // Keys per flash-decoding split. chunk > 0: fixed; chunk < 0: balanced over n_split with at least
-// -chunk keys; chunk == 0: balanced with at least 64 keys below 1024 of context and 128 above (batch-1
-// A/B, profiles/attn_split_policy_b1.txt: 64-key splits win on short contexts, where the split's
-// dependent K/V fetch chain dominates; 128-key splits at 1K-4K, where the merge of many partials does)
-__device__ __forceinline__ int split_chunk(int chunk, int ctx, int n_split, int bs) {
+// -chunk keys; chunk == 0: balanced with at least 64 keys below 1K of context, 128 at 1K-2K and 256 above
+// (batch-1 A/B, profiles/attn_split_policy_b1.txt: 64-key splits win on short contexts, where the split's
+// dependent K/V fetch chain dominates; 128-256-key splits at 1K-4K, where the merge of many partials does).
+// With up to 64 splits at batch 1 (models/llama.py _SPLIT_CAP), 8K-32K contexts get 32-64 splits of
+// 256-512 keys: 512 workgroups keep enough K/V in flight to stream the cache at HBM rate.
+__device__ __forceinline__ int split_chunk(int chunk, int ctx, int n_split, int bs, int short_min = 64) {
   if (chunk > 0) return chunk;
-  const int mn = chunk ? -chunk : (ctx >= 1024 ? 128 : 64);
+  const int mn = chunk ? -chunk : (ctx >= 2048 ? 256 : (ctx >= 1024 ? 128 : short_min));
   return max(mn, ((ctx + n_split - 1) / n_split + bs - 1) / bs * bs);
 }
 
@@ -275,10 +277,10 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_kernel(
 template <int D>
 __global__ void attn_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
                                     const int* __restrict__ ctx_len, int Hq, int n_split, int chunk, int bs,
-                                    act_t* __restrict__ out, long ldo) {
+                                    act_t* __restrict__ out, long ldo, int short_min = 64) {
   const int t = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
   const int ctx = ctx_len[t];
-  chunk = split_chunk(chunk, ctx, n_split, bs);
+  chunk = split_chunk(chunk, ctx, n_split, bs, short_min);
   const int na = min(n_split, (ctx + chunk - 1) / chunk);   // active splits (others never wrote)
   const size_t pb = ((size_t)t * Hq + h) * n_split;
   float M = -INFINITY;
@@ -315,6 +317,59 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o, const floa
 // in flight while the current ones are computed. Splits and the fused combine as the VALU kernel.
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// Merge of the na (<= 64) flash-decoding partials of (token t, kv head kh), run by the last split to
+// finish, with every thread busy and no per-split round trip in series: one wave per head reduces the
+// splits' (m, l) across its lanes into per-split weights f_s = 2^(m_s - M) / L (LDS), then each thread
+// sums f_s * O_s for 4 dims of a head over a share of the splits (16-byte loads, all independent) and
+// the shares are added through LDS. smem: >= 16 * 64 + 64 * WAVES * 4 floats.
+template <int WAVES>
+DEVI void merge_splits(const float* __restrict__ part_o, const float* __restrict__ part_ml, int t, int kh, int G,
+                       int Hq, int n_split, int na, act_t* __restrict__ out, long ldo, float* smem) {
+  constexpr int D = 128, NT = 64 * WAVES;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* f = smem;                                   // [16 heads][64 splits]
+  f32x4* red = reinterpret_cast<f32x4*>(smem + 16 * 64);   // [NT] partial sums
+  for (int h = wave; h < G; h += WAVES) {
+    const size_t pb = ((size_t)t * Hq + kh * G + h) * n_split;
+    const float ms = lane < na ? part_ml[2 * (pb + lane)] : -INFINITY;
+    const float ls = lane < na ? part_ml[2 * (pb + lane) + 1] : 0.f;
+    float M = ms;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
+    float L = w * ls;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
+    f[h * 64 + lane] = L > 0.f ? w / L : 0.f;
+  }
+  __syncthreads();
+  const int items = G * (D / 4);                     // (head, 4 dims)
+  const int parts = items >= NT ? 1 : NT / items;    // split shares per item
+  for (int i0 = 0; i0 < items; i0 += NT) {
+    const int it = i0 + threadIdx.x % min(items, NT), pt = threadIdx.x / min(items, NT);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (it < items && pt < parts) {
+      const int h = it / (D / 4), d4 = it % (D / 4);
+      const size_t pb = ((size_t)t * Hq + kh * G + h) * n_split;
+      const float* fw = f + h * 64;
+#pragma unroll 4
+      for (int s2 = pt; s2 < na; s2 += parts)
+        acc += fw[s2] * *reinterpret_cast<const f32x4*>(part_o + (pb + s2) * D + 4 * d4);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (pt == 0 && it < items) {
+      for (int p2 = 1; p2 < parts; ++p2) acc += red[threadIdx.x + p2 * min(items, NT)];
+      const int h = it / (D / 4), d4 = it % (D / 4);
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<h4*>(out + (size_t)t * ldo + (size_t)(kh * G + h) * D + 4 * d4) =
+          h4{(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
+    }
+    __syncthreads();
+  }
+}
+
+
 template <typename KV, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
     const __bf16* __restrict__ q, long ldq, const KV* __restrict__ kc, const KV* __restrict__ vc,
@@ -332,10 +387,14 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   uint8_t (*Vs)[KG * D * 2] = Vsm[wave];
   const int Hq = Hkv * G;
   const int ctx = ctx_len[t];
-  chunk = split_chunk(chunk, ctx, n_split, bs);
+  // short contexts: at least one 32-key group per wave of the workgroup per split (>= 64 keys)
+  chunk = split_chunk(chunk, ctx, n_split, bs, KG * WAVES > 64 ? KG * WAVES : 64);
   const int start = split * chunk;
   if (n_split > 1 && start >= ctx && ctx > 0) return;       // inactive split: combine skips it
   const int end = min(ctx, start + chunk);
+  // active splits: with ONE (short context) the split writes the output itself -- no partials, no ticket
+  const int na = ctx > 0 ? min(n_split, (ctx + chunk - 1) / chunk) : n_split;
+  const bool direct = n_split == 1 || (na == 1 && cnt);
   const int* bt = block_tables + (size_t)tok_seq[t] * bt_stride;
   const float sl2 = scale * LOG2E;
 
@@ -350,9 +409,35 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   for (int c = 0; c < NDT; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
-  auto kv_row = [&](int p) -> size_t {       // element offset of key p's row for this kv head
+  // Block-table entries come from a register window (lane i holds entry b0 + 64 * win + i, refreshed once
+  // per 64 blocks), broadcast per 32-key group as wave-uniform values: the K/V loads of a group no
+  // longer wait on a dependent block-table fetch (the chain that bound long contexts at small batch).
+  // A group [base, base + 32) touches blocks base / bs .. (base + 31) / bs: at most NGB of them.
+  constexpr int NGB = 4;                       // bs >= 16 (host-checked): <= 3 blocks per group
+  const int b0 = start / bs;
+  int btw = -1, btreg = 0;
+  int gblk[NGB] = {0, 0, 0, 0};
+  auto group_blocks = [&](int base) __attribute__((always_inline)) {
+    const int bi0 = base / bs - b0;
+    const int nbg = (min(base + KG, end) - 1) / bs - base / bs + 1;     // blocks this group touches
+    const int win = bi0 >> 6;
+    if (win != btw) {
+      btw = win;
+      const int e = b0 + win * 64 + lane;
+      btreg = e * bs < end ? bt[e] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NGB; ++i) {
+      const int bi = bi0 + i;
+      // (a block past the register window: one wave-uniform direct read)
+      if (i < nbg) gblk[i] = (bi >> 6) == win ? __builtin_amdgcn_readlane(btreg, bi & 63) : bt[b0 + bi];
+    }
+  };
+  auto kv_row = [&](int p, int base) -> size_t {       // element offset of key p's row for this kv head
     const int pc = min(p, end - 1);
-    return ((size_t)((long)bt[pc / bs] * bs + pc % bs) * Hkv + kh) * D;
+    const int lb = pc / bs - base / bs;                // 0 .. NGB - 1
+    const int blk = lb == 0 ? gblk[0] : (lb == 1 ? gblk[1] : (lb == 2 ? gblk[2] : gblk[3]));
+    return ((size_t)((long)blk * bs + pc % bs) * Hkv + kh) * D;
   };
   // swizzled byte offset of 16-byte chunk ch of V row `row` (256-byte rows): conflict-free for the
   // transposed reads and the row writes (cdna_hip_programming.md T10, layout (b))
@@ -360,14 +445,15 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   // K of 32 keys: [n-tile][k-step]; V of 32 keys: 8 rows-of-4 per lane (row = 4i + lane / 16, chunk lane % 16)
   typename R::raw kr[2][NKK], vr[8];
   auto load = [&](int base, typename R::raw (&K)[2][NKK], typename R::raw (&V)[8]) __attribute__((always_inline)) {
+    group_blocks(base);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-      const size_t o0 = kv_row(base + 16 * nt + r);
+      const size_t o0 = kv_row(base + 16 * nt + r, base);
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) K[nt][kk] = R::ld(kc + o0 + kk * 32 + 8 * g);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) V[i] = R::ld(vc + kv_row(base + 4 * i + (lane >> 4)) + 8 * (lane & 15));
+    for (int i = 0; i < 8; ++i) V[i] = R::ld(vc + kv_row(base + 4 * i + (lane >> 4), base) + 8 * (lane & 15));
   };
   auto store_v = [&](int buf, typename R::raw (&V)[8]) __attribute__((always_inline)) {
 #pragma unroll
@@ -477,7 +563,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
         O += ob[((size_t)w * 16 + h) * D + d] * f;
       }
       const int qh2 = kh * G + h;
-      if (n_split == 1) {
+      if (direct) {
         out[(size_t)t * ldo + (size_t)qh2 * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
       } else {
         const size_t pi = ((size_t)t * Hq + qh2) * n_split + split;
@@ -488,10 +574,10 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
         }
       }
     }
-    if (n_split == 1) return;
+    if (direct) return;
   } else {
     const int qh = kh * G + r;
-    if (n_split == 1) {
+    if (direct) {
       if (r < G) {
         const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
@@ -516,7 +602,6 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   }
   if (!cnt) return;
   // fused combine: the last active split of (token, kv head) to arrive merges them (as the VALU kernel)
-  const int na = ctx > 0 ? min(n_split, (ctx + chunk - 1) / chunk) : n_split;
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -534,24 +619,8 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   }
   __syncthreads();
   if (!last) return;
-  for (int e = threadIdx.x; e < G * D; e += 64 * WAVES) {
-    const int h = e / D, d = e - h * D;
-    const int qh2 = kh * G + h;
-    const size_t pb0 = ((size_t)t * Hq + qh2) * n_split;
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < na; ++s2) M = fmaxf(M, part_ml[2 * (pb0 + s2)]);
-    float L = 0.f, O = 0.f;
-    if (M != -INFINITY) {
-      for (int s2 = 0; s2 < na; ++s2) {
-        const float ms = part_ml[2 * (pb0 + s2)];
-        if (ms == -INFINITY) continue;
-        const float f = exp2f(ms - M);
-        L += part_ml[2 * (pb0 + s2) + 1] * f;
-        O += part_o[(pb0 + s2) * D + d] * f;
-      }
-    }
-    out[(size_t)t * ldo + (size_t)qh2 * D + d] = (act_t)(L > 0.f ? O / L : 0.f);
-  }
+  merge_splits<WAVES>(part_o, part_ml, t, kh, G, Hq, n_split, na, out, ldo,
+                      reinterpret_cast<float*>(&Vsm[0][0][0]));
 }
 
 template <int D, int G>
@@ -589,7 +658,7 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   // else four waves splitting the workgroup's keys (more K/V in flight per (token, kv head, split): long
   // contexts at small batch). NLS_ATTN_MFMA=0 keeps the VALU kernel.
   static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
-  if (D == 128 && G <= 16 && mf != 0) {
+  if (D == 128 && G <= 16 && mf != 0 && block_size >= 16 && n_split <= 64) {
     const bool big = (long)T * Hkv * n_split >= 1024;
 #define NLS_ATTN_M(KVT, W)                                                                                     \
   hipLaunchKernelGGL((attn_decode_mfma_kernel<KVT, W>), grid, dim3(64 * W), 0, st, (const __bf16*)q, ldq,       \
@@ -601,9 +670,9 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
       if (big) NLS_ATTN_M(__bf16, 1); else NLS_ATTN_M(__bf16, 4);
     }
 #undef NLS_ATTN_M
-    if (n_split > 1 && !cnt)
+    if (n_split > 1 && !cnt)      // (the short-context split size of the launched variant)
       hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
-                         n_split, chunk, block_size, (act_t*)out, ldo);
+                         n_split, chunk, block_size, (act_t*)out, ldo, big ? 64 : 128);
     return (int)hipGetLastError();
   }
   // waves per workgroup: 8 (twice the keys in flight per step) while the grid is small -- batch 1 / 16 at

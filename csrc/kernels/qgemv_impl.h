@@ -145,6 +145,95 @@ DEVI unsigned long long argmax_key(float v, int idx) {
 // the GEMM epilogues). exp(-g) = inf for g << 0 gives g * 0 = -0.
 DEVI float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
+
+// Batch-1 activation staging of the XL paths in two halves. xpre() issues every load of the row -- the
+// f16 input row, or for a fused input RMSNorm the f32 residual row, the norm weights and the producer's
+// sum-of-squares shares -- into registers BEFORE the weight prologue; xput() writes the (normalised)
+// row to LDS after it. Loads retire in issue order (in-order vmcnt), so a staging load issued after the
+// weight prologue makes the staging wait for the weights, and the loop-carried share / row reads of
+// the general path cost several dependent L2 round trips on the critical path (why folding the norms
+// into the GEMVs measured neutral in round 2). One row (batch-1 decode) only; false: general path.
+struct XPre {
+  static constexpr int NX = 8;      // 16-byte chunks per thread (fused norm: NX/2 of x, NX/2 of weights)
+  u32x4 v[NX];
+  float sh[2];
+  int nj;
+};
+
+template <int NT>
+DEVI bool xpre(XPre& p, const GemvArgs& a, int M, int K, int k0, int kn) {
+  constexpr int NX = XPre::NX;
+  const int tid = threadIdx.x;
+  if (M != 1) return false;
+  if (!a.xf) {
+    const int nch = kn >> 3;
+    if (nch > NX * NT) return false;
+    p.nj = (nch + NT - 1) / NT;
+#pragma unroll
+    for (int j = 0; j < NX; ++j)
+      if (j < p.nj) p.v[j] = ld16(a.x + k0 + min(tid + j * NT, nch - 1) * 8);
+    return true;
+  }
+  const int nch = kn >> 2;
+  if (nch > (NX / 2) * NT || (a.ssq_in ? a.nss_in > 2 * NT : kn != K)) return false;
+  p.nj = (nch + NT - 1) / NT;
+#pragma unroll
+  for (int j = 0; j < NX / 2; ++j)
+    if (j < p.nj) {
+      const int c = min(tid + j * NT, nch - 1);
+      p.v[j] = ld16(a.xf + k0 + c * 4);
+      p.v[NX / 2 + j] = ld16(a.nw + k0 + c * 4);
+    }
+  if (a.ssq_in) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) p.sh[i] = a.ssq_in[min(tid + i * NT, a.nss_in - 1)];
+  }
+  return true;
+}
+
+// the second half: `off(k)` = LDS element offset of slice element k (a multiple of 4); red: NT/64 floats
+template <int NT, typename Off>
+DEVI void xput(const XPre& p, const GemvArgs& a, int K, int kn, act_t* xs, float* red, Off off) {
+  constexpr int NX = XPre::NX;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!a.xf) {
+    const int nch = kn >> 3;
+#pragma unroll
+    for (int j = 0; j < NX; ++j)
+      if (j < p.nj && tid + j * NT < nch) *reinterpret_cast<u32x4*>(xs + off((tid + j * NT) * 8)) = p.v[j];
+    return;
+  }
+  const int nch = kn >> 2;
+  float ss = 0.f;
+  if (a.ssq_in) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ss += tid + i * NT < a.nss_in ? p.sh[i] : 0.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < NX / 2; ++j)
+      if (j < p.nj && tid + j * NT < nch) {
+        const float4 v = __builtin_bit_cast(float4, p.v[j]);
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (lane == 0) red[wave] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) tot += red[w];
+  const float inv = rsqrtf(tot / (float)K + a.eps);
+  typedef act_t act4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < NX / 2; ++j)
+    if (j < p.nj && tid + j * NT < nch) {
+      const float4 v = __builtin_bit_cast(float4, p.v[j]), w = __builtin_bit_cast(float4, p.v[NX / 2 + j]);
+      *reinterpret_cast<act4*>(xs + off((tid + j * NT) * 4)) =
+          act4{(act_t)(v.x * inv * w.x), (act_t)(v.y * inv * w.y), (act_t)(v.z * inv * w.z), (act_t)(v.w * inv * w.w)};
+    }
+}
+
 // XL: the activation rows are first staged into LDS (batch <= a few rows, no row maps), so the
 // main loop's x reads are ds_reads and the VMEM queue holds only the weight stream: its in-order
 // vmcnt waits then never drain the DEPTH-deep weight prefetch (global x loads issued each step
@@ -184,6 +273,9 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   // conditional load breaks hipcc's vmcnt bookkeeping at the join and it falls back to
   // vmcnt(0). The clamped tail reloads hit L2 and are never consumed.
   const int sbl = max(sb1 - 1, sb0);
+  XPre xp;
+  bool xfast = false;
+  if constexpr (XL) xfast = xpre<WAVES * 64>(xp, a, mcount, S.K, 0, S.K);
   if (sb0 < sb1) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
@@ -206,7 +298,9 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   const act_t* xr[MT];
   if constexpr (XL) {
     act_t* xs = reinterpret_cast<act_t*>(lds + (WAVES + 1) * RT * MT * 256);
-    if (a.xf) {
+    if (xfast) {
+      xput<WAVES * 64>(xp, a, S.K, S.K, xs, lds, [](int k) { return k; });
+    } else if (a.xf) {
       // fused RMSNorm of the residual rows (the decode-time `rmsnorm` launch folded into the GEMV
       // that consumes it: every workgroup normalises the few rows itself, reading them from L2)
       const int K = S.K;
@@ -549,7 +643,9 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     constexpr int DEPTH = RT == 1 ? (sizeof(Raw) <= 48 ? XL_DEPTH : (sizeof(Raw) <= 80 ? 4 : 2)) : 2;
     Raw wb[DEPTH][RT];
     const int sbl = max(sb1 - 1, sb0);
-    if (sb0 < sb1) {      // weight prologue first: the x staging below overlaps its latency
+    XPre xp;              // batch 1: the x slice's loads go out first (xpre), the weight prologue after them
+    const bool xfast = xpre<NT>(xp, a, M, S.K, sb0 * 256, (sb1 - sb0) * 256);
+    if (sb0 < sb1) {      // weight prologue: the x staging below overlaps its latency
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d)
 #pragma unroll
@@ -557,7 +653,10 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     }
     // x slice -> LDS [sb - sb0][M][256] (XOR-swizzled 16-B chunks)
     const int kc = (sb1 - sb0) * 32;
-    if (a.xf) {
+    if (xfast) {
+      xput<NT>(xp, a, S.K, (sb1 - sb0) * 256, lds, reinterpret_cast<float*>(lds + (size_t)M * kc * 8),
+               [M](int k) { return (k >> 8) * M * 256 + lds_off(0, k & 255); });
+    } else if (a.xf) {
       // fused input RMSNorm from the producer's partial sums of squares (the slice may be a
       // split-K part of the row; the norm needs the whole row: launch_b requires ssq_in here)
       float* inv = reinterpret_cast<float*>(lds + (size_t)M * kc * 8);

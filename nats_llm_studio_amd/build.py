@@ -8,6 +8,8 @@
 from __future__ import annotations
 
 import glob
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -19,11 +21,47 @@ CSRC = os.path.join(ROOT, "csrc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 
-def _stale(out: str, srcs) -> bool:
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(s) > t for s in srcs)
+def source_hash(srcs, flags=()) -> str:
+    """sha256 over the sources' names + contents and the compile flags: what a built library is
+    stamped with (`<lib>.srchash`), so staleness is decided by content, not by file times (a fresh
+    checkout or a copied tree has arbitrary mtimes)."""
+    h = hashlib.sha256()
+    for f in sorted(srcs):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
+
+
+def _stamp(out: str) -> str:
+    return out + ".srchash"
+
+
+def read_stamp(out: str):
+    try:
+        with open(_stamp(out)) as f:
+            return json.load(f).get("hash")
+    except (OSError, ValueError):
+        return None
+
+
+def _stale(out: str, srcs, flags=()) -> bool:
+    return not os.path.exists(out) or read_stamp(out) != source_hash(srcs, flags)
+
+
+def _write_stamp(out: str, srcs, flags=()):
+    with open(_stamp(out), "w") as f:
+        json.dump({"hash": source_hash(srcs, flags), "files": sorted(os.path.basename(s) for s in srcs)}, f)
+
+
+def kernel_sources():
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    return srcs, srcs + sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+
+
+def kernel_flags(defines=()):
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", *[f"-D{d}" for d in defines]]
 
 
 def _run(cmd):
@@ -36,23 +74,35 @@ def build_kernels(force: bool = False, defines=(), tag: str = "") -> str:
     `defines` + `tag`: an A/B variant library `_kernels_<tag>.so` (e.g. tools/gemm_ab.py), built in
     its own object directory; the default build is `_kernels.so`."""
     out = os.path.join(PKG, f"_kernels_{tag}.so" if tag else "_kernels.so")
-    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
-    if force or _stale(out, deps):
+    srcs, deps = kernel_sources()
+    flags = kernel_flags(defines)
+    if force or _stale(out, deps, flags):
         from concurrent.futures import ThreadPoolExecutor
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
         bdir = os.path.join(ROOT, "build", f"kernels_{tag}" if tag else "kernels")
         os.makedirs(bdir, exist_ok=True)
-        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-                 *[f"-D{d}" for d in defines]]
+        hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
         objs = [os.path.join(bdir, os.path.basename(s) + ".o") for s in srcs]
-        jobs = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + glob.glob(os.path.join(CSRC, "kernels", "*.h")))]
+        jobs = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + hdrs, flags)]
+
+        def compile_one(so):
+            _run([hipcc, *flags, "-c", so[0], "-o", so[1]])
+            _write_stamp(so[1], [so[0]] + hdrs, flags)
+
         with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
-            list(ex.map(lambda so: _run([hipcc, *flags, "-c", so[0], "-o", so[1]]), jobs))
+            list(ex.map(compile_one, jobs))
         tmp = out + ".tmp"
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp])
         os.replace(tmp, out)
+        _write_stamp(out, deps, flags)
     return out
+
+
+def kernels_current(out: str = None) -> bool:
+    """True when the in-tree `_kernels.so` was built from exactly the current kernel sources."""
+    out = out or os.path.join(PKG, "_kernels.so")
+    srcs, deps = kernel_sources()
+    return os.path.exists(out) and read_stamp(out) == source_hash(deps, kernel_flags())
 
 
 def natscore_path() -> str:
@@ -73,6 +123,7 @@ def build_natscore(force: bool = False) -> str:
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden", *inc, *srcs,
               "-o", tmp, "-lcrypto"])      # libcrypto: ed25519 nkey signatures
         os.replace(tmp, out)
+        _write_stamp(out, deps)
     return out
 
 
@@ -92,6 +143,7 @@ def build_tool(name: str = "nls-nats", src: str = "nls_nats.cpp", extra=(), out_
         _run([cxx, "-O2", "-std=c++17", "-pthread", f"-I{os.path.join(CSRC, 'natscore')}", *extra, *srcs,
               "-o", tmp, "-lcrypto"])
         os.replace(tmp, out)
+        _write_stamp(out, deps)
     return out
 
 

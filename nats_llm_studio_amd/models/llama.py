@@ -29,9 +29,10 @@ from ..ops import QWeight, Seg
 from .config import ModelConfig
 
 
-# flash-decoding splits per (token, kv head): 16 (batch 1 at 4K context 2.94 vs 3.02 ms/token at 32, equal at
-# batch 16 and at short context; profiles/attn_split_cap_4k.txt)
-_SPLIT_CAP = int(os.environ.get("NLS_ATTN_SPLIT_CAP", "16"))
+# flash-decoding splits per (token, kv head): up to 64 (only batch <= 2 reaches it; the kernel's context-adaptive
+# chunk keeps 4K context at 16 x 256 keys, which beat 32 x 128 -- profiles/attn_split_cap_4k.txt -- and gives
+# 8K-32K contexts 32-64 splits; profiles/ctx_sweep_r03_splits.jsonl)
+_SPLIT_CAP = int(os.environ.get("NLS_ATTN_SPLIT_CAP", "64"))
 _SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgroups of a decode attention launch
 # fewest keys per flash-decoding split (0: the kernel's context-adaptive policy, attention.hip
 # split_chunk: 64 keys below 1K of context, 128 above)

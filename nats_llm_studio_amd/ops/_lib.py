@@ -117,6 +117,11 @@ def lib():
             fn.restype = c_int
         if L.nls_fuse_size() != ctypes.sizeof(NlsFuse):
             raise RuntimeError("stale _kernels.so: NlsFuse layout mismatch (rebuild the kernels)")
+        if LIB_PATH.endswith(os.path.join("nats_llm_studio_amd", "_kernels.so")) and not built_from_sources():
+            # the library's content stamp (build.py) does not match the kernel sources of this tree
+            import warnings
+            warnings.warn(f"{LIB_PATH} was not built from the current csrc/kernels sources "
+                          "(run `python -m nats_llm_studio_amd.build`)", RuntimeWarning)
         _lib = L
     return _lib
 
@@ -128,3 +133,9 @@ def check(rc: int, name: str):
 
 def available() -> bool:
     return os.path.exists(LIB_PATH)
+
+
+def built_from_sources() -> bool:
+    """True when `_kernels.so` carries the content hash of this tree's kernel sources (build.py stamp)."""
+    from .. import build
+    return build.kernels_current(LIB_PATH)

@@ -234,7 +234,11 @@ def test_rmsnorm_embed(gpu):
         ids = torch.tensor([0, 49, 7], dtype=torch.int32, device=gpu)
         e = torch.zeros(3, 512, device=gpu)
         ops.embed(ids, qw, e, 3, 2.0)
-        torch.testing.assert_close(e.cpu(), 2.0 * Wd[[0, 49, 7]], rtol=1e-5, atol=1e-6)
+        # Q4_1 / Q5_1 / Q2_K embedding tables are kept as f16 rows (ops/transcode.py device_form, "rows"):
+        # one f16 rounding of the exact value; every other type gathers exactly
+        f16_rows = qw.type == int(GGMLType.F16) and t != GGMLType.F16
+        torch.testing.assert_close(e.cpu(), 2.0 * Wd[[0, 49, 7]], rtol=1e-3 if f16_rows else 1e-5,
+                                   atol=1e-5 if f16_rows else 1e-6)
 
 
 @pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
