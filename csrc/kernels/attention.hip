@@ -379,12 +379,17 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
     int* __restrict__ cnt) {
   constexpr int D = 128, NKK = D / 32, NDT = D / 16, KG = 32;
   typedef KVRaw<KV> R;
-  // per wave: a double-buffered 32-key V tile (2 x 8 KiB); reused for the cross-wave merge at the end
-  __shared__ __attribute__((aligned(16))) uint8_t Vsm[WAVES][2][KG * D * 2];
+  // per wave: one 32-key V tile (8 KiB; a wave's LDS ops run in order, so the next group's V is written
+  // after this group's transposed reads without a second buffer); the space is reused for the cross-wave
+  // merge and the split merge at the end
+  constexpr int VB = WAVES * KG * D * 2, MB = WAVES > 1 ? (2 * WAVES * 16 + WAVES * 16 * D) * 4 : 0,
+                CB = (16 * 64 + 64 * WAVES * 4) * 4;
+  constexpr int SMEM = VB > MB ? (VB > CB ? VB : CB) : (MB > CB ? MB : CB);
+  __shared__ __attribute__((aligned(16))) uint8_t Vsm[SMEM];
   const int t = blockIdx.x, kh = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
   const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t (*Vs)[KG * D * 2] = Vsm[wave];
+  uint8_t* Vs = Vsm + wave * KG * D * 2;
   const int Hq = Hkv * G;
   const int ctx = ctx_len[t];
   // short contexts: at least one 32-key group per wave of the workgroup per split (>= 64 keys)
@@ -458,7 +463,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   auto store_v = [&](int buf, typename R::raw (&V)[8]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      *reinterpret_cast<u32x4*>(Vs[buf] + voff(4 * i + (lane >> 4), lane & 15)) = R::bf16(V[i]);
+      *reinterpret_cast<u32x4*>(Vs + voff(4 * i + (lane >> 4), lane & 15)) = R::bf16(V[i]);
   };
   // wave w takes the 32-key groups w, w + WAVES, ... of the workgroup's range
   const int ngrp_all = end > start ? (end - start + KG - 1) / KG : 0;
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
     m = mn;
     // ---- O^T = O^T * alpha + V^T P^T over the 32 keys; V^T fragment of dim tile c: transposed reads of
     // rows {4g+q} and {16+4g+q}, columns 16c + 4p .. +3 (lane 4q + p of the group supplies the address)
-    const uint8_t* vb = Vs[j & 1];
+    const uint8_t* vb = Vs;
     const int qq = r >> 2, pp = r & 3;
 #pragma unroll
     for (int c = 0; c < NDT; ++c) {
@@ -538,7 +543,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   // space), every thread finishing (head, dim) elements; WAVES == 1: lane (g, r) holds dims 16c + 4g + i of
   // head r in registers
   if constexpr (WAVES > 1) {
-    float* mb = reinterpret_cast<float*>(&Vsm[0][0][0]);            // [WAVES][16] m, [WAVES][16] l
+    float* mb = reinterpret_cast<float*>(Vsm);                      // [WAVES][16] m, [WAVES][16] l
     float* ob = mb + 2 * WAVES * 16;                                  // [WAVES][16 heads][D]
     __syncthreads();                                                  // every wave is done with its V tiles
     if (g == 0) {
@@ -620,7 +625,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   __syncthreads();
   if (!last) return;
   merge_splits<WAVES>(part_o, part_ml, t, kh, G, Hq, n_split, na, out, ldo,
-                      reinterpret_cast<float*>(&Vsm[0][0][0]));
+                      reinterpret_cast<float*>(Vsm));
 }
 
 template <int D, int G>
@@ -660,19 +665,22 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
   if (D == 128 && G <= 16 && mf != 0 && block_size >= 16 && n_split <= 64) {
     const bool big = (long)T * Hkv * n_split >= 1024;
+    // small grids: 8 waves per workgroup (NLS_ATTN_MFMA_WAVES=4 for 4): a 256-key context in one pass, twice
+    // the K/V in flight per split of a long one
+    static const int mw = [] { const char* e = getenv("NLS_ATTN_MFMA_WAVES"); return e && atoi(e) == 4 ? 4 : 8; }();
 #define NLS_ATTN_M(KVT, W)                                                                                     \
   hipLaunchKernelGGL((attn_decode_mfma_kernel<KVT, W>), grid, dim3(64 * W), 0, st, (const __bf16*)q, ldq,       \
                      (const KVT*)kc, (const KVT*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G, block_size, \
                      scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt)
     if (kv8) {
-      if (big) NLS_ATTN_M(uint8_t, 1); else NLS_ATTN_M(uint8_t, 4);
+      if (big) NLS_ATTN_M(uint8_t, 1); else if (mw == 4) NLS_ATTN_M(uint8_t, 4); else NLS_ATTN_M(uint8_t, 8);
     } else {
-      if (big) NLS_ATTN_M(__bf16, 1); else NLS_ATTN_M(__bf16, 4);
+      if (big) NLS_ATTN_M(__bf16, 1); else if (mw == 4) NLS_ATTN_M(__bf16, 4); else NLS_ATTN_M(__bf16, 8);
     }
 #undef NLS_ATTN_M
     if (n_split > 1 && !cnt)      // (the short-context split size of the launched variant)
       hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
-                         n_split, chunk, block_size, (act_t*)out, ldo, big ? 64 : 128);
+                         n_split, chunk, block_size, (act_t*)out, ldo, big ? 64 : 32 * mw);
     return (int)hipGetLastError();
   }
   // waves per workgroup: 8 (twice the keys in flight per step) while the grid is small -- batch 1 / 16 at

@@ -134,10 +134,13 @@ class LlamaModel:
         self.reader = reader
         # RMSNorm folded into the consuming GEMVs for few-row decode steps, split between the O / down
         # GEMVs (per-workgroup shares of sum(x^2)) and the consumers (no norm launch, no reduction pass).
-        # Measured neutral on MI355X at batch 1 (2.24 vs 2.22 ms/token, profiles/b1_split_rmsnorm_ab.txt):
-        # the 65 removed launches come back as latency on the producers' and consumers' critical paths,
-        # so opt-in: NLS_FUSE_NORM=1.
-        self.fuse_norm = bool(int(os.environ.get("NLS_FUSE_NORM", "0"))) if fuse_norm is None else fuse_norm
+        # Round 2 measured it neutral at batch 1 (profiles/b1_split_rmsnorm_ab.txt): the consumers read the
+        # shares and the residual row in loop-carried L2 round trips issued after their weight prologue.
+        # With the one-row staging issued ahead of the weights (qgemv_impl.h xpre / xput) batch 1 gains
+        # (2.11 -> 2.05 ms/token, profiles/b1_latency_r03.txt) while batch 4 still loses, so the default
+        # ("auto") folds the norms at batch 1 only; NLS_FUSE_NORM=1 / 0 forces it on / off.
+        env = os.environ.get("NLS_FUSE_NORM", "auto")
+        self.fuse_norm = (env if env == "auto" else bool(int(env))) if fuse_norm is None else fuse_norm
         self.device = torch.device(device)
         self.cfg = cfg = ModelConfig.from_gguf(reader.metadata, reader.tensors.keys())
         self.shard = shard
@@ -344,6 +347,9 @@ class LlamaModel:
         )
         b.meta = meta
         b.pad = pad
+        # keys hold the reset value (argmax_unpack(rearm=True) leaves them so): the next step skips the reset.
+        # Device keys start zeroed; a CPU buffer starts at zero too, which is not its reset value.
+        b.keys_clean = dev.type == "cuda"
         b.attn_cnt = torch.zeros(pad * self.Hkv, dtype=torch.int32, device=dev)
         if self.shard.size > 1:
             b.part = torch.zeros(pad, cfg.d_model, dtype=torch.float32, device=dev)
@@ -384,9 +390,8 @@ class LlamaModel:
         cfg = self.cfg
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         x = b.x
-        if feed_prev:                          # chained decode: previous step's tokens, on device
-            torch.where(b.use_prev[:T] != 0, b.next_ids[:T], b.ids[:T], out=b.ids[:T])
-        ops.embed(b.ids, self.tok_embd, x, T, cfg.embedding_scale)
+        # chained decode: the previous step's tokens are picked on the device inside the embedding launch
+        ops.embed(b.ids, self.tok_embd, x, T, cfg.embedding_scale, prev=(b.next_ids, b.use_prev) if feed_prev else None)
         need = T * Hq * n_split * (D + 2)
         if n_split > 1 and b.attn_ws.numel() < need:
             # a larger explicit split than the policy's: grow, but keep the old buffer alive -- a graph
@@ -396,7 +401,8 @@ class LlamaModel:
             b.attn_ws = torch.zeros(need, dtype=torch.float32, device=self.device)
         fused = self.shard.size == 1            # row-parallel GEMM + residual + next RMSNorm in one pass
         # few-row decode steps: every RMSNorm is folded into the GEMV that consumes it (no norm launches)
-        fnorm = (self.fuse_norm and fused and not cfg.n_expert and qblocks is None
+        fuse = (T == 1 and x.is_cuda) if self.fuse_norm == "auto" else self.fuse_norm
+        fnorm = (fuse and fused and not cfg.n_expert and qblocks is None
                  and ops.norm_fusable(T, cfg.d_model))
         if fnorm:
             return self._forward_fused_norm(b, kc, vc, T, block_size, n_split, logit_rows, n_logits, need_logits)
@@ -448,12 +454,15 @@ class LlamaModel:
             n = int(n_logits)
             h = b.h.index_select(0, logit_rows[:n].long())
             h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
-        ops.argmax_reset(b.keys)
+        if self.shard.size > 1 or not b.keys_clean:
+            ops.argmax_reset(b.keys)
         # greedy-only steps keep just the fused arg-max keys (no [n, V] logits written)
         ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
                   epi="f32" if need_logits else "argmax")
         if self.shard.size == 1:
-            ops.argmax_unpack(b.keys, n, b.next_ids)
+            # the unpack re-arms the keys it read: the next step's arg-max needs no reset launch
+            ops.argmax_unpack(b.keys, n, b.next_ids, rearm=True)
+            b.keys_clean = b.keys.is_cuda
         else:
             self.comm.vocab_parallel_argmax(b.keys, n, self.vocab_lo, b.next_ids)
         return n
@@ -488,14 +497,17 @@ class LlamaModel:
             n = int(n_logits)
             h = b.h.index_select(0, logit_rows[:n].long())
             h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
-            ops.argmax_reset(b.keys)
+            if not b.keys_clean:
+                ops.argmax_reset(b.keys)
             ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
                       epi="f32" if need_logits else "argmax")
         else:
-            ops.argmax_reset(b.keys)
+            if not b.keys_clean:
+                ops.argmax_reset(b.keys)
             ops.qgemv([Seg(self.lm_head, 0)], b.h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
                       epi="f32" if need_logits else "argmax", norm=nrm(self.out_norm, parts))
-        ops.argmax_unpack(b.keys, n, b.next_ids)
+        ops.argmax_unpack(b.keys, n, b.next_ids, rearm=True)
+        b.keys_clean = b.keys.is_cuda
         return n
 
     def _row_parallel(self, w: QWeight, xin: torch.Tensor, resid: torch.Tensor, T: int, alpha: float):

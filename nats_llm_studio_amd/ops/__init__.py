@@ -583,7 +583,8 @@ def _argmax_keys(v: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 
 
 def argmax_reset(keys: torch.Tensor):
-    """Initial value of a fused-argmax key buffer (smaller than every key)."""
+    """Initial value of a fused-argmax key buffer (smaller than every key). Decode on one GPU re-arms the
+    keys inside argmax_unpack(rearm=True) instead of a separate launch (LlamaModel._keys_clean)."""
     if keys.is_cuda:
         keys.zero_()
     else:
@@ -730,11 +731,22 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
     rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox, bias)
 
 
-def embed(ids: torch.Tensor, w: QWeight, out: torch.Tensor, T: int, scale: float = 1.0):
+def embed(ids: torch.Tensor, w: QWeight, out: torch.Tensor, T: int, scale: float = 1.0, prev=None):
+    """out[:T] = scale * W[ids[:T]]. prev = (next_ids, use_prev) (chained decode): first
+    ids[t] = next_ids[t] where use_prev[t] != 0 (in the same launch on the GPU)."""
     if ids.is_cuda:
+        if prev is not None:
+            nxt, use = prev
+            _lib.check(_lib.lib().nls_embed_prev(ids.data_ptr(), nxt.data_ptr(), use.data_ptr(), T, w.data.data_ptr(),
+                                                 w.type, w.rows, w.K, out.data_ptr(), out.stride(0), float(scale),
+                                                 _stream_ptr(ids)), "nls_embed_prev")
+            return out
         _lib.check(_lib.lib().nls_embed(ids.data_ptr(), T, w.data.data_ptr(), w.type, w.rows, w.K, out.data_ptr(),
                                         out.stride(0), float(scale), _stream_ptr(ids)), "nls_embed")
         return out
+    if prev is not None:
+        nxt, use = prev
+        torch.where(use[:T] != 0, nxt[:T], ids[:T], out=ids[:T])
     out[:T] = scale * w.dense()[ids[:T].long()]
     return out
 
@@ -826,12 +838,15 @@ def argmax(logits: torch.Tensor, M: int, out: torch.Tensor):
     return out
 
 
-def argmax_unpack(keys: torch.Tensor, n: int, out: torch.Tensor):
+def argmax_unpack(keys: torch.Tensor, n: int, out: torch.Tensor, rearm: bool = False):
+    """Token ids from the fused arg-max keys. rearm: reset keys[:n] in the same launch (see argmax_reset)."""
     if keys.is_cuda:
-        _lib.check(_lib.lib().nls_argmax_unpack(keys.data_ptr(), n, out.data_ptr(), _stream_ptr(keys)),
-                   "nls_argmax_unpack")
+        fn = _lib.lib().nls_argmax_unpack_rearm if rearm else _lib.lib().nls_argmax_unpack
+        _lib.check(fn(keys.data_ptr(), n, out.data_ptr(), _stream_ptr(keys)), "nls_argmax_unpack")
         return out
     out[:n] = (0xFFFFFFFF - (keys[:n] & 0xFFFFFFFF)).to(out.dtype)
+    if rearm:
+        argmax_reset(keys[:n])
     return out
 
 

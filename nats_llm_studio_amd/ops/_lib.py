@@ -52,10 +52,13 @@ _SIGS = {
     "nls_rope_kv8": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                     c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nls_embed": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_float, c_void_p],
+    "nls_embed_prev": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_float,
+                       c_void_p],
     "nls_dequant": [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p],
     "nls_swiglu16": [c_void_p, c_long, c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_argmax": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
     "nls_argmax_unpack": [c_void_p, c_int, c_void_p, c_void_p],
+    "nls_argmax_unpack_rearm": [c_void_p, c_int, c_void_p, c_void_p],
     "nls_moe_route": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_void_p],
     "nls_moe_norm_route": [c_void_p, c_long, c_void_p, c_float, c_int, c_void_p, c_void_p, c_long, c_void_p, c_int,

@@ -341,6 +341,35 @@ def test_argmax_kernel(gpu):
     assert out.cpu().tolist() == lg.argmax(1).cpu().tolist()
 
 
+def test_embed_prev_and_argmax_rearm(gpu):
+    """Chained decode: the embedding launch picks next_ids[t] where use_prev[t] (and writes the choice back
+    to ids); the arg-max unpack with rearm zeroes the keys it read (no reset launch before the next step)."""
+    raw = Q.random_blocks(GGMLType.Q6_K, 40 * 256, 0.05, np.random.default_rng(3))
+    qw = ops.QWeight(raw, GGMLType.Q6_K, 40, 256, gpu, layout="rows")
+    Wd = ops.QWeight(raw, GGMLType.Q6_K, 40, 256, "cpu").dense()
+    ids = torch.tensor([1, 2, 3, 4], dtype=torch.int32, device=gpu)
+    nxt = torch.tensor([10, 20, 30, 39], dtype=torch.int32, device=gpu)
+    use = torch.tensor([0, 1, 0, 1], dtype=torch.int32, device=gpu)
+    e = torch.zeros(4, 256, device=gpu)
+    ops.embed(ids, qw, e, 4, 1.0, prev=(nxt, use))
+    assert ids.cpu().tolist() == [1, 20, 3, 39]
+    torch.testing.assert_close(e.cpu(), Wd[[1, 20, 3, 39]], rtol=1e-5, atol=1e-6)
+    lg = torch.randn(4, 4096)
+    ref = lg.argmax(1)
+    # the packed key the fused lm-head arg-max leaves for each row's winner (u32 order-preserving float bits
+    # << 32 | ~index), written as int64 bit patterns
+    u = lg.max(1).values.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    u = torch.where(u >= 2 ** 31, 0xFFFFFFFF - u, u + 2 ** 31)
+    packed = [int(((int(a) << 32) | (0xFFFFFFFF - int(b))) - (1 << 64 if int(a) >= 2 ** 31 else 0))
+              for a, b in zip(u, ref)]
+    dk = torch.zeros(8, dtype=torch.int64, device=gpu)
+    dk[:4] = torch.tensor(packed, dtype=torch.int64)
+    out = torch.zeros(8, dtype=torch.int32, device=gpu)
+    ops.argmax_unpack(dk, 4, out, rearm=True)
+    assert out[:4].cpu().tolist() == ref.tolist()
+    assert int(dk.abs().sum()) == 0
+
+
 def test_moe_route(gpu):
     T, E, k = 10, 8, 2
     lg = torch.randn(T, E, device=gpu)

@@ -217,7 +217,7 @@ def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
     (models/reference.py: numpy ggml codecs + textbook fp32 decoder, on the GPU; also with the engine's
     storage roundings, to separate kernel error from storage precision) for the three GEMM paths
     production runs at 512 rows: the quantised kernels only (as NLS_DENSE_WEIGHTS=0), the f16-copy dense
-    kernels (modes 4/5/8 per the "d:" tuning entries, NLS_LIB_GEMM=0) and the library GEMM (mode 7)."""
+    kernels (modes 4/5/8/10 per the "d:" tuning entries, NLS_LIB_GEMM=0) and the library GEMM (mode 7)."""
     from nats_llm_studio_amd.gguf.reader import GGUFReader
     from nats_llm_studio_amd.models.reference import ReferenceModel
     S = 512
@@ -259,11 +259,16 @@ def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
     with monkeypatch.context() as mp:
         mp.setattr(ops, "LIB_GEMM", False)
         cfg = ops.gemv_config([gu], S)
-        assert cfg[0] in (4, 5, 6, 8), cfg              # the gate|up launch runs on the f16 copy
+        assert cfg[0] in (4, 5, 6, 8, 10), cfg          # the gate|up launch runs on the f16 copy
         check(_prefill_logits(llama8b, ids), "f16-copy dense")
     with monkeypatch.context() as mp:
         mp.setattr(ops, "LIB_GEMM", True)
-        assert ops.lib_gemm_ok([gu], S, "swiglu")
+        # at 512 rows production keeps the library GEMM for the fused Q|K|V only (gate|up, down and the LM
+        # head moved to mode 10 this round)
+        qkv = llama8b.layers[0].qkv
+        y = torch.empty(S, sum(sg.w.rows for sg in qkv), dtype=torch.float32, device=gpu)
+        assert ops.lib_gemm_ok(qkv, S, "f32", 1.0, None, y)
+        del y
         check(_prefill_logits(llama8b, ids), "mode 7")
 
 

@@ -15,6 +15,6 @@ while IFS='|' read -r name envs args; do
   rc=$?
   if [ $rc -ne 0 ]; then echo "$name rc=$rc"; tail -5 $log; exit $rc; fi
   line=$(grep '^{' $log | tail -1)
-  echo "{\"case\": \"$name\", \"env\": \"$envs\", \"args\": \"$args\", \"bench\": $line}" >> $out
+  CASE="$name" ENVS="$envs" ARGS="$args" LINE="$line" python3 -c 'import json, os; print(json.dumps({"case": os.environ["CASE"], "env": os.environ["ENVS"], "args": os.environ["ARGS"], "bench": json.loads(os.environ["LINE"])}))' >> $out
   echo "$name $(echo "$line" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], "tok/s", d["ms_per_step"], "ms/step")')"
 done
