@@ -665,9 +665,11 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
   if (D == 128 && G <= 16 && mf != 0 && block_size >= 16 && n_split <= 64) {
     const bool big = (long)T * Hkv * n_split >= 1024;
-    // small grids: 8 waves per workgroup (NLS_ATTN_MFMA_WAVES=4 for 4): a 256-key context in one pass, twice
-    // the K/V in flight per split of a long one
-    static const int mw = [] { const char* e = getenv("NLS_ATTN_MFMA_WAVES"); return e && atoi(e) == 4 ? 4 : 8; }();
+    // grids of <= 256 workgroups: 8 waves each (one workgroup per CU: 192 VGPRs), so a 256-key context is one
+    // pass; up to 1K workgroups: 4 waves (two per CU). NLS_ATTN_MFMA_WAVES=4|8 forces one. The split policy
+    // (models/llama.py attn_splits) aims at 256 workgroups at small batch.
+    static const int mwf = [] { const char* e = getenv("NLS_ATTN_MFMA_WAVES"); return e ? atoi(e) : 0; }();
+    const int mw = mwf == 4 || mwf == 8 ? mwf : ((long)T * Hkv * n_split <= 256 ? 8 : 4);
 #define NLS_ATTN_M(KVT, W)                                                                                     \
   hipLaunchKernelGGL((attn_decode_mfma_kernel<KVT, W>), grid, dim3(64 * W), 0, st, (const __bf16*)q, ldq,       \
                      (const KVT*)kc, (const KVT*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G, block_size, \

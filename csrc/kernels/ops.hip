@@ -220,10 +220,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
 // format switch kept successive elements' loads in series: 11.7 us for one 4096-wide row at batch 1).
 // Chained decode (`next_ids` set): the token is next_ids[t] where use_prev[t] != 0, else ids[t], and the
 // choice is written back to ids[t] (the separate torch.where launch folded in).
+// Grid (tokens, K / 256): one element per thread, so a row costs one round of loads, not K / 256 of them.
 template <int TYPE>
 DEVI void embed_row(const WDesc& W, int id, float* __restrict__ o, float scale) {
-#pragma unroll 8
-  for (int k = threadIdx.x; k < W.K; k += 256) o[k] = scale * dequant_elem(W, TYPE, id, k);
+  const int k = blockIdx.y * 256 + threadIdx.x;
+  if (k < W.K) o[k] = scale * dequant_elem(W, TYPE, id, k);
 }
 
 __global__ __launch_bounds__(256) void embed_kernel(int* __restrict__ ids, WDesc W, int type,
@@ -234,7 +235,9 @@ __global__ __launch_bounds__(256) void embed_kernel(int* __restrict__ ids, WDesc
   if (next_ids) {
     if (use_prev[t]) id = next_ids[t];
     __syncthreads();                         // every thread has read ids[t] before it is rewritten
-    if (threadIdx.x == 0) ids[t] = id;
+    // slice 0 records the choice; another slice may read ids[t] before or after that store and picks the
+    // same id either way (where use_prev[t] is set, next_ids[t] wins over whatever ids[t] holds)
+    if (threadIdx.x == 0 && blockIdx.y == 0) ids[t] = id;
   }
   // clamped: a bad id (device-chained decode feeds sampled ids back without a host check) must not
   // become a wild address
@@ -587,8 +590,8 @@ int nls_rope_kv8(const float* qkv, long ldqkv, int ks, long slab, const float* b
 int nls_embed(const int* ids, int T, const void* w, int type, int rows, int K, float* out, long ldo,
               float scale, void* stream) {
   WDesc W{(const uint8_t*)w, rows, K};
-  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, const_cast<int*>(ids), W, type, out,
-                     ldo, scale, nullptr, nullptr);
+  hipLaunchKernelGGL(embed_kernel, dim3(T, (K + 255) / 256), dim3(256), 0, (hipStream_t)stream, const_cast<int*>(ids),
+                     W, type, out, ldo, scale, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -596,8 +599,8 @@ int nls_embed(const int* ids, int T, const void* w, int type, int rows, int K, f
 int nls_embed_prev(int* ids, const int* next_ids, const int* use_prev, int T, const void* w, int type, int rows,
                    int K, float* out, long ldo, float scale, void* stream) {
   WDesc W{(const uint8_t*)w, rows, K};
-  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, ids, W, type, out, ldo, scale,
-                     next_ids, use_prev);
+  hipLaunchKernelGGL(embed_kernel, dim3(T, (K + 255) / 256), dim3(256), 0, (hipStream_t)stream, ids, W, type, out,
+                     ldo, scale, next_ids, use_prev);
   return (int)hipGetLastError();
 }
 

@@ -104,8 +104,16 @@ PYBIND11_MODULE(_natscore, m) {
           "connect",
           [](Client& c, const std::string& url, const std::string& name, int timeout_ms, bool reconnect,
              int max_reconnect, int reconnect_wait_ms, const std::string& token, const std::string& user,
-             const std::string& password, const std::string& nkey_seed, const std::string& jwt) {
+             const std::string& password, const std::string& nkey_seed, const std::string& jwt, bool tls,
+             bool tls_first, bool tls_insecure, const std::string& tls_ca, const std::string& tls_cert,
+             const std::string& tls_key) {
             ClientOptions o;
+            o.tls.enable = tls;
+            o.tls.first = tls_first;
+            o.tls.insecure = tls_insecure;
+            o.tls.ca = tls_ca;
+            o.tls.cert = tls_cert;
+            o.tls.key = tls_key;
             o.name = name;
             o.connect_timeout_ms = timeout_ms;
             o.allow_reconnect = reconnect;
@@ -121,7 +129,10 @@ PYBIND11_MODULE(_natscore, m) {
           },
           py::arg("url"), py::arg("name") = "natscore", py::arg("timeout_ms") = 2000, py::arg("reconnect") = true,
           py::arg("max_reconnect") = 60, py::arg("reconnect_wait_ms") = 250, py::arg("token") = "",
-          py::arg("user") = "", py::arg("password") = "", py::arg("nkey_seed") = "", py::arg("jwt") = "")
+          py::arg("user") = "", py::arg("password") = "", py::arg("nkey_seed") = "", py::arg("jwt") = "",
+          py::arg("tls") = false, py::arg("tls_first") = false, py::arg("tls_insecure") = false,
+          py::arg("tls_ca") = "", py::arg("tls_cert") = "", py::arg("tls_key") = "")
+      .def("tls_cipher", &Client::tls_cipher)
       .def("close", &Client::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("connected", &Client::connected)
       .def(

@@ -28,7 +28,10 @@ static std::string pct_decode(const std::string& s) {
 static void parse_url(const std::string& url, std::string& host, int& port, ClientOptions& opt) {
   std::string u = url;
   auto p = u.find("://");
-  if (p != std::string::npos) u = u.substr(p + 3);
+  if (p != std::string::npos) {
+    if (u.compare(0, p, "tls") == 0) opt.tls.enable = true;
+    u = u.substr(p + 3);
+  }
   auto at = u.rfind('@');
   if (at != std::string::npos) {
     const std::string ui = u.substr(0, at);
@@ -57,11 +60,21 @@ static void parse_url(const std::string& url, std::string& host, int& port, Clie
 bool Client::dial() {
   int fd = tcp_connect(host_, port_, opt_.connect_timeout_ms);
   if (fd < 0) return false;
+  std::shared_ptr<TlsConn> tls;
+  auto tls_up = [&]() {
+    tls = std::make_shared<TlsConn>();
+    std::string err;
+    if (tls->handshake(fd, host_, opt_.tls, opt_.connect_timeout_ms, err)) return true;
+    std::lock_guard<std::mutex> g(mu_);
+    last_err_ = err;
+    return false;
+  };
+  if (opt_.tls.first && !tls_up()) { ::close(fd); return false; }   // handshake_first: TLS before INFO
   // read INFO line synchronously
   std::string line;
   char ch;
   while (true) {
-    ssize_t n = ::recv(fd, &ch, 1, 0);
+    const long n = tls ? tls->read(&ch, 1, closing_) : (long)::recv(fd, &ch, 1, 0);
     if (n <= 0) { ::close(fd); return false; }
     line += ch;
     if (line.size() >= 2 && line.compare(line.size() - 2, 2, "\r\n") == 0) break;
@@ -69,6 +82,7 @@ bool Client::dial() {
   }
   if (line.rfind("INFO ", 0) != 0) { ::close(fd); return false; }
   std::string nonce;
+  bool tls_required = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     info_ = line.substr(5, line.size() - 7);
@@ -76,9 +90,12 @@ bool Client::dial() {
       Json j = Json::parse(info_);
       max_payload_ = (size_t)j.num("max_payload", 1 << 20);
       nonce = j.str("nonce");
+      tls_required = j.boolean("tls_required", false);
     } catch (...) {
     }
   }
+  // the NATS upgrade: the client asked for TLS or the server requires it -> handshake after INFO
+  if (!tls && (opt_.tls.enable || tls_required) && !tls_up()) { ::close(fd); return false; }
   Json c = Json::O();
   if (!opt_.token.empty()) c.set("auth_token", Json::S(opt_.token));
   if (!opt_.user.empty()) {
@@ -97,7 +114,7 @@ bool Client::dial() {
   }
   c.set("verbose", Json::B(opt_.verbose));
   c.set("pedantic", Json::B(false));
-  c.set("tls_required", Json::B(false));
+  c.set("tls_required", Json::B(tls != nullptr));
   c.set("name", Json::S(opt_.name));
   c.set("lang", Json::S("cpp-natscore"));
   c.set("version", Json::S("0.1.0"));
@@ -124,10 +141,14 @@ bool Client::dial() {
       }
     }
   }
-  if (!send_all(fd, hello.data(), hello.size())) { ::close(fd); return false; }
+  if (!(tls ? tls->write_all(hello.data(), hello.size()) : send_all(fd, hello.data(), hello.size()))) {
+    ::close(fd);
+    return false;
+  }
   {
     std::lock_guard<std::mutex> g(wmu_);
     fd_ = fd;
+    tls_ = tls;
   }
   connected_ = true;
   return true;
@@ -138,7 +159,11 @@ void Client::connect(const std::string& url, ClientOptions opt) {
   opt_ = opt;
   parse_url(url, host_, port_, opt_);
   closing_ = false;
-  if (!dial()) throw ConnectionClosedError("nats: cannot connect to " + url);
+  dead_ = false;
+  if (!dial()) {
+    std::lock_guard<std::mutex> g(mu_);
+    throw ConnectionClosedError("nats: cannot connect to " + url + (last_err_.empty() ? "" : ": " + last_err_));
+  }
   rth_ = std::thread([this] { reader(); });
   try {
     flush(opt_.connect_timeout_ms);
@@ -172,6 +197,7 @@ void Client::close() {
   if (rth_.joinable()) rth_.join();
   {
     std::lock_guard<std::mutex> g(wmu_);
+    tls_.reset();
     if (fd_ >= 0) ::close(fd_);
     fd_ = -1;
   }
@@ -193,7 +219,7 @@ void Client::fail_all(const std::string& why) {
 void Client::write_raw(const std::string& s) {
   std::lock_guard<std::mutex> g(wmu_);
   if (fd_ < 0 || !connected_) throw ConnectionClosedError("nats: connection closed");
-  if (!send_all(fd_, s.data(), s.size())) {
+  if (!(tls_ ? tls_->write_all(s.data(), s.size()) : send_all(fd_, s.data(), s.size()))) {
     connected_ = false;
     ::shutdown(fd_, SHUT_RDWR);
     throw ConnectionClosedError("nats: write failed");
@@ -328,8 +354,10 @@ void Client::flush(int timeout_ms) {
   }
   write_raw("PING\r\n");
   std::unique_lock<std::mutex> g(mu_);
-  if (!pong_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] { return pongs_recv_ >= target || closing_; }))
+  if (!pong_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms),
+                         [&] { return pongs_recv_ >= target || closing_ || dead_; }))
     throw TimeoutError("nats: flush timeout");
+  if (pongs_recv_ < target && dead_) throw ConnectionClosedError("nats: connection closed");
 }
 
 void Client::on_op(Op& op) {
@@ -393,12 +421,14 @@ void Client::reader() {
   while (!closing_) {
     Parser p;
     int fd;
+    std::shared_ptr<TlsConn> tls;
     {
       std::lock_guard<std::mutex> g(wmu_);
       fd = fd_;
+      tls = tls_;
     }
     while (!closing_) {
-      ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+      const long n = tls ? tls->read(buf, sizeof buf, closing_) : (long)::recv(fd, buf, sizeof buf, 0);
       if (n <= 0) break;
       if (!p.feed(buf, (size_t)n, [&](Op& op) { on_op(op); })) break;
     }
@@ -412,9 +442,11 @@ void Client::reader() {
     }
     {
       std::lock_guard<std::mutex> g(wmu_);
+      tls_.reset();
       ::close(fd_);
       fd_ = -1;
     }
+    tls.reset();
     bool ok = false;
     for (int a = 0; !closing_ && (opt_.max_reconnect < 0 || a < opt_.max_reconnect); ++a) {
       std::this_thread::sleep_for(std::chrono::milliseconds(std::min(opt_.reconnect_wait_ms * (1 << std::min(a, 4)),
@@ -428,6 +460,10 @@ void Client::reader() {
     if (!ok) break;
   }
   connected_ = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    dead_ = true;
+  }
   fail_all("reader exit");
 }
 

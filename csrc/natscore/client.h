@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "proto.h"
+#include "tls.h"
 #include "util.h"
 
 namespace natscore {
@@ -34,6 +35,7 @@ struct ClientOptions {
   // authentication (CONNECT fields): token, user/password, an nkey seed ("SU..." signing the server
   // nonce) and/or a user JWT (from a .creds file, also signed with its seed)
   std::string token, user, pass, nkey_seed, jwt;
+  TlsOptions tls;                    // TLS (tls.h); a tls:// URL sets tls.enable
 };
 
 class TimeoutError : public std::runtime_error {
@@ -73,6 +75,10 @@ class Client {
   }
   size_t max_payload() const { return max_payload_; }
   std::string stats_json();
+  std::string tls_cipher() {
+    std::lock_guard<std::mutex> g(wmu_);
+    return tls_ ? tls_->cipher() : "";
+  }
 
  private:
   struct Sub {
@@ -96,7 +102,9 @@ class Client {
   int port_ = 4222;
   ClientOptions opt_;
   int fd_ = -1;
+  std::shared_ptr<TlsConn> tls_;       // set when the connection runs over TLS (guarded by wmu_)
   std::atomic<bool> connected_{false}, closing_{false};
+  std::atomic<bool> dead_{false};      // the reader gave up (connection lost, no reconnect left)
   std::thread rth_;
   std::mutex wmu_;
   std::mutex mu_;

@@ -121,7 +121,7 @@ def build_natscore(force: bool = False) -> str:
         inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{os.path.join(CSRC, 'natscore')}"]
         tmp = out + ".tmp"
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden", *inc, *srcs,
-              "-o", tmp, "-lcrypto"])      # libcrypto: ed25519 nkey signatures
+              "-o", tmp, "-lssl", "-lcrypto"])      # libssl: NATS TLS; libcrypto: ed25519 nkey signatures
         os.replace(tmp, out)
         _write_stamp(out, deps)
     return out
@@ -141,7 +141,7 @@ def build_tool(name: str = "nls-nats", src: str = "nls_nats.cpp", extra=(), out_
         os.makedirs(os.path.dirname(out), exist_ok=True)
         tmp = out + ".tmp"
         _run([cxx, "-O2", "-std=c++17", "-pthread", f"-I{os.path.join(CSRC, 'natscore')}", *extra, *srcs,
-              "-o", tmp, "-lcrypto"])
+              "-o", tmp, "-lssl", "-lcrypto"])
         os.replace(tmp, out)
         _write_stamp(out, deps)
     return out

@@ -33,7 +33,9 @@ from .config import ModelConfig
 # chunk keeps 4K context at 16 x 256 keys, which beat 32 x 128 -- profiles/attn_split_cap_4k.txt -- and gives
 # 8K-32K contexts 32-64 splits; profiles/ctx_sweep_r03_splits.jsonl)
 _SPLIT_CAP = int(os.environ.get("NLS_ATTN_SPLIT_CAP", "64"))
-_SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "512"))      # target workgroups of a decode attention launch
+# target workgroups of a decode attention launch: 256 = one 8-wave workgroup per CU (attention.hip picks 8 waves
+# for grids of <= 256 workgroups); batch 1 then splits 32 ways, batch 16 two ways
+_SPLIT_WG = int(os.environ.get("NLS_ATTN_SPLIT_WG", "256"))
 # fewest keys per flash-decoding split (0: the kernel's context-adaptive policy, attention.hip
 # split_chunk: 64 keys below 1K of context, 128 above)
 _MIN_CHUNK = int(os.environ.get("NLS_ATTN_MIN_CHUNK", "0"))
@@ -376,7 +378,7 @@ class LlamaModel:
         sizes each split from the actual context (>= 64 keys) and skips splits past it, so a large
         split count only costs parallelism headroom for long contexts."""
         wg = T * Hkv
-        if wg >= 512:
+        if wg >= _SPLIT_WG:
             return 1
         return int(min(_SPLIT_CAP, max(1, _SPLIT_WG // wg)))
 

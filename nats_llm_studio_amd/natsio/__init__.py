@@ -83,15 +83,22 @@ class Client:
 
     def connect(self, url: str = "nats://127.0.0.1:4222", name: str = "nats-llm-studio-amd", timeout: float = 2.0,
                 reconnect: bool = True, max_reconnect: int = 60, reconnect_wait: float = 0.25, token: str = "",
-                user: str = "", password: str = "", nkey_seed: str = "", creds: str = "") -> "Client":
+                user: str = "", password: str = "", nkey_seed: str = "", creds: str = "", tls: bool = False,
+                tls_first: bool = False, tls_insecure: bool = False, tls_ca: str = "", tls_cert: str = "",
+                tls_key: str = "") -> "Client":
         """Authentication as nats.go: `token`, `user`/`password` (or in the URL), `nkey_seed` ("SU..."),
-        or a `.creds` file (user JWT + seed); nkey-based methods sign the server's INFO nonce."""
+        or a `.creds` file (user JWT + seed); nkey-based methods sign the server's INFO nonce.
+        TLS (OpenSSL, csrc/natscore/tls.cpp): a `tls://` URL or `tls=True` requires it, a server INFO with
+        `tls_required` upgrades to it; `tls_ca` (CA bundle, else the system store), `tls_cert` / `tls_key`
+        (mutual TLS), `tls_insecure` (no verification), `tls_first` (handshake before the server's INFO)."""
         jwt = ""
         if creds:
             with open(os.path.expanduser(creds)) as f:
                 jwt, nkey_seed = _nc.parse_creds(f.read())
         self._c.connect(url, name, int(timeout * 1000), reconnect, max_reconnect, int(reconnect_wait * 1000), token,
-                        user, password, nkey_seed, jwt)
+                        user, password, nkey_seed, jwt, tls, tls_first, tls_insecure,
+                        os.path.expanduser(tls_ca) if tls_ca else "", os.path.expanduser(tls_cert) if tls_cert else "",
+                        os.path.expanduser(tls_key) if tls_key else "")
         return self
 
     @property

@@ -66,11 +66,21 @@ class WorkerConfig:
     nats_password: str = ""
     nats_nkey_seed: str = ""
     nats_creds: str = ""
+    # NATS TLS (nats.go: Secure / RootCAs / ClientCert / InsecureSkipVerify / TLSHandshakeFirst); a tls://
+    # NATS_URL also turns it on
+    nats_tls: bool = False
+    nats_tls_ca: str = ""
+    nats_tls_cert: str = ""
+    nats_tls_key: str = ""
+    nats_tls_insecure: bool = False
+    nats_tls_first: bool = False
 
     def nats_auth(self) -> dict:
-        """Keyword arguments of natsio.Client.connect for the configured credentials."""
+        """Keyword arguments of natsio.Client.connect for the configured credentials and TLS."""
         return dict(token=self.nats_token, user=self.nats_user, password=self.nats_password,
-                    nkey_seed=self.nats_nkey_seed, creds=self.nats_creds)
+                    nkey_seed=self.nats_nkey_seed, creds=self.nats_creds, tls=self.nats_tls,
+                    tls_ca=self.nats_tls_ca, tls_cert=self.nats_tls_cert, tls_key=self.nats_tls_key,
+                    tls_insecure=self.nats_tls_insecure, tls_first=self.nats_tls_first)
 
     def subject(self, name: str) -> str:
         return f"{self.subject_prefix}.{name}"
@@ -104,6 +114,13 @@ class WorkerConfig:
             with open(os.path.expanduser(seed_file)) as f:
                 c.nats_nkey_seed = f.read().strip()
         c.nats_creds = e.get("NATS_CREDS", c.nats_creds)
+        yes = ("1", "true", "yes")
+        c.nats_tls = e.get("NATS_TLS", "0").lower() in yes
+        c.nats_tls_ca = e.get("NATS_TLS_CA", c.nats_tls_ca)
+        c.nats_tls_cert = e.get("NATS_TLS_CERT", c.nats_tls_cert)
+        c.nats_tls_key = e.get("NATS_TLS_KEY", c.nats_tls_key)
+        c.nats_tls_insecure = e.get("NATS_TLS_INSECURE", "0").lower() in yes
+        c.nats_tls_first = e.get("NATS_TLS_FIRST", "0").lower() in yes
         return c
 
     @classmethod
@@ -127,6 +144,9 @@ class WorkerConfig:
         ap.add_argument("--store-dir", default=c.store_dir)
         ap.add_argument("--subject-prefix", default=c.subject_prefix)
         ap.add_argument("--nats-creds", default=c.nats_creds, help="NATS .creds file (user JWT + nkey seed)")
+        ap.add_argument("--nats-tls-ca", default=c.nats_tls_ca, help="CA bundle for the NATS server certificate")
+        ap.add_argument("--nats-tls-cert", default=c.nats_tls_cert, help="client certificate (mutual TLS)")
+        ap.add_argument("--nats-tls-key", default=c.nats_tls_key, help="client key (mutual TLS)")
         a = ap.parse_args(argv)
         for k, v in vars(a).items():
             setattr(c, k, v)
