@@ -216,6 +216,12 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
       for (int e = 0; e < 4; ++e) {
         const int b = mbase + 16 * i + 4 * g + e;
         const float v = acc[i][j][e] * a.alpha;
+        if (a.epi == EPI_ROPE) {
+          // RoPE pair (row, row ^ 1) = lanes r, r ^ 1 (same b)
+          const float pv = __shfl_xor(v, 1, 64);
+          if (b < M && row < S.rows) rope_store1(a, S.ycol + row, a.m0 + b, v, pv);
+          continue;
+        }
         if (a.epi == EPI_SWIGLU) {
           // interleaved [g0..g7, u0..u7] per 16 weight rows: the partner row is lane ^ 8 (same b)
           const float u = __shfl_xor(v, 8, 64);

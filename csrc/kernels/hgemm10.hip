@@ -203,6 +203,25 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     return;
   }
   const float al = a.alpha;
+  if (a.epi == EPI_ROPE) {
+    // RoPE pairs (e, e + 1) of the lane's 4 consecutive weight rows: no cross-lane traffic
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = nb + 16 * i + g4;
+      if (n >= S.rows) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mb + 16 * j + r16;
+        if (m >= M) continue;
+        const f32x4 v = acc[i][j] * al;
+        rope_store1(a, S.ycol + n, a.m0 + m, v[0], v[1]);
+        rope_store1(a, S.ycol + n + 1, a.m0 + m, v[1], v[0]);
+        rope_store1(a, S.ycol + n + 2, a.m0 + m, v[2], v[3]);
+        rope_store1(a, S.ycol + n + 3, a.m0 + m, v[3], v[2]);
+      }
+    }
+    return;
+  }
   if (a.epi == EPI_SWIGLU) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

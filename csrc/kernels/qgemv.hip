@@ -77,9 +77,10 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
         fz->onw || M > 32 || (waves * 64) % ncols || fz->ldss < (segs[0].rows + 16 * rt - 1) / (16 * rt))
       return -1;
   }
-  if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A, plain rows, contiguous Q|K|V segments
-    if (mode != 0 || argmax || !fz->pos || !fz->slot || !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 ||
-        fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
+  if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A or a dense GEMM without split-K; plain rows,
+                           // contiguous Q|K|V segments
+    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10) && ks <= 1)) || argmax || !fz->pos || !fz->slot ||
+        !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 || fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
       return -1;
     int c = 0;
     for (int i = 0; i < nseg; ++i) {
@@ -99,7 +100,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
   if (mode < 0 || mode > 10 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
   if (mode == 10) {
-    if (waves != 8 || fz->xf || fz->onw || epi == EPI_ROPE || ldx % 8 ||
+    if (waves != 8 || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
     for (int i = 0; i < nseg; ++i)
@@ -117,7 +118,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
   } else if (mode >= 4 && mode <= 6) {
-    if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE) return -1;
+    if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || (epi == EPI_ROPE && mode == 6))
+      return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16) return -1;
   } else if (mode == 3) {

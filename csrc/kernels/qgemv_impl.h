@@ -135,6 +135,31 @@ DEVI void rows_rmsnorm(const float* y, long ldy, int M, int D, const float* w, f
   }
 }
 
+// EPI_ROPE of the dense GEMMs (modes 4/5/10, split-K 1): Q|K|V column `col` of activation row `b` (global
+// row) with value v and the value p of its RoPE partner column col ^ 1 (adjacent pairs, as path A): add the
+// bias, rotate q / k, store bf16 into q or the paged K / V cache (slot < 0: padding row, no cache write)
+DEVI void rope_store1(const GemvArgs& a, int col, int b, float v, float p) {
+  const bool odd = col & 1;
+  float x0 = odd ? p : v, x1 = odd ? v : p;
+  if (a.bias) {
+    x0 += a.bias[col & ~1];
+    x1 += a.bias[col | 1];
+  }
+  const int h = col / a.D, dd = col - h * a.D;
+  const long s = a.slot[b];
+  float y = odd ? x1 : x0;
+  __bf16* d = nullptr;
+  if (h < a.Hq + a.Hkv) {
+    const float2 c = reinterpret_cast<const float2*>(a.cs + (size_t)a.pos[b] * a.D)[dd >> 1];
+    y = odd ? x0 * c.y + x1 * c.x : x0 * c.x - x1 * c.y;
+    if (h < a.Hq) d = a.q_out + (size_t)b * a.ldq + col;
+    else if (s >= 0) d = a.kc + ((size_t)s * a.Hkv + (h - a.Hq)) * a.D + dd;
+  } else if (s >= 0) {
+    d = a.vc + ((size_t)s * a.Hkv + (h - a.Hq - a.Hkv)) * a.D + dd;
+  }
+  if (d) *d = (__bf16)y;
+}
+
 DEVI unsigned long long argmax_key(float v, int idx) {
   uint32_t u = __builtin_bit_cast(uint32_t, v);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);

@@ -736,14 +736,30 @@ def test_lm_head_argmax_only_epilogue(gpu):
 def test_qkv_rope_kv_fused(gpu, cfg, M, bias):
     """QKV projection (3 segments) + RoPE + KV append: path A rotates in the GEMV epilogue, split-K
     launches sum their slabs inside the RoPE kernel. `bias`: Qwen2 QKV bias added before rotating."""
+    _qkv_rope_case(gpu, cfg, M, bias, dense=False)
+
+
+@pytest.mark.parametrize("cfg", [(4, 16, 2, 1), (4, 16, 4, 1), (5, 8, 4, 1), (10, 8, 1, 1), (10, 8, 1, 2)])
+@pytest.mark.parametrize("M", [70, 300, 520])
+@pytest.mark.parametrize("bias", [False, True])
+def test_qkv_rope_kv_dense(gpu, cfg, M, bias):
+    """The dense GEMMs on the weights' f16 copies (modes 4/5/10) with the RoPE + KV-append epilogue
+    (split-K 1: lane pairs rotated in registers; split-K 2: slabs summed by the RoPE kernel)."""
+    _qkv_rope_case(gpu, cfg, M, bias, dense=True)
+
+
+def _qkv_rope_case(gpu, cfg, M, bias, dense):
     Hq, Hkv, D, K = 4, 2, 128, 512
     wq, Wq = _qw(Hq * D, K, GGMLType.Q4_K, gpu, 21)
     wk, Wk = _qw(Hkv * D, K, GGMLType.Q4_K, gpu, 22)
     wv, Wv = _qw(Hkv * D, K, GGMLType.Q6_K, gpu, 23)
+    if dense:        # the f16 copies ARE the dequantised values the references multiply with
+        for w in (wq, wk, wv):
+            w.expand_dense()
     segs = [ops.Seg(wq, 0), ops.Seg(wk, Hq * D), ops.Seg(wv, (Hq + Hkv) * D)]
     x = _x(M, K, gpu)
     pad = x.shape[0]
-    cs = ops.rope_table(1024, D, 10000.0, gpu)
+    cs = ops.rope_table(4 * pad, D, 10000.0, gpu)
     pos = torch.arange(pad, dtype=torch.int32, device=gpu) * 3
     slot = torch.arange(pad, dtype=torch.int32, device=gpu)
     qkv = torch.zeros(pad, (Hq + 2 * Hkv) * D, device=gpu)
