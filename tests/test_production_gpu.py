@@ -263,8 +263,11 @@ def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
         check(_prefill_logits(llama8b, ids), "f16-copy dense")
     with monkeypatch.context() as mp:
         mp.setattr(ops, "LIB_GEMM", True)
-        # at 512 rows production keeps the library GEMM for the fused Q|K|V only (gate|up, down and the LM
-        # head moved to mode 10 this round)
+        # production runs no library GEMM at 512 rows since r03 (gate|up, down and the LM head on mode 10,
+        # Q|K|V on mode 4): the library path (mode 7, still chosen for 1K-2K-row prefill chunks) is pinned here
+        # by selecting it for the fused Q|K|V
+        from nats_llm_studio_amd.ops import tuning
+        mp.setitem(tuning.table(), tuning.lib_key(llama8b.layers[0].qkv, S), (1,))
         qkv = llama8b.layers[0].qkv
         y = torch.empty(S, sum(sg.w.rows for sg in qkv), dtype=torch.float32, device=gpu)
         assert ops.lib_gemm_ok(qkv, S, "f32", 1.0, None, y)
