@@ -65,7 +65,8 @@ def parse(argv=None):
     ap.add_argument("--tp-leg-model", default=None,
                     help="model of the TP leg (default llama-3-70b; on --device cpu llama-3-70b-1layer)")
     ap.add_argument("--tp-leg-concurrency", type=int, default=64)
-    ap.add_argument("--tp-leg-timeout", type=float, default=900.0, help="seconds before the TP leg is abandoned")
+    ap.add_argument("--tp-leg-timeout", type=float, default=480.0,
+                    help="seconds before the TP leg is abandoned (bounds what it adds to an N-GPU run)")
     ap.add_argument("--step-breakdown", action="store_true",
                     help="report host time vs time blocked on the previous step's tokens (diagnostic)")
     a = ap.parse_args(argv)
@@ -204,12 +205,6 @@ def _run_tp_leg(args, world: int, cuda: bool) -> dict:
             "concurrency": args.tp_leg_concurrency, "value": d["value"], "unit": d["unit"],
             "ms_per_step": d["ms_per_step"], "steps": d["steps"], "weights_gb_per_rank": d["weights_gb_per_rank"],
             "comm": d["comm"], "timings_s": d["timings_s"], "wall_s": round(time.time() - t0, 1)}
-
-
-    _reduce_and_report(args, world, dist, torch, dev, leg["elapsed"], leg["tokens"], leg["info"], rank)
-    if world > 1:
-        dist.destroy_process_group()
-    return 0
 
 
 def _skip_tp_leg(args, tmodel: str) -> bool:

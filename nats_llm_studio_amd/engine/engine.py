@@ -274,8 +274,12 @@ class Engine:
         self._ids = itertools.count()
         self.host_ms = defaultdict(float)
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0,
-                             device_sampled_steps=0, preemptions=0, recompute_tokens=0)
+                             device_sampled_steps=0, preemptions=0, recompute_tokens=0, candidate_sampled_steps=0)
         self.full_logits: Optional[torch.Tensor] = None
+        # TP sampling: per-rank top-CAND candidates gathered instead of the full logits when every sampled row
+        # of the step has 0 < top_k <= CAND - HIST (or samples at temperature 0 with penalties); see _cand_ok
+        self.cand: Optional[tuple] = None
+        self._cand_mode = False
         self._ctrl_hdr = torch.zeros(_HDR + self.max_batch, dtype=torch.int32)
         # In-graph sampling (single GPU): per-row sampling params / seeds / penalty-history rings live on
         # the device, written once when a sequence takes its decode row; sampled rows then stay on the
@@ -509,6 +513,7 @@ class Engine:
                 self.alloc.register(s.blocks[:len(s.keys)], s.keys)
         nrows = max(1, len(rows))
         need = any(not s.req.params.greedy for s in finishing)
+        self._cand_mode = need and self._cand_ok(finishing)
         self._ctrl(_OP_PREFILL, T, nrows, need, rows + [0] * (nrows - len(rows)), len(batch), self.h_meta_p, pad)
         self._exec_prefill(T, rows + [0] * (nrows - len(rows)), need)
         self.counters["prefill_tokens"] += T
@@ -554,8 +559,31 @@ class Engine:
                                need_logits=need_logits)
         self._gather(b, n, need_logits)
 
+    CAND = 128           # TP sampling: candidates per rank and row
+
+    def _cand_ok(self, seqs) -> bool:
+        """Can every sampled row of these sequences be drawn exactly from the gathered top-CAND candidates of
+        each rank? Penalties only lower logits of the <= HIST history tokens, so the post-penalty top-k lies in
+        the pre-penalty top-(k + HIST) of the vocabulary, and top-p / min-p act on the kept top-k set (the
+        sampler's order): exact for 0 < top_k <= CAND - HIST, and for penalised temperature-0 rows."""
+        if self.tp is None or os.environ.get("NLS_TP_CANDIDATES", "1") != "1":
+            return False
+        for s in seqs:
+            p = s.req.params
+            if p.greedy:
+                continue
+            if p.temperature > 0.0 and not (0 < (p.top_k or 0) <= self.CAND - HIST):
+                return False
+        return True
+
     def _gather(self, b, n: int, need_logits: bool):
-        if self.tp is not None and need_logits:
+        self.cand = None
+        if self.tp is not None and need_logits and self._cand_mode:
+            m = self.model
+            valid = max(0, min(m.vocab_hi, m.cfg.vocab) - m.vocab_lo)
+            self.cand = self.tp.gather_candidates(*ops.topc_candidates(b.logits, n, self.CAND, m.vocab_lo, valid))
+            self.full_logits = None
+        elif self.tp is not None and need_logits:
             m = self.model
             self.full_logits = self.tp.gather_logits(b.logits, n, m.cfg.vocab, m.vocab_per)
         else:
@@ -570,7 +598,7 @@ class Engine:
         nb = self.max_blocks
         hdr = self._ctrl_hdr
         hdr.zero_()
-        hdr[:_HDR] = torch.tensor([op, T, nrows, int(need), nseq, pad, 0, 0], dtype=torch.int32)
+        hdr[:_HDR] = torch.tensor([op, T, nrows, int(need), nseq, pad, int(self._cand_mode), 0], dtype=torch.int32)
         if rows:
             hdr[_HDR:_HDR + len(rows)] = torch.tensor(rows, dtype=torch.int32)
         self.tp.bcast_ctrl(hdr)
@@ -595,7 +623,8 @@ class Engine:
         nb = self.max_blocks
         while True:
             hdr = self.tp.bcast_ctrl(self._ctrl_hdr)
-            op, T, nrows, need, nseq, pad = (int(v) for v in hdr[:6])
+            op, T, nrows, need, nseq, pad, cand = (int(v) for v in hdr[:7])
+            self._cand_mode = bool(cand)
             if op == _OP_STOP:
                 return
             if op == _OP_CAPTURE:
@@ -624,6 +653,11 @@ class Engine:
             greedy = self.h_next[:len(rows)].tolist()
         out = list(greedy)
         sampled = [i for i, s in enumerate(seqs) if not s.req.params.greedy]
+        if sampled and self.cand is not None:
+            toks = self._sample_candidates([rows[i] for i in sampled], [seqs[i] for i in sampled])
+            for i, t in zip(sampled, toks):
+                out[i] = t
+            sampled = []
         if sampled:
             lg = self.full_logits if self.full_logits is not None else b.logits
             fn = sample_rows_gpu if lg.is_cuda else sample_rows
@@ -632,6 +666,24 @@ class Engine:
             for i, t in zip(sampled, toks):
                 out[i] = t
         return out
+
+    def _sample_candidates(self, rows: List[int], seqs: List[_Seq]) -> List[int]:
+        """Draw the sampled rows from the gathered candidates (values in vocabulary order, global ids): the
+        sampler runs on the candidate rows with each history token mapped to its candidate position (history
+        tokens outside the candidates cannot reach the kept set); the drawn position maps back to its id.
+        Same kept set, same index order, same variate: the token the full-vocabulary sampler would draw."""
+        vals, ids = self.cand
+        self.counters["candidate_sampled_steps"] += 1
+        v = vals[rows]
+        ix = ids[rows]
+        ixl = ix.cpu().tolist()
+        hist = []
+        for r, s in enumerate(seqs):
+            pos = {t: j for j, t in enumerate(ixl[r]) if t >= 0}
+            hist.append([pos[t] for t in s.tokens[-HIST:] if t in pos])
+        fn = sample_rows_gpu if v.is_cuda else sample_rows
+        picks = fn(v.contiguous(), [s.req.params for s in seqs], hist, [self._u(s) for s in seqs])
+        return [int(ixl[r][j]) if 0 <= j < len(ixl[r]) and ixl[r][j] >= 0 else 0 for r, j in enumerate(picks)]
 
     @staticmethod
     def _u(s: _Seq) -> float:
@@ -752,6 +804,8 @@ class Engine:
         return Bp
 
     def _launch(self, launch: List[_Seq], prev: set, need: bool = False, dsamp: bool = False):
+        if not need:
+            self._cand_mode = False
         t0 = time.perf_counter()
         try:
             return self._launch_inner(launch, prev, need, dsamp)
@@ -892,6 +946,7 @@ class Engine:
         if not chain:
             # synchronous step (sampling / penalties need the host between steps)
             need = any(not s.req.params.greedy for s in launch)
+            self._cand_mode = need and self._cand_ok(launch)
             new = self._launch(launch, prev, need) if launch else None
             if new is not None:
                 self._process_sync(new, launch, need)
@@ -916,6 +971,11 @@ class Engine:
         sampled = [i for i, s in enumerate(launch) if not s.req.params.greedy]
         if need:                               # (TP: followers gather in the same step)
             self._gather(b, self._bucket(max(rows) + 1), True)
+        if sampled and self.cand is not None:
+            toks = self._sample_candidates([rows[i] for i in sampled], [launch[i] for i in sampled])
+            for i, t in zip(sampled, toks):
+                out[i] = t
+            sampled = []
         if sampled:
             lg = self.full_logits if self.full_logits is not None else b.logits
             fn = sample_rows_gpu if lg.is_cuda else sample_rows

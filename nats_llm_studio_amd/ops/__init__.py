@@ -850,6 +850,22 @@ def argmax(logits: torch.Tensor, M: int, out: torch.Tensor):
     return out
 
 
+def topc_candidates(logits: torch.Tensor, n: int, C: int, vocab_lo: int, valid: int):
+    """Per row, the C largest logits of a vocab shard (columns [0, valid) of `logits`; the rest are padding)
+    in increasing vocabulary order: (values f32 [n, C], global token ids int32 [n, C]), padded with
+    (-inf, -1) where the shard holds fewer than C tokens. Tensor-parallel sampling gathers these instead of
+    the [n, vocab] logits (engine: _gather / _sample_candidates)."""
+    k = max(0, min(C, valid))
+    v = torch.full((n, C), float("-inf"), dtype=torch.float32, device=logits.device)
+    i = torch.full((n, C), -1, dtype=torch.int32, device=logits.device)
+    if k and n:
+        tv, ti = torch.topk(logits[:n, :valid].float(), k, dim=1)
+        ti, order = torch.sort(ti, dim=1)                    # vocabulary order within the shard
+        v[:, :k] = torch.gather(tv, 1, order)
+        i[:, :k] = (ti + vocab_lo).to(torch.int32)
+    return v, i
+
+
 def argmax_unpack(keys: torch.Tensor, n: int, out: torch.Tensor, rearm: bool = False):
     """Token ids from the fused arg-max keys. rearm: reset keys[:n] in the same launch (see argmax_reset)."""
     if keys.is_cuda:

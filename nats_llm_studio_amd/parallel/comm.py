@@ -119,6 +119,20 @@ class Comm:
         dist.all_gather_into_tensor(out, loc, group=self.group)
         return out.view(self.size, n, per).permute(1, 0, 2).reshape(n, self.size * per)[:, :vocab]
 
+    def gather_candidates(self, vals: torch.Tensor, idx: torch.Tensor):
+        """Per-rank top-C candidates [n, C] (values, global ids; ops.topc_candidates) -> [n, size * C] on
+        every rank, in rank order = vocabulary order (ranks hold consecutive vocab shards). 8 bytes per
+        candidate instead of 4 per vocabulary entry: C = 128 at TP=8 moves 8 KiB per sampled row, not 500 KiB."""
+        n, C = vals.shape
+        ov = torch.empty(self.size * n, C, dtype=vals.dtype, device=vals.device)
+        oi = torch.empty(self.size * n, C, dtype=idx.dtype, device=idx.device)
+        dist.all_gather_into_tensor(ov, vals.contiguous(), group=self.group)
+        dist.all_gather_into_tensor(oi, idx.contiguous(), group=self.group)
+        self.stats["all_reduce"] += 1
+        self.stats["all_reduce_bytes"] += 8 * n * C * self.size
+        return (ov.view(self.size, n, C).permute(1, 0, 2).reshape(n, self.size * C),
+                oi.view(self.size, n, C).permute(1, 0, 2).reshape(n, self.size * C))
+
     # ------------------------------------------------------------------ control plane
     def bcast_ctrl(self, t: torch.Tensor):
         """Host int32 tensor from rank 0 to all ranks: the shared-memory ring when every rank of the

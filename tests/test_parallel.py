@@ -53,7 +53,16 @@ def _run(eng):
     while not f.done():
         eng.step()
     lg = eng.full_logits if eng.full_logits is not None else eng.pb.logits
-    return toks, lg[:1].clone()
+    lg = lg[:1].clone()
+    # top-k sampling with penalties: under TP the rows are drawn from the gathered per-rank top-128 candidates
+    # (Engine._sample_candidates), which must give exactly the full-vocabulary sampler's tokens
+    topk = SamplingParams(max_tokens=8, temperature=0.9, top_k=20, top_p=0.9, repeat_penalty=1.3,
+                          presence_penalty=0.2, seed=11, ignore_eos=True)
+    futs = [eng.submit(GenRequest(list(p), topk)) for p in PROMPTS]
+    while not all(f.done() for f in futs):
+        eng.step()
+    toks.append([f.result().token_ids for f in futs])
+    return toks, lg
 
 
 def _worker(rank, world, port, path, ep, out):
@@ -69,7 +78,7 @@ def _worker(rank, world, port, path, ep, out):
         if rank == 0:
             toks, lg = _run(eng)
             eng.stop_followers()
-            out.put((toks, lg.numpy(), comm.stats["all_reduce"]))
+            out.put((toks, lg.numpy(), comm.stats["all_reduce"], eng.counters["candidate_sampled_steps"]))
         else:
             eng.follow()
     finally:
@@ -95,7 +104,7 @@ def test_tp2_matches_tp1(tmp_path, fam, ep):
     try:
         while True:
             try:
-                toks, lg, n_ar = q.get(timeout=2)
+                toks, lg, n_ar, n_cand = q.get(timeout=2)
                 break
             except queue.Empty:
                 if any(p.exitcode not in (None, 0) for p in procs) or time.time() - t0 > 300:
@@ -107,6 +116,7 @@ def test_tp2_matches_tp1(tmp_path, fam, ep):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     assert n_ar > 0
+    assert n_cand > 0                  # the top-k requests went through the candidate gather
     assert toks == ref_toks
     ref = ref_lg[:, :lg.shape[1]].numpy()
     assert lg.shape[1] == spec.vocab
