@@ -1344,3 +1344,36 @@ def test_moe_combine_norm(gpu, T, k, D):
     ops.moe_combine_norm(y.to(gpu), w.to(gpu), T, k, xg, 0.7, nw.to(gpu), 1e-5, h)
     _close(xg, ref, 1e-5)
     _close(h, href, 1e-2)
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_candidate_sampling_matches_full_vocab(gpu, shards):
+    """TP sampling draws from the per-rank top-128 candidates (ops.topc_candidates, vocabulary order): the
+    GPU sampler on the concatenated candidate rows, with history ids mapped to candidate positions, gives
+    the token the GPU sampler gives on the full [rows, vocab] logits (top_k <= 64, penalties, top-p, min-p)."""
+    from nats_llm_studio_amd.engine.sampling import SamplingParams, sample_rows_gpu, uniform01
+    V, n, C = 32000, 6, 128
+    g = torch.Generator().manual_seed(5)
+    lg = (torch.randn(n, V, generator=g) * 3.0).to(gpu)
+    params = [SamplingParams(temperature=0.8, top_k=40, top_p=0.95, repeat_penalty=1.2, seed=3),
+              SamplingParams(temperature=1.3, top_k=64, min_p=0.02, presence_penalty=0.5, seed=7),
+              SamplingParams(temperature=0.5, top_k=5),
+              SamplingParams(temperature=1.0, top_k=1),
+              SamplingParams(temperature=0.0, repeat_penalty=1.5),           # penalised arg-max
+              SamplingParams(temperature=0.9, top_k=60, top_p=0.5, frequency_penalty=0.3)]
+    top = torch.topk(lg, 80, dim=1).indices.cpu()
+    hist = [top[r, torch.randperm(80, generator=g)[:30]].tolist() * 2 for r in range(n)]   # repeats: counts
+    us = [uniform01(100 + r, 7) for r in range(n)]
+    ref = sample_rows_gpu(lg.clone(), params, hist, us)
+    per = -(-V // shards)
+    vals, ids = [], []
+    for r in range(shards):
+        lo = r * per
+        cv_r, ci_r = ops.topc_candidates(lg[:, lo:lo + per].contiguous(), n, C, lo, min(per, V - lo))
+        vals.append(cv_r)
+        ids.append(ci_r)
+    cv, ci = torch.cat(vals, 1), torch.cat(ids, 1)
+    ixl = ci.cpu().tolist()
+    mh = [[{t: j for j, t in enumerate(ixl[r])}[t] for t in hist[r][-64:] if t in set(ixl[r])] for r in range(n)]
+    picks = sample_rows_gpu(cv.contiguous(), params, mh, us)
+    assert [ixl[r][j] for r, j in enumerate(picks)] == ref
