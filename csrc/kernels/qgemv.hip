@@ -40,6 +40,8 @@ struct NlsFuse {
   void* hout; long ldh; const float* onw; int* cnt;                          // residual add + RMSNorm
   float* ssq_out; const float* ssq_in; int ldss, nss_in;                     // split RMSNorm (GemvArgs)
   const int* sel; int sel_slots, sel_base, pad1;                             // device-selected segments
+  const void* wr; int E, topk, renorm, rcap;                                 // MoE route after the norm (onw)
+  float* rlogits; float* topw; int* counts; int* xrows; int* yrows; int* rsel;
 };
 
 // mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
@@ -91,6 +93,9 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (fz->onw && (mode != 0 || epi != EPI_ADD_F32 || nseg != 1 || segs[0].ycol || segs[0].xmap || segs[0].ymap ||
                   segs[0].mcount || !fz->cnt || !fz->hout || segs[0].rows % 4 || argmax))
+    return -1;
+  if (fz->wr && (!fz->onw || M > 4 || fz->E < 1 || fz->E > 64 || fz->topk < 1 || fz->topk > fz->E || fz->topk > 8 ||
+                 !fz->rlogits || !fz->topw || !fz->counts || !fz->xrows || !fz->yrows || segs[0].rows % 4))
     return -1;
   if (fz->sel) {           // path A over routed experts only: identical segment shapes
     if (mode != 0 || fz->sel_slots < 1 || fz->sel_slots > 256 || argmax) return -1;
@@ -208,6 +213,17 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   a.sel_base = fz->sel_base;
   a.sel_tiles = (segs[0].rows + tile_rows - 1) / tile_rows;
   if (fz->sel) tiles = fz->sel_slots * a.sel_tiles;
+  a.wr = (const act_t*)fz->wr;
+  a.E = fz->E;
+  a.topk = fz->topk;
+  a.renorm = fz->renorm;
+  a.rcap = fz->rcap;
+  a.rlogits = fz->rlogits;
+  a.topw = fz->topw;
+  a.counts = fz->counts;
+  a.xrows = fz->xrows;
+  a.yrows = fz->yrows;
+  a.rsel = fz->rsel;
   a.ssq_out = fz->ssq_out;
   a.ssq_in = fz->ssq_in;
   a.ldss = fz->ldss;

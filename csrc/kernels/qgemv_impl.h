@@ -17,6 +17,7 @@
 // gate/up rows, and a fused greedy arg-max (packed u64 atomicMax per row).
 #pragma once
 #include "common.h"
+#include "moe_route.h"
 
 namespace nls_gemv {
 
@@ -64,6 +65,11 @@ struct GemvArgs {
   // sel_base (out of range or a repeat of an earlier slot: exit), tile i % sel_tiles of it -- only the
   // routed experts' tiles are launched instead of every expert's (most of which would exit at once)
   const int* sel; int sel_tiles, sel_base, pad1;
+  // MoE decode (with onw): after the residual update + FFN RMSNorm the last workgroup also computes the router
+  // logits hout . wr[e] (wr: the router's f16 copy [E][D]) and the top-k route (route_one) -- the separate
+  // norm + router + route launch folded away. counts [E] are zeroed here first.
+  const act_t* wr; int E, topk, renorm, rcap;
+  float* rlogits; float* topw; int* counts; int* xrows; int* yrows; int* rsel;
 };
 
 // inv[m] = 1 / rms of rows m < M from producer partial sums of squares (see GemvArgs::ssq_in); one
@@ -158,6 +164,47 @@ DEVI void rope_store1(const GemvArgs& a, int col, int b, float v, float p) {
     d = a.vc + ((size_t)s * a.Hkv + (h - a.Hq - a.Hkv)) * a.D + dd;
   }
   if (d) *d = (__bf16)y;
+}
+
+// MoE route in the last workgroup (GemvArgs::wr): router logits of the M normalised rows hout (f16, as
+// moe_norm_route_kernel multiplies them) against the f16 router copy, then one wave per token routes it.
+// scratch: >= NT / 64 * 64 + 4 * 64 floats.
+template <int NT>
+DEVI void route_rows(const GemvArgs& a, int M, int D, float* scratch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int NW = NT / 64;
+  float* red = scratch;                  // [NW][64]
+  float* lg = scratch + NW * 64;         // [4][64]
+  for (int e = threadIdx.x; e < a.E; e += NT) a.counts[e] = 0;
+  __syncthreads();                       // (hout written above and the counts zeroed, visible to the workgroup)
+  for (int t = 0; t < M; ++t) {
+    const act_t* hr = a.hout + (size_t)t * a.ldh;
+    for (int e = 0; e < a.E; ++e) {
+      const act_t* wr = a.wr + (size_t)e * D;
+      float acc = 0.f;
+      for (int i = threadIdx.x * 4; i < D; i += NT * 4) {
+        typedef act_t act4 __attribute__((ext_vector_type(4)));
+        const act4 hv = *reinterpret_cast<const act4*>(hr + i);
+        const act4 wv = *reinterpret_cast<const act4*>(wr + i);
+        acc += (float)hv.x * (float)wv.x + (float)hv.y * (float)wv.y + (float)hv.z * (float)wv.z +
+               (float)hv.w * (float)wv.w;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (lane == 0) red[wave * 64 + e] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < a.E) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s2 += red[w * 64 + threadIdx.x];
+      lg[t * 64 + threadIdx.x] = s2;
+      a.rlogits[(size_t)t * a.E + threadIdx.x] = s2;
+    }
+    __syncthreads();
+  }
+  if (wave < M) route_one(lg + wave * 64, wave, lane, a.E, a.topk, a.renorm, a.topw, a.counts, a.xrows, a.yrows,
+                          a.rcap, a.rsel);
 }
 
 DEVI unsigned long long argmax_key(float v, int idx) {
@@ -542,6 +589,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
     if (!last_arriver(a.cnt, gridDim.x, flag)) return;
     rows_rmsnorm<WAVES * 64>(reinterpret_cast<const float*>(a.y), a.ldy, mcount, a.pad, a.onw, a.eps, a.hout, a.ldh,
                              lds + 16);
+    if (a.wr) route_rows<WAVES * 64>(a, mcount, a.pad, lds + 16);
     return;
   }
   if (a.argmax) {

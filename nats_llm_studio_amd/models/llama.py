@@ -46,6 +46,10 @@ _MOE_GEMM_T = int(os.environ.get("NLS_MOE_GEMM_T", "16"))
 # MoE decode at up to this many tokens (<= 4) fuses the FFN input RMSNorm, the router and the route
 # into one launch (ops.moe_norm_route); 0 disables
 _MOE_NORM_ROUTE_T = min(4, int(os.environ.get("NLS_MOE_NORM_ROUTE", "4")))
+# ... and with NLS_MOE_FOLD_ROUTE=1 that launch is folded into the o projection's last workgroup. Off: the
+# last-arriver tail (norm, E router dot products, route on one workgroup) measured slower than the launch it
+# removes (Mixtral batch 1: 3.50 vs 3.25 ms/token, batch 4: 7.38 vs 6.85; profiles/mixtral_b1_r03.txt)
+_MOE_FOLD_ROUTE = os.environ.get("NLS_MOE_FOLD_ROUTE", "0") == "1"
 # MoE decode (path-A expert GEMVs): launch config (mode, waves, rt, ks) of the DOWN projection, whose
 # K (d_ff) is 3.5x the gate/up's; empty: ops.MOE_GEMV like gate/up
 _MOE_GEMV_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_GEMV_DN", "").split(",") if v)
@@ -423,7 +427,18 @@ class LlamaModel:
                               block_size, cfg.attn_softmax_scale, chunk=-_MIN_CHUNK, n_split=n_split, workspace=b.attn_ws,
                               counters=b.attn_cnt)
             moe_norm = fused and lw.router16 is not None and T <= _MOE_NORM_ROUTE_T
-            if moe_norm:
+            moe_routed = False
+            if moe_norm and _MOE_FOLD_ROUTE and x.is_cuda:
+                # the o projection's last workgroup applies the FFN norm, the router and the route
+                m = b.moe
+                use_sel = T * cfg.n_expert_used < len(self.experts)
+                moe_routed = ops.qgemv_add_norm_route(
+                    Seg(lw.wo), b.ao, x, lw.ffn_norm, b.h, T, cfg.residual_scale, cfg.eps, b.cnt, lw.router16,
+                    m["rlogits"], cfg.n_expert_used, m["topw"], m["counts"], m["xrows"], m["yrows"], x.shape[0],
+                    sel=m["sel"] if use_sel else None)
+            if moe_routed:
+                pass
+            elif moe_norm:
                 # the FFN input norm runs inside the MoE router/route launch (ops.moe_norm_route)
                 ops.qgemv([Seg(lw.wo)], b.ao, x, T, alpha=cfg.residual_scale, epi="add")
             elif fused:
@@ -436,7 +451,8 @@ class LlamaModel:
             nxt = self.layers[L + 1].attn_norm if L + 1 < len(self.layers) else self.out_norm
             fused_prev = False
             if cfg.n_expert:
-                fused_prev = self._moe(lw, b, T, nxt if fused else None, lw.ffn_norm if moe_norm else None)
+                fused_prev = self._moe(lw, b, T, nxt if fused else None,
+                                       lw.ffn_norm if moe_norm and not moe_routed else None, routed=moe_routed)
             else:
                 ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
                 if fused:
@@ -519,7 +535,7 @@ class LlamaModel:
             self.comm.row_parallel_add(w, xin, resid, T, alpha)
 
     def _moe(self, lw: LayerWeights, b: StepBuffers, T: int, next_norm: Optional[torch.Tensor] = None,
-             in_norm: Optional[torch.Tensor] = None) -> bool:
+             in_norm: Optional[torch.Tensor] = None, routed: bool = False) -> bool:
         """Top-k routed experts: router GEMV -> route kernel (per-expert row lists on device)
         -> grouped expert GEMVs (tiles of experts with no routed rows exit before reading
         weights) -> deterministic weighted combine into the residual. `in_norm` (<= 4 tokens): b.h is
@@ -529,8 +545,8 @@ class LlamaModel:
         m = b.moe
         k, E = cfg.n_expert_used, cfg.n_expert
         cap = b.x.shape[0]
-        routed = False
-        if in_norm is not None:
+        # routed: the o projection already normalised b.h and routed the tokens (ops.qgemv_add_norm_route)
+        if in_norm is not None and not routed:
             use_sel = self.device.type == "cuda" and T * k < len(self.experts)
             routed = ops.moe_norm_route(b.x, in_norm, cfg.eps, lw.router16, b.h, m["rlogits"], T, k, m["topw"],
                                         m["counts"], m["xrows"], m["yrows"], cap, sel=m["sel"] if use_sel else None)

@@ -574,6 +574,31 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
     return rmsnorm(x, norm_w, h, M, eps)
 
 
+def qgemv_add_norm_route(seg: Seg, xin: torch.Tensor, x: torch.Tensor, nw: torch.Tensor, h: torch.Tensor, M: int,
+                         alpha: float, eps: float, counter: torch.Tensor, wr: torch.Tensor, logits: torch.Tensor, k: int,
+                         topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor, yrows: torch.Tensor, cap: int,
+                         renorm: bool = True, sel: Optional[torch.Tensor] = None) -> bool:
+    """MoE decode (M <= 4 tokens): the o projection x[:M] += alpha * xin @ W^T, then -- in its last workgroup --
+    the FFN RMSNorm h = f16(rmsnorm(x) * nw), the router logits h @ wr^T and the top-k route (moe_route): the
+    separate norm + router + route launch (moe_norm_route) folded into the projection. False (nothing done)
+    where the fused launch does not apply; the caller then runs the two launches."""
+    if not x.is_cuda or seg.xmap is not None or seg.ycol or seg.w.rows != x.shape[1] or M > 4:
+        return False
+    mode, waves, rt, ks = gemv_config([seg], M)
+    if mode != 0:
+        mode, waves, rt, ks = 0, 4, 1, 1
+    fz = _lib.NlsFuse(hout=h.data_ptr(), ldh=h.stride(0), onw=nw.data_ptr(), cnt=counter.data_ptr(), eps=float(eps),
+                      wr=wr.data_ptr(), E=int(wr.shape[0]), topk=int(k), renorm=int(renorm), rcap=int(cap),
+                      rlogits=logits.data_ptr(), topw=topw.data_ptr(), counts=counts.data_ptr(),
+                      xrows=xrows.data_ptr(), yrows=yrows.data_ptr(), rsel=_p(sel))
+    rc = _lib.lib().nls_qgemv_ex(_segs([seg]), 1, xin.data_ptr(), xin.stride(0), x.data_ptr(), x.stride(0), M,
+                                 float(alpha), EPI["add"], None, waves, rt, 0, 1, None, _stream_ptr(x), ctypes.byref(fz))
+    if rc == -1:
+        return False
+    _lib.check(rc, "nls_qgemv_ex(add+norm+route)")
+    return True
+
+
 def _argmax_keys(v: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     u = v.float().view(torch.int32).long() & 0xFFFFFFFF
     neg = (u & 0x80000000) != 0

@@ -33,7 +33,10 @@ class NlsFuse(ctypes.Structure):
                 ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("pad0", c_int),
                 ("hout", c_void_p), ("ldh", c_long), ("onw", c_void_p), ("cnt", c_void_p),
                 ("ssq_out", c_void_p), ("ssq_in", c_void_p), ("ldss", c_int), ("nss_in", c_int),
-                ("sel", c_void_p), ("sel_slots", c_int), ("sel_base", c_int), ("pad1", c_int)]
+                ("sel", c_void_p), ("sel_slots", c_int), ("sel_base", c_int), ("pad1", c_int),
+                ("wr", c_void_p), ("E", c_int), ("topk", c_int), ("renorm", c_int), ("rcap", c_int),
+                ("rlogits", c_void_p), ("topw", c_void_p), ("counts", c_void_p), ("xrows", c_void_p),
+                ("yrows", c_void_p), ("rsel", c_void_p)]
 
 
 _SIGS = {

@@ -221,3 +221,27 @@ def test_seeded_sampling_same_on_device_and_host_paths(gpu, tiny_models, monkeyp
     b, nb = run(False)
     assert na > 0 and nb == 0
     assert a == b, (a, b)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_moe_folded_route_matches_separate_launch(gpu, tiny_models, graphs, monkeypatch):
+    """MoE decode at <= 4 tokens: the FFN norm + router + top-k route in the o projection's last workgroup
+    (ops.qgemv_add_norm_route) == the separate moe_norm_route launch, token for token (both multiply the same
+    f16 normalised rows with the router's f16 copy)."""
+    from nats_llm_studio_amd.engine.engine import Engine, GenRequest
+    from nats_llm_studio_amd.engine.sampling import SamplingParams
+    from nats_llm_studio_amd.gguf.reader import GGUFReader
+    from nats_llm_studio_amd.models import llama
+    r = GGUFReader(tiny_models["tiny-mixtral"])
+    outs = []
+    for fold in (False, True):
+        monkeypatch.setattr(llama, "_MOE_FOLD_ROUTE", fold)
+        m = llama.LlamaModel(r, gpu)
+        eng = Engine(m, None, max_batch=4, num_blocks=64, use_graphs=graphs, ctx=256)
+        futs = [eng.submit(GenRequest([1, 2, 3, 40 + i], SamplingParams(max_tokens=12, ignore_eos=True)))
+                for i in range(3)]
+        while not all(f.done() for f in futs):
+            eng.step()
+        outs.append([f.result().token_ids for f in futs])
+        eng.shutdown()
+    assert outs[0] == outs[1], outs
