@@ -46,7 +46,13 @@ def heuristic(segs, M: int):
     rows = sum(s.w.rows for s in segs)
     K = segs[0].w.K
     if M <= 8:
-        return (0, 8, 1, 1)
+        # the batch-1 winners of every measured family (Llama-3-8B / -70B, Qwen2.5-7B, Mixtral; r03 sweeps,
+        # profiles/b1_latency_r03.txt, profiles/b1_models_r03.txt): 4-wave workgroups; wide matrices (gate|up,
+        # LM head) on path B's staged-x stream, fused Q|K|V on 32-row path-A tiles, the rest on 16-row ones.
+        # The old (0, 8, 1, 1) default cost Llama-3-70B / Qwen2.5-7B ~30 % at batch 1.
+        if rows >= 4 * K:
+            return (1, 4, 2, 2) if rows >= 16 * K and K >= 1024 else (1, 4, 2, 1)
+        return (0, 4, 2, 1) if len(segs) > 1 else (0, 4, 1, 1)
     if M > 64:
         if all(int(s.w.type) in (12, 13, 14) for s in segs):
             # LDS-dequant GEMM (mode 2): 128 weight rows x 256 (or 128) activation rows per workgroup;

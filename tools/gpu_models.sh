@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export PYTHONPATH=$PWD
 mkdir -p gpurun_out
 run() {  # name model ftype concurrency
-  timeout -k 10 420 python -u bench.py --no-rtt --model $2 --ftype $3 --concurrency $4 --steps 20 --warmup 3 > gpurun_out/models_$1.log 2>&1
+  timeout -k 10 420 python -u bench.py --no-rtt --serve-load 0 --tp-leg 0 --model $2 --ftype $3 --concurrency $4 --steps 20 --warmup 3 > gpurun_out/models_$1.log 2>&1
   local rc=$?
   echo "$1 rc=$rc $(tail -1 gpurun_out/models_$1.log | cut -c1-330)"
   case $rc in 124|134|137|139) exit $rc ;; esac
