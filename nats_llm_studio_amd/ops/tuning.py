@@ -114,6 +114,42 @@ def select_lib(segs, M: int) -> bool:
     return bool(table().get(lib_key(segs, M), (0,))[0])
 
 
+# Llama-3-8B Q4_K_M shapes per projection role: the tuned entries an untuned shape of the same role borrows at
+# the same batch bucket (M <= 64), e.g. Llama-3-70B / Qwen2.5-7B / Mixtral attention and dense FFN shapes
+_ROLE_KEYS = {"qkv": "12+12+12:6144:4096", "o": "12:4096:4096", "gateup": "12:28672:4096", "down": "12:4096:14336",
+              "lm_head": "14:128256:4096"}
+
+
+def _role(segs) -> str:
+    rows = sum(s.w.rows for s in segs)
+    K = segs[0].w.K
+    if len(segs) > 1:
+        return "qkv"
+    if rows >= 16 * K:
+        return "lm_head"
+    if rows >= 4 * K:
+        return "gateup"
+    if K >= 2 * rows:
+        return "down"
+    return "o"
+
+
+def _role_entry(segs, M: int):
+    """The Llama-3-8B entry of this shape's role and batch bucket, for a shape within 1.5x of that role's
+    Llama-3-8B rows and K (Qwen2.5-7B, Mixtral attention: batch 16 / 64 2.70 / 4.30 vs 3.57 / 5.06 ms/step
+    with the generic heuristic). Larger shapes keep the heuristic, whose split-K follows their own tile
+    count (Llama-3-70B batch 64: 22.7 vs 24.4 ms/step borrowing); profiles/b1_models_r03.txt."""
+    ref = _ROLE_KEYS[_role(segs)]
+    _, rrows, rk = ref.split(":")
+    rows, K = sum(s.w.rows for s in segs), segs[0].w.K
+    near = lambda a, b: max(a, b) < 1.5 * min(a, b)
+    if not (near(rows, int(rrows)) and near(K, int(rk))):
+        return None
+    return table().get(f"{ref}:{_mb(M)}")
+
+
 def select(segs, M: int):
     hit = table().get(key(segs, M))
+    if hit is None and M <= 64 and os.environ.get("NLS_TUNING_ROLE", "1") == "1":
+        hit = _role_entry(segs, M)
     return hit if hit is not None else heuristic(segs, M)
