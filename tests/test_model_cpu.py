@@ -184,3 +184,29 @@ def test_reference_streaming_decode_matches_cached(tiny_models):
         a = ReferenceModel(r).logits(ids)
         b = ReferenceModel(r, cache=False, workers=4).logits(ids)
         assert torch.equal(a, b)
+
+
+def test_tuning_role_fallback_scope(monkeypatch):
+    """Untuned few-row shapes within 1.5x of a Llama-3-8B projection (Qwen2.5-7B) borrow that role's tuned
+    entry; larger shapes (Llama-3-70B) keep the generic heuristic; NLS_TUNING_ROLE=0 turns borrowing off;
+    an exact table entry always wins (ops/tuning.py select)."""
+    from types import SimpleNamespace as N
+    from nats_llm_studio_amd.ops import tuning
+
+    def segs(*parts):
+        return [N(w=N(type=t, rows=r, K=k)) for t, r, k in parts]
+
+    tab = tuning.table()
+    qwen_gu, qwen_qkv = segs((12, 37888, 3584)), segs((12, 3584, 3584), (12, 512, 3584), (12, 512, 3584))
+    l70_o = segs((12, 8192, 8192))
+    for M in (16, 64):
+        assert tuning.key(qwen_gu, M) not in tab
+        assert tuning._role(qwen_gu) == "gateup" and tuning._role(qwen_qkv) == "qkv" and tuning._role(l70_o) == "o"
+        assert tuning.select(qwen_gu, M) == tab[f"12:28672:4096:{M}"]
+        assert tuning.select(qwen_qkv, M) == tab[f"12+12+12:6144:4096:{M}"]
+        assert tuning._role_entry(l70_o, M) is None
+        assert tuning.select(l70_o, M) == tuning.heuristic(l70_o, M)
+    monkeypatch.setenv("NLS_TUNING_ROLE", "0")
+    assert tuning.select(qwen_gu, 16) == tuning.heuristic(qwen_gu, 16)
+    monkeypatch.setitem(tab, tuning.key(qwen_gu, 16), (0, 4, 1, 1))
+    assert tuning.select(qwen_gu, 16) == (0, 4, 1, 1)
