@@ -1,10 +1,12 @@
 // Causal flash attention for prefill over the paged KV cache, on MFMA (gfx950).
 // SURVEY.md §2F attn_prefill.
 //
-// Work item = one "query block": up to 16 consecutive prompt tokens of ONE sequence
-// (t0, ntok, seq, pos0) -- the engine cuts each sequence's prefill chunk into such blocks.
-// Workgroup = (query block, kv head, quad of query heads): its 4 waves are 4 query heads of
-// the same GQA group, so every K/V tile is staged in LDS once and used by 4 heads.
+// Work item = one "query block": up to 16 * NSUB consecutive prompt tokens of ONE sequence
+// (t0, ntok, seq, pos0) -- the engine cuts each sequence's prefill chunk into such blocks
+// (ops.prefill_blocks, PREFILL_QT). Workgroup = (query block, kv head, quad of query heads): its 4
+// waves are 4 query heads of the same GQA group and each wave runs the block's NSUB 16-token
+// sub-tiles, so every K/V tile staged in LDS serves 4 heads x 16 * NSUB tokens (NSUB = 2: half the
+// K/V staging per query of 16-token blocks).
 //
 // Per 64-key tile and wave (16 tokens x 1 head):
 //   S^T = K Q^T    v_mfma_f32_16x16x32_bf16, A = K rows from LDS, B = Q^T from registers.
@@ -21,6 +23,8 @@
 namespace {
 
 constexpr float LOG2E_P = 1.4426950408889634f;
+
+constexpr int NSUB = 2;            // 16-token sub-tiles per query block (ops.PREFILL_QT = 16 * NSUB)
 
 template <int D, typename KV>
 __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restrict__ q, long ldq,
@@ -46,18 +50,20 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
   const int* bt = block_tables + (size_t)seq * bt_stride;
   const float sl2 = scale * LOG2E_P;
 
-  bf16x8 qf[NKK];
-  {
-    const __bf16* qrow = q + (size_t)(t0 + min(r, ntok - 1)) * ldq + (size_t)head * D;
+  // per sub-tile u: tokens 16u .. 16u + 15 of the block (lane column r = token 16u + r)
+  bf16x8 qf[NSUB][NKK];
+  float m[NSUB], l[NSUB];
+  f32x4 o[NSUB][NDT];
 #pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + kk * 32 + 8 * g);
+  for (int u = 0; u < NSUB; ++u) {
+    const __bf16* qrow = q + (size_t)(t0 + min(16 * u + r, ntok - 1)) * ldq + (size_t)head * D;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) qf[u][kk] = *reinterpret_cast<const bf16x8*>(qrow + kk * 32 + 8 * g);
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int qpos = pos0 + r;                  // this lane's token (column of S^T)
-  const bool qvalid = r < ntok;
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkeys = pos0 + ntok;
   for (int k0 = 0; k0 < nkeys; k0 += KT) {
@@ -96,82 +102,92 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
     }
     __syncthreads();
 
-    // ---- S^T = K Q^T : s[nt][i] = S[token r][key k0 + nt*16 + 4g + i]
-    f32x4 s[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NSUB; ++u) {
+      if (16 * u >= ntok || k0 > pos0 + 16 * u + 15) continue;     // no token / every key of the tile is masked
+      const int qpos = pos0 + 16 * u + r;       // this lane's token (column of S^T)
+      const bool qvalid = 16 * u + r < ntok;
+      // ---- S^T = K Q^T : s[nt][i] = S[token r][key k0 + nt*16 + 4g + i]
+      f32x4 s[4];
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (nt * 16 + r) * KSTR + kk * 32 + 8 * g);
-        s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[kk], s[nt], 0, 0, 0);
+      for (int nt = 0; nt < 4; ++nt) {
+        s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (nt * 16 + r) * KSTR + kk * 32 + 8 * g);
+          s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[u][kk], s[nt], 0, 0, 0);
+        }
       }
-    }
-    // ---- causal mask + online softmax (base 2)
-    float mx = -INFINITY;
+      // ---- causal mask + online softmax (base 2)
+      float mx = -INFINITY;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = k0 + nt * 16 + 4 * g + i;
+          const float v = (qvalid && key <= qpos) ? s[nt][i] * sl2 : -INFINITY;
+          s[nt][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[u], mx);
+      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[u] - mn);
+      float ps = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = (mn == -INFINITY) ? 0.f : exp2f(s[nt][i] - mn);
+          s[nt][i] = p;
+          ps += p;
+        }
+      l[u] = l[u] * alpha + ps;
+      m[u] = mn;
+      // O rows are tokens 4g+i: their alpha lives in lane column 4g+i
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int key = k0 + nt * 16 + 4 * g + i;
-        const float v = (qvalid && key <= qpos) ? s[nt][i] * sl2 : -INFINITY;
-        s[nt][i] = v;
-        mx = fmaxf(mx, v);
+        const float ai = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) o[u][dt][i] *= ai;
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-    float ps = 0.f;
+      // ---- O += P V over two 32-key groups
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+      for (int kg = 0; kg < 2; ++kg) {
+        bf16x8 pa;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = (mn == -INFINITY) ? 0.f : exp2f(s[nt][i] - mn);
-        s[nt][i] = p;
-        ps += p;
-      }
-    l = l * alpha + ps;
-    m = mn;
-    // O rows are tokens 4g+i: their alpha lives in lane column 4g+i
+        for (int i = 0; i < 4; ++i) {
+          pa[i] = (__bf16)s[2 * kg][i];
+          pa[4 + i] = (__bf16)s[2 * kg + 1][i];
+        }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float ai = __shfl(alpha, 4 * g + i, 64);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) o[dt][i] *= ai;
-    }
-    // ---- O += P V over two 32-key groups
-#pragma unroll
-    for (int kg = 0; kg < 2; ++kg) {
-      bf16x8 pa;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pa[i] = (__bf16)s[2 * kg][i];
-        pa[4 + i] = (__bf16)s[2 * kg + 1][i];
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const __bf16* vrow = Vt + (dt * 16 + r) * VSTR + kg * 32 + 4 * g;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vrow);
-        const uint2 hi = *reinterpret_cast<const uint2*>(vrow + 16);
-        u32x4 bw = u32x4{lo.x, lo.y, hi.x, hi.y};
-        const bf16x8 b = __builtin_bit_cast(bf16x8, bw);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, b, o[dt], 0, 0, 0);
+        for (int dt = 0; dt < NDT; ++dt) {
+          const __bf16* vrow = Vt + (dt * 16 + r) * VSTR + kg * 32 + 4 * g;
+          const uint2 lo = *reinterpret_cast<const uint2*>(vrow);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vrow + 16);
+          u32x4 bw = u32x4{lo.x, lo.y, hi.x, hi.y};
+          const bf16x8 b = __builtin_bit_cast(bf16x8, bw);
+          o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, b, o[u][dt], 0, 0, 0);
+        }
       }
     }
   }
-  // ---- normalise and store: lane holds O[token 4g+i][dt*16 + r]
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  // ---- normalise and store: lane holds O[token 16u + 4g+i][dt*16 + r]
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tok = 4 * g + i;
-    const float li = __shfl(l, tok, 64);
-    if (tok < ntok) {
-      const float inv = li > 0.f ? 1.f / li : 0.f;
-      act_t* orow = out + (size_t)(t0 + tok) * ldo + (size_t)head * D;
+  for (int u = 0; u < NSUB; ++u) {
+    float lu = l[u];
+    lu += __shfl_xor(lu, 16, 64);
+    lu += __shfl_xor(lu, 32, 64);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) orow[dt * 16 + r] = (act_t)(o[dt][i] * inv);
+    for (int i = 0; i < 4; ++i) {
+      const int tok = 16 * u + 4 * g + i;
+      const float li = __shfl(lu, 4 * g + i, 64);
+      if (tok < ntok) {
+        const float inv = li > 0.f ? 1.f / li : 0.f;
+        act_t* orow = out + (size_t)(t0 + tok) * ldo + (size_t)head * D;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) orow[dt * 16 + r] = (act_t)(o[u][dt][i] * inv);
+      }
     }
   }
 }

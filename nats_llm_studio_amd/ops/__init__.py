@@ -831,8 +831,11 @@ def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables:
     return out
 
 
+PREFILL_QT = 32      # tokens per attention_prefill query block: 16 * NSUB of attn_prefill.hip
+
+
 def prefill_blocks(tok_seq, pos, T: int):
-    """Query blocks for attention_prefill: (t0, ntok<=16, seq, pos0) over runs of consecutive
+    """Query blocks for attention_prefill: (t0, ntok<=PREFILL_QT, seq, pos0) over runs of consecutive
     tokens of one sequence (numpy int arrays in, int32 [nqb, 4] out)."""
     ts = np.asarray(tok_seq[:T])
     ps = np.asarray(pos[:T])
@@ -843,8 +846,8 @@ def prefill_blocks(tok_seq, pos, T: int):
     ends = np.concatenate([cut, [T]])
     out = []
     for a, b in zip(starts, ends):
-        for t in range(a, b, 16):
-            out.append((t, min(16, b - t), ts[a], ps[t]))
+        for t in range(a, b, PREFILL_QT):
+            out.append((t, min(PREFILL_QT, b - t), ts[a], ps[t]))
     return np.asarray(out, dtype=np.int32).reshape(-1, 4)
 
 

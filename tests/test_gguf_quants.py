@@ -97,8 +97,9 @@ def test_tiled_layout_is_a_permutation(t):
 
 
 def test_prefill_blocks():
-    from nats_llm_studio_amd.ops import prefill_blocks
-    tseq = np.array([0] * 20 + [1] * 3 + [2] * 16)
-    pos = np.concatenate([np.arange(20), np.arange(50, 53), np.arange(16)])
+    from nats_llm_studio_amd.ops import PREFILL_QT as QT, prefill_blocks
+    assert 20 <= QT < 40 and QT % 16 == 0
+    tseq = np.array([0] * 40 + [1] * 3 + [2] * 16)
+    pos = np.concatenate([np.arange(40), np.arange(50, 53), np.arange(16)])
     qb = prefill_blocks(tseq, pos, len(tseq))
-    assert qb.tolist() == [[0, 16, 0, 0], [16, 4, 0, 16], [20, 3, 1, 50], [23, 16, 2, 0]]
+    assert qb.tolist() == [[0, QT, 0, 0], [QT, 40 - QT, 0, QT], [40, 3, 1, 50], [43, 16, 2, 0]]
