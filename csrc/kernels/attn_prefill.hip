@@ -8,7 +8,7 @@
 // sub-tiles, so every K/V tile staged in LDS serves 4 heads x 16 * NSUB tokens (NSUB = 2: half the
 // K/V staging per query of 16-token blocks).
 //
-// Per 64-key tile and wave (16 tokens x 1 head):
+// Per 96-key tile (KT) and wave sub-tile (16 tokens x 1 head):
 //   S^T = K Q^T    v_mfma_f32_16x16x32_bf16, A = K rows from LDS, B = Q^T from registers.
 //                  The transposed product puts one TOKEN per lane column, so each lane holds
 //                  4 consecutive keys of its token per 16-key n-tile: the row max / sum of the
@@ -27,13 +27,14 @@ constexpr float LOG2E_P = 1.4426950408889634f;
 constexpr int NSUB = 2;            // 16-token sub-tiles per query block (ops.PREFILL_QT = 16 * NSUB)
 
 template <int D, typename KV>
-__global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restrict__ q, long ldq,
+__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const __bf16* __restrict__ q, long ldq,
                                                            const KV* __restrict__ kc,
                                                            const KV* __restrict__ vc,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ qblocks, int Hkv, int G, int bs,
                                                            float scale, act_t* __restrict__ out, long ldo) {
-  constexpr int KT = 64;           // keys per tile
+  constexpr int KT = 96;           // keys per tile (a multiple of 32)
+  constexpr int NT16 = KT / 16;    // 16-key n-tiles of S^T per tile
   constexpr int KSTR = D + 8;      // K tile row stride (elements): conflict-free ds_read_b128
   constexpr int VSTR = KT + 8;     // Vt row stride (keys): conflict-free ds_read_b64
   constexpr int NKK = D / 32;      // k-steps of S^T over the head dim
@@ -108,9 +109,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
       const int qpos = pos0 + 16 * u + r;       // this lane's token (column of S^T)
       const bool qvalid = 16 * u + r < ntok;
       // ---- S^T = K Q^T : s[nt][i] = S[token r][key k0 + nt*16 + 4g + i]
-      f32x4 s[4];
+      f32x4 s[NT16];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < NT16; ++nt) {
         s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
       // ---- causal mask + online softmax (base 2)
       float mx = -INFINITY;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < NT16; ++nt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = k0 + nt * 16 + 4 * g + i;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
       const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[u] - mn);
       float ps = 0.f;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < NT16; ++nt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float p = (mn == -INFINITY) ? 0.f : exp2f(s[nt][i] - mn);
@@ -151,9 +152,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const __bf16* __restr
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) o[u][dt][i] *= ai;
       }
-      // ---- O += P V over two 32-key groups
+      // ---- O += P V over the tile's 32-key groups
 #pragma unroll
-      for (int kg = 0; kg < 2; ++kg) {
+      for (int kg = 0; kg < KT / 32; ++kg) {
         bf16x8 pa;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
