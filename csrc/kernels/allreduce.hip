@@ -262,7 +262,139 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Lossless one-shot all-gather of 32-bit words, and the fused vocab-parallel arg-max built on it --
+// the two exchanges of a tensor-parallel decode step besides the sums, so a captured TP decode graph
+// holds no RCCL call. Every word travels as two tagged dwords carrying 16 payload bits each (token
+// ids, packed arg-max keys and fp32 candidate logits arrive bit-exact, unlike the 30-bit sums above);
+// a 16-byte granule holds two words. Same slot / parity / consumed-tag protocol and bounded polls as
+// the all-reduce, on a buffer set of its own with its own fixed grid (AG_BLOCKS x AG_THREADS, grid-
+// stride over granules) and per-workgroup epochs, shared by the gather and the arg-max.
+#define AG_BLOCKS 16
+#define AG_THREADS 256
+
+__device__ __forceinline__ uint4 ag_pack2(uint32_t a, uint32_t b, uint32_t tag) {
+  return make_uint4(((a & 0xFFFFu) << 2) | tag, ((a >> 16) << 2) | tag, ((b & 0xFFFFu) << 2) | tag,
+                    ((b >> 16) << 2) | tag);
+}
+__device__ __forceinline__ uint2 ag_unpack2(uint4 g) {
+  return make_uint2((g.x >> 2) | ((g.y >> 2) << 16), (g.z >> 2) | ((g.w >> 2) << 16));
+}
+
+// src: this rank's n2 granules (2 * n2 words, laid out as `narr` arrays of rows x C words); dst receives
+// every rank's words with the rank inside the row: dst[a][row][p * C + c] (arrays of rows x world*C) --
+// per-rank top-C candidate lists come out as one vocabulary-ordered row per sequence
+__global__ __launch_bounds__(AG_THREADS) void oneshot_gather_kernel(const uint32_t* __restrict__ src, long n2,
+                                                                     uint32_t* __restrict__ dst, int C, long per_arr,
+                                                                     ArPeers P, int world, int rank, long cap,
+                                                                     unsigned* __restrict__ epochs,
+                                                                     int* __restrict__ err, long max_spins) {
+  __shared__ unsigned s_ep;
+  __shared__ int s_fail;
+  if (threadIdx.x == 0) {
+    s_ep = epochs[blockIdx.x] + 1u;
+    s_fail = 0;
+  }
+  __syncthreads();
+  const unsigned ep = s_ep;
+  const uint32_t tag = ep & 3u;
+  const int par = (int)(ep & 1u);
+  const long stride = (long)AG_BLOCKS * AG_THREADS;
+  auto out_at = [&](long w, int p) -> uint32_t* {
+    const long a = w / per_arr, rem = w - a * per_arr, r = rem / C, c = rem - r * C;
+    return dst + a * per_arr * world + r * (long)world * C + (long)p * C + c;
+  };
+  for (long i = (long)blockIdx.x * AG_THREADS + threadIdx.x; i < n2; i += stride) {
+    const uint2 v = reinterpret_cast<const uint2*>(src)[i];
+    const uint4 g = ag_pack2(v.x, v.y, tag);
+    for (int p = 0; p < world; ++p)
+      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + 4 * i, g);
+    uint32_t* o = out_at(2 * i, rank);
+    o[0] = v.x;
+    o[1] = v.y;
+  }
+  uint32_t* mine = P.buf[rank];
+  const uint32_t ct = (ep + 1u) & 3u;
+  bool failed = false;
+  for (long i = (long)blockIdx.x * AG_THREADS + threadIdx.x; i < n2; i += stride) {
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      uint32_t* s = mine + ((long)(par * world + p)) * cap + 4 * i;
+      const uint2 v = ag_unpack2(ar_poll(s, tag, max_spins, failed));
+      ar_store(s, make_uint4(ct, ct, ct, ct));
+      uint32_t* o = out_at(2 * i, p);       // C even: both words of a granule share the row
+      o[0] = v.x;
+      o[1] = v.y;
+    }
+  }
+  if (failed) s_fail = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    epochs[blockIdx.x] = ep;
+    if (s_fail) ar_raise(P, world, cap, err);
+  }
+}
+
+// Vocab-parallel greedy pick: each rank's fused arg-max key of row i (ordered value bits << 32 | ~local id)
+// is rebased to the global id (~local - vocab_lo == ~(local + vocab_lo)), exchanged (one granule per row),
+// and the unsigned max over ranks gives the same token on every rank; the key is re-armed (0) for the next
+// lm-head launch. Replaces xor / sub / RCCL MAX all-reduce / xor / unpack.
+__global__ __launch_bounds__(AG_THREADS) void oneshot_argmax_kernel(unsigned long long* __restrict__ keys, int n,
+                                                                     unsigned vocab_lo, int* __restrict__ next_ids,
+                                                                     ArPeers P, int world, int rank, long cap,
+                                                                     unsigned* __restrict__ epochs,
+                                                                     int* __restrict__ err, long max_spins) {
+  __shared__ unsigned s_ep;
+  __shared__ int s_fail;
+  if (threadIdx.x == 0) {
+    s_ep = epochs[blockIdx.x] + 1u;
+    s_fail = 0;
+  }
+  __syncthreads();
+  const unsigned ep = s_ep;
+  const uint32_t tag = ep & 3u;
+  const int par = (int)(ep & 1u);
+  const int stride = AG_BLOCKS * AG_THREADS;
+  for (int i = blockIdx.x * AG_THREADS + threadIdx.x; i < n; i += stride) {
+    const unsigned long long k = keys[i];
+    const uint4 g = ag_pack2((uint32_t)k - vocab_lo, (uint32_t)(k >> 32), tag);
+    for (int p = 0; p < world; ++p)
+      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + 4L * i, g);
+  }
+  uint32_t* mine = P.buf[rank];
+  const uint32_t ct = (ep + 1u) & 3u;
+  bool failed = false;
+  for (int i = blockIdx.x * AG_THREADS + threadIdx.x; i < n; i += stride) {
+    const unsigned long long k = keys[i];
+    unsigned long long best = (k & 0xFFFFFFFF00000000ull) | (unsigned long long)((uint32_t)k - vocab_lo);
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      uint32_t* s = mine + ((long)(par * world + p)) * cap + 4L * i;
+      const uint2 v = ag_unpack2(ar_poll(s, tag, max_spins, failed));
+      ar_store(s, make_uint4(ct, ct, ct, ct));
+      const unsigned long long c = ((unsigned long long)v.y << 32) | v.x;
+      best = c > best ? c : best;
+    }
+    next_ids[i] = (int)~(uint32_t)best;
+    keys[i] = 0ull;
+  }
+  if (failed) s_fail = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    epochs[blockIdx.x] = ep;
+    if (s_fail) ar_raise(P, world, cap, err);
+  }
+}
+
 __global__ void ar_err_clear_kernel(uint32_t* w) { *w = 0u; }
+
+// every receive slot back to its initial tag (parity 0: 1, parity 1: 0) and the error word cleared -- the
+// state after nls_ar_alloc; used (with zeroed epochs, on every rank, between barriers) after a timeout
+__global__ void ar_reinit_kernel(uint32_t* buf, long half) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * half + AR_ERR_BYTES / 4; i += stride)
+    buf[i] = i < half ? 0x01010101u : 0u;
+}
 
 extern "C" {
 
@@ -343,6 +475,42 @@ int nls_ar_addnorm_sim(const float* part, long ldp, float* x, long ldx, const fl
   hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(rows * sim, nls_ar_row_blocks(D)), dim3(ARN_THREADS), 0,
                      (hipStream_t)stream, part, ldp, x, ldx, nw, (_Float16*)h, ldh, D, eps, P, world, rank, cap, epochs,
                      tickets, ssq, err, max_spins, sim, sp, sx, sh, se, st, sq);
+  return (int)hipGetLastError();
+}
+
+int nls_ag_blocks() { return AG_BLOCKS; }
+
+// all-gather of 2 * n2 words (narr arrays of per_arr = rows * C words; C even) -> dst (see the kernel)
+int nls_ag_run(const void* src, long n2, void* dst, int C, long per_arr, void* const* peers, int world, int rank,
+               long cap, unsigned* epochs, int* err, long max_spins, void* stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n2 < 0 || 4 * n2 > cap || C < 2 || C % 2 ||
+      per_arr < C || per_arr % C || (2 * n2) % per_arr)
+    return -1;
+  ArPeers P;
+  for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
+  hipLaunchKernelGGL(oneshot_gather_kernel, dim3(AG_BLOCKS), dim3(AG_THREADS), 0, (hipStream_t)stream,
+                     (const uint32_t*)src, n2, (uint32_t*)dst, C, per_arr, P, world, rank, cap, epochs, err, max_spins);
+  return (int)hipGetLastError();
+}
+
+// keys (u64 [n], fused arg-max of this rank's vocab shard starting at vocab_lo) -> next_ids on every rank
+int nls_ag_argmax(void* keys, int n, int vocab_lo, void* next_ids, void* const* peers, int world, int rank, long cap,
+                  unsigned* epochs, int* err, long max_spins, void* stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || 4L * n > cap || vocab_lo < 0)
+    return -1;
+  ArPeers P;
+  for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
+  hipLaunchKernelGGL(oneshot_argmax_kernel, dim3(AG_BLOCKS), dim3(AG_THREADS), 0, (hipStream_t)stream,
+                     (unsigned long long*)keys, n, (unsigned)vocab_lo, (int*)next_ids, P, world, rank, cap, epochs, err,
+                     max_spins);
+  return (int)hipGetLastError();
+}
+
+// this rank's receive buffer back to the freshly allocated state (callers: every rank, no kernel in flight)
+int nls_ar_reinit(void* buf, long cap, int world, void* stream) {
+  if (world < 1 || world > AR_MAX_RANKS || cap % 4) return -1;
+  hipLaunchKernelGGL(ar_reinit_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, (uint32_t*)buf,
+                     (long)world * cap);
   return (int)hipGetLastError();
 }
 

@@ -353,7 +353,68 @@ __global__ __launch_bounds__(NT) void sample_decode_kernel(float* __restrict__ l
   }
 }
 
+// Tensor-parallel variant: the row is the gathered candidate list of every rank (values `cand` [n, M] in
+// vocabulary order, global ids `ids`, (-inf, -1) padding) instead of the full vocabulary. The history ring
+// (token ids) is mapped to candidate positions first -- a history token outside the candidates cannot
+// reach the kept set (the engine only takes this path when penalties can only LOWER logits and top-k fits
+// the candidates: Engine._cand_ok) -- then the same sampler draws a position, whose id is the token.
+constexpr int MAXC = 1024;
+__global__ __launch_bounds__(NT) void sample_decode_cand_kernel(float* __restrict__ cand, long ld, int M,
+                                                                const int* __restrict__ ids, long ldi,
+                                                                const SampleParams* __restrict__ params,
+                                                                const unsigned long long* __restrict__ seeds,
+                                                                const int* __restrict__ pos,
+                                                                const int* __restrict__ ctx_len,
+                                                                int* __restrict__ hist, int hist_stride,
+                                                                int* __restrict__ next_ids) {
+  __shared__ float red[NT / 64];
+  __shared__ float s_chunk[MAXT];
+  __shared__ int s_tok;
+  __shared__ float hbin[NB];
+  __shared__ int s_ids[MAXC];
+  __shared__ int s_hpos[NT];
+  const int row = blockIdx.x;
+  const SampleParams p = params[row];
+  const bool penal = p.repeat_penalty != 1.f || p.presence_penalty != 0.f || p.frequency_penalty != 0.f;
+  if (ctx_len[row] <= 0 || (p.temperature <= 0.f && !penal)) return;     // padding / greedy row
+  const int* idr = ids + (size_t)row * ldi;
+  for (int i = threadIdx.x; i < M; i += NT) s_ids[i] = idr[i];
+  const int ps = pos[row];
+  int* h = hist + (size_t)row * hist_stride;
+  const int n_hist = min(hist_stride, ps + 1);
+  __syncthreads();
+  if (threadIdx.x < n_hist) {
+    const int id = h[threadIdx.x];
+    int at = -1;
+    if (id >= 0)
+      for (int i = 0; i < M; ++i)
+        if (s_ids[i] == id) {
+          at = i;
+          break;
+        }
+    s_hpos[threadIdx.x] = at;
+  }
+  __syncthreads();
+  const int j = sample_one(cand + (size_t)row * ld, M, p, uniform01(seeds[row], ps), s_hpos, n_hist, red, s_chunk,
+                           &s_tok, hbin);
+  if (threadIdx.x == 0) {
+    const int tok = (j >= 0 && j < M && s_ids[j] >= 0) ? s_ids[j] : 0;
+    next_ids[row] = tok;
+    h[(ps + 1) % hist_stride] = tok;
+  }
+}
+
 }  // namespace
+
+extern "C" int nls_sample_decode_cand(void* cand, long ld, int n, int M, const int* ids, long ldi, const void* params,
+                                      const void* seeds, const int* pos, const int* ctx_len, int* hist, int hist_stride,
+                                      int* next_ids, void* stream) {
+  if (n < 1 || M < 1 || M > MAXC || hist_stride < 1 || hist_stride > NT) return -1;
+  hipLaunchKernelGGL(sample_decode_cand_kernel, dim3(n), dim3(NT), 0, (hipStream_t)stream, (float*)cand, ld, M, ids,
+                     ldi, (const SampleParams*)params, (const unsigned long long*)seeds, pos, ctx_len, hist,
+                     hist_stride, next_ids);
+  return (int)hipGetLastError();
+}
 
 extern "C" int nls_sample(void* logits, long ld, int n, int V, const void* params, const int* hist, int hist_stride,
                           int* out, void* stream) {

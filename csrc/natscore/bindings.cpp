@@ -203,7 +203,7 @@ PYBIND11_MODULE(_natscore, m) {
           py::arg("name"), py::arg("data"), py::arg("chunk_size") = 128 * 1024)
       .def("info", &ObjectStore::info, py::call_guard<py::gil_scoped_release>())
       .def("get_file", &ObjectStore::get_file, py::arg("name"), py::arg("path"), py::arg("resume") = true,
-           py::arg("progress") = nullptr, py::call_guard<py::gil_scoped_release>())
+           py::arg("progress") = nullptr, py::arg("deadline_s") = 0.0, py::call_guard<py::gil_scoped_release>())
       .def(
           "get_bytes",
           [](ObjectStore& o, const std::string& name) {

@@ -158,6 +158,10 @@ void Client::connect(const std::string& url, ClientOptions opt) {
   if (connected_) throw std::runtime_error("already connected");
   opt_ = opt;
   parse_url(url, host_, port_, opt_);
+  // a configured CA bundle or client certificate makes TLS REQUIRED (nats.go: RootCAs / ClientCert imply
+  // Secure): never wait for a plaintext INFO's tls_required, which a man in the middle can strip before the
+  // client sends its credentials in the clear
+  if (!opt_.tls.ca.empty() || !opt_.tls.cert.empty() || !opt_.tls.key.empty()) opt_.tls.enable = true;
   closing_ = false;
   dead_ = false;
   if (!dial()) {

@@ -196,7 +196,17 @@ std::string ObjectStore::put_bytes(const std::string& name, const std::string& d
 }
 
 std::string ObjectStore::get_file(const std::string& name, const std::string& path, bool resume,
-                                  const std::function<void(uint64_t, uint64_t)>& progress) {
+                                  const std::function<void(uint64_t, uint64_t)>& progress, double deadline_s) {
+  using clk = std::chrono::steady_clock;
+  const bool has_dl = deadline_s > 0;
+  const auto dl = clk::now() + std::chrono::microseconds((long long)(deadline_s * 1e6));
+  // time left for one wait (capped by the per-operation timeout); throws once the deadline has passed
+  auto wait_ms = [&]() -> int {
+    if (!has_dl) return to_;
+    const long long left = std::chrono::duration_cast<std::chrono::milliseconds>(dl - clk::now()).count();
+    if (left <= 0) throw std::runtime_error("context deadline exceeded");
+    return (int)std::min<long long>(to_, left);
+  };
   Json info = info_json(name, false);
   const std::string nuid = info.str("nuid");
   const uint64_t size = (uint64_t)info.num("size"), nchunks = (uint64_t)info.num("chunks");
@@ -275,6 +285,7 @@ std::string ObjectStore::get_file(const std::string& name, const std::string& pa
     ++nread;
     if ((nread & 63) == 0) save_idx();
     if (progress) progress(got, size);
+    if (has_dl) wait_ms();
   };
   try {
     // 1) ordered push consumer (what nats.go's ObjectStore.Get does): raw chunk payloads streamed to an
@@ -308,7 +319,7 @@ std::string ObjectStore::get_file(const std::string& name, const std::string& pa
       if (cerr.empty()) {
         try {
           while (nread < nchunks) {
-            Msg m = c_.next_msg(sid, to_);
+            Msg m = c_.next_msg(sid, wait_ms());
             if (m.status == 100) {                    // flow control request / idle heartbeat
               if (!m.reply.empty()) c_.publish(m.reply, "");
               continue;
@@ -347,6 +358,7 @@ std::string ObjectStore::get_file(const std::string& name, const std::string& pa
   } catch (...) {
     save_idx();
     ::close(fd);
+    if (has_dl && clk::now() >= dl) throw std::runtime_error("context deadline exceeded");
     throw;
   }
   ::fsync(fd);

@@ -28,8 +28,10 @@ class ObjectStore {
   std::string info(const std::string& name);
   // Streams the object into `path` (via `path`.part, digest-verified, fsync + rename).
   // With resume=true an interrupted `path`.part (+ `path`.part.idx) is continued.
+  // deadline_s > 0: the whole transfer is bounded (the pull_model handler's 10-minute context); on expiry it
+  // stops with "context deadline exceeded", leaving the .part file + index for a resumed pull
   std::string get_file(const std::string& name, const std::string& path, bool resume = true,
-                       const std::function<void(uint64_t, uint64_t)>& progress = nullptr);
+                       const std::function<void(uint64_t, uint64_t)>& progress = nullptr, double deadline_s = 0.0);
   std::string get_bytes(const std::string& name);
   std::string list();                      // JSON array of ObjectInfo (non-deleted)
   void remove(const std::string& name);    // marks deleted + purges chunks

@@ -99,18 +99,26 @@ long TlsConn::read(char* buf, size_t n, const std::atomic<bool>& stop) {
   return -1;
 }
 
+// Callers serialise writers (Client::write_raw holds the connection's write mutex); mu_ guards the SSL
+// object against the reader thread and is held only around SSL_write itself -- the wait for socket space
+// runs unlocked, so a slow link never stops incoming messages. A retried SSL_write gets the same buffer
+// and length, as OpenSSL requires after WANT_WRITE / WANT_READ.
 bool TlsConn::write_all(const char* p, size_t n) {
-  std::lock_guard<std::mutex> g(mu_);
   int waits = 0;
   while (n) {
-    const int r = SSL_write(ssl_, p, (int)std::min<size_t>(n, 1 << 30));
+    const int len = (int)std::min<size_t>(n, 1 << 30);
+    int r, e;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      r = SSL_write(ssl_, p, len);
+      e = r > 0 ? SSL_ERROR_NONE : SSL_get_error(ssl_, r);
+    }
     if (r > 0) {
       p += r;
       n -= (size_t)r;
       waits = 0;
       continue;
     }
-    const int e = SSL_get_error(ssl_, r);
     if ((e != SSL_ERROR_WANT_WRITE && e != SSL_ERROR_WANT_READ) || ++waits > 600) return false;   // ~60 s stalled
     pollfd q{fd_, (short)(e == SSL_ERROR_WANT_WRITE ? POLLOUT : POLLIN), 0};
     if (poll(&q, 1, 100) < 0) return false;

@@ -37,8 +37,9 @@ from .sampling import HIST, SamplingParams, sample_rows, sample_rows_gpu, unifor
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 640, 768, 1024)
 
 # tensor-parallel control messages (rank 0 -> followers), see Engine.follow()
-_OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE, _OP_SYNC = 0, 1, 2, 3, 4
-_HDR = 8
+_OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE, _OP_SYNC, _OP_RESET = 0, 1, 2, 3, 4, 5
+# header: op | T | nrows | need_logits | nseq | pad | candidate mode | in-graph sampling | sampling rows | 0
+_HDR = 10
 _NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
 
 
@@ -274,18 +275,26 @@ class Engine:
         self._ids = itertools.count()
         self.host_ms = defaultdict(float)
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0,
-                             device_sampled_steps=0, preemptions=0, recompute_tokens=0, candidate_sampled_steps=0)
+                             device_sampled_steps=0, preemptions=0, recompute_tokens=0, candidate_sampled_steps=0,
+                             candidate_sampled_prefills=0)
         self.full_logits: Optional[torch.Tensor] = None
         # TP sampling: per-rank top-CAND candidates gathered instead of the full logits when every sampled row
         # of the step has 0 < top_k <= CAND - HIST (or samples at temperature 0 with penalties); see _cand_ok
         self.cand: Optional[tuple] = None
         self._cand_mode = False
         self._ctrl_hdr = torch.zeros(_HDR + self.max_batch, dtype=torch.int32)
-        # In-graph sampling (single GPU): per-row sampling params / seeds / penalty-history rings live on
-        # the device, written once when a sequence takes its decode row; sampled rows then stay on the
-        # chained asynchronous decode path (ops.sample_decode after the lm-head, inside the hipGraph).
-        self.device_sampling = (self.dev.type == "cuda" and self.tp is None
-                                and os.environ.get("NLS_DEVICE_SAMPLING", "1") == "1")
+        # In-graph sampling: per-row sampling params / seeds / penalty-history rings live on the device,
+        # written once when a sequence takes its decode row; sampled rows then stay on the chained
+        # asynchronous decode path (ops.sample_decode after the lm-head, inside the hipGraph). Tensor
+        # parallel: every rank holds the same rows (shipped with the step's control message), gathers the
+        # per-rank top-CAND candidates through the IPC one-shot kernel and runs the same draw
+        # (ops.sample_decode_cand), so the sampled ids agree on every rank with no host round trip. Needs
+        # the one-shot data plane on GPUs (an RCCL gather would put RCCL back into the graph); the CPU gloo
+        # rehearsal runs the same sequence eagerly.
+        oneshot_ = getattr(model.comm, "oneshot", None) if self.tp is not None else None
+        self.device_sampling = (os.environ.get("NLS_DEVICE_SAMPLING", "1") == "1" and (
+            (self.dev.type == "cuda" and self.tp is None)
+            or (self.tp is not None and (self.dev.type == "cpu" or oneshot_ is not None))))
         if self.device_sampling:
             self.d_sparams = torch.zeros(self.max_batch, ops.SAMPLE_PARAMS_BYTES, dtype=torch.uint8, device=self.dev)
             self.d_seeds = torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev)
@@ -295,10 +304,10 @@ class Engine:
             # pageable copies stall the host and serialise behind the step in flight (a 512-request
             # burst paid ~1.5K of them)
             nb_ = ops.SAMPLE_PARAMS_BYTES
-            self._srow_pin = [dict(idx=torch.zeros(self.max_batch, dtype=torch.int64, pin_memory=True),
-                                   par=torch.zeros(self.max_batch, nb_, dtype=torch.uint8, pin_memory=True),
-                                   seed=torch.zeros(self.max_batch, dtype=torch.int64, pin_memory=True),
-                                   hist=torch.zeros(self.max_batch, HIST, dtype=torch.int32, pin_memory=True))
+            self._srow_pin = [dict(idx=torch.zeros(self.max_batch, dtype=torch.int64, pin_memory=pin),
+                                   par=torch.zeros(self.max_batch, nb_, dtype=torch.uint8, pin_memory=pin),
+                                   seed=torch.zeros(self.max_batch, dtype=torch.int64, pin_memory=pin),
+                                   hist=torch.zeros(self.max_batch, HIST, dtype=torch.int32, pin_memory=pin))
                               for _ in range(2)]
             self._srow_dev = dict(idx=torch.zeros(self.max_batch, dtype=torch.int64, device=self.dev),
                                   par=torch.zeros(self.max_batch, nb_, dtype=torch.uint8, device=self.dev),
@@ -309,7 +318,7 @@ class Engine:
         # tensor parallel with the IPC one-shot all-reduce: its error words (raised on every rank when any
         # rank's poll timed out) travel to the host with each step's tokens; a raised word fails the step
         self._oneshot = getattr(model.comm, "oneshot", None) if self.tp is not None else None
-        self.h_err2 = ([torch.zeros(2, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        self.h_err2 = ([torch.zeros(self._oneshot.ERR_WORDS, dtype=torch.int32, pin_memory=True) for _ in range(2)]
                        if self._oneshot is not None else None)
 
     # ------------------------------------------------------------------ API
@@ -572,6 +581,10 @@ class Engine:
             p = s.req.params
             if p.greedy:
                 continue
+            # a repeat penalty < 1 or a negative presence / frequency penalty RAISES history logits: a history
+            # token outside every rank's candidates could then enter the kept set -- not exact, full logits
+            if p.repeat_penalty < 1.0 or p.presence_penalty < 0.0 or p.frequency_penalty < 0.0:
+                return False
             if p.temperature > 0.0 and not (0 < (p.top_k or 0) <= self.CAND - HIST):
                 return False
         return True
@@ -591,19 +604,42 @@ class Engine:
 
     # ------------------------------------------------------------------ tensor parallel control
     def _ctrl(self, op: int, T: int, nrows: int, need: bool, rows: List[int], nseq: int, hmeta: torch.Tensor,
-              pad: int):
-        """Rank 0: broadcast the step (header + used part of the packed metadata) to followers."""
+              pad: int, dsamp: bool = False, srows: Optional[list] = None):
+        """Rank 0: broadcast the step (header + used part of the packed metadata + the sampling rows that
+        took a decode row since the last step) to followers."""
         if self.tp is None:
             return
         nb = self.max_blocks
         hdr = self._ctrl_hdr
         hdr.zero_()
-        hdr[:_HDR] = torch.tensor([op, T, nrows, int(need), nseq, pad, int(self._cand_mode), 0], dtype=torch.int32)
+        hdr[:_HDR] = torch.tensor([op, T, nrows, int(need), nseq, pad, int(self._cand_mode), int(dsamp),
+                                   len(srows or ()), 0], dtype=torch.int32)
         if rows:
             hdr[_HDR:_HDR + len(rows)] = torch.tensor(rows, dtype=torch.int32)
         self.tp.bcast_ctrl(hdr)
         if op in (_OP_PREFILL, _OP_DECODE):
             self.tp.bcast_ctrl(hmeta[:_NSEG * pad + nseq * nb].clone())
+        if srows:
+            self.tp.bcast_ctrl(self._pack_srows(srows))
+
+    _SROW = 1 + ops.SAMPLE_PARAMS_BYTES // 4 + 2 + HIST     # int32 words of one shipped sampling row
+
+    @staticmethod
+    def _pack_srows(srows) -> torch.Tensor:
+        out = np.zeros((len(srows), Engine._SROW), dtype=np.int32)
+        for i, (r, raw, seed, hist) in enumerate(srows):
+            out[i, 0] = r
+            o = 1 + ops.SAMPLE_PARAMS_BYTES // 4
+            out[i, 1:o] = np.frombuffer(raw, dtype=np.int32)
+            out[i, o:o + 2] = np.array([seed], dtype=np.int64).view(np.int32)
+            out[i, o + 2:] = hist
+        return torch.from_numpy(out.reshape(-1))
+
+    @staticmethod
+    def _unpack_srows(buf: torch.Tensor) -> list:
+        a = buf.numpy().reshape(-1, Engine._SROW)
+        o = 1 + ops.SAMPLE_PARAMS_BYTES // 4
+        return [(int(x[0]), x[1:o].tobytes(), int(x[o:o + 2].view(np.int64)[0]), x[o + 2:].copy()) for x in a]
 
     def sync(self, hook: Callable[[], None]):
         """Rank 0: make every follower run its `sync_hook` now, then run `hook` here (used by the
@@ -623,12 +659,15 @@ class Engine:
         nb = self.max_blocks
         while True:
             hdr = self.tp.bcast_ctrl(self._ctrl_hdr)
-            op, T, nrows, need, nseq, pad, cand = (int(v) for v in hdr[:7])
+            op, T, nrows, need, nseq, pad, cand, dsamp, nsr = (int(v) for v in hdr[:9])
             self._cand_mode = bool(cand)
             if op == _OP_STOP:
                 return
             if op == _OP_CAPTURE:
-                self._capture(T, LlamaModel.attn_splits(T, self.model.Hkv))
+                self._capture(T, LlamaModel.attn_splits(T, self.model.Hkv), dsamp=bool(dsamp))
+                continue
+            if op == _OP_RESET:
+                self._oneshot.reset()
                 continue
             if op == _OP_SYNC:
                 if self.sync_hook is not None:
@@ -638,11 +677,21 @@ class Engine:
             buf = torch.zeros(_NSEG * pad + nseq * nb, dtype=torch.int32)
             self.tp.bcast_ctrl(buf)
             hm[:buf.numel()] = buf
+            if nsr:
+                sb = torch.zeros(nsr * self._SROW, dtype=torch.int32)
+                self.tp.bcast_ctrl(sb)
+                for r, raw, seed, hist in self._unpack_srows(sb):
+                    self._srow_dirty[r] = (raw, seed, hist)
             if op == _OP_PREFILL:
                 self._exec_prefill(T, [int(v) for v in hdr[_HDR:_HDR + nrows]], bool(need))
             else:
+                if self.device_sampling:
+                    self._kbuf ^= 1
+                    self._flush_sampling_rows(self._kbuf)
                 self.db.meta.copy_(hm)
-                self._run_decode(T, bool(need))
+                self._run_decode(T, bool(need), bool(dsamp))
+                if dsamp:
+                    self.counters["device_sampled_steps"] += 1
                 if need:
                     self._gather(self.db, T, True)
 
@@ -654,7 +703,7 @@ class Engine:
         out = list(greedy)
         sampled = [i for i, s in enumerate(seqs) if not s.req.params.greedy]
         if sampled and self.cand is not None:
-            toks = self._sample_candidates([rows[i] for i in sampled], [seqs[i] for i in sampled])
+            toks = self._sample_candidates([rows[i] for i in sampled], [seqs[i] for i in sampled], prefill=True)
             for i, t in zip(sampled, toks):
                 out[i] = t
             sampled = []
@@ -667,13 +716,15 @@ class Engine:
                 out[i] = t
         return out
 
-    def _sample_candidates(self, rows: List[int], seqs: List[_Seq]) -> List[int]:
+    def _sample_candidates(self, rows: List[int], seqs: List[_Seq], prefill: bool = False) -> List[int]:
         """Draw the sampled rows from the gathered candidates (values in vocabulary order, global ids): the
         sampler runs on the candidate rows with each history token mapped to its candidate position (history
         tokens outside the candidates cannot reach the kept set); the drawn position maps back to its id.
         Same kept set, same index order, same variate: the token the full-vocabulary sampler would draw."""
         vals, ids = self.cand
-        self.counters["candidate_sampled_steps"] += 1
+        # host-driven draws: the first token of sampled requests (after their prefill), and decode steps whose
+        # sampled rows could not stay in the graph
+        self.counters["candidate_sampled_prefills" if prefill else "candidate_sampled_steps"] += 1
         v = vals[rows]
         ix = ids[rows]
         ixl = ix.cpu().tolist()
@@ -814,11 +865,14 @@ class Engine:
 
     def _launch_inner(self, launch: List[_Seq], prev: set, need: bool, dsamp: bool):
         k = self._kbuf = self._kbuf ^ 1
+        srows = None
         if self.device_sampling:
+            if self.tp is not None and self._srow_dirty:     # followers get the same rows with the step
+                srows = [(r,) + v for r, v in sorted(self._srow_dirty.items())]
             self._flush_sampling_rows(k)
         Bp = self._build_meta(k, launch, prev)
         pad = self.db.pad
-        self._ctrl(_OP_DECODE, Bp, 0, need, [], Bp, self.h_meta_d2[k], pad)
+        self._ctrl(_OP_DECODE, Bp, 0, need, [], Bp, self.h_meta_d2[k], pad, dsamp=dsamp, srows=srows)
         b = self.db
         if self.dev.type == "cuda":
             b.meta.copy_(self.h_meta_d2[k], non_blocking=True)
@@ -841,10 +895,14 @@ class Engine:
 
     def _check_comm(self, k: int):
         """Raise (failing the step's requests in _loop) when a tensor-parallel all-reduce of step buffer k
-        timed out on any rank: its sums -- and so its tokens -- are not trustworthy."""
+        timed out on any rank: its sums -- and so its tokens -- are not trustworthy. Before raising, every
+        rank re-initialises its one-shot buffers (_OP_RESET): late granules of the timed-out call must never
+        be taken for a later call's data."""
         if self.h_err2 is not None and int(self.h_err2[k].max()):
-            self.h_err2[k].zero_()
-            self._oneshot.err_clear()
+            for h in self.h_err2:
+                h.zero_()
+            self._ctrl(_OP_RESET, 0, 0, False, [], 0, None, 0)
+            self._oneshot.reset()
             raise RuntimeError("tensor-parallel all-reduce timed out waiting for a peer rank")
 
     def _process(self, infl):
@@ -928,7 +986,9 @@ class Engine:
             self._drain()
             return
         greedy = all(s.req.params.greedy for s in seqs)
-        dsamp = not greedy and self.device_sampling    # sampled rows drawn inside the decode graph
+        # sampled rows drawn inside the decode graph (tensor parallel: when the candidates are exact for
+        # every sampled row of the step, else the host-driven full-logits path)
+        dsamp = not greedy and self.device_sampling and (self.tp is None or self._cand_ok(seqs))
         chain = self.async_decode and (greedy or dsamp)
         if not chain:
             self._drain()
@@ -992,7 +1052,15 @@ class Engine:
                            need_logits=need_logits or dsamp)
         if dsamp:
             b = self.db
-            ops.sample_decode(b.logits, Bp, self.d_sparams, self.d_seeds, b.pos, b.ctx_len, self.d_hist, b.next_ids)
+            if self.tp is None:
+                ops.sample_decode(b.logits, Bp, self.d_sparams, self.d_seeds, b.pos, b.ctx_len, self.d_hist,
+                                  b.next_ids)
+                return
+            m = self.model
+            valid = max(0, min(m.vocab_hi, m.cfg.vocab) - m.vocab_lo)
+            cv, ci = self.tp.gather_candidates(*ops.topc_candidates(b.logits, Bp, self.CAND, m.vocab_lo, valid))
+            ops.sample_decode_cand(cv.contiguous(), ci.contiguous(), Bp, self.d_sparams, self.d_seeds, b.pos,
+                                   b.ctx_len, self.d_hist, b.next_ids)
 
     def _run_decode(self, Bp: int, need_logits: bool = False, dsamp: bool = False):
         ns = LlamaModel.attn_splits(Bp, self.model.Hkv)
@@ -1038,10 +1106,11 @@ class Engine:
             if (Bp, False) not in self.graphs:
                 self._ctrl(_OP_CAPTURE, Bp, 0, False, [], 0, None, 0)
                 self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv))
-            # the in-graph sampling variant too: captured lazily, it stalls the first sampled burst at
-            # every bucket (an eager step + capture + two device syncs each, ~0.2-0.4 s over a 512-request
-            # ramp). Padded rows have ctx 0 and every row's params are greedy here: no history writes.
+            # the in-graph sampling variant too (on every rank): captured lazily, it stalls the first sampled
+            # burst at every bucket (an eager step + capture + two device syncs each, ~0.2-0.4 s over a
+            # 512-request ramp). Padded rows have ctx 0 and every row's params are greedy here: no history writes.
             if self.device_sampling and (Bp, False, True) not in self.graphs:
+                self._ctrl(_OP_CAPTURE, Bp, 0, False, [], 0, None, 0, dsamp=True)
                 self._capture(Bp, LlamaModel.attn_splits(Bp, self.model.Hkv), dsamp=True)
 
     # ------------------------------------------------------------------ completion

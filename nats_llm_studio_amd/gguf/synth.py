@@ -67,6 +67,11 @@ SPECS: Dict[str, ModelSpec] = {
     # Llama-3-70B per-layer shapes (d 8192, 64 q / 8 kv heads, FFN 28672) with ONE layer and a 4K vocab: the
     # CPU rehearsal of the TP=4/8 data plane (bench.py TP leg on --device cpu, tests/test_parallel_shapes.py)
     "llama-3-70b-1layer": ModelSpec("llama-3-70b-1layer", "llama", 1, 8192, 64, 8, 28672, 4096, 512, 500000.0),
+    # two Llama-3-70B layers / one Mixtral-8x7B layer with a 32K vocab: the multi-process, one-GPU rehearsal of
+    # the TP / EP decode graphs (parallel/rehearsal.py, tests/test_tp_rehearsal_gpu.py)
+    "llama-3-70b-2layer": ModelSpec("llama-3-70b-2layer", "llama", 2, 8192, 64, 8, 28672, 32000, 1024, 500000.0),
+    "mixtral-8x7b-1layer": ModelSpec("mixtral-8x7b-1layer", "llama", 1, 4096, 32, 8, 14336, 32000, 1024, 1e6,
+                                     n_expert=8, n_expert_used=2, tokenizer="llama"),
     "tiny-mixtral-tp": ModelSpec("tiny-mixtral-tp", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,
                                  n_expert=4, n_expert_used=2, tokenizer="llama"),
     "tiny-mixtral": ModelSpec("tiny-mixtral", "llama", 2, 512, 4, 2, 512, 1024, 512, 10000.0,

@@ -213,8 +213,11 @@ class ObjectStore:
     def info(self, name: str) -> dict:
         return json.loads(self._o.info(name))
 
-    def get_file(self, name: str, path: str, resume: bool = True, progress: Callable[[int, int], None] = None) -> dict:
-        return json.loads(self._o.get_file(name, path, resume, progress))
+    def get_file(self, name: str, path: str, resume: bool = True, progress: Callable[[int, int], None] = None,
+                 deadline_s: float = 0.0) -> dict:
+        """Stream an object to `path` (.part + resume index, SHA-256 verified); deadline_s > 0 bounds the
+        whole transfer (RuntimeError "context deadline exceeded", resumable)."""
+        return json.loads(self._o.get_file(name, path, resume, progress, float(deadline_s)))
 
     def get_bytes(self, name: str) -> bytes:
         return self._o.get_bytes(name)

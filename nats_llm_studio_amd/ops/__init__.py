@@ -933,6 +933,45 @@ def sample_decode(logits: torch.Tensor, n: int, params: torch.Tensor, seeds: tor
                "nls_sample_decode")
 
 
+def sample_decode_cand(vals: torch.Tensor, ids: torch.Tensor, n: int, params: torch.Tensor, seeds: torch.Tensor,
+                       pos: torch.Tensor, ctx_len: torch.Tensor, hist: torch.Tensor, next_ids: torch.Tensor):
+    """In-graph sampling of tensor-parallel decode rows [0, n) from the gathered candidates (values `vals`
+    [n, M] in vocabulary order -- scratch, penalties are applied in place -- and global ids `ids` [n, M]):
+    sample_decode's semantics with the history ring mapped onto candidate positions."""
+    M = vals.shape[1]
+    if vals.is_cuda:
+        if vals.dtype != torch.float32 or vals.stride(1) != 1 or ids.stride(1) != 1:
+            raise TypeError("sample_decode_cand: fp32 / int32 row-major candidates")
+        _lib.check(_lib.lib().nls_sample_decode_cand(vals.data_ptr(), vals.stride(0), n, M, ids.data_ptr(),
+                                                     ids.stride(0), params.data_ptr(), seeds.data_ptr(), pos.data_ptr(),
+                                                     ctx_len.data_ptr(), hist.data_ptr(), hist.shape[1],
+                                                     next_ids.data_ptr(), _stream_ptr(vals)), "nls_sample_decode_cand")
+        return
+    # CPU twin of sample.hip sample_decode_cand_kernel (gloo rehearsals of the tensor-parallel path)
+    from ..engine.sampling import SamplingParams, sample_rows, uniform01
+    raw = params.cpu().numpy()
+    S = hist.shape[1]
+    for r in range(n):
+        if int(ctx_len[r]) <= 0:
+            continue
+        sp = _lib.SampleParams.from_buffer_copy(raw[r].tobytes())
+        p = SamplingParams(temperature=sp.temperature, top_k=sp.top_k, top_p=sp.top_p, min_p=sp.min_p,
+                           repeat_penalty=sp.repeat_penalty, presence_penalty=sp.presence_penalty,
+                           frequency_penalty=sp.frequency_penalty)
+        if p.greedy:
+            continue
+        ps = int(pos[r])
+        nh = min(S, ps + 1)
+        idl = ids[r].tolist()
+        at = {t: j for j, t in enumerate(idl) if t >= 0}
+        hp = [at[t] for t in hist[r, :nh].tolist() if t in at]
+        seed = int(seeds[r]) & 0xFFFFFFFFFFFFFFFF
+        j = sample_rows(vals[r:r + 1].float(), [p], [hp], [uniform01(seed, ps)])[0]
+        tok = idl[j] if 0 <= j < M and idl[j] >= 0 else 0
+        next_ids[r] = tok
+        hist[r, (ps + 1) % S] = tok
+
+
 def moe_norm_route(x: torch.Tensor, nw: torch.Tensor, eps: float, wr: torch.Tensor, h: torch.Tensor,
                    logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
                    yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None) -> bool:

@@ -83,6 +83,8 @@ _SIGS = {
     "nls_sample_params_size": [],
     "nls_sample_decode": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                           c_void_p, c_void_p],
+    "nls_sample_decode_cand": [c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "nls_ar_alloc": [c_long, c_int, c_void_p, c_void_p],
     "nls_ar_open": [c_void_p, c_void_p],
     "nls_ar_close": [c_void_p],
@@ -97,6 +99,12 @@ _SIGS = {
     "nls_ar_row_blocks": [c_int],
     "nls_ar_err_fetch": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "nls_ar_err_clear": [c_void_p, c_long, c_int, c_void_p],
+    "nls_ag_blocks": [],
+    "nls_ag_run": [c_void_p, c_long, c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p,
+                   c_long, c_void_p],
+    "nls_ag_argmax": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_long,
+                      c_void_p],
+    "nls_ar_reinit": [c_void_p, c_long, c_int, c_void_p],
     "nls_ar_run": [c_void_p, c_long, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p, c_long, c_void_p],
 }
 

@@ -101,6 +101,12 @@ class Comm:
 
     def vocab_parallel_argmax(self, keys: torch.Tensor, n: int, vocab_lo: int, next_ids: torch.Tensor):
         """Per-rank fused-argmax keys (value<<32 | ~local_idx) -> global greedy ids on every rank."""
+        if self.oneshot is not None and keys.is_cuda:
+            # one IPC launch: rebase, exchange, max, unpack and re-arm (no RCCL call in the decode graph)
+            self.stats["all_reduce"] += 1
+            self.stats["all_reduce_bytes"] += 8 * n
+            self.oneshot.argmax(keys, n, vocab_lo, next_ids)
+            return
         k = keys[:n]
         if keys.is_cuda:                       # device keys are unsigned: make signed order match
             k.bitwise_xor_(_SIGN)
@@ -124,6 +130,15 @@ class Comm:
         every rank, in rank order = vocabulary order (ranks hold consecutive vocab shards). 8 bytes per
         candidate instead of 4 per vocabulary entry: C = 128 at TP=8 moves 8 KiB per sampled row, not 500 KiB."""
         n, C = vals.shape
+        os_ = self.oneshot
+        if os_ is not None and vals.is_cuda and os_.gather_ok(2 * n * C):
+            # lossless IPC all-gather of (values | ids) in one launch, rows already in vocabulary order
+            self.stats["all_reduce"] += 1
+            self.stats["all_reduce_bytes"] += 8 * n * C * self.size
+            src = torch.stack([vals.contiguous().view(torch.int32), idx.contiguous().view(torch.int32)])
+            dst = torch.empty(2, n, self.size * C, dtype=torch.int32, device=vals.device)
+            os_.gather(src, dst)
+            return dst[0].view(torch.float32), dst[1]
         ov = torch.empty(self.size * n, C, dtype=vals.dtype, device=vals.device)
         oi = torch.empty(self.size * n, C, dtype=idx.dtype, device=idx.device)
         dist.all_gather_into_tensor(ov, vals.contiguous(), group=self.group)

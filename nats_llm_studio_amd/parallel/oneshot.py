@@ -47,14 +47,19 @@ class OneShotAllReduce:
         # a second buffer set for the fused all-reduce + residual + RMSNorm (its own epoch counters:
         # the two protocols must never read each other's granules)
         self.nbuf, self.npeers = self._exchange(L, hs, comm)
+        # a third set for the lossless all-gather + fused vocab-parallel arg-max (ids, keys, sampling
+        # candidates), again with epochs of its own
+        self.gbuf, self.gpeers = self._exchange(L, hs, comm)
         if comm.min_int(int(self.ok)) == 0:
             self.close()
             raise RuntimeError("one-shot all-reduce: IPC buffer setup failed on some rank")
         dev = comm.device
         self.device = dev
         self.epochs = torch.zeros(L.nls_ar_blocks(), dtype=torch.int32, device=dev)
+        self.gepochs = torch.zeros(L.nls_ag_blocks(), dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._norm = {}               # D -> (epochs, tickets, ssq) of the fused add+norm
+        self.resets = 0
         comm.barrier()
 
     def _exchange(self, L, hs, comm):
@@ -108,20 +113,66 @@ class OneShotAllReduce:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= self.cap
                 and t.numel() % 4 == 0)
 
+    ERR_WORDS = 3      # one error word per buffer set (sum, fused add+norm, gather / arg-max)
+
     def err_fetch(self, host: torch.Tensor):
-        """Enqueue the copy of this rank's error word (raised by ANY rank's timed-out poll, in either buffer
-        set) into pinned int32 host[0:2] on the current stream; read it after the stream has passed."""
+        """Enqueue the copy of this rank's error words (raised by ANY rank's timed-out poll, one per buffer
+        set) into pinned int32 host[0:3] on the current stream; read them after the stream has passed."""
         L = _lib.lib()
         st = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(L.nls_ar_err_fetch(self.buf, self.cap, self.world, host.data_ptr(), st), "nls_ar_err_fetch")
-        _lib.check(L.nls_ar_err_fetch(self.nbuf, self.cap, self.world, host.data_ptr() + 4, st), "nls_ar_err_fetch")
+        for i, b in enumerate((self.buf, self.nbuf, self.gbuf)):
+            _lib.check(L.nls_ar_err_fetch(b, self.cap, self.world, host.data_ptr() + 4 * i, st), "nls_ar_err_fetch")
 
     def err_clear(self):
         L = _lib.lib()
         st = torch.cuda.current_stream(self.device).cuda_stream
-        for b in (self.buf, self.nbuf):
+        for b in (self.buf, self.nbuf, self.gbuf):
             _lib.check(L.nls_ar_err_clear(b, self.cap, self.world, st), "nls_ar_err_clear")
         self.err.zero_()
+
+    def reset(self):
+        """After a timed-out poll: put every rank's receive slots, epochs and tickets back to the freshly
+        allocated state. A late peer may still have written granules nobody consumed, and a later call of
+        the same parity could take them for current data once the 2-bit tag wraps; re-initialising is the
+        only safe continuation. Collective: every rank calls it (the engine's _OP_RESET), and the barriers
+        on both sides make sure no rank has a kernel in flight while the buffers are rewritten."""
+        L = _lib.lib()
+        torch.cuda.synchronize(self.device)
+        self.comm.barrier()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        for b in (self.buf, self.nbuf, self.gbuf):
+            _lib.check(L.nls_ar_reinit(b, self.cap, self.world, st), "nls_ar_reinit")
+        for t in [self.epochs, self.gepochs, self.err] + [x for st_ in self._norm.values() for x in st_]:
+            t.zero_()
+        torch.cuda.synchronize(self.device)
+        self.comm.barrier()
+        self.resets += 1
+
+    def argmax(self, keys: torch.Tensor, n: int, vocab_lo: int, next_ids: torch.Tensor):
+        """Vocab-parallel greedy pick in one launch: this rank's fused arg-max keys of rows [0, n) (its vocab
+        shard starts at vocab_lo) -> the global token ids in next_ids on every rank; keys re-armed (0)."""
+        if 4 * n > self.cap:
+            raise ValueError(f"one-shot arg-max: {n} rows exceed the buffer")
+        rc = _lib.lib().nls_ag_argmax(keys.data_ptr(), n, int(vocab_lo), next_ids.data_ptr(), self.gpeers,
+                                      self.world, self.rank, self.cap, self.gepochs.data_ptr(), self.err.data_ptr(),
+                                      self.max_spins, _stream(keys))
+        _lib.check(rc, "nls_ag_argmax")
+
+    def gather_ok(self, words: int) -> bool:
+        return 2 * words <= self.cap
+
+    def gather(self, src: torch.Tensor, dst: torch.Tensor):
+        """Lossless all-gather: src [A, rows, C] of 32-bit words (this rank) -> dst [A, rows, world * C] with
+        rank p's words at columns [p * C, (p + 1) * C) of every row (C even)."""
+        A, rows, C = src.shape
+        if (src.element_size() != 4 or dst.element_size() != 4 or not src.is_contiguous() or not dst.is_contiguous()
+                or tuple(dst.shape) != (A, rows, self.world * C) or C % 2 or not self.gather_ok(src.numel())):
+            raise ValueError("one-shot gather: bad operands")
+        rc = _lib.lib().nls_ag_run(src.data_ptr(), src.numel() // 2, dst.data_ptr(), C, rows * C, self.gpeers,
+                                   self.world, self.rank, self.cap, self.gepochs.data_ptr(), self.err.data_ptr(),
+                                   self.max_spins, _stream(src))
+        _lib.check(rc, "nls_ag_run")
+        return dst
 
     def all_reduce(self, t: torch.Tensor):
         rc = _lib.lib().nls_ar_run(t.data_ptr(), t.numel(), self.peers, self.world, self.rank, self.cap,
@@ -131,10 +182,10 @@ class OneShotAllReduce:
 
     def check(self):
         """Raise if any rank's call timed out waiting for a peer (call outside graph capture)."""
-        host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        host = torch.zeros(self.ERR_WORDS, dtype=torch.int32, pin_memory=True)
         self.err_fetch(host)
         torch.cuda.current_stream(self.device).synchronize()
-        if int(self.err.item()) or int(host[0]) or int(host[1]):
+        if int(self.err.item()) or int(host.max()):
             raise RuntimeError("one-shot all-reduce timed out waiting for a peer")
 
     def close(self):

@@ -59,6 +59,10 @@ def _messages(req: dict):
     return msgs
 
 
+
+class DeadlineExceeded(Exception):
+    """A handler's context expired (Go: context.DeadlineExceeded, "context deadline exceeded")."""
+
 class StubBackend:
     """Echo backend: returns the last user message (token counts = whitespace words)."""
 
@@ -227,6 +231,36 @@ class EngineBackend:
             fut.set_result(st)
             return st
 
+    def _load_until(self, entry: ModelEntry, deadline: Optional[float]) -> dict:
+        """load(), bounded by the request's monotonic deadline: a cold build runs on a helper thread and the
+        caller gives up (DeadlineExceeded) when the deadline passes first; a build that completes after that
+        releases the pin it took for the abandoned request."""
+        if deadline is None or entry.id in self._ids:
+            return self.load(entry)
+        lk, ev, box = threading.Lock(), threading.Event(), {}
+
+        def run():
+            try:
+                st, err = self.load(entry), None
+            except BaseException as e:          # noqa: BLE001 -- handed to the waiting request
+                st, err = None, e
+            with lk:
+                if box.get("abandoned"):
+                    if st is not None:
+                        self.release(st)
+                    return
+                box.update(st=st, err=err)
+                ev.set()
+        threading.Thread(target=run, name=f"nls-load-{entry.id}", daemon=True).start()
+        ev.wait(max(0.0, deadline - time.monotonic()))
+        with lk:
+            if not ev.is_set():
+                box["abandoned"] = True
+                raise DeadlineExceeded(entry.id)
+        if box["err"] is not None:
+            raise box["err"]
+        return box["st"]
+
     def release(self, st: dict):
         with self._lock:
             st["inflight"] -= 1
@@ -261,7 +295,12 @@ class EngineBackend:
             done(400, _error_body(str(e)))
             return
         try:
-            st = self.load(entry)
+            st = self._load_until(entry, deadline)
+        except DeadlineExceeded:
+            # the chat's context (reference: 2 min from receipt, `nats_llm_studio.go:328`) expired during a
+            # cold JIT load: reply now; the build goes on and serves the next request
+            done(0, _error_body("context deadline exceeded"))
+            return
         except Exception as e:
             done(500, _error_body(f"failed to load model '{model_id}': {e}"))
             return

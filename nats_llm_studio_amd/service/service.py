@@ -26,7 +26,7 @@ from collections import defaultdict
 from typing import Optional
 
 from . import envelope
-from .backends import EngineBackend, HttpBackend, StubBackend
+from .backends import DeadlineExceeded, EngineBackend, HttpBackend, StubBackend
 from .config import WorkerConfig
 from .registry import Registry
 from .store import ModelStore, PullError
@@ -101,6 +101,29 @@ class Service:
                 self.latency[name].add(time.perf_counter() - t0)
         return handler
 
+    @staticmethod
+    def _bounded(fn, seconds: float):
+        """fn() under a handler context of `seconds` (the reference's per-subject context.WithTimeout:
+        list 30 s, delete 2 min, `nats_llm_studio.go:229`, `:289`): the work runs on a helper thread and
+        DeadlineExceeded is raised when it has not finished in time (it may still complete afterwards, as
+        a Go RemoveAll does after its caller's context expired)."""
+        if seconds is None or seconds <= 0:
+            return fn()
+        box, ev = {}, threading.Event()
+
+        def run():
+            try:
+                box["v"] = fn()
+            except BaseException as e:        # noqa: BLE001 -- re-raised in the handler
+                box["e"] = e
+            ev.set()
+        threading.Thread(target=run, name="nls-handler-op", daemon=True).start()
+        if not ev.wait(seconds):
+            raise DeadlineExceeded("context deadline exceeded")
+        if "e" in box:
+            raise box["e"]
+        return box.get("v")
+
     def respond(self, msg, body: bytes):
         """respondJSON (`nats_llm_studio.go:207-217`): log (not raise) when there is no reply subject."""
         if not msg.reply:
@@ -122,7 +145,11 @@ class Service:
     def on_list_models(self, msg):
         if isinstance(self.backend, HttpBackend):           # `nats_llm_studio.go:228-248`
             try:
-                status, body = self.backend.list_models_raw()
+                status, body = self._bounded(self.backend.list_models_raw, self.cfg.timeout_list)
+            except DeadlineExceeded:
+                self.respond(msg, envelope.error("error calling LM Studio: context deadline exceeded",
+                                                 {"http_status": 0}))
+                return
             except Exception as e:
                 self.respond(msg, envelope.error(f"error calling LM Studio: {e}", {"http_status": 0}))
                 return
@@ -131,7 +158,11 @@ class Service:
                          envelope.ok({"http_status": status, "models": raw}))
             return
         try:
-            models = self.registry.list_api(self.backend.loaded_ids())
+            models = self._bounded(lambda: self.registry.list_api(self.backend.loaded_ids()), self.cfg.timeout_list)
+        except DeadlineExceeded:
+            self.respond(msg, envelope.error("error reading model registry: context deadline exceeded",
+                                             {"http_status": 0}))
+            return
         except Exception as e:
             self.respond(msg, envelope.error(f"error reading model registry: {e}", {"http_status": 0}))
             return
@@ -147,8 +178,9 @@ class Service:
             self.respond(msg, envelope.error("'identifier' is required"))
             return
         req = json.loads(msg.data)
+        deadline = time.monotonic() + self.cfg.timeout_pull      # `nats_llm_studio.go:251` (10 min)
         try:
-            res = self.store.pull(ident)
+            res = self.store.pull(ident, deadline=deadline)
         except PullError as e:
             self.respond(msg, envelope.failure(str(e), {"model": ident, "output": e.output}))
             return
@@ -180,27 +212,35 @@ class Service:
         if not mid:
             self.respond(msg, envelope.error("'model_id' is required"))
             return
+        replies = []
+        # unload + lookup + rmtree under the handler's 2-minute context (`nats_llm_studio.go:289`)
+        try:
+            self._bounded(lambda: self._delete(mid, replies.append), self.cfg.timeout_delete)
+        except DeadlineExceeded:
+            replies[:] = [envelope.failure("context deadline exceeded", {"model_id": mid, "dir": ""})]
+        self.respond(msg, replies[0] if replies else envelope.failure("delete failed", {"model_id": mid, "dir": ""}))
+
+    def _delete(self, mid: str, reply):
         self.registry.scan()
         ent = self.registry.resolve(mid)
         if ent is None:
-            self.respond(msg, envelope.failure(f"model not found: {mid}", {"model_id": mid, "dir": ""}))
+            reply(envelope.failure(f"model not found: {mid}", {"model_id": mid, "dir": ""}))
             return
         self.backend.unload(ent.id)                       # best effort, like `lms unload` (`:87-97`)
         d = ent.dir
         if not self.registry.safe_dir(d):
-            self.respond(msg, envelope.failure(f"refusing to delete outside MODELS_DIR: {d}",
-                                               {"model_id": mid, "dir": d}))
+            reply(envelope.failure(f"refusing to delete outside MODELS_DIR: {d}", {"model_id": mid, "dir": d}))
             return
         if not os.path.isdir(d):
-            self.respond(msg, envelope.failure(f"model directory not found: {d}", {"model_id": mid, "dir": d}))
+            reply(envelope.failure(f"model directory not found: {d}", {"model_id": mid, "dir": d}))
             return
         try:
             ModelStore.remove_dir(d)
         except OSError as e:
-            self.respond(msg, envelope.failure(f"error removing model directory {d}: {e}", {"model_id": mid, "dir": d}))
+            reply(envelope.failure(f"error removing model directory {d}: {e}", {"model_id": mid, "dir": d}))
             return
         self.registry.scan()
-        self.respond(msg, envelope.ok({"model_id": mid, "deleted_dir": d}))
+        reply(envelope.ok({"model_id": mid, "deleted_dir": d}))
 
     def on_chat_model(self, msg):
         t_recv = time.monotonic()
@@ -230,7 +270,7 @@ class Service:
         if entry is None and isinstance(self.backend, EngineBackend):
             self.registry.scan()
             entry = self.registry.resolve(model)
-        deadline = time.monotonic() + self.cfg.timeout_chat
+        deadline = t_recv + self.cfg.timeout_chat      # from receipt (`nats_llm_studio.go:328`), JIT load included
         stream_cb = None
         ssubj = req.get("stream_subject")
         if req.get("stream") and isinstance(ssubj, str) and ssubj:
@@ -277,7 +317,7 @@ class Service:
         bucket = req.get("bucket") or self.cfg.bucket
         try:
             res = self.store.sync(bucket, req["object_name"], req["publisher"], req["model_dir"],
-                                  req.get("filename", "model.gguf"))
+                                  req.get("filename", "model.gguf"), deadline=time.monotonic() + self.cfg.timeout_pull)
         except Exception as e:
             self.respond(msg, envelope.failure(str(e), {"bucket": bucket, "object_name": req["object_name"]}))
             return

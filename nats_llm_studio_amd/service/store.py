@@ -56,18 +56,31 @@ class ModelStore:
         self.models_dir = os.path.abspath(os.path.expanduser(models_dir))
         self.bucket = bucket
 
-    def _os(self, bucket: Optional[str] = None) -> ObjectStore:
+    def _os(self, bucket: Optional[str] = None, timeout: float = 30.0) -> ObjectStore:
+        """Per-operation timeout 30 s, or what is left of the caller's deadline when that is shorter."""
         if self.client is None:
             raise PullError("no NATS connection for the object store")
-        return ObjectStore(self.client, bucket or self.bucket, timeout=30.0)
+        return ObjectStore(self.client, bucket or self.bucket, timeout=max(0.05, min(30.0, timeout)))
 
-    def pull(self, identifier: str, progress: Callable[[int, int], None] = None) -> dict:
+    def pull(self, identifier: str, progress: Callable[[int, int], None] = None,
+             deadline: Optional[float] = None) -> dict:
+        """deadline: time.monotonic() bound of the whole pull (the handler's 10-minute context,
+        `nats_llm_studio.go:251`); an expired pull keeps its .part files and resumes on the next call."""
         out_lines = []
         t0 = time.time()
+
+        def left() -> float:
+            if deadline is None:
+                return 0.0
+            r = deadline - time.monotonic()
+            if r <= 0:
+                raise PullError(f"failed to pull '{identifier}': context deadline exceeded", "\n".join(out_lines))
+            return r
         try:
-            store = self._os()
+            store = self._os(timeout=left() or 30.0)
             objs = store.list()
         except Exception as e:
+            left()
             raise PullError(f"failed to list bucket '{self.bucket}': {e}", "")
         matches = [o for o in objs if _match(identifier, o["name"]) and o["name"].lower().endswith(".gguf")]
         if not matches:
@@ -85,8 +98,12 @@ class ModelStore:
                 paths.append(dest)
                 continue
             try:
-                store.get_file(o["name"], dest, True, progress)
+                budget = left()
+                self._os(timeout=budget or 30.0).get_file(o["name"], dest, True, progress, budget)
+            except PullError:
+                raise
             except Exception as e:
+                left()
                 raise PullError(f"failed to download '{o['name']}': {e}", "\n".join(out_lines))
             total += int(o.get("size", 0))
             out_lines.append(f"{o['name']}: {o.get('size', 0)} bytes -> {dest} ({o.get('digest', '')} verified)")
@@ -96,7 +113,8 @@ class ModelStore:
                          + (f" ({total / dt / 1e9:.2f} GB/s)" if dt > 0 and total else ""))
         return {"output": "\n".join(out_lines), "paths": paths, "bytes": total, "seconds": dt}
 
-    def sync(self, bucket: str, object_name: str, publisher: str, model_dir: str, filename: str = "model.gguf") -> dict:
+    def sync(self, bucket: str, object_name: str, publisher: str, model_dir: str, filename: str = "model.gguf",
+             deadline: Optional[float] = None) -> dict:
         for part in (publisher, model_dir, filename):
             if not part or "/" in part or part in (".", ".."):
                 raise PullError(f"invalid path component {part!r}")
@@ -104,7 +122,12 @@ class ModelStore:
         os.makedirs(d, exist_ok=True)
         dest = os.path.join(d, filename)
         t0 = time.time()
-        info = self._os(bucket).get_file(object_name, dest, True, None)
+        budget = 0.0
+        if deadline is not None:
+            budget = deadline - time.monotonic()
+            if budget <= 0:
+                raise PullError("context deadline exceeded")
+        info = self._os(bucket, budget or 30.0).get_file(object_name, dest, True, None, budget)
         return {"local_path": dest, "size": info.get("size"), "digest": info.get("digest"),
                 "seconds": time.time() - t0}
 

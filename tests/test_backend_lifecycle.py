@@ -142,3 +142,32 @@ def test_concurrent_first_loads_of_two_models_are_serialised(svc_env):
         assert r["ok"] and r["data"]["http_status"] == 200, r
         assert r["data"]["response"]["usage"]["completion_tokens"] == 4
     assert len(be.loaded_ids()) == 1
+
+
+def test_chat_deadline_covers_jit_load(svc_env):
+    """The chat context starts at receipt and includes the JIT load (reference: 2 min, nats_llm_studio.go:328):
+    a load slower than the context answers with the deadline envelope; the build completes in the background,
+    releases the abandoned request's pin, and serves the next chat."""
+    svc, cli = svc_env
+    be = svc.backend
+    orig = be.build_state
+
+    def slow_build(*a, **k):
+        time.sleep(2.0)
+        return orig(*a, **k)
+    be.build_state = slow_build
+    svc.cfg.timeout_chat = 0.5
+    body = {"model": "tiny-llama", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 2}
+    t0 = time.time()
+    r = req(cli, "chat_model", body)
+    assert time.time() - t0 < 1.8
+    assert r == {"ok": False, "error": "context deadline exceeded", "data": {"http_status": 0}}, r
+    t_end = time.time() + 20
+    while be.loaded_ids() != ["tiny-llama"] and time.time() < t_end:
+        time.sleep(0.05)
+    assert be.loaded_ids() == ["tiny-llama"]
+    svc.cfg.timeout_chat = 120.0
+    r = req(cli, "chat_model", body)
+    assert r["ok"] is True and r["data"]["http_status"] == 200, r
+    time.sleep(0.2)
+    assert be.stats()["models"]["tiny-llama"]["inflight"] == 0      # the abandoned pin was released

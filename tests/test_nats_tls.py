@@ -214,3 +214,14 @@ def test_worker_config_tls_env():
     kw = c.nats_auth()
     assert kw["tls"] and kw["tls_first"] and not kw["tls_insecure"]
     assert (kw["tls_ca"], kw["tls_cert"], kw["tls_key"]) == ("/x/ca.pem", "/x/c.pem", "/x/k.pem")
+
+
+def test_configured_ca_requires_tls(server, pki):
+    """A CA bundle (or client certificate) makes TLS required: against a plaintext server whose INFO does not
+    ask for TLS (e.g. a man in the middle stripped tls_required) the client must refuse rather than send its
+    credentials in the clear (nats.go: RootCAs / ClientCert imply Secure)."""
+    with pytest.raises(ConnectionClosedError):
+        Client().connect(f"nats://127.0.0.1:{server.port}", tls_ca=pki["ca"][0], reconnect=False, timeout=2.0)
+    c = Client().connect(f"nats://127.0.0.1:{server.port}", reconnect=False)     # no TLS options: plaintext ok
+    c.flush(2.0)
+    c.close()

@@ -53,6 +53,37 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             ref = base + sum(parts)
             out[f"an{it}"] = float((x.cpu() - ref).abs().max())
+        # vocab-parallel arg-max: rank r holds logits[:, r*V:(r+1)*V]; every rank must get the global argmax
+        import numpy as np
+        n, V = 37, 1000
+        full = torch.randn(n, world * V, generator=g.manual_seed(99))
+        full[3, 5] = full[3, V + 5] = full[3].max() + 1.0           # a tie across ranks: lowest id wins
+        loc = full[:, rank * V:(rank + 1) * V].numpy()
+        u = loc.view(np.uint32).astype(np.uint64)
+        u = np.where(u & 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+        keys = (u << np.uint64(32)) | (np.uint64(0xFFFFFFFF) - np.arange(V, dtype=np.uint64))
+        kmax = keys.max(axis=1).view(np.int64)
+        kt = torch.from_numpy(kmax.copy()).to(dev)
+        nid = torch.zeros(n, dtype=torch.int32, device=dev)
+        for _ in range(3):   # repeated calls: epochs / parity alternate
+            ar.argmax(kt, n, rank * V, nid)
+            torch.cuda.synchronize()
+            ok = bool((nid.cpu().long() == full.argmax(dim=1)).all()) and int(kt.abs().sum()) == 0
+            out["argmax_bad"] = float(not ok)
+            kt.copy_(torch.from_numpy(kmax.copy()))
+        # lossless gather: [2, rows, C] words -> [2, rows, world*C], bit-exact (fp32 values and ids)
+        rows, C = 5, 128
+        vals = torch.randn(rows, C, generator=g.manual_seed(300 + rank))
+        ids = torch.randint(0, 1 << 30, (rows, C), generator=g.manual_seed(400 + rank), dtype=torch.int32)
+        src = torch.stack([vals.view(torch.int32), ids]).to(dev)
+        dst = torch.zeros(2, rows, world * C, dtype=torch.int32, device=dev)
+        ar.gather(src, dst)
+        torch.cuda.synchronize()
+        exp_v = torch.cat([torch.randn(rows, C, generator=g.manual_seed(300 + r)) for r in range(world)], dim=1)
+        exp_i = torch.cat([torch.randint(0, 1 << 30, (rows, C), generator=g.manual_seed(400 + r), dtype=torch.int32)
+                           for r in range(world)], dim=1)
+        d = dst.cpu()
+        out["gather_bad"] = float(not (torch.equal(d[0].view(torch.float32), exp_v) and torch.equal(d[1], exp_i)))
         out["err"] = int(ar.err.item())
         ar.close()
         dist.barrier()

@@ -62,6 +62,14 @@ def _run(eng):
     while not all(f.done() for f in futs):
         eng.step()
     toks.append([f.result().token_ids for f in futs])
+    # penalties that RAISE history logits (repeat_penalty < 1, negative presence): the candidates are not exact
+    # there, so these rows must take the full-logits path -- and still match the full-vocabulary sampler
+    boost = SamplingParams(max_tokens=5, temperature=0.8, top_k=10, repeat_penalty=0.7, presence_penalty=-0.5,
+                           seed=5, ignore_eos=True)
+    futs = [eng.submit(GenRequest(list(p), boost)) for p in PROMPTS]
+    while not all(f.done() for f in futs):
+        eng.step()
+    toks.append([f.result().token_ids for f in futs])
     return toks, lg
 
 
@@ -78,7 +86,7 @@ def _worker(rank, world, port, path, ep, out):
         if rank == 0:
             toks, lg = _run(eng)
             eng.stop_followers()
-            out.put((toks, lg.numpy(), comm.stats["all_reduce"], eng.counters["candidate_sampled_steps"]))
+            out.put((toks, lg.numpy(), comm.stats["all_reduce"], dict(eng.counters)))
         else:
             eng.follow()
     finally:
@@ -104,7 +112,7 @@ def test_tp2_matches_tp1(tmp_path, fam, ep):
     try:
         while True:
             try:
-                toks, lg, n_ar, n_cand = q.get(timeout=2)
+                toks, lg, n_ar, ctr = q.get(timeout=2)
                 break
             except queue.Empty:
                 if any(p.exitcode not in (None, 0) for p in procs) or time.time() - t0 > 300:
@@ -116,7 +124,10 @@ def test_tp2_matches_tp1(tmp_path, fam, ep):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     assert n_ar > 0
-    assert n_cand > 0                  # the top-k requests went through the candidate gather
+    # the top-k requests' decode steps drew from the gathered candidates INSIDE the step (in-graph sampler,
+    # chained decode); only their first tokens (after prefill) were drawn on the host
+    assert ctr["device_sampled_steps"] > 0, ctr
+    assert ctr["candidate_sampled_prefills"] > 0 and ctr["candidate_sampled_steps"] == 0, ctr
     assert toks == ref_toks
     ref = ref_lg[:, :lg.shape[1]].numpy()
     assert lg.shape[1] == spec.vocab
@@ -180,3 +191,19 @@ def test_tp_worker_serves_chat_over_nats(tmp_path):
                 p.kill()
         srv.stop()
     assert [p.exitcode for p in procs] == [0, 0]
+
+
+def test_rehearsal_driver_cpu(tmp_path):
+    """The one-GPU TP rehearsal driver (parallel/rehearsal.py) end to end on gloo: TP=1 reference process,
+    then 2 ranks; greedy + seeded top-k tokens equal, sampled decode rows drawn by the in-step sampler."""
+    from nats_llm_studio_amd.parallel import rehearsal
+    spec = _TP_SPECS["llama"]
+    path = str(tmp_path / "tp-llama.gguf")
+    write_synthetic_gguf(path, spec.name, "Q4_K_M", seed=4, spec=spec)
+    r = rehearsal.run(path, world=2, new_tokens=5, timeout=240, device="cpu")
+    assert "exception" not in r["tp"], r["tp"]
+    assert "exception" not in r["followers"][0], r["followers"][0]
+    assert r["tp"]["tokens"] == r["ref"]["tokens"]
+    c = r["tp"]["counters"]
+    assert c["device_sampled_steps"] > 0 and c["candidate_sampled_steps"] == 0, c
+    assert r["followers"][0]["counters"]["device_sampled_steps"] == c["device_sampled_steps"]

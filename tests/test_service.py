@@ -292,3 +292,55 @@ def test_engine_chat_rtt_helper(tiny_models):
     out = measure_engine_chat_rtt(eng, r.metadata, model_id="tiny-llama", n=3, warmup=1)
     assert out["n"] == 3 and 0 < out["p50_ms"] <= out["p99_ms"] and out["prompt_tokens"] > 0
     assert eng.thread is None
+
+
+def test_pull_deadline_stalled_bucket_then_resume(env, tiny_models):
+    """pull_model runs under its handler context (reference: 10 min, nats_llm_studio.go:251): a stalled bucket
+    (every client publish delayed by the embedded server's fault injection) answers ok:false with the deadline
+    error instead of hanging, and the next pull completes."""
+    srv, cfg, svc, cli = env
+    name = "synthetic/tiny-llama-GGUF/tiny-llama-Q4_K_M.gguf"
+    _push_tiny(srv.url, tiny_models["tiny-llama"], name)
+    cfg.timeout_pull = 1.0
+    srv.set_fault(0.0, delay_ms=400)
+    try:
+        t0 = time.time()
+        r = req(cli, "pull_model", {"identifier": "synthetic/tiny-llama"}, timeout=30)
+        took = time.time() - t0
+    finally:
+        srv.set_fault(0.0, 0)
+    assert r["ok"] is False and "context deadline exceeded" in r["error"], r
+    assert r["data"]["model"] == "synthetic/tiny-llama"
+    assert took < 10, took
+    cfg.timeout_pull = 600.0
+    r = req(cli, "pull_model", {"identifier": "synthetic/tiny-llama"}, timeout=60)
+    assert r["ok"] is True, r
+    local = os.path.join(cfg.models_dir, "synthetic", "tiny-llama-GGUF", "tiny-llama-Q4_K_M.gguf")
+    assert os.path.getsize(local) == os.path.getsize(tiny_models["tiny-llama"])
+
+
+def test_list_and_delete_deadlines(env):
+    """list_models (30 s) and delete_model (2 min) contexts: a stuck registry read / engine unload answers
+    with the deadline error at the configured bound."""
+    srv, cfg, svc, cli = env
+    d = os.path.join(cfg.models_dir, "synthetic", "slow-GGUF")
+    os.makedirs(d)
+    from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
+    write_synthetic_gguf(os.path.join(d, "slow-Q4_K_M.gguf"), "tiny-llama", "Q4_K_M")
+    real_list = svc.registry.list_api
+    cfg.timeout_list = 0.3
+    svc.registry.list_api = lambda *a, **k: (time.sleep(2.0), real_list(*a, **k))[1]
+    r = req(cli, "list_models", {})
+    assert r == {"ok": False, "error": "error reading model registry: context deadline exceeded",
+                 "data": {"http_status": 0}}
+    svc.registry.list_api = real_list
+    cfg.timeout_delete = 0.3
+    real_unload = svc.backend.unload
+    svc.backend.unload = lambda mid: time.sleep(2.0)
+    r = req(cli, "delete_model", {"model_id": "slow"})
+    assert r["ok"] is False and r["error"] == "context deadline exceeded", r
+    svc.backend.unload = real_unload
+    cfg.timeout_delete = 120.0
+    time.sleep(2.2)                       # the timed-out delete finished in the background
+    r = req(cli, "delete_model", {"model_id": "slow"})
+    assert r["ok"] is False and "not found" in r["error"]

@@ -1,0 +1,77 @@
+"""Tensor- and expert-parallel decode of the REAL engine on a GPU box with ONE MI355X: 2 processes share
+cuda:0 (gloo control plane, IPC one-shot data plane), capture their decode hipGraphs on every rank and
+decode greedy + seeded top-k requests; tokens must equal the same model at TP=1
+(nats_llm_studio_amd/parallel/rehearsal.py). The captured TP graphs hold no RCCL call: the vocab-parallel
+arg-max and the sampling-candidate gather run through the IPC kernels, sampled rows are drawn in-graph."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def models(tmp_path_factory):
+    from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
+    d = tmp_path_factory.mktemp("tp_models")
+    out = {}
+    for name, ft in (("llama-3-70b-2layer", "Q4_K_M"), ("mixtral-8x7b-1layer", "Q5_K_M")):
+        out[name] = write_synthetic_gguf(str(d / f"{name}-{ft}.gguf"), name, ft, seed=3)
+    return out
+
+
+@pytest.mark.parametrize("name,ep", [("llama-3-70b-2layer", False), ("mixtral-8x7b-1layer", True),
+                                     ("mixtral-8x7b-1layer", False)])
+def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep):
+    from nats_llm_studio_amd.parallel import rehearsal
+    r = rehearsal.run(models[name], world=2, ep=ep, new_tokens=8, timeout=300)
+    ref, tp, fol = r["ref"], r["tp"], r["followers"][0]
+    for v in (ref, tp, fol):
+        assert "exception" not in v, v
+    c = tp["counters"]
+    # every decode step replayed a captured graph on both ranks; sampled rows never left the graph
+    assert c["graph_replays"] > 0 and c["device_sampled_steps"] > 0, c
+    assert c["candidate_sampled_steps"] == 0, c
+    assert fol["counters"]["device_sampled_steps"] == c["device_sampled_steps"], (fol["counters"], c)
+    assert sorted(map(tuple, fol["graphs"])) == sorted(map(tuple, tp["graphs"]))
+    assert tp["oneshot_resets"] == 0
+    n = len(rehearsal.PROMPTS)
+    assert tp["tokens"][:n] == ref["tokens"][:n], (tp["tokens"], ref["tokens"])      # greedy
+    assert tp["tokens"][n:] == ref["tokens"][n:], (tp["tokens"], ref["tokens"])      # seeded top-k
+
+
+def test_sample_decode_cand_matches_cpu_twin(gpu):
+    """The in-graph candidate sampler (sample.hip) against its CPU twin (ops.sample_decode_cand)."""
+    import numpy as np
+    import torch
+    from nats_llm_studio_amd import ops
+    from nats_llm_studio_amd.engine.sampling import HIST, SamplingParams
+    g = torch.Generator().manual_seed(5)
+    n, M = 6, 512
+    vals = torch.randn(n, M, generator=g) * 3
+    ids = torch.sort(torch.randperm(50000, generator=g)[:M]).values.to(torch.int32).repeat(n, 1)
+    vals[5, 100:] = float("-inf")                   # a short candidate list (padding)
+    ids[5, 100:] = -1
+    ps = [SamplingParams(temperature=0.7, top_k=40, top_p=0.9),
+          SamplingParams(temperature=1.0, top_k=8, repeat_penalty=1.3, presence_penalty=0.4, frequency_penalty=0.1),
+          SamplingParams(),                                           # greedy: untouched
+          SamplingParams(temperature=0.0, repeat_penalty=1.5),        # penalised greedy
+          SamplingParams(temperature=1.2, min_p=0.05),
+          SamplingParams(temperature=0.9, top_k=20)]
+    params = torch.from_numpy(np.frombuffer(b"".join(ops.sample_params_bytes(p) for p in ps), dtype=np.uint8)
+                              .reshape(n, -1).copy())
+    seeds = torch.tensor([11, 12, 13, 14, 15, 16], dtype=torch.int64)
+    pos = torch.tensor([30, 70, 5, 9, 0, 3], dtype=torch.int32)
+    ctx = pos + 1
+    hist = torch.full((n, HIST), -1, dtype=torch.int32)
+    for r in range(n):
+        for q in range(max(0, int(pos[r]) + 1 - HIST), int(pos[r]) + 1):
+            hist[r, q % HIST] = int(ids[r, (q * 37) % 100])             # history tokens among the candidates
+    nid = torch.full((n,), 7, dtype=torch.int32)
+    cpu = dict(v=vals.clone(), h=hist.clone(), o=nid.clone())
+    ops.sample_decode_cand(cpu["v"], ids, n, params, seeds, pos, ctx, cpu["h"], cpu["o"])
+    d = dict(v=vals.to(gpu), h=hist.to(gpu), o=nid.to(gpu))
+    ops.sample_decode_cand(d["v"], ids.to(gpu), n, params.to(gpu), seeds.to(gpu), pos.to(gpu), ctx.to(gpu), d["h"],
+                           d["o"])
+    torch.cuda.synchronize()
+    assert d["o"].cpu().tolist() == cpu["o"].tolist()
+    assert torch.equal(d["h"].cpu(), cpu["h"])
+    assert int(d["o"][2]) == 7                                         # greedy row left alone
