@@ -127,6 +127,27 @@ def build_natscore(force: bool = False) -> str:
     return out
 
 
+def tokcore_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG, "tokenizer", "_tokcore" + suffix)
+
+
+def build_tokcore(force: bool = False) -> str:
+    """The native BPE merge loops of the tokenizers (csrc/tokcore), pybind11."""
+    out = tokcore_path()
+    srcs = sorted(glob.glob(os.path.join(CSRC, "tokcore", "*.cpp")))
+    if not srcs:
+        return ""
+    if force or _stale(out, srcs):
+        import pybind11
+        inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+        tmp = out + ".tmp"
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", *inc, *srcs, "-o", tmp])
+        os.replace(tmp, out)
+        _write_stamp(out, srcs)
+    return out
+
+
 def _natscore_lib_srcs():
     return [s for s in sorted(glob.glob(os.path.join(CSRC, "natscore", "*.cpp"))) if not s.endswith("bindings.cpp")]
 
@@ -150,6 +171,7 @@ def build_tool(name: str = "nls-nats", src: str = "nls_nats.cpp", extra=(), out_
 def build_all(force: bool = False):
     k = build_kernels(force)
     n = build_natscore(force)
+    build_tokcore(force)
     build_tool(force=force)
     return k, n
 

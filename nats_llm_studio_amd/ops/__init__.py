@@ -831,7 +831,10 @@ def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables:
     return out
 
 
-PREFILL_QT = 32      # tokens per attention_prefill query block: 16 * NSUB of attn_prefill.hip
+# attn_prefill.hip: the 8-wave 32x32x16 kernel takes 64-token query blocks; NLS_PREFILL_V1=1 selects the first
+# kernel (4 waves, 32-token blocks) for A/B
+PREFILL_V1 = _os.environ.get("NLS_PREFILL_V1", "0") == "1"
+PREFILL_QT = 32 if PREFILL_V1 else 64      # tokens per attention_prefill query block
 
 
 def prefill_blocks(tok_seq, pos, T: int):
@@ -858,9 +861,10 @@ def attention_prefill_ok(Hq: int, Hkv: int, D: int) -> bool:
 def attention_prefill(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, block_tables: torch.Tensor,
                       qblocks: torch.Tensor, nqb: int, tok_seq: torch.Tensor, ctx_len: torch.Tensor,
                       out: torch.Tensor, T: int, Hq: int, Hkv: int, D: int, block_size: int, scale: float):
-    """Causal MFMA flash attention over the paged cache for prompt chunks (query blocks of 16)."""
+    """Causal MFMA flash attention over the paged cache for prompt chunks (query blocks of PREFILL_QT tokens,
+    ops.prefill_blocks)."""
     if q.is_cuda:
-        _lib.check(_kv_fn("nls_attn_prefill", kc)(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
+        _lib.check(_kv_fn("nls_attn_prefill_v1" if PREFILL_V1 else "nls_attn_prefill", kc)(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(),
                                                block_tables.data_ptr(), block_tables.stride(0), qblocks.data_ptr(),
                                                nqb, Hq, Hkv, D, block_size, float(scale), out.data_ptr(),
                                                out.stride(0), _stream_ptr(q)), "nls_attn_prefill")

@@ -79,6 +79,10 @@ _SIGS = {
                          c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_attn_prefill8": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_void_p, c_long, c_void_p],
+    "nls_attn_prefill_v1": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                            c_int, c_int, c_float, c_void_p, c_long, c_void_p],
+    "nls_attn_prefill_v18": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                             c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_sample": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "nls_sample_params_size": [],
     "nls_sample_decode": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,

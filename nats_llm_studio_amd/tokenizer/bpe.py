@@ -16,6 +16,11 @@ from typing import Dict, List, Optional, Sequence
 
 import regex as re
 
+try:    # native merge loops (csrc/tokcore, GIL released); the pure-Python loops below are the reference
+    from . import _tokcore
+except ImportError:          # not built (python -m nats_llm_studio_amd.build)
+    _tokcore = None
+
 # Llama-3 pre-tokeniser (llama.cpp LLAMA_VOCAB_PRE_TYPE_LLAMA3)
 LLAMA3_PRETOK = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*"
                  r"|\s*[\r\n]+|\s+(?!\S)|\s+")
@@ -105,6 +110,24 @@ class ByteLevelBPE(_Base):
         self.pretok = re.compile(GPT2_PRETOK if pre in ("gpt2", "default") else
                                  QWEN2_PRETOK if pre == "qwen2" else LLAMA3_PRETOK)
         self._cache: Dict[str, List[int]] = {}
+        self.native = self._native_core()
+
+    def _native_core(self):
+        """The C++ merge loop when every byte has its own token and every merge's result is a vocabulary
+        entry (true of real BPE vocabularies; otherwise the Python loop, whose fallback splits unknown
+        symbols into bytes, stays in charge)."""
+        if _tokcore is None:
+            return None
+        byte_ids = [self.vocab.get(self.b2u[b]) for b in range(256)]
+        if any(i is None for i in byte_ids):
+            return None
+        merges = []
+        for (a, b), _ in sorted(self.ranks.items(), key=lambda kv: kv[1]):
+            ia, ib, im = self.vocab.get(a), self.vocab.get(b), self.vocab.get(a + b)
+            if ia is None or ib is None or im is None:
+                return None
+            merges.append((ia, ib, im))
+        return _tokcore.ByteLevel(byte_ids, merges)
 
     def _bpe(self, word: str) -> List[str]:
         parts = list(word)
@@ -122,6 +145,11 @@ class ByteLevelBPE(_Base):
             parts = parts[:best] + [parts[best] + parts[best + 1]] + parts[best + 2:]
 
     def _encode_plain(self, text: str) -> List[int]:
+        if self.native is not None:
+            return self.native.encode_pieces([p.encode("utf-8") for p in self.pretok.findall(text)])
+        return self._encode_plain_py(text)
+
+    def _encode_plain_py(self, text: str) -> List[int]:
         out: List[int] = []
         for piece in self.pretok.findall(text):
             hit = self._cache.get(piece)
@@ -169,6 +197,8 @@ class SentencePieceBPE(_Base):
         for i, t in enumerate(self.tokens):
             if self.token_types[i] == TOKEN_TYPE_BYTE and len(t) == 6 and t.startswith("<0x"):
                 self.byte_ids[int(t[3:5], 16)] = i
+        self.native = (_tokcore.Spm(self.tokens, [float(x) for x in self.scores],
+                                    [self.byte_ids.get(b, -1) for b in range(256)]) if _tokcore is not None else None)
 
     def _encode_plain(self, text: str) -> List[int]:
         if not text:
@@ -176,6 +206,11 @@ class SentencePieceBPE(_Base):
         s = text.replace(" ", self.SPACE)
         if self.add_space_prefix:
             s = self.SPACE + s
+        if self.native is not None:
+            return self.native.encode(s)
+        return self._merge_py(s)
+
+    def _merge_py(self, s: str) -> List[int]:
         # symbols as a doubly linked list; merge best-scoring pair first
         sym = list(s)
         prev = list(range(-1, len(sym) - 1))

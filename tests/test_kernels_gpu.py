@@ -1377,3 +1377,59 @@ def test_candidate_sampling_matches_full_vocab(gpu, shards):
     mh = [[{t: j for j, t in enumerate(ixl[r])}[t] for t in hist[r][-64:] if t in set(ixl[r])] for r in range(n)]
     picks = sample_rows_gpu(cv.contiguous(), params, mh, us)
     assert [ixl[r][j] for r, j in enumerate(picks)] == ref
+
+
+def _prefill_ref_gpu(q, kc, vc, bt, chunks, Hq, Hkv, D, bs, scale):
+    """Plain fp32 PyTorch causal attention over the paged cache, per chunk (seq, pos0, n): the reference of
+    attn_prefill at long offsets (the CPU per-token reference is too slow for 32K contexts)."""
+    out, t = [], 0
+    G = Hq // Hkv
+    for s, p0, n in chunks:
+        nk = p0 + n
+        keys = torch.arange(nk, device=q.device)
+        slots = bt[s, keys // bs].long() * bs + keys % bs
+        K = kc[slots].float()                     # [nk, Hkv, D]
+        V = vc[slots].float()
+        Q = q[t:t + n].float().view(n, Hkv, G, D)
+        S = torch.einsum("nhgd,khd->hgnk", Q, K) * scale
+        qpos = torch.arange(p0, p0 + n, device=q.device)
+        S = S.masked_fill(keys[None, None, None, :] > qpos[None, None, :, None], float("-inf"))
+        P = torch.softmax(S, dim=-1)
+        O = torch.einsum("hgnk,khd->nhgd", P, V).reshape(n, Hq * D)
+        out.append(O)
+        t += n
+    return torch.cat(out)
+
+
+@pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
+@pytest.mark.parametrize("D,G,Hkv", [(128, 4, 2), (128, 8, 1), (64, 4, 2)])
+def test_attention_prefill_long_offsets(gpu, D, G, Hkv, kvt):
+    """attn_prefill at production shapes: a 2048-token chunk continuing a 30K-token prefix (the last chunk of
+    a 32K prompt), next to short chunks of two other sequences (one fresh, one mid-context), pages scattered
+    over the pool; fp32 PyTorch reference."""
+    torch.manual_seed(1)
+    bs = 16
+    Hq = Hkv * G
+    chunks = [(0, 30720, 2048), (1, 5000, 100), (2, 0, 70)]
+    nblk = (32768 + bs - 1) // bs
+    nseq = 3
+    perm = torch.randperm(nseq * nblk, device=gpu).view(nseq, nblk).int()
+    slots = nseq * nblk * bs
+    kc = (torch.randn(slots, Hkv, D, device=gpu) * 0.5).to(kvt)
+    vc = torch.randn(slots, Hkv, D, device=gpu).to(kvt)
+    T = sum(n for _, _, n in chunks)
+    pos, tseq = [], []
+    for s, p0, n in chunks:
+        pos += list(range(p0, p0 + n))
+        tseq += [s] * n
+    pos = np.array(pos, np.int32)
+    tseq = np.array(tseq, np.int32)
+    q = torch.randn(T, Hq * D, device=gpu).to(torch.bfloat16)
+    ref = _prefill_ref_gpu(q, kc, vc, perm, chunks, Hq, Hkv, D, bs, D ** -0.5)
+    qb = ops.prefill_blocks(tseq, pos, T)
+    out = torch.zeros(T, Hq * D, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.attention_prefill(q, kc, vc, perm, torch.from_numpy(qb).to(gpu), len(qb), None, None, out, T, Hq, Hkv, D, bs,
+                          D ** -0.5)
+    torch.cuda.synchronize()
+    err = (out.float() - ref).abs().max().item()
+    assert err < 2e-2, err

@@ -67,3 +67,26 @@ def test_qwen2_chatml_and_single_digit_pretokeniser(tiny_models):
     assert s.startswith("<|im_start|>system\n") and s.endswith("<|im_start|>assistant\n")
     assert tok.tokens[tok.eos_id] == "<|im_end|>"
     assert [p for p in tok.pretok.findall("x 2024")] == ["x", " ", "2", "0", "2", "4"]
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-qwen2", "tiny-granite"])
+def test_native_merge_loop_matches_python(tiny_models, name):
+    """csrc/tokcore (C++ merge loops, GIL released) gives exactly the Python reference's ids."""
+    import random
+    from nats_llm_studio_amd.gguf.reader import GGUFReader
+    from nats_llm_studio_amd.tokenizer.bpe import tokenizer_from_metadata
+    tok = tokenizer_from_metadata(GGUFReader(tiny_models[name]).metadata)
+    assert tok.native is not None, "native tokenizer core not built"
+    rnd = random.Random(7)
+    alphabet = list("abcdefghijklmnopqrstuvwxyz ABCXYZ0123456789  \n\t.,;:!?'\"-()") + \
+        ["é", "ü", "中", "文", "😀", "ß", "  ", "\n\n", "'s", "'ll", "12345", "hello", " world"]
+    texts = ["", "a", "hello world", "The quick brown fox jumps over the lazy dog 1234567 times!"]
+    texts += ["".join(rnd.choice(alphabet) for _ in range(rnd.randint(1, 200))) for _ in range(150)]
+    for t in texts:
+        nat = tok.encode(t, add_bos=False)
+        keep, tok.native = tok.native, None
+        try:
+            ref = tok.encode(t, add_bos=False)
+        finally:
+            tok.native = keep
+        assert nat == ref, (t, nat, ref)
