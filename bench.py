@@ -434,7 +434,7 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
         "weights_gb_per_rank": info["weights_gb"],
         "comm": info["comm_stats"],
         "timings_s": info["timings"],
-        "kernels_built_from_sources": _kernels_current(),
+        "kernels_stamp_current": _kernels_current(),
         **info["extra"],
     }
     print(json.dumps(out), flush=True)

@@ -239,6 +239,10 @@ class Engine:
         # preemptions right after a burst of admissions); NLS_KV_RESERVE=full restores worst-case
         # reservation of prompt + max_tokens at admission (no growth, no preemption)
         self.watermark = max(1, num_blocks // 100)
+        # preemption hysteresis: for PRESSURE_STEPS steps after a preemption, admission (new and preempted
+        # sequences alike) keeps one free block per running sequence (~16 decode steps of growth for all of
+        # them) instead of the 1 % watermark, so a sequence just re-admitted is not the next victim at once
+        self._pressure_until = -1
         self.reserve_full = os.environ.get("NLS_KV_RESERVE", "ondemand") == "full"
         self.max_prefill = max_prefill_tokens
         self.prefill_attn = prefill_attn      # MFMA flash-prefill attention (else per-token decode kernel)
@@ -474,6 +478,8 @@ class Engine:
                 s.keys = BlockAllocator.chain_keys(s.tokens, self.bs, (s.n_target - 1) // self.bs)
                 hit = self.alloc.match(s.keys)
                 reserve = self.watermark if (self.running and not self.reserve_full) else 0
+                if self.running and self.counters["steps"] < self._pressure_until:
+                    reserve = max(reserve, len(self.running))
                 blocks = None
                 if need - len(hit) + reserve <= self.alloc.n_free:
                     blocks = self.alloc.alloc(need - len(hit))
@@ -569,6 +575,7 @@ class Engine:
         self._gather(b, n, need_logits)
 
     CAND = 128           # TP sampling: candidates per rank and row
+    PRESSURE_STEPS = 64  # preemption hysteresis window (steps), see _pressure_until
 
     def _cand_ok(self, seqs) -> bool:
         """Can every sampled row of these sequences be drawn exactly from the gathered top-CAND candidates of
@@ -972,6 +979,7 @@ class Engine:
         s.n_fed = 0
         s.preempted += 1
         self.counters["preemptions"] += 1
+        self._pressure_until = self.counters["steps"] + self.PRESSURE_STEPS
         self.counters["recompute_tokens"] += s.n_target
         self.running = [x for x in self.running if x is not s]
         with self.lock:

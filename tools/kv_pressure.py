@@ -75,7 +75,10 @@ def main():
                           mean_running=round(float(np.mean([s["running"] for s in samples])), 1) if samples else peak,
                           finished=done, finished_full_length=ok, decode_tokens=c["decode_tokens"],
                           decode_tok_s=round(c["decode_tokens"] / el, 1), preemptions=c["preemptions"],
-                          recompute_tokens=c["recompute_tokens"], pool_tokens=pool_tokens)), flush=True)
+                          recompute_tokens=c["recompute_tokens"], prefill_tokens=c["prefill_tokens"],
+                          # share of all forward tokens spent re-prefilling preempted sequences
+                          recompute_waste=round(c["recompute_tokens"] / max(1, c["decode_tokens"] + c["prefill_tokens"]), 4),
+                          pool_tokens=pool_tokens)), flush=True)
     eng.shutdown()
 
 
