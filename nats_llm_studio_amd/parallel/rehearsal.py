@@ -55,6 +55,36 @@ def _engine(path: str, dev, shard=None, comm=None, graphs: bool = True):
                   ctx=512)
 
 
+def _kernel_profile(eng, futs, steps: int) -> Dict:
+    """torch.profiler (roctracer) around `steps` greedy decode steps of THIS rank: every kernel of the captured
+    TP decode graph by name, count and device time. (rocprofv3 intercepts every process's queues, and the
+    two ranks sharing the GPU must run concurrently for the IPC kernels to meet: under it a rank's poll
+    times out, which the engine then reports as a one-shot timeout -- so the trace is taken in-process.)"""
+    import torch
+    from torch.profiler import ProfilerActivity, profile
+    n = 0
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(steps):
+            if all(f.done() for f in futs):
+                break
+            eng.step()
+            n += 1
+        eng._drain()
+        torch.cuda.synchronize()
+    kern = {}
+    for ev in prof.events():
+        if getattr(ev, "device_type", None) is None or "CUDA" not in str(ev.device_type):
+            continue
+        name = ev.name
+        k = kern.setdefault(name, [0, 0.0])
+        k[0] += 1
+        dt = getattr(ev, "device_time_total", None)
+        k[1] += float(dt if dt is not None else getattr(ev, "cuda_time_total", 0.0))
+    rows = sorted(([v[0] / max(1, n), round(v[1] / max(1, n), 1), k] for k, v in kern.items()), key=lambda r: -r[1])
+    return dict(steps=n, per_step=[[round(c, 2), us, nm[:90]] for c, us, nm in rows],
+                rccl_kernels=[nm for _, _, nm in rows if "nccl" in nm.lower() or "rccl" in nm.lower()])
+
+
 def _drive(eng, new_tokens: int, profile_steps: int = 0) -> Dict:
     """Leader: greedy requests, then seeded top-k requests (all in flight together)."""
     from ..engine.engine import GenRequest
@@ -85,6 +115,8 @@ def _drive(eng, new_tokens: int, profile_steps: int = 0) -> Dict:
         eng._drain()
         _sync(eng.dev)
         out["profile_window_ms_per_step"] = round((time.perf_counter() - t1) / profile_steps * 1e3, 3)
+        if eng.dev.type == "cuda":
+            out["kernel_profile"] = _kernel_profile(eng, futs, profile_steps)
         while not all(f.done() for f in futs):
             eng.step()
     return out
@@ -126,8 +158,10 @@ def _rank_main(rank: int, world: int, port: int, path: str, ep: bool, new_tokens
             comm.oneshot = OneShotAllReduce(comm)
         eng = _engine(path, dev, ShardSpec(rank, world, ep), comm)
         if rank == 0:
-            res = _drive(eng, new_tokens, profile_steps)
-            eng.stop_followers()
+            try:
+                res = _drive(eng, new_tokens, profile_steps)
+            finally:
+                eng.stop_followers()          # also on failure: followers must not wait for a next step
             res["comm"] = dict(comm.stats)
             res["oneshot_resets"] = comm.oneshot.resets if comm.oneshot is not None else None
             res["ctrl_transport"] = "shm-ring" if comm.ring is not None else "gloo"
@@ -150,12 +184,17 @@ def _collect(procs, q, n: int, timeout: float) -> Dict:
     import queue
     res = {}
     t0 = time.time()
+    t_fail = None
     try:
         while len(res) < n:
             try:
                 k, v = q.get(timeout=2)
                 res[k] = v
+                if "exception" in v and t_fail is None:
+                    t_fail = time.time()
             except queue.Empty:
+                if t_fail is not None and time.time() - t_fail > 30:
+                    break                    # a rank failed: give the others 30 s, then stop waiting
                 if time.time() - t0 > timeout:
                     raise TimeoutError(f"rehearsal: {len(res)}/{n} results after {timeout} s")
                 dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]

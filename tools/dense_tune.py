@@ -5,7 +5,7 @@ needs an epilogue pass). Every launch is captured in a hipGraph over rotating we
 weights stream from HBM as in serving) and timed as the median of rounds.
 
 Candidates: mode 10 (hgemm10.hip, 256x256 8-phase) x split-K, modes 4/5 (hgemm.hip, 128/256 weight rows,
-128/256 activation rows) x split-K. With --emit the winners are printed as "d:<rows>:<K>:<Mbucket>" tuning
+128/256 activation rows, 8 or 16 waves) x split-K. With --emit the winners are printed as "d:<rows>:<K>:<Mbucket>" tuning
 entries (ops/gemv_tuning.json) -- the table that replaced the library-GEMM ("L:") selections.
 
     python tools/dense_tune.py --model llama-3-70b --M 256,512,1024,2048 [--roles qkv,o,gateup,down,lm_head] --emit
@@ -62,9 +62,10 @@ def roles(spec):
 def candidates(M, K, epi):
     out = [(10, 8, 1, ks) for ks in (1, 2, 3, 4, 6, 8)]
     for mode in (4, 5):
-        for wm in ((2, 4) if M >= 192 else (2,)):
-            for ks in (1, 2, 4):
-                out.append((mode, 8, wm, ks))
+        for waves in (8, 16):
+            for wm in ((2, 4) if M >= 192 else (2,)):
+                for ks in (1, 2, 4):
+                    out.append((mode, waves, wm, ks))
     if epi == "argmax":
         out = [c for c in out if c[3] == 1]
     nkt = K // 64
