@@ -34,10 +34,27 @@ using namespace nls_gemv;
 using nls_dma::glds16;
 using nls_dma::lds_addr;
 
-constexpr int BM = 256, BN = 256;
+// BN = 256 (rt 1) or 128 (rt 2: narrow-N shapes get twice the workgroups -- Q|K|V, o at M = 512..2048): the
+// weight half of a K-tile buffer and each wave's weight rows halve; the activation half, the phase schedule
+// and the unit order stay, only the DMA instruction counts of the two weight units (and so the counted
+// vmcnt of each phase) change.
+constexpr int BM = 256;
 constexpr int KT = 64;                       // K per tile
-constexpr int TB = 64 * 1024;                // bytes of one K-tile buffer: A 32 KiB | B 32 KiB
-constexpr int LDS = 2 * TB;
+template <int BN>
+struct H10 {
+  static constexpr int AB = BN * KT * 2;     // weight half of a K-tile buffer (32 or 16 KiB)
+  static constexpr int TB = AB + BM * KT * 2;
+  static constexpr int LDS = 2 * TB;
+  static constexpr int RTG = BN / 32;        // 16-row weight tiles per wave group (wr)
+  static constexpr int NQH = RTG / 2;        // ... per quadrant half (nq)
+  static constexpr int NA = BN / 128;        // DMA instructions per lane of a weight unit (B units: 2)
+  // counted waits: the last three units issued stay in flight (units U0/U3 carry NA, U1/U2 two)
+  static constexpr int VM_PRO = NA + 2;      // after the prologue: U0(1) U1(1)
+  static constexpr int VM_Q0 = NA + 4;       // U0(T+1) U1(T+1) U2(T+1)
+  static constexpr int VM_Q1 = NA + 4;       // U1(T+1) U2(T+1) U3(T+1)
+  static constexpr int VM_Q2 = 2 * NA + 2;   // U2(T+1) U3(T+1) U0(T+2)
+  static constexpr int VM_Q3 = 2 * NA + 2;   // U3(T+1) U0(T+2) U1(T+2)
+};
 
 DEVI int swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }
 
@@ -46,17 +63,23 @@ DEVI void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-// unit u's 16 (row-tile, k-step) subtiles; a subtile = 16 rows x 32 k = 1 KiB at (rt * 2 + ks) * 1 KiB of
+// unit u's (row-tile, k-step) subtiles; a subtile = 16 rows x 32 k = 1 KiB at (rt * 2 + ks) * 1 KiB of
 // its operand region. A units (0, 3): weight row-tiles; B units (1, 2): activation row-tiles.
-DEVI int unit_rt(int u, int idx) {           // idx = 0..7 (row-tile slot of the unit)
-  // U0: A {0-3, 8-11}; U3: A {4-7, 12-15}; U1: B {0,1,4,5,8,9,12,13}; U2: B {2,3,6,7,10,11,14,15}
-  if (u == 0) return (idx & 3) + 8 * (idx >> 2);
-  if (u == 3) return 4 + (idx & 3) + 8 * (idx >> 2);
+template <int BN>
+DEVI int unit_rt(int u, int idx) {           // idx: row-tile slot of the unit
+  // BN 256: U0: A {0-3, 8-11}; U3: A {4-7, 12-15}. BN 128: U0: A {0-1, 4-5}; U3: A {2-3, 6-7}.
+  // U1: B {0,1,4,5,8,9,12,13}; U2: B {2,3,6,7,10,11,14,15}
+  constexpr int NQH = H10<BN>::NQH, RTG = H10<BN>::RTG;
+  if (u == 0) return (idx % NQH) + RTG * (idx / NQH);
+  if (u == 3) return NQH + (idx % NQH) + RTG * (idx / NQH);
   if (u == 1) return (idx & 1) + 4 * (idx >> 1);
   return 2 + (idx & 1) + 4 * (idx >> 1);
 }
 
+template <int BN>
 DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
+  typedef H10<BN> C;
+  constexpr int TB = C::TB, NQH = C::NQH, NA = C::NA;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -66,18 +89,21 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   const int M = a.M;
   const act_t* Wd = reinterpret_cast<const act_t*>(S.w);
 
-  // ---- DMA: unit u of K-tile T -> buffer T & 1. This wave issues subtiles idx = 2 * wave + j (j = 0, 1)
-  // of every unit: row-tile unit_rt(u, idx >> 1), k-step idx & 1. Lane L -> row 16 rt + (L >> 2), physical
-  // chunk L & 3 <- logical chunk (L & 3) ^ swz(L >> 2).
+  // ---- DMA: unit u of K-tile T -> buffer T & 1. This wave issues subtiles idx = n * wave + j (j < n; n = 2,
+  // or NA for a weight unit) of every unit: row-tile unit_rt(u, idx >> 1), k-step idx & 1. Lane L -> row
+  // 16 rt + (L >> 2), physical chunk L & 3 <- logical chunk (L & 3) ^ swz(L >> 2).
   const int lc = (lane & 3) ^ swz(lane >> 2);
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   auto dma = [&](int u, int T) __attribute__((always_inline)) {
     const int Tc = t0 + min(T, nkt - 1);       // clamped: past the end re-stages the last tile (same bytes)
-    const uint32_t buf = base + (uint32_t)(T & 1) * TB + ((u == 1 || u == 2) ? 32768u : 0u);
+    const bool bu = u == 1 || u == 2;
+    const uint32_t buf = base + (uint32_t)(T & 1) * TB + (bu ? (uint32_t)C::AB : 0u);
+    const int n = bu ? 2 : NA;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int idx = 2 * wave + j;
-      const int rt = unit_rt(u, idx >> 1), kstep = idx & 1;
+      if (j >= n) break;
+      const int idx = n * wave + j;
+      const int rt = unit_rt<BN>(u, idx >> 1), kstep = idx & 1;
       const act_t* src;
       if (u == 1 || u == 2) {
         const int row = min(16 * rt + (lane >> 2), M - 1);
@@ -92,34 +118,35 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 
   // ---- fragments: lane reads row (l & 15) of a 16-row subtile, logical chunk l >> 4
   const int fro = (lane & 15) * 64 + (((lane >> 4) ^ swz(lane & 15)) << 4);
-  f16x8 FA[4][2], FB0[2][2], FB1[2][2];
+  f16x8 FA[NQH][2], FB0[2][2], FB1[2][2];
   auto rdA = [&](int T, int nq) __attribute__((always_inline)) {
     const uint8_t* p = lds + (T & 1) * TB + fro;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NQH; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        FA[i][s] = *reinterpret_cast<const f16x8*>(p + ((wr * 8 + nq * 4 + i) * 2 + s) * 1024);
+        FA[i][s] = *reinterpret_cast<const f16x8*>(p + ((wr * C::RTG + nq * NQH + i) * 2 + s) * 1024);
   };
   auto rdB = [&](f16x8 (&F)[2][2], int T, int mh) __attribute__((always_inline)) {
-    const uint8_t* p = lds + (T & 1) * TB + 32768 + fro;
+    const uint8_t* p = lds + (T & 1) * TB + C::AB + fro;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) F[i][s] = *reinterpret_cast<const f16x8*>(p + ((wc * 4 + mh * 2 + i) * 2 + s) * 1024);
   };
-  f32x4 acc[8][4];
+  f32x4 acc[2 * NQH][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 2 * NQH; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](int nq, int mh, const f16x8 (&F)[2][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NQH; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[nq * 4 + i][mh * 2 + j] = mfma16(FA[i][s], F[j][s], acc[nq * 4 + i][mh * 2 + j]);
+        for (int j = 0; j < 2; ++j)
+          acc[nq * NQH + i][mh * 2 + j] = mfma16(FA[i][s], F[j][s], acc[nq * NQH + i][mh * 2 + j]);
   };
   auto bar = []() __attribute__((always_inline)) {
     __builtin_amdgcn_s_barrier();
@@ -135,7 +162,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     dma(3, 0);
     dma(0, 1);
     dma(1, 1);
-    wait_vm<4>();
+    wait_vm<C::VM_PRO>();
     bar();
     if (wr == 1) bar();
     for (int T = 0; T < nkt; ++T) {
@@ -148,7 +175,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       __builtin_amdgcn_s_setprio(1);
       mma(0, 0, FB0);
       __builtin_amdgcn_s_setprio(0);
-      wait_vm<6>();
+      wait_vm<C::VM_Q0>();
       bar();
       // ---- Q1: (nq0, mh1); stage U3(T+1)
       rdB(FB1, T, 1);
@@ -158,7 +185,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       __builtin_amdgcn_s_setprio(1);
       mma(0, 1, FB1);
       __builtin_amdgcn_s_setprio(0);
-      wait_vm<6>();
+      wait_vm<C::VM_Q1>();
       bar();
       // ---- Q2: (nq1, mh1); stage U0(T+2)
       rdA(T, 1);
@@ -168,7 +195,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       __builtin_amdgcn_s_setprio(1);
       mma(1, 1, FB1);
       __builtin_amdgcn_s_setprio(0);
-      wait_vm<6>();
+      wait_vm<C::VM_Q2>();
       bar();
       // ---- Q3: (nq1, mh0) from registers; stage U1(T+2)
       dma(1, T + 2);
@@ -176,7 +203,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       __builtin_amdgcn_s_setprio(1);
       mma(1, 0, FB0);
       __builtin_amdgcn_s_setprio(0);
-      wait_vm<6>();
+      wait_vm<C::VM_Q3>();
       bar();
     }
     if (wr == 0) bar();                         // barrier counts even again
@@ -187,10 +214,10 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 
   // ---- epilogue (mode 8's): lane holds weight rows nb + 16i + 4(l >> 4) + e, activation row mb + 16j + (l & 15)
   const int g4 = 4 * (lane >> 4), r16 = lane & 15;
-  const int nb = row0 + wr * 128, mb = wc * 64;
+  const int nb = row0 + wr * (BN / 2), mb = wc * 64;
   if (ks > 1 || a.epi == EPI_SLABS) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2 * NQH; ++i) {
       const int n = nb + 16 * i + g4;
       if (n >= S.rows) continue;
 #pragma unroll
@@ -206,7 +233,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   if (a.epi == EPI_ROPE) {
     // RoPE pairs (e, e + 1) of the lane's 4 consecutive weight rows: no cross-lane traffic
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2 * NQH; ++i) {
       const int n = nb + 16 * i + g4;
       if (n >= S.rows) continue;
 #pragma unroll
@@ -224,7 +251,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
   if (a.epi == EPI_SWIGLU) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2 * NQH; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         f32x4 u;
@@ -244,7 +271,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
   if (a.epi != EPI_ARGMAX) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2 * NQH; ++i) {
       const int n = nb + 16 * i + g4;
       if (n >= S.rows) continue;
 #pragma unroll
@@ -268,7 +295,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     for (int j = 0; j < 4; ++j) {
       unsigned long long k = 0ull;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 2 * NQH; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int n = nb + 16 * i + g4 + e;
@@ -285,6 +312,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
 }
 
+template <int BN>
 __global__ __launch_bounds__(512, 1) void hgemm10_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                           int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t h10lds[];
@@ -304,21 +332,31 @@ __global__ __launch_bounds__(512, 1) void hgemm10_kernel(SegList segs, GemvArgs 
   a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
   if (a.argmax) a.argmax += m0;
   a.M = min(BM, a.M - m0);
-  const int row0 = (tile - S.tile_begin) * BN;
-  h10_tile(S, row0, kslice, ks, a, ws, h10lds);
+  const int row0 = (tile - S.tile_begin) * BN;       // (host tile counts use BN-row tiles)
+  h10_tile<BN>(S, row0, kslice, ks, a, ws, h10lds);
 }
 
-int launch_dense10(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
+template <int BN>
+int launch_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
+  constexpr int LDS = H10<BN>::LDS;
   const int nmb = (a.M + BM - 1) / BM;
   const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
-    if (hipFuncSetAttribute((const void*)hgemm10_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)hgemm10_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
+        hipSuccess)
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL(hgemm10_kernel, dim3(grid), dim3(512), LDS, st, sl, a, ks, ws, ntiles, nmb);
+  hipLaunchKernelGGL(hgemm10_kernel<BN>, dim3(grid), dim3(512), LDS, st, sl, a, ks, ws, ntiles, nmb);
   return (int)hipGetLastError();
+}
+
+// bn: weight rows per workgroup tile (256 or 128)
+int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
+  if (bn == 256) return launch_t<256>(sl, ntiles, ks, ws, a, st);
+  if (bn == 128) return launch_t<128>(sl, ntiles, ks, ws, a, st);
+  return -1;
 }
 
 }  // namespace nls_hg10

@@ -13,7 +13,7 @@ namespace nls_hg8 {
 int launch_dense8(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
 }
 namespace nls_hg10 {
-int launch_dense10(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
+int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
 }
 namespace nls_q9 {
 int launch_q9(int kset, int waves, int rt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
@@ -104,8 +104,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
   if (mode < 0 || mode > 10 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
-  if (mode == 10) {
-    if (waves != 8 || fz->xf || fz->onw || ldx % 8 ||
+  if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
+    if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
     for (int i = 0; i < nseg; ++i)
@@ -141,7 +141,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 10 ? 256 : mode == 9 ? 16 * waves * rt : mode == 8 ? 32 * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : mode == 8 ? 32 * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -241,7 +241,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     if (ks < 1) ks = 1;
     int rc;
     if (mode == 10)
-      rc = nls_hg10::launch_dense10(sl, tiles, ks, (float*)ws, a, st);
+      rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 8)

@@ -674,6 +674,10 @@ constexpr size_t XL_LDS_BYTES = 48 * 1024;    // path-B XL: largest staged x sli
 #define NLS_XL_DEPTH 8
 #endif
 constexpr int XL_DEPTH = NLS_XL_DEPTH;         // path-B XL: weight super-blocks in flight per wave
+#ifndef NLS_XL_DEPTH2
+#define NLS_XL_DEPTH2 2
+#endif
+constexpr int XL_DEPTH2 = NLS_XL_DEPTH2;       // ... with two 16-row tiles per wave (RT = 2: batch-1 gate|up)
 
 DEVI int lds_off(int row, int k) {            // element offset in a [rows][256] f16 tile
   const int ch = (k >> 3) ^ (row & 15);
@@ -713,7 +717,8 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     static_assert(MT == 1, "XL stages one activation tile");
     typedef typename RawOf<T>::type Raw;
     // no per-step x traffic here, so the weight stream can run XL_DEPTH super-blocks ahead
-    constexpr int DEPTH = RT == 1 ? (sizeof(Raw) <= 48 ? XL_DEPTH : (sizeof(Raw) <= 80 ? 4 : 2)) : 2;
+    constexpr int DEPTH = RT == 1 ? (sizeof(Raw) <= 48 ? XL_DEPTH : (sizeof(Raw) <= 80 ? 4 : 2))
+                                  : (sizeof(Raw) <= 48 ? XL_DEPTH2 : 2);
     Raw wb[DEPTH][RT];
     const int sbl = max(sb1 - 1, sb0);
     XPre xp;              // batch 1: the x slice's loads go out first (xpre), the weight prologue after them

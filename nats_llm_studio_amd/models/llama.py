@@ -299,9 +299,6 @@ class LlamaModel:
             if budget_bytes is not None and need > budget_bytes - added:
                 break
             added += sum(w.expand_dense() for w in ws)
-            if not tier:                  # fused Q|K|V: one f16 matrix for the library GEMM (mode 7)
-                for lw in self.layers:
-                    ops.fuse_dense(lw.qkv)
         self.dense_bytes = getattr(self, "dense_bytes", 0) + added
         return added
 

@@ -34,11 +34,10 @@ DENSE_MIN_M = int(_os.environ.get("NLS_DENSE_GEMM_M", "128"))
 # (Mixtral-8x7B batch 1 / 16, profiles/moe_selected_experts.txt: 0,4,2,1 3.90 / 10.0 ms per step vs 0,8,1,1
 # 4.94 / 15.1)
 MOE_GEMV = tuple(int(v) for v in _os.environ.get("NLS_MOE_GEMV", "0,4,2,1").split(","))
-# "Mode 7": a plain dense projection on the weights' f16 copies may run as a library GEMM (hipBLASLt via
-# torch.mm) followed by its epilogue as a separate HIP pass, for the shapes and batch buckets where that
-# measured faster than the fused hand-written kernels (tuning table "L:" entries, tools/blaslt_ab.py:
-# gate/up M=512 99.8 us + SwiGLU pass vs 177 us fused). NLS_LIB_GEMM=0 disables it.
-LIB_GEMM = _os.environ.get("NLS_LIB_GEMM", "1") == "1"
+# Every large-M projection runs on the hand-written dense GEMMs (modes 4/5/10, tuning "d:" entries). The
+# library GEMM that r02-r03 dispatched for some shapes ("mode 7": hipBLASLt via torch.mm + a separate epilogue)
+# is gone from the engine; tools/dense_tune.py keeps measuring against it as the reference
+# (profiles/dense_tune_r04.jsonl).
 ACT_DTYPE = torch.float16   # activation dtype of every GEMM/GEMV input and SwiGLU/RMSNorm/attention output
 
 
@@ -263,84 +262,6 @@ def _contiguous_cols(segs: Sequence[Seg]) -> bool:
     return all(s.ycol == segs[0].ycol + sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
 
 
-def lib_gemm_ok(segs: Sequence[Seg], M: int, epi: str, alpha: float = 1.0, argmax=None, y=None) -> bool:
-    """May this launch run as mode 7 (library GEMM + epilogue pass)? Epilogues: SwiGLU (f16 out), a
-    plain f32 store into a row-contiguous output, and "addnorm" (one f32 slab for the fused residual add +
-    RMSNorm pass); no arg-max, no row maps."""
-    if not LIB_GEMM or argmax is not None or epi not in ("swiglu", "f32", "addnorm") or not dense_ok(segs, M):
-        return False
-    if not _contiguous_cols(segs):
-        return False
-    if epi == "f32" and (alpha != 1.0 or segs[0].ycol != 0 or y is None or y.dtype != torch.float32
-                         or y.stride(1) != 1 or y.stride(0) != sum(s.w.rows for s in segs)):
-        return False
-    from . import tuning
-    return tuning.select_lib(segs, M)
-
-
-def fuse_dense(segs: Sequence[Seg]) -> None:
-    """Give a multi-segment launch (fused Q|K|V) ONE [sum(rows), K] f16 matrix for mode 7: the
-    segments' f16 copies are concatenated and become views into it (no extra memory). Call it at load,
-    before any launch: a captured hipGraph holds the d16 pointers, so they must never move afterwards."""
-    if len(segs) < 2 or any(s.w.d16 is None for s in segs):
-        return
-    cache = segs[0].w.__dict__.setdefault("_lib_cat", {})
-    key = tuple(id(s.w) for s in segs)
-    if key in cache:
-        return
-    W = torch.cat([s.w.d16 for s in segs], 0)
-    r0 = 0
-    for s in segs:
-        s.w.d16 = W[r0:r0 + s.w.rows]
-        r0 += s.w.rows
-    cache[key] = W
-
-
-def _lib_weight(segs: Sequence[Seg]) -> torch.Tensor:
-    """[sum(rows), K] f16 operand of a mode-7 launch: fuse_dense()'s concatenation, else (segments never
-    fused) a separate concatenated copy -- the segments' own copies stay where captured graphs point."""
-    if len(segs) == 1:
-        return segs[0].w.d16
-    cache = segs[0].w.__dict__.setdefault("_lib_cat", {})
-    key = tuple(id(s.w) for s in segs)
-    W = cache.get(key)
-    if W is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("mode 7 on unfused segments inside graph capture: call ops.fuse_dense at load")
-        W = torch.cat([s.w.d16 for s in segs], 0)
-        cache[key] = W
-    return W
-
-
-_WS16 = {}
-
-
-def _workspace16(dev, n: int) -> torch.Tensor:
-    """f16 scratch of mode-7 GEMM outputs (only grows; superseded buffers stay alive for captured graphs)."""
-    w = _WS16.get(dev)
-    if w is None or w.numel() < n:
-        if w is not None:
-            _WS_OLD.append(w)
-        w = torch.empty(max(n, 8 << 20), dtype=torch.float16, device=dev)
-        _WS16[dev] = w
-    return w
-
-
-def lib_gemm(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float, epi: str):
-    """Mode 7: hipBLASLt GEMM on the f16 copies (torch.mm, fp32 accumulate), then the epilogue."""
-    W = _lib_weight(segs)
-    N = W.shape[0]
-    if epi == "swiglu":
-        h = _workspace16(x.device, M * N)[:M * N].view(M, N)
-        torch.mm(x[:M], W.t(), out=h)
-        yo = y[:, segs[0].ycol:]
-        _lib.check(_lib.lib().nls_swiglu16(h.data_ptr(), N, M, N, float(alpha), yo.data_ptr(), y.stride(0),
-                                           _stream_ptr(x)), "nls_swiglu16")
-    else:
-        torch.mm(x[:M], W.t(), out_dtype=torch.float32, out=y[:M])
-    return y
-
-
 def gemv_config(segs: Sequence[Seg], M: int):
     """(mode, waves, rt, ks) for a launch. mode 0 = waves split K (small batch, mapped rows);
     mode 1 = waves split rows over an LDS-staged activation tile (+ split-K across workgroups);
@@ -446,8 +367,6 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         if not mapped and (x.shape[0] < M or (epi != "argmax" and y.shape[0] < M)):
             # the kernels index rows 0..M-1 unchecked: fail here, not with a device fault
             raise ValueError(f"qgemv: M={M} rows but x has {x.shape[0]}, y {y.shape[0]}")
-        if mode == 7 or ((mode < 0 or waves == 0) and lib_gemm_ok(segs, M, epi, alpha, argmax, y)):
-            return lib_gemm(segs, x, y, M, alpha, epi)
         if mode < 0 or waves == 0:
             mode, waves, rt, ks = gemv_config(segs, M) if not mapped else MOE_GEMV
         if M > 64 and mode == 0:
@@ -535,16 +454,6 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
     launch config the partial slabs are reduced by the fused reduce+residual+RMSNorm kernel; a few-row
     path-A launch (M <= ADDNORM_MAX_M, `counter`: a zeroed int32 device word) normalises in its last
     workgroup, so the norm costs no launch at all."""
-    if (x.is_cuda and cfg is None and seg.ycol == 0 and seg.w.rows == x.shape[1]
-            and lib_gemm_ok([seg], M, "addnorm")):
-        # mode 7: the library GEMM writes ONE f32 slab, the split-K reduce kernel (ks = 1) adds it to the
-        # residual and normalises
-        ws = _workspace(x.device, M * seg.w.rows)
-        torch.mm(xin[:M], seg.w.d16.t(), out_dtype=torch.float32, out=ws[:M * seg.w.rows].view(M, seg.w.rows))
-        _lib.check(_lib.lib().nls_splitk_add_rmsnorm(ws.data_ptr(), 1, M, float(alpha), x.data_ptr(), x.stride(0),
-                                                     norm_w.data_ptr(), h.data_ptr(), h.stride(0), x.shape[1],
-                                                     float(eps), _stream_ptr(x)), "nls_splitk_add_rmsnorm")
-        return h
     if x.is_cuda and seg.xmap is None:
         mode, waves, rt, ks = cfg or gemv_config([seg], M)
         if (mode == 0 and counter is not None and M <= ADDNORM_MAX_M and seg.ycol == 0
@@ -731,11 +640,6 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
                                                qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt, 0, 1, None,
                                                _stream_ptr(h), ctypes.byref(fz)), "nls_qgemv_ex(rope)")
             return
-    if h.is_cuda and all(s.xmap is None for s in segs) and norm is None and cfg is None and \
-            lib_gemm_ok(segs, T, "f32", 1.0, None, qkv):
-        lib_gemm(segs, h, qkv, T, 1.0, "f32")       # mode 7: library GEMM, then the RoPE/KV pass
-        rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox, bias)
-        return
     if h.is_cuda and all(s.xmap is None for s in segs) and norm is None:
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)

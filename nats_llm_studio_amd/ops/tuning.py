@@ -34,8 +34,7 @@ def table():
         if os.path.exists(_PATH):
             with open(_PATH) as f:
                 _TABLE = {k: tuple(v) for k, v in json.load(f).items()}
-        # A/B overrides without editing the table: NLS_TUNING_EXTRA='{"<key>": [..], ...}' (an entry of
-        # [0] under an "L:" key removes a library-GEMM selection)
+        # A/B overrides without editing the table: NLS_TUNING_EXTRA='{"<key>": [..], ...}'
         extra = os.environ.get("NLS_TUNING_EXTRA")
         if extra:
             _TABLE.update({k: tuple(v) for k, v in json.loads(extra).items()})
@@ -101,17 +100,6 @@ def select_dense(segs, M: int):
     if hit is not None and hit[0] < 0:
         return None
     return hit if hit is not None else dense_heuristic(segs, M)
-
-
-def lib_key(segs, M: int) -> str:
-    return f"L:{sum(s.w.rows for s in segs)}:{segs[0].w.K}:{_mb(M)}"
-
-
-def select_lib(segs, M: int) -> bool:
-    """Did the library GEMM (hipBLASLt on the f16 copies + a separate epilogue pass, ops "mode 7")
-    measure faster than the hand-written large-M kernels for this shape and batch bucket
-    (tools/blaslt_ab.py)? Only shapes with an entry take it."""
-    return bool(table().get(lib_key(segs, M), (0,))[0])
 
 
 # Llama-3-8B Q4_K_M shapes per projection role: the tuned entries an untuned shape of the same role borrows at

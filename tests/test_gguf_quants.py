@@ -98,8 +98,9 @@ def test_tiled_layout_is_a_permutation(t):
 
 def test_prefill_blocks():
     from nats_llm_studio_amd.ops import PREFILL_QT as QT, prefill_blocks
-    assert 20 <= QT < 40 and QT % 16 == 0
-    tseq = np.array([0] * 40 + [1] * 3 + [2] * 16)
-    pos = np.concatenate([np.arange(40), np.arange(50, 53), np.arange(16)])
+    assert QT in (32, 64)            # attn_prefill: 64-token blocks (NLS_PREFILL_V1: 32)
+    n0 = QT + QT // 4                # sequence 0 spans a full block and a partial one
+    tseq = np.array([0] * n0 + [1] * 3 + [2] * 16)
+    pos = np.concatenate([np.arange(n0), np.arange(50, 53), np.arange(16)])
     qb = prefill_blocks(tseq, pos, len(tseq))
-    assert qb.tolist() == [[0, QT, 0, 0], [QT, 40 - QT, 0, QT], [40, 3, 1, 50], [43, 16, 2, 0]]
+    assert qb.tolist() == [[0, QT, 0, 0], [QT, n0 - QT, 0, QT], [n0, 3, 1, 50], [n0 + 3, 16, 2, 0]]

@@ -739,7 +739,7 @@ def test_qkv_rope_kv_fused(gpu, cfg, M, bias):
     _qkv_rope_case(gpu, cfg, M, bias, dense=False)
 
 
-@pytest.mark.parametrize("cfg", [(4, 16, 2, 1), (4, 16, 4, 1), (5, 8, 4, 1), (10, 8, 1, 1), (10, 8, 1, 2)])
+@pytest.mark.parametrize("cfg", [(4, 16, 2, 1), (4, 16, 4, 1), (5, 8, 4, 1), (10, 8, 1, 1), (10, 8, 1, 2), (10, 8, 2, 1)])
 @pytest.mark.parametrize("M", [70, 300, 520])
 @pytest.mark.parametrize("bias", [False, True])
 def test_qkv_rope_kv_dense(gpu, cfg, M, bias):
@@ -1036,8 +1036,9 @@ def test_hgemm8_swiglu_multiseg(gpu, rt, ks):
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
 
 
+@pytest.mark.parametrize("rt", [1, 2])
 @pytest.mark.parametrize("M,ks", [(512, 1), (333, 1), (100, 2), (256, 3), (1024, 1), (64, 4)])
-def test_hgemm10_dense(gpu, M, ks):
+def test_hgemm10_dense(gpu, M, ks, rt):
     """Mode 10 (hgemm10.hip: 256 x 256 tiles, 4 phases per 64-deep K-tile, the two wave groups staggered by
     a barrier, one LDS-DMA unit per phase under a counted vmcnt): partial last weight tile (264 rows),
     partial / multiple activation blocks, k-slices of 1..12 K-tiles (the clamped tail units), split-K
@@ -1049,7 +1050,7 @@ def test_hgemm10_dense(gpu, M, ks):
     pad = x.shape[0]
     y = torch.zeros(pad, rows, device=gpu)
     keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, mode=10, waves=8, rt=1, ks=ks, argmax=keys if ks == 1 else None)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=10, waves=8, rt=rt, ks=ks, argmax=keys if ks == 1 else None)
     ref = x[:M].float().cpu() @ Wd.t()
     _close(y[:M], ref)
     if M < pad:
@@ -1060,15 +1061,16 @@ def test_hgemm10_dense(gpu, M, ks):
         assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
     base = torch.randn(pad, rows, device=gpu)
     y2 = base.clone()
-    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=10, waves=8, rt=1, ks=ks)
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=10, waves=8, rt=rt, ks=ks)
     _close(y2[:M], base[:M].cpu() + 0.5 * ref)
     y3 = torch.zeros(pad, rows, device=gpu)
     ops.qgemv([ops.Seg(w)], x, y3, M, mode=8, waves=8, rt=8, ks=1)
     _close(y3[:M], y[:M], 1e-3)
 
 
+@pytest.mark.parametrize("rt", [1, 2])
 @pytest.mark.parametrize("ks", [1, 2])
-def test_hgemm10_swiglu_multiseg(gpu, ks):
+def test_hgemm10_swiglu_multiseg(gpu, ks, rt):
     """Mode 10 SwiGLU epilogue (interleaved gate/up rows: partner lane ^ 32) and a Q|K|V-style launch."""
     K, F = 512, 256
     rng = np.random.default_rng(9)
@@ -1082,7 +1084,7 @@ def test_hgemm10_swiglu_multiseg(gpu, ks):
     x = _x(M, K, gpu)
     xf = x[:M].float().cpu()
     y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=10, waves=8, rt=1, ks=ks)
+    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=10, waves=8, rt=rt, ks=ks)
     _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
     a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
     b, Bd = _qw(256, K, GGMLType.Q4_K, gpu, 2)
@@ -1091,7 +1093,7 @@ def test_hgemm10_swiglu_multiseg(gpu, ks):
         q.expand_dense()
     segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 512)]
     yq = torch.zeros(x.shape[0], 768, device=gpu)
-    ops.qgemv(segs, x, yq, M, mode=10, waves=8, rt=1, ks=ks)
+    ops.qgemv(segs, x, yq, M, mode=10, waves=8, rt=rt, ks=ks)
     _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
 
 
@@ -1155,87 +1157,6 @@ def test_qgemm9_swiglu_multiseg(gpu, waves, rt, ks):
     y2 = torch.zeros(x.shape[0], 768, device=gpu)
     ops.qgemv(segs, x, y2, M, mode=2, waves=8, rt=4, ks=1)
     _close(yq[:M], y2[:M], 1e-3)
-
-
-@pytest.mark.parametrize("M", [65, 300, 512])
-def test_lib_gemm_mode7(gpu, M):
-    """Mode 7: hipBLASLt GEMM on the f16 copies + the HIP SwiGLU pass (interleaved gate/up) / plain f32
-    store of a concatenated Q|K|V launch; vs the fp32 oracle. Then the automatic selection: mode 7
-    only for shapes with an "L:" tuning entry, never with an arg-max or a non-contiguous output."""
-    K, F = 512, 256
-    rng = np.random.default_rng(11)
-    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
-    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
-    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
-    w.expand_dense()
-    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
-    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
-    x = _x(M, K, gpu)
-    xf = x[:M].float().cpu()
-    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=7)
-    _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
-    assert float(y[M:].abs().max().cpu()) == 0.0 if M < x.shape[0] else True
-    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
-    b, Bd = _qw(128, K, GGMLType.Q4_K, gpu, 2)
-    c, Cd = _qw(128, K, GGMLType.Q6_K, gpu, 3)
-    for q in (a, b, c):
-        q.expand_dense()
-    segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 384)]
-    yq = torch.zeros(x.shape[0], 512, device=gpu)
-    ops.qgemv(segs, x, yq, M, mode=7)                 # unfused: a separate concatenated copy
-    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
-    d16 = [s.w.d16 for s in segs]
-    ops.fuse_dense(segs)                              # after a launch: a no-op (copies never move)
-    assert all(s.w.d16.data_ptr() == p.data_ptr() for s, p in zip(segs, d16))
-    fresh = [_qw(256, K, GGMLType.Q4_K, gpu, 1)[0], _qw(128, K, GGMLType.Q4_K, gpu, 2)[0],
-             _qw(128, K, GGMLType.Q6_K, gpu, 3)[0]]
-    for q in fresh:
-        q.expand_dense()
-    segs = [ops.Seg(fresh[0], 0), ops.Seg(fresh[1], 256), ops.Seg(fresh[2], 384)]
-    ops.fuse_dense(segs)                              # at load: the copies become views of one matrix
-    base = segs[0].w.d16.data_ptr()
-    assert [s.w.d16.data_ptr() - base for s in segs] == [0, 256 * K * 2, 384 * K * 2]
-    yq.zero_()
-    ops.qgemv(segs, x, yq, M, mode=7)
-    ref = xf @ torch.cat([Ad, Bd, Cd]).t()
-    _close(yq[:M], ref)
-    # the segments' f16 copies are now views into the concatenation: the fused kernels still agree
-    y4 = torch.zeros_like(yq)
-    ops.qgemv(segs, x, y4, M, mode=4, waves=8, rt=4, ks=1)
-    _close(y4[:M], yq[:M], 1e-3)
-    from nats_llm_studio_amd.ops import tuning
-    tab = tuning.table()
-    key = tuning.lib_key(segs, M)
-    try:
-        tab[key] = (1,)
-        if M < ops.DENSE_MIN_M:              # below the dense-GEMM threshold: never mode 7
-            assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
-            return
-        assert ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
-        assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, torch.zeros(4, dtype=torch.int64, device=gpu), yq)
-        assert not ops.lib_gemm_ok(segs, M, "add", 1.0, None, yq)
-        assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, torch.zeros(x.shape[0], 520, device=gpu))
-        yq.zero_()
-        ops.qgemv(segs, x, yq, M)            # auto: mode 7
-        _close(yq[:M], ref)
-        # residual add + RMSNorm: the library GEMM's single f32 slab through the fused reduce/norm kernel
-        o, Od = _qw(512, K, GGMLType.Q4_K, gpu, 5)
-        o.expand_dense()
-        tab[tuning.lib_key([ops.Seg(o)], M)] = (1,)
-        assert ops.lib_gemm_ok([ops.Seg(o)], M, "addnorm")
-        r = torch.randn(x.shape[0], 512, device=gpu)
-        r0 = r[:M].cpu().clone()
-        nw = torch.rand(512, device=gpu) + 0.5
-        hn = torch.zeros(x.shape[0], 512, dtype=ops.ACT_DTYPE, device=gpu)
-        ops.qgemv_add_rmsnorm(ops.Seg(o), x, r, nw, hn, M, 0.5, 1e-5)
-        want = r0 + 0.5 * xf @ Od.t()
-        _close(r[:M], want)
-        _close(hn[:M], want * torch.rsqrt(want.pow(2).mean(1, keepdim=True) + 1e-5) * nw.cpu(), 2e-2)
-    finally:
-        tab.pop(key, None)
-        tab.pop(tuning.lib_key([ops.Seg(o)], M), None) if "o" in locals() else None
-    assert not ops.lib_gemm_ok(segs, M, "f32", 1.0, None, yq)
 
 
 def test_hgemm_dense_add_rmsnorm_slabs(gpu):

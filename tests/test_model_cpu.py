@@ -152,27 +152,6 @@ def test_cpu_moe_norm_route_reference():
         assert torch.equal(a[key], b[key]), key
 
 
-def test_lib_gemm_gating_cpu():
-    """Mode 7 is a GPU path for weights with f16 copies: never selected on CPU weights, for arg-max
-    launches, row maps or epilogues it lacks."""
-    from nats_llm_studio_amd import ops
-    from nats_llm_studio_amd.gguf import quants as Q
-    from nats_llm_studio_amd.gguf.constants import GGMLType
-    from nats_llm_studio_amd.ops import tuning
-    w = ops.QWeight(Q.random_blocks(GGMLType.Q4_K, 256 * 512, 0.05, np.random.default_rng(0)), 12, 256, 512, "cpu")
-    segs = [ops.Seg(w)]
-    tab = tuning.table()
-    key = tuning.lib_key(segs, 512)
-    assert key == "L:256:512:512"
-    try:
-        tab[key] = (1,)
-        assert tuning.select_lib(segs, 512)
-        assert not ops.lib_gemm_ok(segs, 512, "f32", 1.0, None, torch.zeros(512, 256))   # no f16 copy on CPU
-    finally:
-        tab.pop(key)
-    assert not tuning.select_lib(segs, 512)
-
-
 def test_reference_streaming_decode_matches_cached(tiny_models):
     """The oracle's streaming mode (cache=False, parallel row-range decoding, gathered embedding rows)
     computes exactly what the cached whole-tensor mode does."""

@@ -26,11 +26,8 @@ from nats_llm_studio_amd.ops import tuning
 pytestmark = pytest.mark.gpu
 
 _TABLE = json.load(open(tuning._PATH))
-_SHAPES = sorted({k.rsplit(":", 1)[0] for k in _TABLE if not k.startswith(("d:", "L:"))})
+_SHAPES = sorted({k.rsplit(":", 1)[0] for k in _TABLE if not k.startswith("d:")})
 _DENSE = sorted({k.rsplit(":", 1)[0] for k, v in _TABLE.items() if k.startswith("d:") and v[0] >= 0})
-# mode-7 shapes up to ~0.6 G weights (the 70B LM head's 1.05 G random blocks take too long to synthesise)
-_LIB = sorted({k.rsplit(":", 1)[0] for k in _TABLE if k.startswith("L:")
-               and int(k.split(":")[1]) * int(k.split(":")[2]) <= 600_000_000})
 
 
 def _weights(types, rows, K, dev, rng):
@@ -107,48 +104,6 @@ def test_dense_tuning_entries_at_real_shapes(gpu, shape):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("shape", _LIB)
-def test_lib_gemm_entries_at_real_shapes(gpu, shape):
-    """Every mode-7 entry ("L:<rows>:<K>:<M>": hipBLASLt on the f16 copies + epilogue pass) at its real
-    shape and M bucket, selected automatically: f32 store for every shape, SwiGLU for the gate/up shape."""
-    _, rows_s, K_s = shape.split(":")
-    rows, K = int(rows_s), int(K_s)
-    rng = np.random.default_rng(abs(hash(shape)) % (1 << 31))
-    types = [12, 12, 14] if rows == 6144 else [14 if rows > 100000 else 12]
-    segs, Wd = _weights(types, rows, K, gpu, rng)
-    for s in segs:
-        s.w.expand_dense()
-    sample = torch.from_numpy(np.sort(rng.choice(rows // 16, size=min(rows // 16, 256), replace=False))).to(gpu)
-    rsel = (sample[:, None] * 16 + torch.arange(16, device=gpu)[None, :]).reshape(-1)   # whole 16-row groups
-    Ws = Wd.index_select(0, rsel).float()
-    g = torch.Generator(device="cpu").manual_seed(13)
-    for k, cfg in sorted(_TABLE.items()):
-        if not k.startswith(shape + ":") or not cfg[0]:
-            continue
-        M = int(k.rsplit(":", 1)[1])
-        x = (torch.randn(M, K, generator=g) * 0.5).to(ops.ACT_DTYPE).to(gpu)
-        y = torch.full((M, rows), float("nan"), device=gpu)
-        assert ops.lib_gemm_ok(segs, M, "f32", 1.0, None, y), k
-        ops.qgemv(segs, x, y, M)
-        ref = x.float() @ Ws.t()
-        got = y.index_select(1, rsel)
-        err = (got - ref).abs().max().item()
-        assert err <= 2e-2 * ref.abs().max().item(), f"{k}: err {err:.4g}"
-        assert not torch.isnan(y).any(), f"{k}: unwritten outputs"
-        if rows == 28672:     # gate/up: interleaved [g0..g7, u0..u7] rows -> SwiGLU pass
-            a = torch.full((M, rows // 2), float("nan"), dtype=ops.ACT_DTYPE, device=gpu)
-            ops.qgemv(segs, x, a, M, epi="swiglu")
-            r4 = ref.view(M, -1, 2, 8)
-            want = (torch.nn.functional.silu(r4[:, :, 0]) * r4[:, :, 1]).reshape(M, -1)
-            cols = (sample[:, None] * 8 + torch.arange(8, device=gpu)[None, :]).reshape(-1)
-            got = a.index_select(1, cols).float()
-            assert (got - want).abs().max().item() <= 3e-2 * want.abs().max().item(), f"{k} swiglu"
-            del a
-        del x, y
-    del segs, Wd
-    torch.cuda.empty_cache()
-
-
 @pytest.fixture(scope="module")
 def llama8b(gpu, tmp_path_factory):
     from nats_llm_studio_amd.gguf.reader import GGUFReader
@@ -215,9 +170,9 @@ def _prefill_logits(model, ids):
 def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
     """Llama-3-8B (random-init Q4_K_M) prefill logits of a 512-token prompt against the fp32 oracle
     (models/reference.py: numpy ggml codecs + textbook fp32 decoder, on the GPU; also with the engine's
-    storage roundings, to separate kernel error from storage precision) for the three GEMM paths
-    production runs at 512 rows: the quantised kernels only (as NLS_DENSE_WEIGHTS=0), the f16-copy dense
-    kernels (modes 4/5/8/10 per the "d:" tuning entries, NLS_LIB_GEMM=0) and the library GEMM (mode 7)."""
+    storage roundings, to separate kernel error from storage precision) for the two GEMM paths
+    production runs at 512 rows: the quantised kernels only (as NLS_DENSE_WEIGHTS=0) and the f16-copy dense
+    kernels (modes 4/5/8/10 per the "d:" tuning entries). No library GEMM runs anywhere in the engine."""
     from nats_llm_studio_amd.gguf.reader import GGUFReader
     from nats_llm_studio_amd.models.reference import ReferenceModel
     S = 512
@@ -256,23 +211,9 @@ def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
     llama8b.expand_dense(None)
     gu = ops.Seg(llama8b.layers[0].gateup)
     assert gu.w.d16 is not None
-    with monkeypatch.context() as mp:
-        mp.setattr(ops, "LIB_GEMM", False)
-        cfg = ops.gemv_config([gu], S)
-        assert cfg[0] in (4, 5, 6, 8, 10), cfg          # the gate|up launch runs on the f16 copy
-        check(_prefill_logits(llama8b, ids), "f16-copy dense")
-    with monkeypatch.context() as mp:
-        mp.setattr(ops, "LIB_GEMM", True)
-        # production runs no library GEMM at 512 rows since r03 (gate|up, down and the LM head on mode 10,
-        # Q|K|V on mode 4): the library path (mode 7, still chosen for 1K-2K-row prefill chunks) is pinned here
-        # by selecting it for the fused Q|K|V
-        from nats_llm_studio_amd.ops import tuning
-        mp.setitem(tuning.table(), tuning.lib_key(llama8b.layers[0].qkv, S), (1,))
-        qkv = llama8b.layers[0].qkv
-        y = torch.empty(S, sum(sg.w.rows for sg in qkv), dtype=torch.float32, device=gpu)
-        assert ops.lib_gemm_ok(qkv, S, "f32", 1.0, None, y)
-        del y
-        check(_prefill_logits(llama8b, ids), "mode 7")
+    cfg = ops.gemv_config([gu], S)
+    assert cfg[0] in (4, 5, 6, 8, 10), cfg              # the gate|up launch runs on the f16 copy
+    check(_prefill_logits(llama8b, ids), "f16-copy dense")
 
 
 def test_graph_split_workspace_survives_growth(gpu, tiny_models):

@@ -4,7 +4,7 @@ against hipBLASLt (torch.mm on the same f16 copy, GEMM only -- a floor for the l
 needs an epilogue pass). Every launch is captured in a hipGraph over rotating weight copies (>= 1 GiB, so
 weights stream from HBM as in serving) and timed as the median of rounds.
 
-Candidates: mode 10 (hgemm10.hip, 256x256 8-phase) x split-K, modes 4/5 (hgemm.hip, 128/256 weight rows,
+Candidates: mode 10 (hgemm10.hip, 8-phase, 256 (rt 1) or 128 (rt 2) weight rows x 256 activation rows) x split-K, modes 4/5 (hgemm.hip, 128/256 weight rows,
 128/256 activation rows, 8 or 16 waves) x split-K. With --emit the winners are printed as "d:<rows>:<K>:<Mbucket>" tuning
 entries (ops/gemv_tuning.json) -- the table that replaced the library-GEMM ("L:") selections.
 
@@ -60,7 +60,7 @@ def roles(spec):
 
 
 def candidates(M, K, epi):
-    out = [(10, 8, 1, ks) for ks in (1, 2, 3, 4, 6, 8)]
+    out = [(10, 8, rt, ks) for rt in (1, 2) for ks in (1, 2, 3, 4, 6, 8)]
     for mode in (4, 5):
         for waves in (8, 16):
             for wm in ((2, 4) if M >= 192 else (2,)):
@@ -92,7 +92,6 @@ def main():
             w.expand_dense()
             segs.append(ops.Seg(w, col))
             col += rows
-        ops.fuse_dense(segs)
         nbytes = col * K * 2
         ncopy = min(REPS, max(1, -(-(1 << 30) // nbytes)))
         copies = [segs]

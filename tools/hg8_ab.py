@@ -85,7 +85,6 @@ def main():
             w.expand_dense()
             segs.append(ops.Seg(w, col))
             col += rows
-        ops.fuse_dense(segs)
         nbytes = col * K * 2
         ncopy = min(REPS, max(1, -(-(1 << 30) // nbytes)))
         copies = [segs]
