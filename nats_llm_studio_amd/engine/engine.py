@@ -40,6 +40,9 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 640, 768, 10
 _OP_STOP, _OP_PREFILL, _OP_DECODE, _OP_CAPTURE, _OP_SYNC, _OP_RESET = 0, 1, 2, 3, 4, 5
 # header: op | T | nrows | need_logits | nseq | pad | candidate mode | in-graph sampling | sampling rows | 0
 _HDR = 10
+# NLS_TP_TRACE=1: every rank logs each control op it sends / replays (stderr), to line up the ranks' op
+# sequences after a one-shot timeout
+_TP_TRACE = os.environ.get("NLS_TP_TRACE", "0") == "1"
 _NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
 
 
@@ -243,6 +246,13 @@ class Engine:
         # sequences alike) keeps one free block per running sequence (~16 decode steps of growth for all of
         # them) instead of the 1 % watermark, so a sequence just re-admitted is not the next victim at once
         self._pressure_until = -1
+        # expected-growth admission: a sequence is admitted only while the pool covers the EXPECTED blocks of
+        # every running sequence plus its own -- prompt + gen_ratio * max_tokens, gen_ratio an EMA of
+        # generated / max_tokens over finished requests (starts at 1: as safe as worst-case reservation until
+        # requests are seen to stop early, then approaching on-demand). Preemption stays the safety net when
+        # the estimate is exceeded. 512 x 1152-token requests over a 9x oversubscribed pool: on-demand alone
+        # recomputed 30 % of all forward tokens (profiles/kv_pressure_r04.txt).
+        self.gen_ratio = 1.0
         self.reserve_full = os.environ.get("NLS_KV_RESERVE", "ondemand") == "full"
         self.max_prefill = max_prefill_tokens
         self.prefill_attn = prefill_attn      # MFMA flash-prefill attention (else per-token decode kernel)
@@ -466,10 +476,23 @@ class Engine:
             self.waiting = keep
         self.running = [s for s in self.running if not s.done]
 
+    def _expected_blocks(self, s: _Seq) -> int:
+        """Blocks s is expected to hold at its end: all its tokens so far + gen_ratio of what it may still
+        generate (the context caps it)."""
+        gen = len(s.tokens) - s.n_prompt
+        rest = max(0.0, self.gen_ratio * s.max_new - gen)
+        return math.ceil(min(self.ctx, s.n_target + max(0, len(s.tokens) - s.n_target) + rest) / self.bs)
+
     def _admit(self):
         with self.lock:
+            growth = None                     # expected further blocks of the running sequences
             while self.waiting and len(self.running) < self.max_batch:
                 s = self.waiting[0]
+                if not self.reserve_full and self.running:
+                    if growth is None:
+                        growth = sum(max(0, self._expected_blocks(x) - len(x.blocks)) for x in self.running)
+                    if growth + self._expected_blocks(s) > self.alloc.n_free:
+                        break
                 if self.reserve_full:
                     need = math.ceil((s.n_prompt + s.max_new) / self.bs)
                 else:                          # the prompt now, decode blocks on demand (_ensure_blocks)
@@ -492,6 +515,8 @@ class Engine:
                 s.t_admit = time.monotonic()
                 self.waiting.popleft()
                 self.running.append(s)
+                if growth is not None:
+                    growth += max(0, self._expected_blocks(s) - len(s.blocks))
 
     def _slot(self, s: _Seq, p: int) -> int:
         return s.blocks[p // self.bs] * self.bs + p % self.bs
@@ -624,10 +649,18 @@ class Engine:
         if rows:
             hdr[_HDR:_HDR + len(rows)] = torch.tensor(rows, dtype=torch.int32)
         self.tp.bcast_ctrl(hdr)
+        if _TP_TRACE:
+            self._trace_op("send", hdr)
         if op in (_OP_PREFILL, _OP_DECODE):
             self.tp.bcast_ctrl(hmeta[:_NSEG * pad + nseq * nb].clone())
         if srows:
             self.tp.bcast_ctrl(self._pack_srows(srows))
+
+    def _trace_op(self, what: str, hdr: torch.Tensor):
+        import sys
+        self._nops = getattr(self, "_nops", 0) + 1
+        print(f"[tp r{self.rank}] {time.monotonic():.6f} #{self._nops} {what} " + " ".join(str(int(v)) for v in hdr[:9]),
+              file=sys.stderr, flush=True)
 
     _SROW = 1 + ops.SAMPLE_PARAMS_BYTES // 4 + 2 + HIST     # int32 words of one shipped sampling row
 
@@ -666,6 +699,8 @@ class Engine:
         nb = self.max_blocks
         while True:
             hdr = self.tp.bcast_ctrl(self._ctrl_hdr)
+            if _TP_TRACE:
+                self._trace_op("recv", hdr)
             op, T, nrows, need, nseq, pad, cand, dsamp, nsr = (int(v) for v in hdr[:9])
             self._cand_mode = bool(cand)
             if op == _OP_STOP:
@@ -906,6 +941,10 @@ class Engine:
         rank re-initialises its one-shot buffers (_OP_RESET): late granules of the timed-out call must never
         be taken for a later call's data."""
         if self.h_err2 is not None and int(self.h_err2[k].max()):
+            if _TP_TRACE:
+                import sys
+                print(f"[tp r{self.rank}] one-shot error words (sum, add+norm, gather) {self.h_err2[k].tolist()} "
+                      f"after op #{getattr(self, '_nops', 0)}", file=sys.stderr, flush=True)
             for h in self.h_err2:
                 h.zero_()
             self._ctrl(_OP_RESET, 0, 0, False, [], 0, None, 0)
@@ -1168,6 +1207,8 @@ class Engine:
             return
         s.done = True
         s.t_done = time.monotonic()
+        if finish in ("stop", "length") and s.max_new > 0:     # admission's expected-growth estimate
+            self.gen_ratio += 0.1 * (min(1.0, (len(s.tokens) - s.n_prompt) / s.max_new) - self.gen_ratio)
         if s.blocks:
             self.alloc.release(s.blocks)
             s.blocks = []
@@ -1190,6 +1231,6 @@ class Engine:
     def stats(self) -> dict:
         return dict(self.counters, running=len(self.running), waiting=len(self.waiting),
                     kv_blocks_free=self.alloc.n_free, kv_blocks_total=self.num_blocks,
-                    kv_reserve="full" if self.reserve_full else "ondemand",
+                    kv_reserve="full" if self.reserve_full else "ondemand", gen_ratio=round(self.gen_ratio, 3),
                     prefix_cache_hit_tokens=self.alloc.hits, prefix_cache_blocks=len(self.alloc.block_of),
                     graphs=sorted(self.graphs), host_ms={k: round(v, 1) for k, v in self.host_ms.items()})

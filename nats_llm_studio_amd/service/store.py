@@ -69,18 +69,20 @@ class ModelStore:
         out_lines = []
         t0 = time.time()
 
-        def left() -> float:
+        def left(grace: float = 0.0) -> float:
+            """Seconds left (0: no deadline); raises once the deadline is within `grace` (an operation timed
+            out on the remaining budget handed to it just now)."""
             if deadline is None:
                 return 0.0
             r = deadline - time.monotonic()
-            if r <= 0:
+            if r <= grace:
                 raise PullError(f"failed to pull '{identifier}': context deadline exceeded", "\n".join(out_lines))
             return r
         try:
             store = self._os(timeout=left() or 30.0)
             objs = store.list()
         except Exception as e:
-            left()
+            left(0.25)
             raise PullError(f"failed to list bucket '{self.bucket}': {e}", "")
         matches = [o for o in objs if _match(identifier, o["name"]) and o["name"].lower().endswith(".gguf")]
         if not matches:
@@ -103,7 +105,7 @@ class ModelStore:
             except PullError:
                 raise
             except Exception as e:
-                left()
+                left(0.25)
                 raise PullError(f"failed to download '{o['name']}': {e}", "\n".join(out_lines))
             total += int(o.get("size", 0))
             out_lines.append(f"{o['name']}: {o.get('size', 0)} bytes -> {dest} ({o.get('digest', '')} verified)")

@@ -34,6 +34,18 @@ def _run_all(eng, reqs):
     return [f.result().token_ids for f in futs]
 
 
+def _run_all_pinned(eng, reqs, ratio):
+    """_run_all with the admission estimate held at `ratio` (finished requests would otherwise raise it)."""
+    futs = [eng.submit(GenRequest(list(t), p)) for t, p in reqs]
+    steps = 0
+    while not all(f.done() for f in futs):
+        eng.gen_ratio = ratio
+        eng.step()
+        steps += 1
+        assert steps < 5000
+    return [f.result().token_ids for f in futs]
+
+
 def _margin(m, tokens):
     """Top-2 logit margin after `tokens` (single-sequence prefill; a sampled request materialises logits)."""
     eng = Engine(m, None, max_batch=1, max_prefill_tokens=128, num_blocks=16, use_graphs=False, ctx=128)
@@ -78,7 +90,9 @@ def test_preemption_completes_requests_larger_than_pool(tiny_models):
     # 16 blocks x 16 = 256 token slots for ~6 x 95 tokens of KV
     tight = Engine(m, None, max_batch=8, max_prefill_tokens=32, num_blocks=16, use_graphs=False, ctx=256,
                    async_decode=True)
-    got = _run_all(tight, reqs)
+    # as if earlier requests had stopped early: expected-growth admission is as optimistic as on-demand
+    tight.gen_ratio = 0.05
+    got = _run_all_pinned(tight, reqs, 0.05)
     assert tight.counters["preemptions"] > 0, tight.stats()
     for (t, p), a, b in zip(reqs, got, ref):
         assert len(a) == len(b) == p.max_tokens
@@ -97,3 +111,27 @@ def test_full_reservation_mode_never_preempts(tiny_models, monkeypatch):
     got = _run_all(eng, reqs)
     assert eng.counters["preemptions"] == 0 and eng.stats()["kv_reserve"] == "full"
     assert [len(g) for g in got] == [p.max_tokens for _, p in reqs]
+
+
+def test_expected_growth_admission_avoids_thrash(tiny_models):
+    """The same oversubscribed workload with the admission estimate learnt from completions (every request
+    runs to max_tokens, so the ratio stays at 1): sequences wait for room instead of being admitted and
+    preempted, nothing is recomputed, and the tokens are the roomy engine's."""
+    m = LlamaModel(GGUFReader(tiny_models["tiny-llama"]), "cpu")
+    rng = np.random.default_rng(11)
+    reqs = [([int(v) for v in rng.integers(20, 200, int(rng.integers(4, 14)))],
+             SamplingParams(max_tokens=int(rng.integers(60, 100)), ignore_eos=True)) for _ in range(6)]
+    roomy = Engine(m, None, max_batch=8, max_prefill_tokens=64, num_blocks=256, use_graphs=False, ctx=256,
+                   async_decode=False)
+    ref = _run_all(roomy, reqs)
+    tight = Engine(m, None, max_batch=8, max_prefill_tokens=32, num_blocks=16, use_graphs=False, ctx=256,
+                   async_decode=True)
+    got = _run_all(tight, reqs)
+    assert tight.counters["preemptions"] == 0 and tight.counters["recompute_tokens"] == 0, tight.stats()
+    assert tight.gen_ratio > 0.99
+    for (t, p), a, b in zip(reqs, got, ref):
+        assert len(a) == len(b) == p.max_tokens
+        k = next((i for i in range(len(a)) if a[i] != b[i]), None)
+        if k is not None:
+            assert _margin(m, list(t) + b[:k]) < 1e-3, (a, b)
+    assert tight.alloc.n_free == tight.num_blocks
