@@ -709,6 +709,9 @@ class Engine:
                 self._capture(T, LlamaModel.attn_splits(T, self.model.Hkv), dsamp=bool(dsamp))
                 continue
             if op == _OP_RESET:
+                if _TP_TRACE:
+                    import sys
+                    print(f"[tp r{self.rank}] state {self._oneshot.debug_state()}", file=sys.stderr, flush=True)
                 self._oneshot.reset()
                 continue
             if op == _OP_SYNC:
@@ -945,6 +948,7 @@ class Engine:
                 import sys
                 print(f"[tp r{self.rank}] one-shot error words (sum, add+norm, gather) {self.h_err2[k].tolist()} "
                       f"after op #{getattr(self, '_nops', 0)}", file=sys.stderr, flush=True)
+                print(f"[tp r{self.rank}] state {self._oneshot.debug_state()}", file=sys.stderr, flush=True)
             for h in self.h_err2:
                 h.zero_()
             self._ctrl(_OP_RESET, 0, 0, False, [], 0, None, 0)

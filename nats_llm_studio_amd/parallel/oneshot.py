@@ -130,6 +130,18 @@ class OneShotAllReduce:
             _lib.check(L.nls_ar_err_clear(b, self.cap, self.world, st), "nls_ar_err_clear")
         self.err.zero_()
 
+    def debug_state(self, rows: int = 48) -> dict:
+        """Small host snapshot of the protocol state (NLS_TP_TRACE): per-workgroup epochs of the three
+        buffer sets (fused add+norm: first slice of each of the first `rows` rows) and the row tickets --
+        compared across ranks, a divergence names the collective whose call counts differ."""
+        torch.cuda.synchronize(self.device)
+        out = dict(ar=self.epochs[:8].tolist(), gather=self.gepochs.tolist())
+        for D, (ep, tk, _sq) in self._norm.items():
+            nblk = ep.numel() // tk.numel()
+            out[f"addnorm{D}"] = ep.view(-1, nblk)[:rows, 0].tolist()
+            out[f"tickets{D}"] = tk[:rows].tolist()
+        return out
+
     def reset(self):
         """After a timed-out poll: put every rank's receive slots, epochs and tickets back to the freshly
         allocated state. A late peer may still have written granules nobody consumed, and a later call of

@@ -32,12 +32,12 @@ def _port() -> int:
     return p
 
 
-def _requests(new_tokens: int):
+def _requests(new_tokens: int, greedy_only: bool = False):
     from ..engine.sampling import SamplingParams
     greedy = SamplingParams(max_tokens=new_tokens, ignore_eos=True)
     topk = SamplingParams(max_tokens=new_tokens, temperature=0.8, top_k=40, top_p=0.95, repeat_penalty=1.1,
                           seed=7, ignore_eos=True)
-    return [(p, greedy) for p in PROMPTS] + [(p, topk) for p in PROMPTS]
+    return [(p, greedy) for p in PROMPTS] + ([] if greedy_only else [(p, topk) for p in PROMPTS])
 
 
 def _sync(dev):
@@ -51,8 +51,8 @@ def _engine(path: str, dev, shard=None, comm=None, graphs: bool = True):
     from ..gguf.reader import GGUFReader
     from ..models.llama import LlamaModel, ShardSpec
     m = LlamaModel(GGUFReader(path), dev, shard or ShardSpec(), comm)
-    return Engine(m, None, max_batch=8, max_prefill_tokens=256, num_blocks=256, use_graphs=graphs and dev.type == "cuda",
-                  ctx=512)
+    graphs = graphs and dev.type == "cuda" and os.environ.get("NLS_REHEARSAL_GRAPHS", "1") == "1"
+    return Engine(m, None, max_batch=8, max_prefill_tokens=256, num_blocks=256, use_graphs=graphs, ctx=512)
 
 
 def _kernel_profile(eng, futs, steps: int) -> Dict:
@@ -85,11 +85,12 @@ def _kernel_profile(eng, futs, steps: int) -> Dict:
                 rccl_kernels=[nm for _, _, nm in rows if "nccl" in nm.lower() or "rccl" in nm.lower()])
 
 
-def _drive(eng, new_tokens: int, profile_steps: int = 0) -> Dict:
-    """Leader: greedy requests, then seeded top-k requests (all in flight together)."""
+def _drive(eng, new_tokens: int, profile_steps: int = 0, greedy_only: bool = False) -> Dict:
+    """Leader: greedy requests, then seeded top-k requests (all in flight together); greedy_only: the
+    greedy ones alone (every step takes the vocab-parallel arg-max path instead of in-graph sampling)."""
     from ..engine.engine import GenRequest
     eng.capture_all()
-    reqs = _requests(new_tokens)
+    reqs = _requests(new_tokens, greedy_only)
     t0 = time.perf_counter()
     futs = [eng.submit(GenRequest(list(p), sp)) for p, sp in reqs]
     steps = 0
@@ -132,18 +133,18 @@ def _device(kind: str):
     return dev
 
 
-def _ref_main(path: str, new_tokens: int, q, kind: str = "cuda"):
+def _ref_main(path: str, new_tokens: int, q, kind: str = "cuda", greedy_only: bool = False):
     try:
         dev = _device(kind)
         eng = _engine(path, dev)
-        q.put(("ref", _drive(eng, new_tokens)))
+        q.put(("ref", _drive(eng, new_tokens, greedy_only=greedy_only)))
     except Exception as e:           # report, never hang the parent
         import traceback
         q.put(("ref", {"exception": repr(e), "tb": traceback.format_exc()[-2000:]}))
 
 
 def _rank_main(rank: int, world: int, port: int, path: str, ep: bool, new_tokens: int, profile_steps: int, q,
-               kind: str = "cuda"):
+               kind: str = "cuda", greedy_only: bool = False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     try:
         import torch
@@ -159,7 +160,7 @@ def _rank_main(rank: int, world: int, port: int, path: str, ep: bool, new_tokens
         eng = _engine(path, dev, ShardSpec(rank, world, ep), comm)
         if rank == 0:
             try:
-                res = _drive(eng, new_tokens, profile_steps)
+                res = _drive(eng, new_tokens, profile_steps, greedy_only)
             finally:
                 eng.stop_followers()          # also on failure: followers must not wait for a next step
             res["comm"] = dict(comm.stats)
@@ -209,7 +210,7 @@ def _collect(procs, q, n: int, timeout: float) -> Dict:
 
 
 def run(path: str, world: int = 2, ep: bool = False, new_tokens: int = 8, ref: bool = True,
-        profile_steps: int = 0, timeout: float = 400.0, device: str = "cuda") -> Dict:
+        profile_steps: int = 0, timeout: float = 400.0, device: str = "cuda", greedy_only: bool = False) -> Dict:
     """TP=1 reference (one process) then the W-rank run (W processes), each on cuda:0 (device="cpu": the
     same flow on gloo, for CPU tests of the driver); returns both."""
     import torch.multiprocessing as mp
@@ -217,12 +218,13 @@ def run(path: str, world: int = 2, ep: bool = False, new_tokens: int = 8, ref: b
     out = {}
     if ref:
         q = ctx.Queue()
-        p = ctx.Process(target=_ref_main, args=(path, new_tokens, q, device))
+        p = ctx.Process(target=_ref_main, args=(path, new_tokens, q, device, greedy_only))
         p.start()
         out["ref"] = _collect([p], q, 1, timeout)["ref"]
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, path, ep, new_tokens, profile_steps, q, device))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, path, ep, new_tokens, profile_steps, q, device,
+                                                  greedy_only))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -241,15 +243,20 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--tokens", type=int, default=8)
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--greedy-only", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true", help="eager decode on every rank (NLS_REHEARSAL_GRAPHS=0)")
     ap.add_argument("--dir", default=os.environ.get("NLS_BENCH_DIR", "/tmp/nls_bench"))
     a = ap.parse_args(argv)
+    if a.no_graphs:
+        os.environ["NLS_REHEARSAL_GRAPHS"] = "0"        # inherited by the spawned ranks
     from ..gguf.synth import write_synthetic_gguf
     ft = a.ftype or ("Q5_K_M" if "mixtral" in a.model else "Q4_K_M")
     path = os.path.join(a.dir, f"{a.model}-{ft}.gguf")
     if not os.path.exists(path):
         os.makedirs(a.dir, exist_ok=True)
         write_synthetic_gguf(path, a.model, ft, seed=3)
-    r = run(path, a.world, a.ep, a.tokens, ref=not a.no_ref, profile_steps=a.profile_steps)
+    r = run(path, a.world, a.ep, a.tokens, ref=not a.no_ref, profile_steps=a.profile_steps,
+            greedy_only=a.greedy_only)
     print(json.dumps(r), flush=True)
     ok = all("exception" not in (v or {"exception": 1}) for v in [r.get("tp")] + r["followers"])
     if ok and "ref" in r:

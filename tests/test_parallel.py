@@ -207,3 +207,8 @@ def test_rehearsal_driver_cpu(tmp_path):
     c = r["tp"]["counters"]
     assert c["device_sampled_steps"] > 0 and c["candidate_sampled_steps"] == 0, c
     assert r["followers"][0]["counters"]["device_sampled_steps"] == c["device_sampled_steps"]
+    # greedy-only batches: every step on the vocab-parallel arg-max, plus the post-run marker window
+    g = rehearsal.run(path, world=2, new_tokens=5, timeout=240, device="cpu", greedy_only=True, profile_steps=3)
+    assert "exception" not in g["tp"], g["tp"]
+    assert g["tp"]["tokens"] == g["ref"]["tokens"] == r["ref"]["tokens"][:len(rehearsal.PROMPTS)]
+    assert g["tp"]["counters"]["device_sampled_steps"] == 0
