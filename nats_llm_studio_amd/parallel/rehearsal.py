@@ -103,6 +103,9 @@ def _drive(eng, new_tokens: int, profile_steps: int = 0, greedy_only: bool = Fal
                counters=dict(eng.counters), graphs=[list(k) for k in sorted(eng.graphs)])
     if profile_steps:
         # a marker window for kernel traces: greedy-only decode steps after a host sync
+        if os.environ.get("NLS_REHEARSAL_BARRIER", "0") == "1":
+            import torch.distributed as dist
+            eng.sync(lambda: (_sync(eng.dev), dist.barrier()))    # every rank idle before the window
         futs = [eng.submit(GenRequest(list(p), sp)) for p, sp in reqs[:len(PROMPTS)]]
         while any(s.n_prefilled < s.n_target for s in eng.running) or eng.waiting:
             eng.step()
@@ -167,6 +170,7 @@ def _rank_main(rank: int, world: int, port: int, path: str, ep: bool, new_tokens
             res["oneshot_resets"] = comm.oneshot.resets if comm.oneshot is not None else None
             res["ctrl_transport"] = "shm-ring" if comm.ring is not None else "gloo"
         else:
+            eng.sync_hook = lambda: (_sync(dev), dist.barrier())
             eng.follow()
             res = dict(counters=dict(eng.counters), graphs=[list(k) for k in sorted(eng.graphs)])
         if comm.oneshot is not None:
