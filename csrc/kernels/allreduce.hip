@@ -75,6 +75,12 @@ __device__ void ar_raise(const ArPeers& P, int world, long cap, int* err) {
     __hip_atomic_store(ar_err_word(P.buf[p], world, cap), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// per-workgroup epoch counters: read / advanced with `sc0 sc1` (volatile) accesses, never through a possibly
+// stale line of another XCD's L2 -- a counter's workgroup need not run on the same XCD from one launch to the
+// next (the fused add+norm's grid depends on the row count, and hipGraph replays alternate with eager calls)
+__device__ __forceinline__ unsigned ep_load(const unsigned* p) { return *reinterpret_cast<const volatile unsigned*>(p); }
+__device__ __forceinline__ void ep_store(unsigned* p, unsigned v) { *reinterpret_cast<volatile unsigned*>(p) = v; }
+
 // poll one 16-byte granule of peer data until every dword carries `tag` (bounded)
 __device__ __forceinline__ uint4 ar_poll(const uint32_t* src, uint32_t tag, long max_spins, bool& failed) {
   uint4 g = ar_load(src);
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
   __shared__ unsigned s_ep;
   __shared__ int s_fail;
   if (threadIdx.x == 0) {
-    s_ep = epochs[blockIdx.x] + 1u;
+    s_ep = ep_load(epochs + blockIdx.x) + 1u;
     s_fail = 0;
   }
   __syncthreads();
@@ -141,7 +147,7 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
   if (failed) s_fail = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
-    epochs[blockIdx.x] = ep;
+    ep_store(epochs + blockIdx.x, ep);
     if (s_fail) ar_raise(P, world, cap, err);
   }
 }
@@ -161,14 +167,16 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     long max_spins, int sim, long sp, long sx, long sh, long se, long st, long sq) {
   __shared__ unsigned s_ep;
   __shared__ int s_last;
-  int b = blockIdx.x;
-  const int c = blockIdx.y, nblk = gridDim.y;
+  // grid (slices, rows): the slice index is the fastest, so workgroup (b, c) sits on XCD c % 8 whatever the
+  // row count of the launch (nblk is a multiple of 8 for D % 2048 == 0)
+  int b = blockIdx.y;
+  const int c = blockIdx.x, nblk = gridDim.x;
   if (sim > 1) {
-    // single-GPU simulation: ALL ranks in one grid, rank fastest (blockIdx.x = row * sim + rank, per-rank
+    // single-GPU simulation: ALL ranks in one grid, rank fastest (blockIdx.y = row * sim + rank, per-rank
     // operand strides), so the ranks' workgroups of one slice are dispatched together and no slice
     // waits on a workgroup the dispatcher has not placed yet
-    rank = blockIdx.x % sim;
-    b = blockIdx.x / sim;
+    rank = blockIdx.y % sim;
+    b = blockIdx.y / sim;
     part += rank * sp;
     x += rank * sx;
     h += rank * sh;
@@ -177,7 +185,7 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     ssq += rank * sq;
   }
   const int eidx = b * nblk + c;
-  if (threadIdx.x == 0) s_ep = epochs[eidx] + 1u;
+  if (threadIdx.x == 0) s_ep = ep_load(epochs + eidx) + 1u;
   __syncthreads();
   const unsigned ep = s_ep;
   const uint32_t tag = ep & 3u;
@@ -226,7 +234,7 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) {
     ssq[eidx] = ss;
-    epochs[eidx] = ep;
+    ep_store(epochs + eidx, ep);
     if (fm) ar_raise(P, world, cap, err);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -292,7 +300,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_gather_kernel(const uint32
   __shared__ unsigned s_ep;
   __shared__ int s_fail;
   if (threadIdx.x == 0) {
-    s_ep = epochs[blockIdx.x] + 1u;
+    s_ep = ep_load(epochs + blockIdx.x) + 1u;
     s_fail = 0;
   }
   __syncthreads();
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_gather_kernel(const uint32
   if (failed) s_fail = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
-    epochs[blockIdx.x] = ep;
+    ep_store(epochs + blockIdx.x, ep);
     if (s_fail) ar_raise(P, world, cap, err);
   }
 }
@@ -347,7 +355,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_argmax_kernel(unsigned lon
   __shared__ unsigned s_ep;
   __shared__ int s_fail;
   if (threadIdx.x == 0) {
-    s_ep = epochs[blockIdx.x] + 1u;
+    s_ep = ep_load(epochs + blockIdx.x) + 1u;
     s_fail = 0;
   }
   __syncthreads();
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_argmax_kernel(unsigned lon
   if (failed) s_fail = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
-    epochs[blockIdx.x] = ep;
+    ep_store(epochs + blockIdx.x, ep);
     if (s_fail) ar_raise(P, world, cap, err);
   }
 }
@@ -472,7 +480,7 @@ int nls_ar_addnorm_sim(const float* part, long ldp, float* x, long ldx, const fl
   for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   if (sim_ranks > 1 && sim_ranks != world) return -1;
   const int sim = sim_ranks > 1 ? sim_ranks : 1;
-  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(rows * sim, nls_ar_row_blocks(D)), dim3(ARN_THREADS), 0,
+  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(nls_ar_row_blocks(D), rows * sim), dim3(ARN_THREADS), 0,
                      (hipStream_t)stream, part, ldp, x, ldx, nw, (_Float16*)h, ldh, D, eps, P, world, rank, cap, epochs,
                      tickets, ssq, err, max_spins, sim, sp, sx, sh, se, st, sq);
   return (int)hipGetLastError();
