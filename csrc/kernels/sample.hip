@@ -223,6 +223,136 @@ DEVI int draw_index_order(const float* __restrict__ l, int V, float lo, float mx
   return *s_tok;
 }
 
+// ---- top-k fast path (0 < top_k <= KFAST, the usual chat payload: top_k 40): after the top-k threshold
+// (two histogram passes) every kept logit is compacted into LDS in ONE more pass, and min-p, top-p and the
+// draw run on those <= CCAP entries -- 4 passes over the vocabulary instead of 8. The k-th largest value is
+// taken exactly from the sorted candidates (the binned threshold keeps its sub-bin ties), so the kept set,
+// the top-p cut and the index-order draw are those of the CPU twin (engine/sampling.py sample_rows).
+constexpr int KFAST = 256;
+constexpr int CCAP = 512;
+
+// block bitonic sort of CCAP (key, idx) pairs in LDS: by value, descending (ties: lower index first), or by
+// index, ascending. Padding entries carry (-inf, INT_MAX) and end up last either way.
+DEVI void bitonic_pairs(float* key, int* idx, bool byval) {
+  for (int k = 2; k <= CCAP; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < CCAP; i += NT) {
+        const int l = i ^ j;
+        if (l > i) {
+          const float ka = key[i], kb = key[l];
+          const int ia = idx[i], ib = idx[l];
+          const bool a_first = byval ? (ka > kb || (ka == kb && ia < ib)) : ia < ib;
+          if (((i & k) == 0) != a_first) {
+            key[i] = kb;
+            key[l] = ka;
+            idx[i] = ib;
+            idx[l] = ia;
+          }
+        }
+      }
+    }
+  __syncthreads();
+}
+
+// inclusive block scan of one value per thread (NT threads)
+DEVI float block_incl_scan(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  __syncthreads();
+  if (lane == 63) red[w] = incl;
+  __syncthreads();
+  float off = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) off += i < w ? red[i] : 0.f;
+  return off + incl;
+}
+
+// Returns the token (every thread), or -1 (every thread) when the compacted set overflows CCAP (a row with
+// massive ties at the threshold): the caller then takes the general path.
+DEVI int sample_topk_fast(const float* __restrict__ l, int V, const SampleParams& p, float u, float mx, float mn,
+                          float it, float* red, float* sk, int* sidx, float* hbin) {
+  __shared__ int s_n, s_pick, s_last;
+  __shared__ float s_tot, s_thr, s_z;
+  const float t = hist_threshold(l, V, mn, mx, -INFINITY, true, mx, it, (float)p.top_k, hbin, red);
+  if (threadIdx.x == 0) {
+    s_n = 0;
+    s_pick = 0x7FFFFFFF;
+    s_last = -1;
+    s_thr = 0.f;              // (no crossing found through rounding: keep the whole top-k set)
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < V; i += NT) {
+    const float v = l[i];
+    if (v >= t && v > -INFINITY) {
+      const int at = atomicAdd(&s_n, 1);
+      if (at < CCAP) {
+        sk[at] = v;
+        sidx[at] = i;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = s_n;
+  if (n > CCAP || n < 1) return -1;
+  for (int i = n + threadIdx.x; i < CCAP; i += NT) {
+    sk[i] = -INFINITY;
+    sidx[i] = 0x7FFFFFFF;
+  }
+  bitonic_pairs(sk, sidx, true);
+  // exact k-th largest (ties kept), then min-p
+  float lo = sk[min(p.top_k, n) - 1];
+  if (p.min_p > 0.f) lo = fmaxf(lo, mx + p.temperature * __logf(p.min_p));
+  const int j = threadIdx.x;
+  const bool in = j < n && sk[j] >= lo;
+  float w = in ? __expf((sk[j] - mx) * it) : 0.f;
+  if (p.top_p < 1.f) {
+    // smallest top set (by value) whose mass reaches top_p of the kept mass; ties of its last weight kept
+    const float cum = block_incl_scan(w, red);
+    if (j == NT - 1) s_tot = cum;
+    __syncthreads();
+    const float target = p.top_p * s_tot;
+    if (in && cum >= target && cum - w < target) s_thr = w;
+    __syncthreads();
+    if (w < s_thr) w = 0.f;
+  }
+  // the draw: inverse CDF in INDEX order over the kept entries
+  __syncthreads();
+  if (j < CCAP) sk[j] = w;
+  // by index (weights ride along as keys)
+  for (int k = 2; k <= CCAP; k <<= 1)
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < CCAP; i += NT) {
+        const int o = i ^ jj;
+        if (o > i && (((i & k) == 0) != (sidx[i] < sidx[o]))) {
+          const float kt = sk[i];
+          sk[i] = sk[o];
+          sk[o] = kt;
+          const int it2 = sidx[i];
+          sidx[i] = sidx[o];
+          sidx[o] = it2;
+        }
+      }
+    }
+  __syncthreads();
+  const float wj = j < CCAP ? sk[j] : 0.f;
+  const float cdf = block_incl_scan(wj, red);
+  if (j == NT - 1) s_z = cdf;
+  __syncthreads();
+  const float target = u * s_z;
+  if (wj > 0.f && cdf > target) atomicMin(&s_pick, j);
+  if (wj > 0.f) atomicMax(&s_last, j);
+  __syncthreads();
+  const int at = s_pick != 0x7FFFFFFF ? s_pick : s_last;
+  return at >= 0 ? sidx[at] : 0;
+}
+
 // One row: penalties over the history window h[0, n_hist) (any order), then greedy / temperature /
 // top-k / min-p / top-p and the draw with uniform u. The token is returned in EVERY thread.
 DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u, const int* __restrict__ h,
@@ -252,6 +382,22 @@ DEVI int sample_one(float* __restrict__ l, int V, const SampleParams& p, float u
   // 2) greedy: plain arg-max (lowest index on ties)
   const bool trunc = (p.top_k > 0 && p.top_k < V) || p.min_p > 0.f;
   const float it = p.temperature > 0.f ? 1.f / p.temperature : 0.f;
+  if (p.temperature > 0.f && p.top_k > 0 && p.top_k <= KFAST && p.top_k < V && s_chunk != nullptr) {
+    float m = -INFINITY, mnv = INFINITY;
+    for (int i = threadIdx.x; i < V; i += NT) {
+      const float v = l[i];
+      if (v > -INFINITY) {
+        m = fmaxf(m, v);
+        mnv = fminf(mnv, v);
+      }
+    }
+    const float fmx = block_max(m, red), fmn = -block_max(-mnv, red);
+    if (fmx > -INFINITY) {
+      const int tok = sample_topk_fast(l, V, p, u, fmx, fmn, it, red, s_chunk,
+                                       reinterpret_cast<int*>(s_chunk + CCAP), hbin);
+      if (tok >= 0) return tok;
+    }
+  }
   float mx = -INFINITY, Z = 0.f;
   if (p.temperature > 0.f && !trunc) {
     block_max_z(l, V, it, mx, Z, red);               // max and the untruncated mass in one pass

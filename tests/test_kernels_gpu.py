@@ -463,8 +463,8 @@ def test_oneshot_allreduce_simulated(gpu, world):
     (W=2: with GPU_MAX_HW_QUEUES=4 more simulated ranks can share a hardware queue and then
     serialise, which the bounded spin reports as a timeout rather than a hang):
     every rank must get the rank-ordered fp32 sum (of values rounded to 30 bits: 2-bit epoch tags),
-    bit-identical across ranks, over calls of varying size -- small calls skip most slots, so a
-    later call of the same parity must not take a stale granule (consumed slots are re-tagged)."""
+    bit-identical across ranks, over calls of varying size -- small calls skip most slot blocks, so a
+    later call of the same parity must not take a stale granule (per-block epochs, blocks written whole)."""
     from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
     cap = 1 << 16
     g = SimulatedGroup(world, cap, gpu)
@@ -491,7 +491,7 @@ def test_oneshot_allreduce_addnorm_simulated(gpu, world, rows, D):
     """Fused TP decode epilogue (one launch, each row over D/256 workgroups, the last to arrive at the
     row ticket normalises): x += sum of the ranks' partials in rank order, then h = f16(rmsnorm(x) * w)
     -- vs the fp32 reference, bit-identical x and h across ranks; repeated with a varying row count to
-    exercise both epoch parities, slot re-tagging and the per-row ticket reset. World 8, D 8192, rows
+    exercise both epoch parities, per-slice epochs and the per-row ticket reset. World 8, D 8192, rows
     1/16/64 is the Llama-3-70B TP=8 decode regime."""
     from nats_llm_studio_amd.parallel.oneshot import SimulatedGroup
     g = SimulatedGroup(world, 1 << 20, gpu)
@@ -645,6 +645,28 @@ def test_sample_kernel(gpu):
     g2 = [torch.Generator().manual_seed(7) for _ in range(8)]
     pp = [SamplingParams(temperature=1.5)] * 8
     assert sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g1) == sample_rows_gpu(lg[:8].clone(), pp, [[]] * 8, g2)
+
+
+@pytest.mark.parametrize("params", [dict(temperature=0.7, top_p=0.95, top_k=40),       # the reference payload
+                                    dict(temperature=1.0, top_k=5),
+                                    dict(temperature=0.9, top_k=256, top_p=0.8, min_p=0.02),
+                                    dict(temperature=1.1, top_k=40, repeat_penalty=1.3, presence_penalty=0.2),
+                                    dict(temperature=0.8, top_k=300, top_p=0.9)])          # past the fast path
+def test_sample_kernel_matches_cpu_twin(gpu, params):
+    """GPU sampler (csrc/kernels/sample.hip; top_k <= 256 takes the compacted fast path) vs the CPU twin
+    (engine/sampling.py sample_rows, float64 sort-based): same variate per row -> the same token, apart
+    from rows whose variate lands within float rounding of a CDF step."""
+    from nats_llm_studio_amd.engine.sampling import SamplingParams, sample_rows, sample_rows_gpu
+    g = torch.Generator().manual_seed(3)
+    n, V = 256, 32000
+    lg = torch.randn(n, V, generator=g) * 2.5
+    us = [float(u) for u in torch.rand(n, generator=g)]
+    hist = [[int(t) for t in torch.randint(0, V, (12,), generator=g)] for _ in range(n)]
+    ps = [SamplingParams(**params)] * n
+    want = sample_rows(lg.clone(), ps, hist, us)
+    got = sample_rows_gpu(lg.clone().to(gpu), ps, hist, us)
+    same = sum(a == b for a, b in zip(want, got))
+    assert same >= n - 2, (same, [(a, b) for a, b in zip(want, got) if a != b][:8])
 
 
 def test_sample_top_k_with_masked_logits(gpu):
