@@ -15,10 +15,10 @@
 //
 // Why a 2-bit tag suffices: slots are double-buffered by epoch parity and a rank can be at most one
 // call ahead of any peer (it cannot finish call c+1 without every peer's call-c+1 data, which a peer
-// writes only after finishing c). A consumer overwrites every granule it has read with the tag of
-// the OTHER parity, and the buffers start out that way (parity-0 slots tag 1, parity-1 slots tag 0),
-// so a slot that a later epoch of its parity finds was either just written by that epoch or carries
-// a tag no epoch of that parity ever has -- also when calls of different sizes skip some slots.
+// writes only after finishing c). Epochs are kept per SLOT BLOCK (per row slice in the fused add+norm)
+// and a call writes every granule of every block it advances, so at epoch e a slot holds the peer's
+// epoch e - 2 granule or its epoch e granule -- a skipped block keeps its epoch too. The consumer never
+// writes its own receive slots (see SlotBlocks below for why that matters).
 // Every rank uses the ROUNDED value of its own partial too, so the sums stay bit-identical.
 //
 // Element -> workgroup maps are fixed (the plain all-reduce runs a FIXED grid, grid-stride; the
@@ -30,6 +30,7 @@
 // the engine reads its error word after each decode step and fails the step's requests.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define AR_MAX_RANKS 8
 #define AR_BLOCKS 32
@@ -49,20 +50,38 @@ __device__ __forceinline__ float ar_val(uint32_t g) { return __uint_as_float(g &
 __device__ __forceinline__ bool ar_tagged(uint4 g, uint32_t tag) {
   return ((g.x & 3u) == tag) & ((g.y & 3u) == tag) & ((g.z & 3u) == tag) & ((g.w & 3u) == tag);
 }
-typedef uint32_t ar_u4 __attribute__((ext_vector_type(4)));
-// 16-byte volatile (cache-bypassing, never merged or hoisted) store / load of four tagged dwords
-__device__ __forceinline__ void ar_store(uint32_t* p, uint4 g) {
-  *reinterpret_cast<volatile ar_u4*>(p) = ar_u4{g.x, g.y, g.z, g.w};
-}
-__device__ __forceinline__ uint4 ar_load(const uint32_t* p) {
-  const ar_u4 r = *reinterpret_cast<const volatile ar_u4*>(p);
-  return make_uint4(r[0], r[1], r[2], r[3]);
-}
 __device__ __forceinline__ uint4 ar_pack4(float4 v, uint32_t tag) {
   return make_uint4(ar_pack(v.x, tag), ar_pack(v.y, tag), ar_pack(v.z, tag), ar_pack(v.w, tag));
 }
 __device__ __forceinline__ float4 ar_val4(uint4 g) {
   return make_float4(ar_val(g.x), ar_val(g.y), ar_val(g.z), ar_val(g.w));
+}
+
+// Every word another workgroup or another rank reads goes through GLOBAL (address space 1) atomic accesses
+// with an explicit scope -- never flat, never plain (cdna_hip_programming.md Guideline 16 recipe; round 3
+// used flat `volatile` accesses, and a granule pushed through the peer's IPC mapping could stay invisible to
+// the owner's poll: 2-process rehearsal, round 4). A 16-byte granule is two 8-byte halves; every dword
+// carries the tag, so a torn granule just fails the tag check until both halves have landed.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void ar_store(uint32_t* p, uint4 g) {
+  gu64* q = (gu64*)p;
+  __hip_atomic_store(q, ((unsigned long long)g.y << 32) | g.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 1, ((unsigned long long)g.w << 32) | g.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint4 ar_load(const uint32_t* p) {
+  const gu64* q = (const gu64*)p;
+  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+// a float4 other workgroups of this launch read (the residual slice of the fused add+norm): write-through
+__device__ __forceinline__ void wt_store4(float* p, float4 v) {
+  gu64* q = (gu64*)p;
+  __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // this rank's error word and the peers' (after the 2 x world x cap receive slots)
@@ -72,84 +91,139 @@ __device__ __forceinline__ uint32_t* ar_err_word(uint32_t* buf, int world, long 
 __device__ void ar_raise(const ArPeers& P, int world, long cap, int* err) {
   atomicExch(err, 1);
   for (int p = 0; p < world; ++p)
-    __hip_atomic_store(ar_err_word(P.buf[p], world, cap), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((gu32*)ar_err_word(P.buf[p], world, cap), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // per-workgroup epoch counters: read / advanced with `sc0 sc1` (volatile) accesses, never through a possibly
 // stale line of another XCD's L2 -- a counter's workgroup need not run on the same XCD from one launch to the
 // next (the fused add+norm's grid depends on the row count, and hipGraph replays alternate with eager calls)
-__device__ __forceinline__ unsigned ep_load(const unsigned* p) { return *reinterpret_cast<const volatile unsigned*>(p); }
-__device__ __forceinline__ void ep_store(unsigned* p, unsigned v) { *reinterpret_cast<volatile unsigned*>(p) = v; }
+__device__ __forceinline__ unsigned ep_load(const unsigned* p) {
+  return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ep_store(unsigned* p, unsigned v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// diagnostics of the first timed-out poll of a buffer set: words 1..7 of this rank's error area (a, b, epoch,
+// peer, the first dword seen -- its tag is the low 2 bits --, a marker, the kernel: 1 sum, 2 add+norm,
+// 3 gather, 4 arg-max), read back by OneShotAllReduce.debug_state
+__device__ void ar_diag(uint32_t* mine, int world, long cap, int kid, long a, long b, unsigned ep, int peer,
+                        uint32_t seen) {
+  uint32_t* dw = ar_err_word(mine, world, cap);
+  if (atomicCAS(dw + 6, 0u, 0xA11u) == 0u) {
+    dw[1] = (uint32_t)a;
+    dw[2] = (uint32_t)b;
+    dw[3] = ep;
+    dw[4] = (uint32_t)peer;
+    dw[5] = seen;
+    dw[7] = (uint32_t)kid;
+  }
+}
+
+// launch-option bits carried above the spin budget (host: ar_opts(), env NLS_AR_POLL_INV / NLS_AR_RETAG)
+constexpr long AR_OPT_POLL_INV = 1L << 62;    // system-scope acquire (L2 invalidate) before every re-poll
+constexpr long AR_OPT_RETAG = 1L << 61;       // fused add+norm: re-tag consumed granules (the round-3 protocol)
+constexpr long AR_SPIN_MASK = (1L << 48) - 1;
 
 // poll one 16-byte granule of peer data until every dword carries `tag` (bounded)
 __device__ __forceinline__ uint4 ar_poll(const uint32_t* src, uint32_t tag, long max_spins, bool& failed) {
   uint4 g = ar_load(src);
   long spins = 0;
+  const long budget = max_spins & AR_SPIN_MASK;
   while (!failed && !ar_tagged(g, tag)) {
-    if (++spins > max_spins) {
+    if (++spins > budget) {
       failed = true;
       break;
     }
     __builtin_amdgcn_s_sleep(2);
+    if (max_spins & AR_OPT_POLL_INV) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     g = ar_load(src);
   }
   return g;
 }
 
 // ---------------------------------------------------------------------------------------------
-// plain all-reduce (MoE expert outputs, generic decode-size sums): fixed grid, grid-stride over
-// 16-byte granules (n % 4 == 0), data reduced in place
+// Epochs per SLOT BLOCK, full coverage, no consumed-tag rewrite. The receive slots of a grid-stride
+// collective are cut into fixed blocks of BLK granules; a call advances the epoch of every block that
+// overlaps its message and writes ALL granules of those blocks (the tail past the message carries a
+// dummy payload with the current tag), so at epoch e a slot of a block holds the peer's epoch e - 2
+// granule (tag (e - 2) & 3) or its epoch e granule, whatever the message sizes of the calls in between.
+// Round 3 re-tagged each consumed granule instead (the consumer's own store into its receive slot), and
+// on one GPU shared by two ranks an eager call after decode-graph replays could read that rewrite back
+// instead of the peer's newer granule (2-process rehearsal, round 4). Block b belongs to workgroup
+// b % gridDim.x in every call (fixed grids), which keeps its epoch counter's reads and writes ordered.
+template <int BLK>
+struct SlotBlocks {
+  long nb;                     // blocks of this call
+  int first, step, mine;       // this workgroup's blocks: first, first + step, ... (mine of them)
+  __device__ SlotBlocks(long granules) {
+    nb = (granules + BLK - 1) / BLK;
+    first = blockIdx.x;
+    step = gridDim.x;
+    mine = nb > first ? (int)((nb - 1 - first) / step + 1) : 0;
+  }
+};
+constexpr int AR_MAX_WG_BLOCKS = 64;   // slot blocks per workgroup at the largest message (host-checked)
+
+// this workgroup's block epochs -> LDS (advanced by one: the epoch of THIS call)
+__device__ __forceinline__ void blocks_begin(const unsigned* epochs, int first, int step, int mine, unsigned* s_ep) {
+  for (int j = threadIdx.x; j < mine; j += blockDim.x) s_ep[j] = ep_load(epochs + first + (long)j * step) + 1u;
+  __syncthreads();
+}
+__device__ __forceinline__ void blocks_end(unsigned* epochs, int first, int step, int mine, const unsigned* s_ep) {
+  __syncthreads();
+  for (int j = threadIdx.x; j < mine; j += blockDim.x) ep_store(epochs + first + (long)j * step, s_ep[j]);
+}
+
+// plain all-reduce (MoE expert outputs, generic decode-size sums): fixed grid, slot blocks of
+// AR_THREADS granules (16 B, n % 4 == 0), data reduced in place
 __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restrict__ data, long n, ArPeers P,
                                                                  int world, int rank, long cap,
                                                                  unsigned* __restrict__ epochs,
                                                                  int* __restrict__ err, long max_spins) {
-  __shared__ unsigned s_ep;
+  __shared__ unsigned s_ep[AR_MAX_WG_BLOCKS];
   __shared__ int s_fail;
-  if (threadIdx.x == 0) {
-    s_ep = ep_load(epochs + blockIdx.x) + 1u;
-    s_fail = 0;
-  }
-  __syncthreads();
-  const unsigned ep = s_ep;
-  const uint32_t tag = ep & 3u;
-  const int par = (int)(ep & 1u);
-  const long stride = (long)AR_BLOCKS * AR_THREADS;
   const long n4 = n >> 2;
+  const SlotBlocks<AR_THREADS> B(n4);
+  if (threadIdx.x == 0) s_fail = 0;
+  blocks_begin(epochs, B.first, B.step, B.mine, s_ep);
   // 1) push: my (rounded, tagged) values -> slot [par][rank] of every peer, 16 B per lane
-  for (long i = (long)blockIdx.x * AR_THREADS + threadIdx.x; i < n4; i += stride) {
-    const uint4 g = ar_pack4(reinterpret_cast<const float4*>(data)[i], tag);
+  for (int j = 0; j < B.mine; ++j) {
+    const unsigned ep = s_ep[j];
+    const long i = ((long)B.first + (long)j * B.step) * AR_THREADS + threadIdx.x;
+    const float4 d = i < n4 ? reinterpret_cast<const float4*>(data)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint4 g = ar_pack4(d, ep & 3u);
     for (int p = 0; p < world; ++p)
-      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + 4 * i, g);
+      if (p != rank) ar_store(P.buf[p] + ((long)((ep & 1u) * world + rank)) * cap + 4 * i, g);
   }
-  // 2) gather + reduce in rank order (bit-identical on every rank); consumed granules get the
-  //    other parity's tag
+  // 2) gather + reduce in rank order (bit-identical on every rank)
   uint32_t* mine = P.buf[rank];
-  const uint32_t ct = (ep + 1u) & 3u;
-  const uint4 clr = make_uint4(ct, ct, ct, ct);
   bool failed = false;   // after one timeout, stop waiting (the error word is raised below)
-  for (long i = (long)blockIdx.x * AR_THREADS + threadIdx.x; i < n4; i += stride) {
-    const float4 own = ar_val4(ar_pack4(reinterpret_cast<const float4*>(data)[i], tag));
+  for (int j = 0; j < B.mine; ++j) {
+    const unsigned ep = s_ep[j];
+    const uint32_t tag = ep & 3u;
+    const long i = ((long)B.first + (long)j * B.step) * AR_THREADS + threadIdx.x;
+    const float4 d = i < n4 ? reinterpret_cast<const float4*>(data)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 own = ar_val4(ar_pack4(d, tag));
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = 0; p < world; ++p) {
       float4 v = own;
       if (p != rank) {
-        uint32_t* src = mine + ((long)(par * world + p)) * cap + 4 * i;
-        v = ar_val4(ar_poll(src, tag, max_spins, failed));
-        ar_store(src, clr);
+        const bool was = failed;
+        const uint4 gv = ar_poll(mine + ((long)((ep & 1u) * world + p)) * cap + 4 * i, tag, max_spins, failed);
+        if (failed && !was) ar_diag(mine, world, cap, 1, i, n4, ep, p, gv.x);
+        v = ar_val4(gv);
       }
       acc.x += v.x;
       acc.y += v.y;
       acc.z += v.z;
       acc.w += v.w;
     }
-    reinterpret_cast<float4*>(data)[i] = acc;
+    if (i < n4) reinterpret_cast<float4*>(data)[i] = acc;
   }
   if (failed) s_fail = 1;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ep_store(epochs + blockIdx.x, ep);
-    if (s_fail) ar_raise(P, world, cap, err);
-  }
+  blocks_end(epochs, B.first, B.step, B.mine, s_ep);
+  if (threadIdx.x == 0 && s_fail) ar_raise(P, world, cap, err);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -164,19 +238,21 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     const float* __restrict__ part, long ldp, float* __restrict__ x, long ldx, const float* __restrict__ nw,
     _Float16* __restrict__ h, long ldh, int D, float eps, ArPeers P, int world, int rank, long cap,
     unsigned* __restrict__ epochs, int* __restrict__ tickets, float* __restrict__ ssq, int* __restrict__ err,
-    long max_spins, int sim, long sp, long sx, long sh, long se, long st, long sq) {
+    long max_spins, int sim, long sp, long sx, long sh, long se, long st, long sq, int nblk, int nrr) {
   __shared__ unsigned s_ep;
   __shared__ int s_last;
-  // grid (slices, rows): the slice index is the fastest, so workgroup (b, c) sits on XCD c % 8 whatever the
-  // row count of the launch (nblk is a multiple of 8 for D % 2048 == 0)
-  int b = blockIdx.y;
-  const int c = blockIdx.x, nblk = gridDim.x;
+  // 1-D grid, XCD-aligned (workgroup L runs on XCD L % 8): every slice of row-rank r = b * sim + rank sits on
+  // XCD r % 8, whatever the row count of the launch -- the row's ticket, sum-of-squares shares and residual
+  // slices are exchanged inside one L2 (a row spread over XCDs normalised with stale shares: round 4), and a
+  // slice's epoch counter is always touched from the same XCD. Workgroups past the last row exit at once.
+  const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
+  const int c = q % nblk, rr = (q / nblk) * 8 + xcd;
+  if (rr >= nrr) return;
+  int b = rr;
   if (sim > 1) {
-    // single-GPU simulation: ALL ranks in one grid, rank fastest (blockIdx.y = row * sim + rank, per-rank
-    // operand strides), so the ranks' workgroups of one slice are dispatched together and no slice
-    // waits on a workgroup the dispatcher has not placed yet
-    rank = blockIdx.y % sim;
-    b = blockIdx.y / sim;
+    // single-GPU simulation: ALL ranks in one grid (rr = row * sim + rank, per-rank operand strides)
+    rank = rr % sim;
+    b = rr / sim;
     part += rank * sp;
     x += rank * sx;
     h += rank * sh;
@@ -200,18 +276,27 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     // 1) push this rank's partial slice to every peer
     for (int p = 0; p < world; ++p)
       if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + (long)b * D + col, g);
-    // 2) rank-ordered sum + residual add (bit-identical on every rank); consumed granules get the
-    //    other parity's tag
+    // 2) rank-ordered sum + residual add (bit-identical on every rank). No consumed-tag rewrite here:
+    //    every call that advances eidx's epoch has the peer write ALL of the slice's granules, so at epoch
+    //    e a slot holds the peer's epoch e - 2 data (tag (e - 2) & 3) or its epoch e data -- never a stale
+    //    granule with the current tag. (The rewrite by the consumer itself was what went wrong: on one GPU
+    //    shared by two ranks, an eager call after decode-graph replays read its OWN epoch e - 2 rewrite
+    //    back instead of the peer's epoch e granule, 2-process rehearsal, round 4.)
     uint32_t* mine = P.buf[rank];
-    const uint32_t ct = (ep + 1u) & 3u;
     const float4 own = ar_val4(g);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = 0; p < world; ++p) {
       float4 v = own;
       if (p != rank) {
         uint32_t* src = mine + ((long)(par * world + p)) * cap + (long)b * D + col;
-        v = ar_val4(ar_poll(src, tag, max_spins, failed));
-        ar_store(src, make_uint4(ct, ct, ct, ct));
+        const bool was = failed;
+        const uint4 gv = ar_poll(src, tag, max_spins, failed);
+        if (failed && !was) ar_diag(mine, world, cap, 2, b, c, ep, p, gv.x);
+        v = ar_val4(gv);
+        if (max_spins & AR_OPT_RETAG) {
+          const uint32_t ct = (ep + 1u) & 3u;
+          ar_store(src, make_uint4(ct, ct, ct, ct));
+        }
       }
       acc.x += v.x;
       acc.y += v.y;
@@ -224,7 +309,7 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     xv.y += acc.y;
     xv.z += acc.z;
     xv.w += acc.w;
-    *xp = xv;
+    wt_store4(reinterpret_cast<float*>(xp), xv);
     ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
   }
 #pragma unroll
@@ -233,24 +318,27 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
   // 3) publish the slice (x stores + share), then the row ticket: the last slice normalises the row
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) {
-    ssq[eidx] = ss;
+    __hip_atomic_store((gu32*)(ssq + eidx), __float_as_uint(ss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ep_store(epochs + eidx, ep);
     if (fm) ar_raise(P, world, cap, err);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add(tickets + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+    s_last = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(tickets + b), 1, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
   }
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    tickets[b] = 0;          // stream order makes the reset visible to the next launch
+    __hip_atomic_store((gu32*)(tickets + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   float tot = 0.f;
-  for (int i = threadIdx.x; i < nblk; i += ARN_THREADS) tot += ssq[(size_t)b * nblk + i];
+  for (int i = threadIdx.x; i < nblk; i += ARN_THREADS)
+    tot += __uint_as_float(__hip_atomic_load((const gu32*)(ssq + (size_t)b * nblk + i), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
   const float inv = rsqrtf(tot / (float)D + eps);
@@ -291,107 +379,104 @@ __device__ __forceinline__ uint2 ag_unpack2(uint4 g) {
 
 // src: this rank's n2 granules (2 * n2 words, laid out as `narr` arrays of rows x C words); dst receives
 // every rank's words with the rank inside the row: dst[a][row][p * C + c] (arrays of rows x world*C) --
-// per-rank top-C candidate lists come out as one vocabulary-ordered row per sequence
+// per-rank top-C candidate lists come out as one vocabulary-ordered row per sequence. Slot blocks of
+// AG_THREADS granules (see SlotBlocks).
 __global__ __launch_bounds__(AG_THREADS) void oneshot_gather_kernel(const uint32_t* __restrict__ src, long n2,
                                                                      uint32_t* __restrict__ dst, int C, long per_arr,
                                                                      ArPeers P, int world, int rank, long cap,
                                                                      unsigned* __restrict__ epochs,
                                                                      int* __restrict__ err, long max_spins) {
-  __shared__ unsigned s_ep;
+  __shared__ unsigned s_ep[AR_MAX_WG_BLOCKS];
   __shared__ int s_fail;
-  if (threadIdx.x == 0) {
-    s_ep = ep_load(epochs + blockIdx.x) + 1u;
-    s_fail = 0;
-  }
-  __syncthreads();
-  const unsigned ep = s_ep;
-  const uint32_t tag = ep & 3u;
-  const int par = (int)(ep & 1u);
-  const long stride = (long)AG_BLOCKS * AG_THREADS;
+  const SlotBlocks<AG_THREADS> B(n2);
+  if (threadIdx.x == 0) s_fail = 0;
+  blocks_begin(epochs, B.first, B.step, B.mine, s_ep);
   auto out_at = [&](long w, int p) -> uint32_t* {
     const long a = w / per_arr, rem = w - a * per_arr, r = rem / C, c = rem - r * C;
     return dst + a * per_arr * world + r * (long)world * C + (long)p * C + c;
   };
-  for (long i = (long)blockIdx.x * AG_THREADS + threadIdx.x; i < n2; i += stride) {
-    const uint2 v = reinterpret_cast<const uint2*>(src)[i];
-    const uint4 g = ag_pack2(v.x, v.y, tag);
+  for (int j = 0; j < B.mine; ++j) {
+    const unsigned ep = s_ep[j];
+    const long i = ((long)B.first + (long)j * B.step) * AG_THREADS + threadIdx.x;
+    const uint2 v = i < n2 ? reinterpret_cast<const uint2*>(src)[i] : make_uint2(0u, 0u);
+    const uint4 g = ag_pack2(v.x, v.y, ep & 3u);
     for (int p = 0; p < world; ++p)
-      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + 4 * i, g);
-    uint32_t* o = out_at(2 * i, rank);
-    o[0] = v.x;
-    o[1] = v.y;
-  }
-  uint32_t* mine = P.buf[rank];
-  const uint32_t ct = (ep + 1u) & 3u;
-  bool failed = false;
-  for (long i = (long)blockIdx.x * AG_THREADS + threadIdx.x; i < n2; i += stride) {
-    for (int p = 0; p < world; ++p) {
-      if (p == rank) continue;
-      uint32_t* s = mine + ((long)(par * world + p)) * cap + 4 * i;
-      const uint2 v = ag_unpack2(ar_poll(s, tag, max_spins, failed));
-      ar_store(s, make_uint4(ct, ct, ct, ct));
-      uint32_t* o = out_at(2 * i, p);       // C even: both words of a granule share the row
+      if (p != rank) ar_store(P.buf[p] + ((long)((ep & 1u) * world + rank)) * cap + 4 * i, g);
+    if (i < n2) {
+      uint32_t* o = out_at(2 * i, rank);
       o[0] = v.x;
       o[1] = v.y;
     }
   }
-  if (failed) s_fail = 1;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ep_store(epochs + blockIdx.x, ep);
-    if (s_fail) ar_raise(P, world, cap, err);
+  uint32_t* mine = P.buf[rank];
+  bool failed = false;
+  for (int j = 0; j < B.mine; ++j) {
+    const unsigned ep = s_ep[j];
+    const long i = ((long)B.first + (long)j * B.step) * AG_THREADS + threadIdx.x;
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      const bool was = failed;
+      const uint4 gv = ar_poll(mine + ((long)((ep & 1u) * world + p)) * cap + 4 * i, ep & 3u, max_spins, failed);
+      if (failed && !was) ar_diag(mine, world, cap, 3, i, n2, ep, p, gv.x);
+      const uint2 v = ag_unpack2(gv);
+      if (i < n2) {
+        uint32_t* o = out_at(2 * i, p);       // C even: both words of a granule share the row
+        o[0] = v.x;
+        o[1] = v.y;
+      }
+    }
   }
+  if (failed) s_fail = 1;
+  blocks_end(epochs, B.first, B.step, B.mine, s_ep);
+  if (threadIdx.x == 0 && s_fail) ar_raise(P, world, cap, err);
 }
 
 // Vocab-parallel greedy pick: each rank's fused arg-max key of row i (ordered value bits << 32 | ~local id)
 // is rebased to the global id (~local - vocab_lo == ~(local + vocab_lo)), exchanged (one granule per row),
 // and the unsigned max over ranks gives the same token on every rank; the key is re-armed (0) for the next
-// lm-head launch. Replaces xor / sub / RCCL MAX all-reduce / xor / unpack.
+// lm-head launch. Replaces xor / sub / RCCL MAX all-reduce / xor / unpack. Slot blocks as the gather.
 __global__ __launch_bounds__(AG_THREADS) void oneshot_argmax_kernel(unsigned long long* __restrict__ keys, int n,
                                                                      unsigned vocab_lo, int* __restrict__ next_ids,
                                                                      ArPeers P, int world, int rank, long cap,
                                                                      unsigned* __restrict__ epochs,
                                                                      int* __restrict__ err, long max_spins) {
-  __shared__ unsigned s_ep;
+  __shared__ unsigned s_ep[AR_MAX_WG_BLOCKS];
   __shared__ int s_fail;
-  if (threadIdx.x == 0) {
-    s_ep = ep_load(epochs + blockIdx.x) + 1u;
-    s_fail = 0;
-  }
-  __syncthreads();
-  const unsigned ep = s_ep;
-  const uint32_t tag = ep & 3u;
-  const int par = (int)(ep & 1u);
-  const int stride = AG_BLOCKS * AG_THREADS;
-  for (int i = blockIdx.x * AG_THREADS + threadIdx.x; i < n; i += stride) {
-    const unsigned long long k = keys[i];
-    const uint4 g = ag_pack2((uint32_t)k - vocab_lo, (uint32_t)(k >> 32), tag);
+  const SlotBlocks<AG_THREADS> B(n);
+  if (threadIdx.x == 0) s_fail = 0;
+  blocks_begin(epochs, B.first, B.step, B.mine, s_ep);
+  for (int j = 0; j < B.mine; ++j) {
+    const unsigned ep = s_ep[j];
+    const long i = ((long)B.first + (long)j * B.step) * AG_THREADS + threadIdx.x;
+    const unsigned long long k = i < n ? keys[i] : 0ull;
+    const uint4 g = ag_pack2((uint32_t)k - vocab_lo, (uint32_t)(k >> 32), ep & 3u);
     for (int p = 0; p < world; ++p)
-      if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + 4L * i, g);
+      if (p != rank) ar_store(P.buf[p] + ((long)((ep & 1u) * world + rank)) * cap + 4L * i, g);
   }
   uint32_t* mine = P.buf[rank];
-  const uint32_t ct = (ep + 1u) & 3u;
   bool failed = false;
-  for (int i = blockIdx.x * AG_THREADS + threadIdx.x; i < n; i += stride) {
-    const unsigned long long k = keys[i];
+  for (int j = 0; j < B.mine; ++j) {
+    const unsigned ep = s_ep[j];
+    const long i = ((long)B.first + (long)j * B.step) * AG_THREADS + threadIdx.x;
+    const unsigned long long k = i < n ? keys[i] : 0ull;
     unsigned long long best = (k & 0xFFFFFFFF00000000ull) | (unsigned long long)((uint32_t)k - vocab_lo);
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
-      uint32_t* s = mine + ((long)(par * world + p)) * cap + 4L * i;
-      const uint2 v = ag_unpack2(ar_poll(s, tag, max_spins, failed));
-      ar_store(s, make_uint4(ct, ct, ct, ct));
+      const bool was = failed;
+      const uint4 gv = ar_poll(mine + ((long)((ep & 1u) * world + p)) * cap + 4L * i, ep & 3u, max_spins, failed);
+      if (failed && !was) ar_diag(mine, world, cap, 4, i, n, ep, p, gv.x);
+      const uint2 v = ag_unpack2(gv);
       const unsigned long long c = ((unsigned long long)v.y << 32) | v.x;
       best = c > best ? c : best;
     }
-    next_ids[i] = (int)~(uint32_t)best;
-    keys[i] = 0ull;
+    if (i < n) {
+      next_ids[i] = (int)~(uint32_t)best;
+      keys[i] = 0ull;
+    }
   }
   if (failed) s_fail = 1;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ep_store(epochs + blockIdx.x, ep);
-    if (s_fail) ar_raise(P, world, cap, err);
-  }
+  blocks_end(epochs, B.first, B.step, B.mine, s_ep);
+  if (threadIdx.x == 0 && s_fail) ar_raise(P, world, cap, err);
 }
 
 __global__ void ar_err_clear_kernel(uint32_t* w) { *w = 0u; }
@@ -404,6 +489,18 @@ __global__ void ar_reinit_kernel(uint32_t* buf, long half) {
     buf[i] = i < half ? 0x01010101u : 0u;
 }
 
+static long ar_opts(long max_spins) {
+  static const long opts = [] {
+    long o = 0;
+    const char* a = getenv("NLS_AR_POLL_INV");
+    const char* b = getenv("NLS_AR_RETAG");
+    if (a && atoi(a)) o |= AR_OPT_POLL_INV;
+    if (b && atoi(b)) o |= AR_OPT_RETAG;
+    return o;
+  }();
+  return (max_spins & AR_SPIN_MASK) | opts;
+}
+
 extern "C" {
 
 // bytes of one rank's receive buffer for messages of up to `cap` floats (+ its error word area)
@@ -412,7 +509,15 @@ long nls_ar_buffer_bytes(long cap, int world) { return 2L * world * cap * 4L + A
 int nls_ar_alloc(long cap, int world, void** buf, void* ipc_handle /* hipIpcMemHandle_t, 64 B */) {
   if (world < 1 || world > AR_MAX_RANKS || cap % 4) return -1;
   size_t bytes = (size_t)nls_ar_buffer_bytes(cap, world);
-  hipError_t e = hipExtMallocWithFlags(buf, bytes, hipDeviceMallocUncached);
+  // receive buffers: uncached device memory by default; NLS_AR_ALLOC=fine (fine-grained, coherent across
+  // agents) or coarse (plain hipMalloc) for A/Bs of the IPC visibility on one shared GPU
+  static const int kind = [] {
+    const char* e = getenv("NLS_AR_ALLOC");
+    return !e ? 0 : (e[0] == 'f' ? 1 : (e[0] == 'c' ? 2 : 0));
+  }();
+  hipError_t e = kind == 2 ? hipMalloc(buf, bytes)
+                           : hipExtMallocWithFlags(buf, bytes, kind == 1 ? hipDeviceMallocFinegrained
+                                                                         : hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
   // parity-0 slots start with tag 1, parity-1 slots (and the error word) with tag 0: no epoch of a
   // slot's parity ever carries its initial tag
@@ -441,12 +546,21 @@ int nls_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
 int nls_ar_blocks() { return AR_BLOCKS; }
 
+// epoch counters of the plain all-reduce / the gather + arg-max: one per slot block of a `cap`-float buffer
+long nls_ar_epoch_slots(long cap) { return (cap / 4 + AR_THREADS - 1) / AR_THREADS; }
+long nls_ag_epoch_slots(long cap) { return (cap / 4 + AG_THREADS - 1) / AG_THREADS; }
+
 // workgroups per row of the fused add+norm (its epoch / share / ticket layout: [rows][nls_ar_row_blocks])
 int nls_ar_row_blocks(int D) { return (D + ARN_VPB - 1) / ARN_VPB; }
 
 // this rank's error word (raised by any rank whose poll timed out): async copy to `host` (pinned), clear
 int nls_ar_err_fetch(void* buf, long cap, int world, void* host, void* stream) {
   return (int)hipMemcpyAsync(host, (char*)buf + 2L * world * cap * 4L, 4, hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+// the first words of this rank's error area (word 0: the error word; 1..6: diagnostics of the first timeout)
+int nls_ar_err_words(void* buf, long cap, int world, void* host, int n, void* stream) {
+  return (int)hipMemcpyAsync(host, (char*)buf + 2L * world * cap * 4L, 4L * n, hipMemcpyDeviceToHost,
+                             (hipStream_t)stream);
 }
 int nls_ar_err_clear(void* buf, long cap, int world, void* stream) {
   hipLaunchKernelGGL(ar_err_clear_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
@@ -480,9 +594,10 @@ int nls_ar_addnorm_sim(const float* part, long ldp, float* x, long ldx, const fl
   for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   if (sim_ranks > 1 && sim_ranks != world) return -1;
   const int sim = sim_ranks > 1 ? sim_ranks : 1;
-  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(nls_ar_row_blocks(D), rows * sim), dim3(ARN_THREADS), 0,
+  const int nblk = nls_ar_row_blocks(D), nrr = rows * sim;
+  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(8 * nblk * ((nrr + 7) / 8)), dim3(ARN_THREADS), 0,
                      (hipStream_t)stream, part, ldp, x, ldx, nw, (_Float16*)h, ldh, D, eps, P, world, rank, cap, epochs,
-                     tickets, ssq, err, max_spins, sim, sp, sx, sh, se, st, sq);
+                     tickets, ssq, err, ar_opts(max_spins), sim, sp, sx, sh, se, st, sq, nblk, nrr);
   return (int)hipGetLastError();
 }
 
@@ -491,26 +606,31 @@ int nls_ag_blocks() { return AG_BLOCKS; }
 // all-gather of 2 * n2 words (narr arrays of per_arr = rows * C words; C even) -> dst (see the kernel)
 int nls_ag_run(const void* src, long n2, void* dst, int C, long per_arr, void* const* peers, int world, int rank,
                long cap, unsigned* epochs, int* err, long max_spins, void* stream) {
-  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n2 < 0 || 4 * n2 > cap || C < 2 || C % 2 ||
-      per_arr < C || per_arr % C || (2 * n2) % per_arr)
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n2 < 0 || C < 2 || C % 2 ||
+      per_arr < C || per_arr % C || (2 * n2) % per_arr || cap % (4 * AG_THREADS) ||
+      4 * ((n2 + AG_THREADS - 1) / AG_THREADS) * AG_THREADS > cap ||
+      (n2 + AG_THREADS - 1) / AG_THREADS > (long)AG_BLOCKS * AR_MAX_WG_BLOCKS)
     return -1;
   ArPeers P;
   for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   hipLaunchKernelGGL(oneshot_gather_kernel, dim3(AG_BLOCKS), dim3(AG_THREADS), 0, (hipStream_t)stream,
-                     (const uint32_t*)src, n2, (uint32_t*)dst, C, per_arr, P, world, rank, cap, epochs, err, max_spins);
+                     (const uint32_t*)src, n2, (uint32_t*)dst, C, per_arr, P, world, rank, cap, epochs, err,
+                     ar_opts(max_spins));
   return (int)hipGetLastError();
 }
 
 // keys (u64 [n], fused arg-max of this rank's vocab shard starting at vocab_lo) -> next_ids on every rank
 int nls_ag_argmax(void* keys, int n, int vocab_lo, void* next_ids, void* const* peers, int world, int rank, long cap,
                   unsigned* epochs, int* err, long max_spins, void* stream) {
-  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || 4L * n > cap || vocab_lo < 0)
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n < 1 || vocab_lo < 0 ||
+      cap % (4 * AG_THREADS) || 4L * ((n + AG_THREADS - 1) / AG_THREADS) * AG_THREADS > cap ||
+      (n + AG_THREADS - 1) / AG_THREADS > (long)AG_BLOCKS * AR_MAX_WG_BLOCKS)
     return -1;
   ArPeers P;
   for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   hipLaunchKernelGGL(oneshot_argmax_kernel, dim3(AG_BLOCKS), dim3(AG_THREADS), 0, (hipStream_t)stream,
                      (unsigned long long*)keys, n, (unsigned)vocab_lo, (int*)next_ids, P, world, rank, cap, epochs, err,
-                     max_spins);
+                     ar_opts(max_spins));
   return (int)hipGetLastError();
 }
 
@@ -524,11 +644,13 @@ int nls_ar_reinit(void* buf, long cap, int world, void* stream) {
 
 int nls_ar_run(float* data, long n, void* const* peers, int world, int rank, long cap, unsigned* epochs,
                int* err, long max_spins, void* stream) {
-  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n > cap || n % 4) return -1;
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n > cap || n % 4 || cap % (4 * AR_THREADS) ||
+      (n / 4 + AR_THREADS - 1) / AR_THREADS > (long)AR_BLOCKS * AR_MAX_WG_BLOCKS)
+    return -1;
   ArPeers P;
   for (int i = 0; i < AR_MAX_RANKS; ++i) P.buf[i] = i < world ? (uint32_t*)peers[i] : nullptr;
   hipLaunchKernelGGL(oneshot_ar_kernel, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, (hipStream_t)stream, data, n, P,
-                     world, rank, cap, epochs, err, max_spins);
+                     world, rank, cap, epochs, err, ar_opts(max_spins));
   return (int)hipGetLastError();
 }
 

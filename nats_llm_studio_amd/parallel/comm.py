@@ -39,6 +39,9 @@ class Comm:
         self.src = dist.get_global_rank(group, 0) if group is not None else 0
         self.device = torch.device(device) if device is not None else None
         self.oneshot = None          # optional small-message all-reduce (parallel/oneshot.py)
+        # NLS_ONESHOT_EAGER=0: the IPC one-shot kernels only inside captured (decode-graph) launches; eager
+        # calls (prefill, first-use steps) take RCCL
+        self.oneshot_eager = os.environ.get("NLS_ONESHOT_EAGER", "1") == "1"
         self.stats = dict(all_reduce=0, all_reduce_bytes=0, ctrl=0, ctrl_s=0.0)
         self.ring = None             # shared-memory control ring (ranks on one host), else gloo broadcasts
         if self.size > 1 and os.environ.get("NLS_SHM_CTRL", "1") == "1":
@@ -50,10 +53,18 @@ class Comm:
                 self.ring = ShmCtrlRing(self.ctrl, self.rank, self.size)
 
     # ------------------------------------------------------------------ data plane
+    def _os(self, t: torch.Tensor):
+        """The one-shot engine for a call on `t`, or None (RCCL)."""
+        if self.oneshot is None or not t.is_cuda:
+            return None
+        if not self.oneshot_eager and not torch.cuda.is_current_stream_capturing():
+            return None
+        return self.oneshot
+
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
         self.stats["all_reduce"] += 1
         self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
-        if op == dist.ReduceOp.SUM and self.oneshot is not None and self.oneshot.eligible(t):
+        if op == dist.ReduceOp.SUM and self._os(t) is not None and self.oneshot.eligible(t):
             self.oneshot.all_reduce(t)
             return t
         dist.all_reduce(t, op=op, group=self.group)
@@ -90,8 +101,8 @@ class Comm:
         partials in rank order into the residual and writes the next RMSNorm (h) -- 2 launches per
         row-parallel projection instead of GEMV + all-reduce + norm. False: not applicable (caller
         falls back to row_parallel_add + rmsnorm)."""
-        os_ = self.oneshot
-        if os_ is None or not resid.is_cuda or not os_.addnorm_ok(T, resid.shape[1]):
+        os_ = self._os(resid)
+        if os_ is None or not os_.addnorm_ok(T, resid.shape[1]):
             return False
         ops.qgemv([Seg(w)], xin, part, T, alpha=alpha, epi="f32")
         self.stats["all_reduce"] += 1
@@ -101,7 +112,7 @@ class Comm:
 
     def vocab_parallel_argmax(self, keys: torch.Tensor, n: int, vocab_lo: int, next_ids: torch.Tensor):
         """Per-rank fused-argmax keys (value<<32 | ~local_idx) -> global greedy ids on every rank."""
-        if self.oneshot is not None and keys.is_cuda:
+        if self._os(keys) is not None:
             # one IPC launch: rebase, exchange, max, unpack and re-arm (no RCCL call in the decode graph)
             self.stats["all_reduce"] += 1
             self.stats["all_reduce_bytes"] += 8 * n
@@ -130,8 +141,8 @@ class Comm:
         every rank, in rank order = vocabulary order (ranks hold consecutive vocab shards). 8 bytes per
         candidate instead of 4 per vocabulary entry: C = 128 at TP=8 moves 8 KiB per sampled row, not 500 KiB."""
         n, C = vals.shape
-        os_ = self.oneshot
-        if os_ is not None and vals.is_cuda and os_.gather_ok(2 * n * C):
+        os_ = self._os(vals)
+        if os_ is not None and os_.gather_ok(2 * n * C):
             # lossless IPC all-gather of (values | ids) in one launch, rows already in vocabulary order
             self.stats["all_reduce"] += 1
             self.stats["all_reduce_bytes"] += 8 * n * C * self.size

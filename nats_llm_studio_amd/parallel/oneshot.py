@@ -55,8 +55,9 @@ class OneShotAllReduce:
             raise RuntimeError("one-shot all-reduce: IPC buffer setup failed on some rank")
         dev = comm.device
         self.device = dev
-        self.epochs = torch.zeros(L.nls_ar_blocks(), dtype=torch.int32, device=dev)
-        self.gepochs = torch.zeros(L.nls_ag_blocks(), dtype=torch.int32, device=dev)
+        # one epoch counter per slot block of the receive buffers (allreduce.hip SlotBlocks)
+        self.epochs = torch.zeros(L.nls_ar_epoch_slots(self.cap), dtype=torch.int32, device=dev)
+        self.gepochs = torch.zeros(L.nls_ag_epoch_slots(self.cap), dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._norm = {}               # D -> (epochs, tickets, ssq) of the fused add+norm
         self.resets = 0
@@ -135,11 +136,24 @@ class OneShotAllReduce:
         buffer sets (fused add+norm: first slice of each of the first `rows` rows) and the row tickets --
         compared across ranks, a divergence names the collective whose call counts differ."""
         torch.cuda.synchronize(self.device)
-        out = dict(ar=self.epochs[:8].tolist(), gather=self.gepochs.tolist())
+        out = dict(ar=self.epochs[:8].tolist(), gather=self.gepochs[:16].tolist())
         for D, (ep, tk, _sq) in self._norm.items():
             nblk = ep.numel() // tk.numel()
-            out[f"addnorm{D}"] = ep.view(-1, nblk)[:rows, 0].tolist()
+            e = ep.view(-1, nblk)[:rows]
+            out[f"addnorm{D}"] = e[:, 0].tolist()
+            # rows whose slices disagree with slice 0 (a workgroup that missed a call)
+            out[f"addnorm{D}_ragged"] = {int(r): e[r].tolist() for r in range(e.shape[0])
+                                         if int((e[r] != e[r, 0]).sum())}
             out[f"tickets{D}"] = tk[:rows].tolist()
+        L = _lib.lib()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        # per buffer set: [error, a, b, epoch, peer, first dword seen (tag = low 2 bits), marker, kernel]
+        # (add+norm: a row, b slice; the others: a granule, b granules of the call)
+        for name, buf in (("sum", self.buf), ("addnorm", self.nbuf), ("gather", self.gbuf)):
+            host = torch.zeros(8, dtype=torch.int32)
+            _lib.check(L.nls_ar_err_words(buf, self.cap, self.world, host.data_ptr(), 8, st), "nls_ar_err_words")
+            torch.cuda.synchronize(self.device)
+            out[f"timeout_{name}"] = host.tolist()
         return out
 
     def reset(self):
@@ -243,7 +257,7 @@ class SimulatedGroup:
             _lib.check(L.nls_ar_alloc(cap, world, ctypes.byref(b), None), "nls_ar_alloc")
             self.bufs.append(b.value)
         self.peers = (ctypes.c_void_p * world)(*self.bufs)
-        nb = L.nls_ar_blocks()
+        nb = L.nls_ar_epoch_slots(self.cap)
         self.epochs = [torch.zeros(nb, dtype=torch.int32, device=device) for _ in range(world)]
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.streams = [torch.cuda.Stream(device) for _ in range(world)]

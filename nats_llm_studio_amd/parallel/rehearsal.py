@@ -101,6 +101,24 @@ def _drive(eng, new_tokens: int, profile_steps: int = 0, greedy_only: bool = Fal
     wall = time.perf_counter() - t0
     out = dict(tokens=[f.result().token_ids for f in futs], steps=steps, wall_s=round(wall, 3),
                counters=dict(eng.counters), graphs=[list(k) for k in sorted(eng.graphs)])
+    if os.environ.get("NLS_REHEARSAL_WAVES", "0") == "1":
+        # batch-size churn: a wave whose requests end at different lengths (the decode batch shrinks through
+        # the graph buckets 8 -> 4 -> 2 -> 1), then a second wave joining (back up to 8): rows idle for many
+        # steps come back through other captured graphs
+        from ..engine.sampling import SamplingParams
+        waves = []
+        for w in range(2):
+            fs = [eng.submit(GenRequest(list(p) + [w + 3], SamplingParams(max_tokens=2 + 3 * j, ignore_eos=True)))
+                  for j, p in enumerate(PROMPTS + PROMPTS)]
+            waves.append(fs)
+            for _ in range(4 if w == 0 else 10 ** 6):
+                if all(f.done() for f in fs):
+                    break
+                eng.step()
+        while not all(f.done() for ws in waves for f in ws):
+            eng.step()
+        _sync(eng.dev)
+        out["waves_tokens"] = [[f.result().token_ids for f in ws] for ws in waves]
     if profile_steps:
         # a marker window for kernel traces: greedy-only decode steps after a host sync
         if os.environ.get("NLS_REHEARSAL_BARRIER", "0") == "1":
