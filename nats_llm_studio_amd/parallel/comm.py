@@ -39,9 +39,13 @@ class Comm:
         self.src = dist.get_global_rank(group, 0) if group is not None else 0
         self.device = torch.device(device) if device is not None else None
         self.oneshot = None          # optional small-message all-reduce (parallel/oneshot.py)
-        # NLS_ONESHOT_EAGER=0: the IPC one-shot kernels only inside captured (decode-graph) launches; eager
-        # calls (prefill, first-use steps) take RCCL
-        self.oneshot_eager = os.environ.get("NLS_ONESHOT_EAGER", "1") == "1"
+        # The IPC one-shot kernels run only inside captured (decode-graph) launches; eager calls (prefill
+        # chunks, capture warm-ups, first-use steps) take RCCL. Measured on one MI355X shared by two ranks
+        # (profiles/tp_oneshot_eager_r04.txt): eager one-shot calls interleaved with graph replays timed out
+        # waiting for a granule the peer had pushed (any buffer kind, with or without per-poll invalidate),
+        # while graph-only one-shot traffic -- also across bucket changes -- never did. NLS_ONESHOT_EAGER=1
+        # restores eager one-shot calls.
+        self.oneshot_eager = os.environ.get("NLS_ONESHOT_EAGER", "0") == "1"
         self.stats = dict(all_reduce=0, all_reduce_bytes=0, ctrl=0, ctrl_s=0.0)
         self.ring = None             # shared-memory control ring (ranks on one host), else gloo broadcasts
         if self.size > 1 and os.environ.get("NLS_SHM_CTRL", "1") == "1":

@@ -40,18 +40,26 @@ def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep):
 
 @pytest.mark.parametrize("name,ep", [("llama-3-70b-2layer", False), ("mixtral-8x7b-1layer", True)])
 def test_tp2_greedy_prefill_after_graph_replays(gpu, models, name, ep):
-    """Greedy-only batches (every step on the vocab-parallel arg-max), then a second round of requests: its
-    eager prefill runs the fused add+norm one-shot on more rows than the replayed decode graphs did (the
-    consumer used to re-tag its own receive slots and read such a rewrite back here; round-4 regression).
-    Mixtral EP also runs the plain one-shot all-reduce of the expert outputs."""
+    """Greedy-only batches (every step on the vocab-parallel arg-max), waves of requests that end at different
+    lengths (the decode batch walks down and back up the graph buckets, rows idle for many steps return),
+    then a second round of requests whose eager prefill follows the graph replays (eager one-shot calls timed
+    out here on a shared GPU; eager collectives now take RCCL / gloo: round-4 regression). Mixtral EP also
+    runs the plain one-shot all-reduce of the expert outputs."""
     from nats_llm_studio_amd.parallel import rehearsal
-    r = rehearsal.run(models[name], world=2, ep=ep, new_tokens=8, timeout=300, greedy_only=True, profile_steps=4)
+    import os
+    os.environ["NLS_REHEARSAL_WAVES"] = "1"      # + batch churn through the graph buckets (spawned ranks inherit)
+    try:
+        r = rehearsal.run(models[name], world=2, ep=ep, new_tokens=8, timeout=300, greedy_only=True,
+                          profile_steps=4)
+    finally:
+        os.environ.pop("NLS_REHEARSAL_WAVES", None)
     ref, tp, fol = r["ref"], r["tp"], r["followers"][0]
     for v in (ref, tp, fol):
         assert "exception" not in v, v
     assert tp["oneshot_resets"] == 0
     assert tp["counters"]["graph_replays"] > 0
     assert tp["tokens"] == ref["tokens"], (tp["tokens"], ref["tokens"])
+    assert tp["waves_tokens"] == ref["waves_tokens"]
 
 
 def test_sample_decode_cand_matches_cpu_twin(gpu):

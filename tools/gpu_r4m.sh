@@ -14,4 +14,14 @@ done
 step b1_w8 120 python3 -u bench.py --concurrency 1 --steps 100 --warmup 10 --serve-load 0 --no-rtt --tp-leg 0
 step b1_w4 120 env NLS_ATTN_MFMA_WAVES=4 python3 -u bench.py --concurrency 1 --steps 100 --warmup 10 --serve-load 0 --no-rtt --tp-leg 0
 grep -h '^{' gpurun_out/b1_w8.log gpurun_out/b1_w4.log | cut -c1-160
+# quantised large-M (no f16 copies): mode 9 among the candidates, then B=512 without the copies, old vs new table
+step tune_q 600 python3 -u tools/tune_gemv.py --model llama-3-8b --ms 256,512 --out gpurun_out/tune_q8b.json --log gpurun_out/tune_q8b.log
+python3 - > gpurun_out/tune_q8b_extra.json <<'PY'
+import json
+t = json.load(open("gpurun_out/tune_q8b.json"))
+print(json.dumps({k: v for k, v in t.items() if not k.startswith("d:") and k.split(":")[-1] in ("256", "512")}))
+PY
+step b512_q_old 300 env NLS_DENSE_WEIGHTS=0 python3 -u bench.py --steps 20 --warmup 5 --serve-load 0 --no-rtt --tp-leg 0
+step b512_q_new 300 env NLS_DENSE_WEIGHTS=0 NLS_TUNING_EXTRA="$(cat gpurun_out/tune_q8b_extra.json)" python3 -u bench.py --steps 20 --warmup 5 --serve-load 0 --no-rtt --tp-leg 0
+grep -h '^{' gpurun_out/b512_q_old.log gpurun_out/b512_q_new.log | cut -c1-200
 exit $STEPS_RC
