@@ -207,8 +207,15 @@ def test_rehearsal_driver_cpu(tmp_path):
     c = r["tp"]["counters"]
     assert c["device_sampled_steps"] > 0 and c["candidate_sampled_steps"] == 0, c
     assert r["followers"][0]["counters"]["device_sampled_steps"] == c["device_sampled_steps"]
-    # greedy-only batches: every step on the vocab-parallel arg-max, plus the post-run marker window
-    g = rehearsal.run(path, world=2, new_tokens=5, timeout=240, device="cpu", greedy_only=True, profile_steps=3)
+    # greedy-only batches: every step on the vocab-parallel arg-max, batch churn (waves of requests ending at
+    # different lengths), plus the post-run marker window
+    import os
+    os.environ["NLS_REHEARSAL_WAVES"] = "1"
+    try:
+        g = rehearsal.run(path, world=2, new_tokens=5, timeout=240, device="cpu", greedy_only=True, profile_steps=3)
+    finally:
+        os.environ.pop("NLS_REHEARSAL_WAVES", None)
     assert "exception" not in g["tp"], g["tp"]
     assert g["tp"]["tokens"] == g["ref"]["tokens"] == r["ref"]["tokens"][:len(rehearsal.PROMPTS)]
+    assert g["tp"]["waves_tokens"] == g["ref"]["waves_tokens"]
     assert g["tp"]["counters"]["device_sampled_steps"] == 0
