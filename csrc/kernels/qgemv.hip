@@ -102,7 +102,9 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     for (int i = 1; i < nseg; ++i)
       if (segs[i].rows != segs[0].rows || segs[i].K != segs[0].K) return -1;
   }
-  if (nseg < 1 || nseg > 8 || M < 1 || (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4))) return -1;
+  if (nseg < 1 || nseg > 8 || M < 1 ||
+      (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
+    return -1;
   if (mode < 0 || mode > 10 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
   if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||

@@ -1180,9 +1180,13 @@ int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a
     }
   }
   if (a.xf) return -1;          // fused input norm: the staged (XL) path only
-  hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, KSET>), dim3(grid), dim3(WAVES * 64), lds, st, sl, a, ks, ws,
-                     ntiles, nmb);
-  return (int)hipGetLastError();
+  if constexpr (WAVES == 7) {   // (the 7-wave instance exists for the staged batch-1 path only)
+    return -1;
+  } else {
+    hipLaunchKernelGGL((qmm_kernel<WAVES, RT, MT, KSET>), dim3(grid), dim3(WAVES * 64), lds, st, sl, a, ks, ws,
+                       ntiles, nmb);
+    return (int)hipGetLastError();
+  }
 }
 
 template <int WAVES, int RT, int KSET>
@@ -1202,6 +1206,9 @@ template <int KSET>
 int launch_kset(int mode, int waves, int rt, int mt, const SegList& sl, int tiles, int ks, float* ws,
                 const GemvArgs& a, hipStream_t st, int nmb) {
   if (mode == 1) {
+    // 7 waves x one 16-row tile (112 rows per workgroup): 28672 gate|up rows = 256 workgroups, one per CU
+    // (4 waves x 2 tiles leave 32 CUs idle at 224); batch-1 staged (XL) launches only
+    if (waves == 7) return rt == 1 && mt == 1 ? launch_b<7, 1, 1, KSET>(sl, tiles, ks, ws, a, st, nmb) : -1;
     if (waves == 8) return rt == 1 ? launch_b_mt<8, 1, KSET>(mt, sl, tiles, ks, ws, a, st, nmb)
                                    : launch_b_mt<8, 2, KSET>(mt, sl, tiles, ks, ws, a, st, nmb);
     return rt == 1 ? launch_b_mt<4, 1, KSET>(mt, sl, tiles, ks, ws, a, st, nmb)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4, call N (= O): the whole GPU suite at the head, the smoke entry point, the default bench (the driver's
+# round 4, call O: the whole GPU suite at the head, the smoke entry point, the default bench (the driver's
 # 20-step form and the sustained 200 steps with the service load)
 source tools/gpu_steps.sh
 step gpu_suite 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider

@@ -64,6 +64,7 @@ def main():
     rng = np.random.default_rng(0)
     sweep = "--sweep" in sys.argv
     only = sys.argv[sys.argv.index("--shape") + 1] if "--shape" in sys.argv else None
+    cfgs = [tuple(c) for c in json.loads(sys.argv[sys.argv.index("--cfgs") + 1])] if "--cfgs" in sys.argv else None
     for name, types, rows, K in SHAPES:
         if (sweep and name not in ("gateup", "down")) or (only and name != only):
             continue
@@ -73,7 +74,7 @@ def main():
         x = torch.zeros(64, K, dtype=ops.ACT_DTYPE, device="cuda")
         x[0] = torch.randn(K, device="cuda").to(ops.ACT_DTYPE)
         y = torch.zeros(64, rows, device="cuda")
-        for cfg in (CFGS if sweep else [tuning.select(segs, 1)]):
+        for cfg in (cfgs or (CFGS if sweep else [tuning.select(segs, 1)])):
             mode, waves, rt, ks = cfg
             run = lambda c: ops.qgemv(c, x, y, 1, mode=mode, waves=waves, rt=rt, ks=ks)
             try:
