@@ -671,7 +671,7 @@ __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArg
 // ===========================================================================
 constexpr size_t XL_LDS_BYTES = 48 * 1024;    // path-B XL: largest staged x slice
 #ifndef NLS_XL_DEPTH
-#define NLS_XL_DEPTH 8
+#define NLS_XL_DEPTH 2
 #endif
 constexpr int XL_DEPTH = NLS_XL_DEPTH;         // path-B XL: weight super-blocks in flight per wave
 #ifndef NLS_XL_DEPTH2
