@@ -2,7 +2,7 @@
 //
 //   y[m, n] (epilogue) alpha * sum_k x[m, k] * W[n, k]      x f16 [M, K], W K-quant tile-blocks (common.h)
 //
-// Why (tools/hg8_probe.hip on the 8B gate|up at 512 rows, profiles/gemm_probes_r03.txt): the dense f16
+// Why (the round-3 probes on the 8B gate|up at 512 rows, profiles/gemm_probes_r03.txt): the dense f16
 // kernel of mode 8 takes 105 us, 99 us of it with the MFMAs switched off -- it is bound by what one CU
 // pulls into LDS (~41 GB/s per CU at full load: 256 activation rows + 224 f16 weight rows per 32-deep
 // K-step = 30 KiB). A 256 x 256 tile that streams the RAW Q4_K tile-blocks instead takes 16 + 4.5 KiB per
@@ -31,7 +31,7 @@
 // on ONE XCD (the tile's HBM bytes are fetched once per XCD L2).
 #include "qgemm_dma.h"
 
-// tools/hg8_probe.hip builds speed-of-light variants: bit 0 = no MFMA (fragments still read), bit 1 = no
+// H9_PROBE builds speed-of-light variants (the round-3 probe harness): bit 0 = no MFMA (fragments still read), bit 1 = no
 // DMA, bit 2 = no vmcnt waits, bit 3 = no dequantisation (raw bits as fragments). 0 in the library.
 #ifndef H9_PROBE
 #define H9_PROBE 0

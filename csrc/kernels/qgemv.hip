@@ -9,9 +9,6 @@ namespace nls_hgemm {
 int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
                  const GemvArgs& a, hipStream_t st);
 }
-namespace nls_hg8 {
-int launch_dense8(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
-}
 namespace nls_hg10 {
 int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
 }
@@ -56,9 +53,6 @@ struct NlsFuse {
 //         blocks, 2: 128-row), optional split-K as mode 1.
 // mode 5: mode 4 with 256-row weight tiles (twice the MFMA work per fetched activation byte).
 // mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
-// mode 8: dense f16 GEMM with a 5-deep 32-k stage ring and register-double-buffered fragments
-//         (hgemm8.hip): 256-row activation blocks x 32*rt weight rows (rt 8: 256, 7: 224, 4: 128),
-//         plain rows only (no row maps), optional split-K as mode 1.
 // mode 10: dense f16 GEMM, 256 x 256 tiles, 4 phases per 64-deep K-tile with the two wave groups staggered
 //         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
 // mode 9: quantised GEMM on the raw tile-blocks (qgemm9.hip; Q4_K/Q5_K/Q6_K/Q8_0/Q51): 256-row activation
@@ -105,7 +99,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 10 || mode == 7 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
   if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
@@ -118,12 +112,6 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
-  } else if (mode == 8) {
-    if (waves != 8 || (rt != 8 && rt != 7 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE || ldx % 8 ||
-        ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
-      return -1;
-    for (int i = 0; i < nseg; ++i)
-      if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
   } else if (mode >= 4 && mode <= 6) {
     if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || (epi == EPI_ROPE && mode == 6))
       return -1;
@@ -143,7 +131,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : mode == 8 ? 32 * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -246,8 +234,6 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st);
-    else if (mode == 8)
-      rc = nls_hg8::launch_dense8(32 * rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode >= 4)
       rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : 3, sl, tiles, ks, (float*)ws, a,
                                    st);

@@ -446,9 +446,15 @@ class Engine:
         self._admit()
         t1 = clk()
         hm["schedule"] += (t1 - t0) * 1e3
-        if any(s.n_prefilled < s.n_target for s in self.running):
-            # the prefill chunk is queued behind the in-flight decode step (separate step buffers) and
-            # the next decode step still chains on that step's device-side tokens: no pipeline drain
+        # the prefill chunk is queued behind the in-flight decode step (separate step buffers) and the next
+        # decode step still chains on that step's device-side tokens: no pipeline drain. With a deep prompt
+        # backlog (a burst of arrivals) up to PREFILL_CHUNKS chunks run before the next decode step: fewer
+        # small decode steps while the batch ramps up, earlier first tokens (NLS_PREFILL_CHUNKS)
+        for c in range(self.PREFILL_CHUNKS):
+            if not any(s.n_prefilled < s.n_target for s in self.running):
+                break
+            if c:
+                self._admit()
             self._prefill()
         t2 = clk()
         hm["prefill"] += (t2 - t1) * 1e3
@@ -600,6 +606,7 @@ class Engine:
         self._gather(b, n, need_logits)
 
     CAND = 128           # TP sampling: candidates per rank and row
+    PREFILL_CHUNKS = int(os.environ.get("NLS_PREFILL_CHUNKS", "1"))   # prefill chunks per step (backlog)
     PRESSURE_STEPS = 64  # preemption hysteresis window (steps), see _pressure_until
 
     def _cand_ok(self, seqs) -> bool:

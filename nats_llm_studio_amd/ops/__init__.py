@@ -281,7 +281,7 @@ def _seg_arr(segs: Sequence[Seg], mode: int):
     included: the dense GEMM gathers/scatters mapped rows like mode 2)."""
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
-        if mode in (4, 5, 6, 8, 10):
+        if mode in (4, 5, 6, 10):
             if s.w.d16 is None:
                 raise ValueError(f"{s.w.name}: dense modes (4-6, 8, 10) need QWeight.expand_dense()")
             arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, s.w.rows, s.w.K,
