@@ -606,7 +606,7 @@ class Engine:
         self._gather(b, n, need_logits)
 
     CAND = 128           # TP sampling: candidates per rank and row
-    PREFILL_CHUNKS = int(os.environ.get("NLS_PREFILL_CHUNKS", "1"))   # prefill chunks per step (backlog)
+    PREFILL_CHUNKS = int(os.environ.get("NLS_PREFILL_CHUNKS", "4"))   # prefill chunks per step (backlog)
     PRESSURE_STEPS = 64  # preemption hysteresis window (steps), see _pressure_until
 
     def _cand_ok(self, seqs) -> bool:
