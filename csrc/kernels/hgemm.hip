@@ -326,9 +326,6 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
   NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
   NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
   NLS_HG(2, 128, 8, 2)
-  // 4 waves (one per SIMD), 64 x 64 accumulator tile per wave: 0.5 fragment reads per MFMA (the 8- and
-  // 16-wave tiles read 0.75 / 1.25) for the narrow-N projections at 256-512 rows
-  NLS_HG(2, 128, 4, 3) NLS_HG(2, 128, 4, 2) NLS_HG(2, 256, 4, 3)
 #undef NLS_HG
   return -1;
 }

@@ -99,7 +99,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && ((waves != 8 && waves != 4) || rt != 2))) return -1;
+  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
   if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
@@ -113,7 +113,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     for (int i = 0; i < nseg; ++i)
       if (segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
   } else if (mode >= 4 && mode <= 6) {
-    if ((waves != 4 && waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || (epi == EPI_ROPE && mode == 6))
+    if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || (epi == EPI_ROPE && mode == 6))
       return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16) return -1;

@@ -56,6 +56,10 @@ _MOE_GEMV_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_GEMV_DN", "").split
 # MoE expert GEMMs on the experts' f16 copies: (mode, waves, rt[, ks]) of gate/up and down
 _MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2").split(","))
 _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
+# expert parallelism: eager steps of >= NLS_EP_A2A_T tokens dispatch / combine over all-to-all (LlamaModel._moe_a2a);
+# NLS_EP_A2A=0 keeps the combine-then-all-reduce everywhere
+_EP_A2A = os.environ.get("NLS_EP_A2A", "1")
+_EP_A2A_T = int(os.environ.get("NLS_EP_A2A_T", "64"))
 
 
 # device buffers superseded by larger ones; captured hipGraphs may still point at them
@@ -531,12 +535,106 @@ class LlamaModel:
         else:
             self.comm.row_parallel_add(w, xin, resid, T, alpha)
 
+    @staticmethod
+    def _moe_gemm_cfg(lw: LayerWeights, rows: int, n_exp: int):
+        """Launch configs (gate/up, down, down split-K) of the grouped expert GEMMs for `rows` routed rows
+        over `n_exp` experts."""
+        if all(w.d16 is not None for w in lw.exp_gateup + lw.exp_down):
+            # f16 expert copies (expand_dense tier 2): the dense DMA GEMM, bandwidth- rather than
+            # dequant-bound at ~64 rows per expert (NLS_MOE_DENSE_GU/_DN = mode,waves,rt)
+            gu = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_GU[:3]), ks=1)
+            dn = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_DN[:3]), ks=1)
+            return gu, dn, (_MOE_DENSE_DN[3] if len(_MOE_DENSE_DN) > 3 else 1)
+        # few routed rows per expert: 128-row blocks (64 KiB of LDS, two workgroups per CU hide each
+        # other's dequant/barrier waits; Mixtral B=64: 13.8 vs 15.2 ms/step), else 256-row blocks
+        rt = 2 if rows < 32 * n_exp else 4
+        gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", rt)), ks=1)
+        dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", rt)), ks=1)
+        if os.environ.get("NLS_MOE_QCFG_GU"):      # explicit (mode, waves, rt) overrides
+            gu = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_GU"].split(","))), ks=1)
+        if os.environ.get("NLS_MOE_QCFG_DN"):
+            dn = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_DN"].split(","))), ks=1)
+        return gu, dn, int(os.environ.get("NLS_MOE_KS_DN", "1"))
+
+    def _ep_a2a(self, T: int) -> bool:
+        """Take the all-to-all dispatch / combine (_moe_a2a) for this MoE step? Eager EP steps of
+        >= NLS_EP_A2A_T tokens (prefill chunks, large eager batches); captured decode graphs keep the
+        host-sync-free combine-then-all-reduce (the all-to-all needs its split sizes on the host)."""
+        if not self.ep or _EP_A2A == "0" or T < _EP_A2A_T:
+            return False
+        if self.device.type == "cuda":
+            # grouped-GEMM path only (the path-A GEMVs take <= 64 rows) and never inside a capture
+            return T > _MOE_GEMM_T and not torch.cuda.is_current_stream_capturing()
+        return True
+
+    def _moe_a2a(self, lw: LayerWeights, b: StepBuffers, T: int) -> bool:
+        """Expert parallelism as dispatch / combine over all-to-all (BASELINE config 5, "expert all-to-all on
+        xGMI"). Rank r routes its 1/W slice of the (replicated) tokens, sends each (token, slot) row to the rank
+        owning that slot's expert (RCCL all-to-all: each pair of ranks exchanges only its own rows on its own
+        xGMI link), runs its local experts as ONE grouped GEMM over the rows it received, sends the expert
+        outputs back (all-to-all), combines its slice's k slots in slot order -- the single-GPU combine, so the
+        result does not depend on the rank count -- and all-gathers the residual slices. Per rank and layer:
+        (T/W) k d (2 + 4) bytes each way plus the f32 residual all-gather, against the 2 T d 4 (W-1)/W of the
+        combine-then-all-reduce path (profiles/ep_alltoall_model_r04.md)."""
+        cfg, m, comm = self.cfg, b.moe, self.comm
+        k, d = cfg.n_expert_used, cfg.d_model
+        W, r = self.shard.size, self.shard.rank
+        per, e0 = len(self.experts), self.experts[0]
+        cap = b.x.shape[0]
+        ts = -(-T // W)                                   # tokens per rank slice
+        t0 = min(T, r * ts)
+        n = min(T, t0 + ts) - t0
+        sel = m["sel"]
+        if n:
+            ops.qgemv([Seg(lw.router)], b.h[t0:], m["rlogits"], n)
+            ops.moe_route(m["rlogits"], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap, sel=sel)
+        # dispatch: the slice's (token, slot) rows grouped by the rank owning the slot's expert
+        eid = sel[:n * k].long()
+        dest = torch.div(eid, per, rounding_mode="floor")
+        order = torch.argsort(dest, stable=True)
+        send = torch.bincount(dest, minlength=W).tolist()
+        recv = comm.exchange_counts(send)
+        nr = sum(recv)
+        xr = comm.all_to_all_rows(b.h[t0:t0 + n].index_select(0, torch.div(order, k, rounding_mode="floor")),
+                                  send, recv)
+        er = comm.all_to_all_rows(eid.index_select(0, order).to(torch.int32), send, recv).long() - e0
+        # local experts' row lists over the received rows (expert i: rows[i * cap:], counts[i]); the GEMMs
+        # gather their inputs and place their outputs by the same received-row index
+        o2 = torch.argsort(er, stable=True)
+        cnt = torch.bincount(er, minlength=per)
+        le = er.index_select(0, o2)
+        pos = torch.arange(nr, device=er.device) - (torch.cumsum(cnt, 0) - cnt).index_select(0, le)
+        rows, counts = m["xrows"], m["counts"]
+        rows[le * cap + pos] = o2.to(torch.int32)
+        counts[:per] = cnt.to(torch.int32)
+        if nr:
+            gu, dn, _ = self._moe_gemm_cfg(lw, nr, per) if self.device.type == "cuda" else ({}, {}, 1)
+            M = min(nr, T)                                # an expert gets each token at most once
+            segs = [Seg(w, 0, rows[i * cap:], rows[i * cap:], counts[i:i + 1]) for i, w in enumerate(lw.exp_gateup)]
+            for s0 in range(0, per, 8):
+                ops.qgemv(segs[s0:s0 + 8], xr, b.act, M, epi="swiglu", **gu)
+            segs = [Seg(w, 0, rows[i * cap:], rows[i * cap:], counts[i:i + 1]) for i, w in enumerate(lw.exp_down)]
+            for s0 in range(0, per, 8):
+                ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], M, epi="f32", **dn)
+        # combine: the outputs return to the slice's rank in dispatch order -> slot order -> weighted sum
+        yb = comm.all_to_all_rows(m["yexp"][:nr], recv, send)
+        ys = torch.empty_like(yb)
+        ys.index_copy_(0, order, yb)
+        blk = b.x.new_zeros(ts, d)
+        if n:
+            ops.moe_combine(ys, m["topw"], n, k, b.x[t0:t0 + n], cfg.residual_scale)
+            blk[:n] = b.x[t0:t0 + n]
+        b.x[:T] = comm.all_gather_rows(blk)[:T]
+        return False
+
     def _moe(self, lw: LayerWeights, b: StepBuffers, T: int, next_norm: Optional[torch.Tensor] = None,
              in_norm: Optional[torch.Tensor] = None, routed: bool = False) -> bool:
         """Top-k routed experts: router GEMV -> route kernel (per-expert row lists on device)
         -> grouped expert GEMVs (tiles of experts with no routed rows exit before reading
         weights) -> deterministic weighted combine into the residual. `in_norm` (<= 4 tokens): b.h is
         not normalised yet; the FFN input RMSNorm, the router and the route run as ONE launch."""
+        if in_norm is None and not routed and self._ep_a2a(T):
+            return self._moe_a2a(lw, b, T)
         cfg = self.cfg
         normed = False
         m = b.moe
@@ -566,24 +664,8 @@ class LlamaModel:
         if not gemm and len(_MOE_GEMV_DN) == 4:
             dn = dict(zip(("mode", "waves", "rt", "ks"), _MOE_GEMV_DN))
         dn_rows = T
-        if gemm and all(w.d16 is not None for w in lw.exp_gateup + lw.exp_down):
-            # f16 expert copies (expand_dense tier 2): the dense DMA GEMM, bandwidth- rather than
-            # dequant-bound at ~64 rows per expert (NLS_MOE_DENSE_GU/_DN = mode,waves,rt)
-            gu = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_GU[:3]), ks=1)
-            dn = dict(zip(("mode", "waves", "rt"), _MOE_DENSE_DN[:3]), ks=1)
-            kdn = _MOE_DENSE_DN[3] if len(_MOE_DENSE_DN) > 3 else 1
-        elif gemm:
-            # few routed rows per expert: 128-row blocks (64 KiB of LDS, two workgroups per CU hide each
-            # other's dequant/barrier waits; Mixtral B=64: 13.8 vs 15.2 ms/step), else 256-row blocks
-            rt = 2 if T * k < 32 * E else 4
-            gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", rt)), ks=1)
-            dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", rt)), ks=1)
-            if os.environ.get("NLS_MOE_QCFG_GU"):      # explicit (mode, waves, rt) overrides
-                gu = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_GU"].split(","))), ks=1)
-            if os.environ.get("NLS_MOE_QCFG_DN"):
-                dn = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_DN"].split(","))), ks=1)
-            kdn = int(os.environ.get("NLS_MOE_KS_DN", "1"))
         if gemm:
+            gu, dn, kdn = self._moe_gemm_cfg(lw, T * k, E)
             # down projection (K = d_ff): split K over workgroups when ONE launch covers every routed row
             # (<= 8 local experts, no EP: every y row written by exactly one expert in every K slice);
             # the slabs are indexed by the y row, so that launch's M is the T*k output rows

@@ -163,6 +163,41 @@ class Comm:
         return (ov.view(self.size, n, C).permute(1, 0, 2).reshape(n, self.size * C),
                 oi.view(self.size, n, C).permute(1, 0, 2).reshape(n, self.size * C))
 
+    # ------------------------------------------------------------------ expert-parallel dispatch / combine
+    def _staged(self, t: torch.Tensor) -> bool:
+        """gloo moves host tensors only for all-to-all (the 1-GPU rehearsal's data group): stage through host."""
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
+    def exchange_counts(self, send: list) -> list:
+        """send[r] = rows this rank sends to rank r -> recv[r] = rows rank r sends here (one int64 all-to-all)."""
+        dev = self.device if (self.device is not None and self.device.type == "cuda"
+                              and dist.get_backend(self.group) != "gloo") else torch.device("cpu")
+        c = torch.tensor(send, dtype=torch.int64, device=dev)
+        o = torch.empty_like(c)
+        dist.all_to_all_single(o, c, group=self.group)
+        return o.tolist()
+
+    def all_to_all_rows(self, t: torch.Tensor, send: list, recv: list) -> torch.Tensor:
+        """Rows of `t` grouped by destination (send[r] rows for rank r, in rank order) -> the rows every rank
+        sent here, grouped by source rank (recv[r] rows from rank r). RCCL all-to-all over xGMI: each pair of
+        ranks exchanges only its own rows on its own link."""
+        staged = self._staged(t)
+        src = (t.cpu() if staged else t).contiguous()
+        out = src.new_empty((sum(recv),) + tuple(t.shape[1:]))
+        dist.all_to_all_single(out, src, recv, send, group=self.group)
+        self.stats["all_to_all"] = self.stats.get("all_to_all", 0) + 1
+        self.stats["all_to_all_bytes"] = self.stats.get("all_to_all_bytes", 0) + src.numel() * src.element_size()
+        return out.to(t.device) if staged else out
+
+    def all_gather_rows(self, rows: torch.Tensor) -> torch.Tensor:
+        """Equal-size row blocks [n, ...] of every rank -> [size * n, ...] in rank order."""
+        staged = self._staged(rows)
+        src = (rows.cpu() if staged else rows).contiguous()
+        out = src.new_empty((self.size * src.shape[0],) + tuple(src.shape[1:]))
+        dist.all_gather_into_tensor(out, src, group=self.group)
+        self.stats["all_gather"] = self.stats.get("all_gather", 0) + 1
+        return out.to(rows.device) if staged else out
+
     # ------------------------------------------------------------------ control plane
     def bcast_ctrl(self, t: torch.Tensor):
         """Host int32 tensor from rank 0 to all ranks: the shared-memory ring when every rank of the

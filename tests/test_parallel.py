@@ -77,16 +77,22 @@ def _worker(rank, world, port, path, ep, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
+    from nats_llm_studio_amd.models import llama
     from nats_llm_studio_amd.models.llama import ShardSpec
+    if ep == "a2a":
+        # every EP step (prefill of two prompts and decode) dispatches / combines over all-to-all
+        llama._EP_A2A, llama._EP_A2A_T = "1", 1
+    elif ep:
+        llama._EP_A2A = "0"
     from nats_llm_studio_amd.parallel.comm import init_distributed
     import torch.distributed as dist
     comm = init_distributed("cpu")
     try:
-        eng = _engine(path, ShardSpec(rank, world, ep), comm)
+        eng = _engine(path, ShardSpec(rank, world, bool(ep)), comm)
         if rank == 0:
             toks, lg = _run(eng)
             eng.stop_followers()
-            out.put((toks, lg.numpy(), comm.stats["all_reduce"], dict(eng.counters)))
+            out.put((toks, lg.numpy(), comm.stats["all_reduce"], dict(eng.counters, all_to_all=comm.stats.get("all_to_all", 0))))
         else:
             eng.follow()
     finally:
@@ -94,7 +100,7 @@ def _worker(rank, world, port, path, ep, out):
 
 
 @pytest.mark.parametrize("fam,ep", [("llama", False), ("granite", False), ("mixtral", False), ("mixtral", True),
-                                    ("qwen2", False)])
+                                    ("mixtral", "a2a"), ("qwen2", False)])
 def test_tp2_matches_tp1(tmp_path, fam, ep):
     spec = _TP_SPECS[fam]
     path = str(tmp_path / f"{spec.name}.gguf")
@@ -124,6 +130,7 @@ def test_tp2_matches_tp1(tmp_path, fam, ep):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     assert n_ar > 0
+    assert (ctr["all_to_all"] > 0) == (ep == "a2a"), ctr
     # the top-k requests' decode steps drew from the gathered candidates INSIDE the step (in-graph sampler,
     # chained decode); only their first tokens (after prefill) were drawn on the host
     assert ctr["device_sampled_steps"] > 0, ctr

@@ -70,12 +70,17 @@ def _worker(rank, world, port, path, ep, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
+    from nats_llm_studio_amd.models import llama
     from nats_llm_studio_amd.models.llama import ShardSpec
     from nats_llm_studio_amd.parallel.comm import init_distributed
     import torch.distributed as dist
+    if ep == "a2a":     # every step dispatches / combines over all-to-all (slices of 2 / 1 / 0 tokens per rank)
+        llama._EP_A2A, llama._EP_A2A_T = "1", 1
+    elif ep:
+        llama._EP_A2A = "0"
     comm = init_distributed("cpu")
     try:
-        eng = _engine(path, ShardSpec(rank, world, ep), comm)
+        eng = _engine(path, ShardSpec(rank, world, bool(ep)), comm)
         m = eng.model
         shapes = dict(Hq=m.Hq, Hkv=m.Hkv, ffn=m.ffn, experts=list(m.experts), vocab=m.vocab_hi - m.vocab_lo)
         if rank == 0:
@@ -147,11 +152,14 @@ def test_llama70b_shapes_tp(l70, world):
     assert stats["all_reduce"] > 0 and stats["all_reduce_bytes"] >= 2 * 8192 * 4
 
 
-def test_mixtral_shapes_ep8(tmp_path):
+@pytest.mark.parametrize("mode", ["allreduce", "a2a"])
+def test_mixtral_shapes_ep8(tmp_path, mode):
+    """EP=8 both ways: combine-then-all-reduce, and dispatch / combine over all-to-all (LlamaModel._moe_a2a)."""
     path = str(tmp_path / "ep-mixtral-1layer.gguf")
     write_synthetic_gguf(path, MIX.name, "Q4_K_M", seed=4, spec=MIX)
     ref = _run(_engine(path))
-    res = _tp(path, 8, ep=True)
-    _check(res, ref, MIX.vocab)
+    res = _tp(path, 8, ep="a2a" if mode == "a2a" else True)
+    stats = _check(res, ref, MIX.vocab)
+    assert (stats.get("all_to_all", 0) > 0) == (mode == "a2a"), stats
     assert [res[r][4]["experts"] for r in range(8)] == [[r] for r in range(8)]
     assert all(res[r][4]["Hkv"] == 1 for r in range(8))

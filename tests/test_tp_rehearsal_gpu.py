@@ -99,3 +99,22 @@ def test_sample_decode_cand_matches_cpu_twin(gpu):
     assert d["o"].cpu().tolist() == cpu["o"].tolist()
     assert torch.equal(d["h"].cpu(), cpu["h"])
     assert int(d["o"][2]) == 7                                         # greedy row left alone
+
+
+def test_ep2_alltoall_prefill_matches_tp1(gpu, models):
+    """Mixtral EP=2 with the all-to-all dispatch / combine (LlamaModel._moe_a2a) on every eager step of >= 17
+    tokens -- the prefill of the rehearsal's prompts -- through the grouped expert GEMM over the received rows;
+    decode graphs keep the combine-then-all-reduce. Tokens must equal TP=1."""
+    from nats_llm_studio_amd.parallel import rehearsal
+    import os
+    os.environ["NLS_EP_A2A_T"] = "17"            # (spawned ranks inherit)
+    try:
+        r = rehearsal.run(models["mixtral-8x7b-1layer"], world=2, ep=True, new_tokens=8, timeout=300)
+    finally:
+        os.environ.pop("NLS_EP_A2A_T", None)
+    ref, tp, fol = r["ref"], r["tp"], r["followers"][0]
+    for v in (ref, tp, fol):
+        assert "exception" not in v, v
+    assert tp["comm"].get("all_to_all", 0) > 0, tp["comm"]
+    assert tp["counters"]["graph_replays"] > 0
+    assert tp["tokens"] == ref["tokens"], (tp["tokens"], ref["tokens"])

@@ -66,9 +66,6 @@ def candidates(M, K, epi):
             for wm in ((2, 4) if M >= 192 else (2,)):
                 for ks in (1, 2, 4):
                     out.append((mode, waves, wm, ks))
-    # 4 waves x 64 x 64 per wave (0.5 fragment reads per MFMA): 128 x 128 (mode 4, 3-deep rings; mode 6,
-    # 2-deep: two workgroups per CU) and 128 x 256 (mode 5) tiles
-    out += [(m, 4, 2, ks) for m in (4, 5, 6) for ks in (1, 2, 3, 4)]
     if epi == "argmax":
         out = [c for c in out if c[3] == 1]
     nkt = K // 64
