@@ -391,15 +391,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   const int wave = WAVES == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* Vs = Vsm + wave * KG * D * 2;
   const int Hq = Hkv * G;
-  // one-token launches (batch-1 decode, where this dependent chain is the kernel's latency): split 0 starts
-  // at block 0 whatever the context, so its first block-table window (row 0 = the token's sequence in
-  // decode steps, checked below) is fetched together with the context length and the token -> sequence row
-  // instead of after them -- one dependent global load fewer ahead of the first K/V loads
-  const bool spec = split == 0 && gridDim.x == 1;
-  int btspec = 0;
-  if (spec && lane < bt_stride) btspec = block_tables[lane];
   const int ctx = ctx_len[t];
-  const int sq = tok_seq[t];
   // short contexts: at least one 32-key group per wave of the workgroup per split (>= 64 keys)
   chunk = split_chunk(chunk, ctx, n_split, bs, KG * WAVES > 64 ? KG * WAVES : 64);
   const int start = split * chunk;
@@ -408,7 +400,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   // active splits: with ONE (short context) the split writes the output itself -- no partials, no ticket
   const int na = ctx > 0 ? min(n_split, (ctx + chunk - 1) / chunk) : n_split;
   const bool direct = n_split == 1 || (na == 1 && cnt);
-  const int* bt = block_tables + (size_t)sq * bt_stride;
+  const int* bt = block_tables + (size_t)tok_seq[t] * bt_stride;
   const float sl2 = scale * LOG2E;
 
   bf16x8 qf[NKK];
@@ -429,10 +421,6 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   constexpr int NGB = 4;                       // bs >= 16 (host-checked): <= 3 blocks per group
   const int b0 = start / bs;
   int btw = -1, btreg = 0;
-  if (spec && sq == 0) {                       // the speculative window is the one group_blocks would load
-    btw = 0;
-    btreg = btspec;
-  }
   int gblk[NGB] = {0, 0, 0, 0};
   auto group_blocks = [&](int base) __attribute__((always_inline)) {
     const int bi0 = base / bs - b0;
