@@ -263,7 +263,14 @@ class Engine:
         # prepared and launched while step N's copies may still be in flight)
         self.h_meta_d2 = [torch.zeros(self.db.meta.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self.h_meta_d = self.h_meta_d2[0]
-        self.h_meta_p = torch.zeros(self.pb.meta.numel(), dtype=torch.int32, pin_memory=pin)
+        # prefill metadata and its logit-row / query-block staging: double-buffered too. A prompt longer than
+        # one chunk queues chunk after chunk with no host sync in between (no token is read back), and a
+        # non_blocking copy from pinned memory reads the host buffer when it EXECUTES -- so the next chunk
+        # writes the other set, after waiting on the event recorded behind this set's last uploads
+        self.h_meta_p2 = [torch.zeros(self.pb.meta.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.h_meta_p = self.h_meta_p2[0]
+        self._pfk = 0
+        self._pf_ev = [torch.cuda.Event() for _ in range(2)] if pin else [None, None]
         self.h_next = torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin)
         self.h_next2 = [torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self._ev = [torch.cuda.Event() for _ in range(2)] if pin else [None, None]
@@ -527,7 +534,16 @@ class Engine:
     def _slot(self, s: _Seq, p: int) -> int:
         return s.blocks[p // self.bs] * self.bs + p % self.bs
 
+    def _next_prefill_buf(self):
+        """Switch to the other prefill staging set once the uploads that last read it have executed."""
+        self._pfk ^= 1
+        ev = self._pf_ev[self._pfk]
+        if ev is not None:
+            ev.synchronize()
+        self.h_meta_p = self.h_meta_p2[self._pfk]
+
     def _prefill(self):
+        self._next_prefill_buf()
         b, pad = self.pb, self.pb.pad
         h = self.h_meta_p.numpy()
         ids, pos, slot, tseq, ctxl = (h[i * pad:(i + 1) * pad] for i in range(5))
@@ -578,16 +594,16 @@ class Engine:
         pad = b.pad
         h = self.h_meta_p.numpy()
         qb = ops.prefill_blocks(h[3 * pad:4 * pad], h[pad:2 * pad], T) if self.prefill_attn else None
-        # logit rows and query blocks through pinned staging (async, stream-ordered): pageable uploads
-        # block the host until the decode step in flight has drained
+        # logit rows and query blocks through pinned staging (async, stream-ordered: pageable uploads block
+        # the host until the decode step in flight has drained), one set per prefill metadata buffer
         if not hasattr(self, "_pf_pin"):
             nq = (self.max_prefill + 15) // 16 + self.max_batch
-            self._pf_pin = (torch.zeros(self.max_batch, dtype=torch.int32, pin_memory=cuda),
-                            torch.zeros(nq, 4, dtype=torch.int32, pin_memory=cuda))
+            self._pf_pin = [(torch.zeros(self.max_batch, dtype=torch.int32, pin_memory=cuda),
+                             torch.zeros(nq, 4, dtype=torch.int32, pin_memory=cuda)) for _ in range(2)]
             self._pf_dev = (torch.zeros(self.max_batch, dtype=torch.int32, device=self.dev),
                             torch.zeros(nq, 4, dtype=torch.int32, device=self.dev))
-        # (the previous prefill's uploads have executed: its tokens were read back before this one)
-        lp, qp = self._pf_pin
+        # (set _pfk's previous uploads have executed: _next_prefill_buf waited on their event)
+        lp, qp = self._pf_pin[self._pfk]
         ld, qd = self._pf_dev
         lp.numpy()[:len(rows)] = rows
         lr = ld[:len(rows)]
@@ -600,6 +616,8 @@ class Engine:
                 qp.numpy()[:len(qb)] = qb
                 qbt = qd[:len(qb)]
                 qbt.copy_(qp[:len(qb)], non_blocking=cuda)
+        if self._pf_ev[self._pfk] is not None:
+            self._pf_ev[self._pfk].record()
         n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
                                logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb),
                                need_logits=need_logits)
@@ -725,6 +743,8 @@ class Engine:
                 if self.sync_hook is not None:
                     self.sync_hook()
                 continue
+            if op == _OP_PREFILL:
+                self._next_prefill_buf()
             hm = self.h_meta_p if op == _OP_PREFILL else self.h_meta_d
             buf = torch.zeros(_NSEG * pad + nseq * nb, dtype=torch.int32)
             self.tp.bcast_ctrl(buf)

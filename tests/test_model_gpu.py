@@ -112,6 +112,29 @@ def test_engine_greedy_matches_reference(gpu, tiny_models, name, graphs):
         assert eng.counters["graph_replays"] > 0
 
 
+def test_engine_long_prompt_back_to_back_chunks(gpu, tiny_models):
+    """A 300-token prompt at 32-token chunks: the engine queues several chunks per step with no token read back
+    in between (a non_blocking upload from pinned memory reads the host buffer when it runs, so each chunk's
+    metadata needs its own staging set), and the GPU is kept busy ahead of them so the uploads run late.
+    The first tokens must equal the fp32 reference."""
+    r = GGUFReader(tiny_models["tiny-llama"])
+    m = LlamaModel(r, gpu)
+    ref = ReferenceModel(r)
+    eng = Engine(m, None, max_batch=4, max_prefill_tokens=32, use_graphs=False, ctx=512)
+    rng = np.random.default_rng(7)
+    p = [int(t) for t in rng.integers(0, 900, 300)]
+    x = torch.randn(4096, 4096, device=gpu, dtype=torch.float16)
+    for _ in range(8):                       # queued GPU work ahead of the first chunk's uploads
+        x = x @ x.t() * 1e-4
+    fut = eng.submit(GenRequest(p, SamplingParams(max_tokens=4, ignore_eos=True)))
+    while not fut.done():
+        eng.step()
+    exp = ref.greedy(p, 4)
+    got = fut.result().token_ids
+    assert got[0] == exp[0], (got, exp)
+    assert sum(int(a == b) for a, b in zip(got, exp)) >= 3, (got, exp)
+
+
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
 def test_engine_fp8_kv_cache(gpu, tiny_models, name, monkeypatch):
     """NLS_KV_DTYPE=fp8: an OCP e4m3 paged KV cache (half the attention bytes) through prefill (MFMA flash
