@@ -32,7 +32,7 @@ import torch
 
 from .. import ops
 from ..models.llama import LlamaModel
-from .sampling import HIST, SamplingParams, sample_rows, sample_rows_gpu, uniform01
+from .sampling import HIST, SamplingParams, sample_rows, sample_rows_dev, sample_rows_gpu, uniform01
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 640, 768, 1024)
 
@@ -43,6 +43,8 @@ _HDR = 10
 # NLS_TP_TRACE=1: every rank logs each control op it sends / replays (stderr), to line up the ranks' op
 # sequences after a one-shot timeout
 _TP_TRACE = os.environ.get("NLS_TP_TRACE", "0") == "1"
+# single-GPU prefill: the first tokens of finished prompts are read back once per engine step, not per chunk
+_ASYNC_FIRST = os.environ.get("NLS_ASYNC_FIRST", "1") == "1"
 _NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
 
 
@@ -270,6 +272,8 @@ class Engine:
         self.h_meta_p2 = [torch.zeros(self.pb.meta.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self.h_meta_p = self.h_meta_p2[0]
         self._pfk = 0
+        self._first_pending: list = []          # (event, pinned ids, seqs, sampled rows): first tokens in flight
+        self._first_pool: List[torch.Tensor] = []
         self._pf_ev = [torch.cuda.Event() for _ in range(2)] if pin else [None, None]
         self.h_next = torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin)
         self.h_next2 = [torch.zeros(self.db.pad, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
@@ -463,6 +467,7 @@ class Engine:
             if c:
                 self._admit()
             self._prefill()
+        self._flush_first_tokens()
         t2 = clk()
         hm["prefill"] += (t2 - t1) * 1e3
         dec = [s for s in self.running if s.n_prefilled >= s.n_target and not s.done]
@@ -580,12 +585,49 @@ class Engine:
         self._exec_prefill(T, rows + [0] * (nrows - len(rows)), need)
         self.counters["prefill_tokens"] += T
         if finishing:
-            toks = self._pick(finishing, b, list(range(len(finishing))))
-            now = time.monotonic()
-            for s, t in zip(finishing, toks):
-                if s.t_first is None:
-                    s.t_first = now
-                self._append(s, t)
+            if self.dev.type == "cuda" and self.tp is None and _ASYNC_FIRST:
+                self._pick_async(finishing, b)
+            else:
+                self._first_tokens(finishing, self._pick(finishing, b, list(range(len(finishing)))))
+
+    def _first_tokens(self, seqs: List[_Seq], toks: List[int]):
+        now = time.monotonic()
+        for s, t in zip(seqs, toks):
+            if s.t_first is None:
+                s.t_first = now
+            self._append(s, t)
+
+    def _pick_async(self, seqs: List[_Seq], b):
+        """_pick without waiting for the chunk: the greedy ids and the device sampler's draws of the sequences
+        whose prefill ended in this chunk are copied to a pinned buffer behind an event, and
+        _flush_first_tokens appends them once per engine step, before its decode step. Back-to-back prefill
+        chunks then queue with no host sync between them (each sync left the GPU idle while the host built
+        and launched the next chunk)."""
+        n, mb = len(seqs), self.max_batch
+        if not self._first_pool:
+            self._first_pool.append(torch.empty(2 * mb, dtype=torch.int32, pin_memory=True))
+        pin = self._first_pool.pop()
+        pin[:n].copy_(b.next_ids[:n], non_blocking=True)
+        sampled = [i for i, s in enumerate(seqs) if not s.req.params.greedy]
+        if sampled:
+            idx = torch.tensor(sampled, dtype=torch.long).pin_memory().to(self.dev, non_blocking=True)
+            toks = sample_rows_dev(b.logits.index_select(0, idx), [seqs[i].req.params for i in sampled],
+                                   [seqs[i].tokens for i in sampled], [self._u(seqs[i]) for i in sampled])
+            pin[mb:mb + len(sampled)].copy_(toks, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._first_pending.append((ev, pin, seqs, sampled))
+
+    def _flush_first_tokens(self):
+        pend, self._first_pending = self._first_pending, []
+        mb = self.max_batch
+        for ev, pin, seqs, sampled in pend:
+            ev.synchronize()
+            toks = pin[:len(seqs)].tolist()
+            for i, t in zip(sampled, pin[mb:mb + len(sampled)].tolist()):
+                toks[i] = t
+            self._first_tokens(seqs, toks)
+            self._first_pool.append(pin)
 
     def _exec_prefill(self, T: int, rows: List[int], need_logits: bool):
         b = self.pb

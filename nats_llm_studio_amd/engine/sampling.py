@@ -137,6 +137,12 @@ def sample_rows_gpu(logits: torch.Tensor, params: Sequence[SamplingParams], hist
                     uniforms: Sequence) -> List[int]:
     """All sampled rows of a step in ONE kernel launch (csrc/kernels/sample.hip).
     `logits` [n, V] fp32 on the GPU is used as scratch (penalties are applied in place)."""
+    return sample_rows_dev(logits, params, histories, uniforms).cpu().tolist()
+
+
+def sample_rows_dev(logits: torch.Tensor, params: Sequence[SamplingParams], histories: Sequence[Sequence[int]],
+                    uniforms: Sequence) -> torch.Tensor:
+    """sample_rows_gpu without the read-back: the drawn ids as an int32 device tensor, stream-ordered."""
     import ctypes
     import numpy as np
     from ..ops import _lib
@@ -153,10 +159,11 @@ def sample_rows_gpu(logits: torch.Tensor, params: Sequence[SamplingParams], hist
         P[i] = _lib.SampleParams(p.temperature, p.top_p, p.min_p, p.repeat_penalty, p.presence_penalty,
                                  p.frequency_penalty, uniform(uniforms[i]), int(p.top_k or 0), len(h), 0)
     dev = lg.device
-    pbytes = torch.frombuffer(bytearray(bytes(P)), dtype=torch.uint8).to(dev)
-    hd = torch.from_numpy(hist).to(dev)
+    # pinned, non_blocking uploads: a pageable upload would wait for the whole stream (the prefill chunk)
+    pbytes = torch.frombuffer(bytearray(bytes(P)), dtype=torch.uint8).pin_memory().to(dev, non_blocking=True)
+    hd = torch.from_numpy(hist).pin_memory().to(dev, non_blocking=True)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     _lib.check(_lib.lib().nls_sample(lg.data_ptr(), lg.stride(0), n, V, pbytes.data_ptr(), hd.data_ptr(), HIST,
                                      out.data_ptr(), stream), "nls_sample")
-    return out.cpu().tolist()
+    return out

@@ -112,6 +112,32 @@ def test_engine_greedy_matches_reference(gpu, tiny_models, name, graphs):
         assert eng.counters["graph_replays"] > 0
 
 
+def test_engine_async_first_tokens_match_sync(gpu, tiny_models, monkeypatch):
+    """The first tokens of finished prompts read back once per engine step (greedy ids and device-sampler draws
+    behind an event, engine._ASYNC_FIRST) equal the per-chunk synchronous picks, greedy and seeded sampled."""
+    from nats_llm_studio_amd.engine import engine as E
+    r = GGUFReader(tiny_models["tiny-llama"])
+    m = LlamaModel(r, gpu)
+    rng = np.random.default_rng(3)
+    prompts = [[int(t) for t in rng.integers(0, 900, n)] for n in (5, 40, 17, 90, 33, 8)]
+    params = [SamplingParams(max_tokens=6, ignore_eos=True),
+              SamplingParams(max_tokens=6, temperature=0.8, top_k=40, seed=1, ignore_eos=True),
+              SamplingParams(max_tokens=6, temperature=1.1, top_p=0.9, repeat_penalty=1.2, seed=2, ignore_eos=True),
+              SamplingParams(max_tokens=6, ignore_eos=True),
+              SamplingParams(max_tokens=1, temperature=0.7, seed=3, ignore_eos=True),
+              SamplingParams(max_tokens=6, temperature=0.9, min_p=0.05, seed=4, ignore_eos=True)]
+    outs = []
+    for flag in (False, True):
+        monkeypatch.setattr(E, "_ASYNC_FIRST", flag)
+        eng = Engine(m, None, max_batch=8, max_prefill_tokens=48, use_graphs=True)
+        futs = [eng.submit(GenRequest(p, sp)) for p, sp in zip(prompts, params)]
+        while not all(f.done() for f in futs):
+            eng.step()
+        outs.append([f.result().token_ids for f in futs])
+        assert not eng._first_pending
+    assert outs[0] == outs[1]
+
+
 def test_engine_long_prompt_back_to_back_chunks(gpu, tiny_models):
     """A 300-token prompt at 32-token chunks: the engine queues several chunks per step with no token read back
     in between (a non_blocking upload from pinned memory reads the host buffer when it runs, so each chunk's
