@@ -226,3 +226,56 @@ def test_rehearsal_driver_cpu(tmp_path):
     assert g["tp"]["tokens"] == g["ref"]["tokens"] == r["ref"]["tokens"][:len(rehearsal.PROMPTS)]
     assert g["tp"]["waves_tokens"] == g["ref"]["waves_tokens"]
     assert g["tp"]["counters"]["device_sampled_steps"] == 0
+
+
+def _a2a_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from nats_llm_studio_amd.parallel.comm import init_distributed
+    import torch.distributed as dist
+    comm = init_distributed("cpu")
+    try:
+        # rank r sends (r + d) % 3 rows to rank d (some zero), each row tagged (source, destination, index)
+        send = [(rank + d) % 3 for d in range(world)]
+        rows = torch.tensor([[rank, d, i] for d in range(world) for i in range(send[d])], dtype=torch.float32)
+        recv = comm.exchange_counts(send)
+        got = comm.all_to_all_rows(rows.view(-1, 3), send, recv)
+        back = comm.all_to_all_rows(got, recv, send)           # the inverse exchange restores the original rows
+        blk = torch.full((2, 4), float(rank))
+        gathered = comm.all_gather_rows(blk)
+        out.put((rank, recv, got.tolist(), bool(torch.equal(back, rows.view(-1, 3))), gathered.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_all_to_all_rows_uneven():
+    """Comm.exchange_counts / all_to_all_rows / all_gather_rows (the EP dispatch / combine primitives) over
+    gloo at world 3 with uneven and empty splits: rows arrive grouped by source rank in send order, and the
+    inverse exchange restores every rank's rows."""
+    import queue
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r = q.get(timeout=120)
+            res[r[0]] = r[1:]
+    except queue.Empty:
+        raise AssertionError(f"workers failed: {[p.exitcode for p in procs]}")
+    finally:
+        for p in procs:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    for d in range(world):
+        recv, got, inverse_ok, gathered = res[d]
+        assert recv == [(s + d) % 3 for s in range(world)]
+        assert got == [[s, d, i] for s in range(world) for i in range((s + d) % 3)]
+        assert inverse_ok
+        assert gathered == [[float(r)] * 4 for r in range(world) for _ in range(2)]
