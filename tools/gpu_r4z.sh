@@ -15,4 +15,7 @@ s = d.get("service_load") or {}
 print(n, d["value"], d["ms_per_step"], s.get("tok_s"), s.get("ttft_p50_ms"), (s.get("engine") or {}).get("host_ms"))
 PY
 done
+step pf_prof 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pf_prof_z -o run -- python3 tools/prefill_probe.py --lens 32768 --reps 1
+python3 tools/prefill_probe.py --analyze "$(find gpurun_out/pf_prof_z -name '*kernel_trace.csv' | head -1)" --lens 32768 > gpurun_out/pf_breakdown_z.txt 2>&1; head -12 gpurun_out/pf_breakdown_z.txt; tail -2 gpurun_out/pf_breakdown_z.txt
+rm -rf gpurun_out/pf_prof_z
 exit $STEPS_RC
