@@ -1,13 +1,17 @@
 #!/bin/bash
-# round 4, call L: the fused add+norm one-shot under its launch options (consumed-granule re-tag on/off,
-# L2 invalidate before every re-poll on/off): simulated ranks per call / row, then the traced greedy rehearsal
+# round 4, call Q: Llama-3-8B batch-1 GEMV re-tune (r04 candidates), then Llama-3-8B batch-1 decode with the
+# current table vs the re-tuned M=1 entries
 source tools/gpu_steps.sh
-for r in 0 1; do for i in 0 1; do
-  step sim_r${r}_i${i} 120 env NLS_AR_RETAG=$r NLS_AR_POLL_INV=$i python3 -u tools/addnorm_sim_probe.py
-  cat gpurun_out/sim_r${r}_i${i}.log | grep '^{'
-done; done
-for r in 0 1; do
-  step reh_r${r}_i1 200 env NLS_TP_TRACE=1 NLS_AR_RETAG=$r NLS_AR_POLL_INV=1 python3 -u -m nats_llm_studio_amd.parallel.rehearsal --greedy-only --profile-steps 8
-  grep -h "error words\|timeout_addnorm" gpurun_out/reh_r${r}_i1.log | cut -c1-200 | head -3
-done
+step tune8b1 400 python3 -u tools/tune_gemv.py --model llama-3-8b --ms 1 --out gpurun_out/tune8b1.json --log gpurun_out/tune8b1.log
+python3 - > gpurun_out/tune8b1_extra.json <<'PY'
+import json
+t = json.load(open("gpurun_out/tune8b1.json"))
+print(json.dumps({k: v for k, v in t.items() if not k.startswith("d:") and k.endswith(":1") and (":4096" in k or "4096:" in k)}))
+PY
+cat gpurun_out/tune8b1_extra.json
+step l8_b1_base 300 python3 -u bench.py --no-rtt --serve-load 0 --tp-leg 0 --model llama-3-8b --ftype Q4_K_M --concurrency 1 --steps 100 --warmup 10
+step l8_b1_tuned 300 env NLS_TUNING_EXTRA="$(cat gpurun_out/tune8b1_extra.json)" python3 -u bench.py --no-rtt --serve-load 0 --tp-leg 0 --model llama-3-8b --ftype Q4_K_M --concurrency 1 --steps 100 --warmup 10
+step l8_b1_base2 300 python3 -u bench.py --no-rtt --serve-load 0 --tp-leg 0 --model llama-3-8b --ftype Q4_K_M --concurrency 1 --steps 100 --warmup 10
+grep -h '^{' gpurun_out/l8_b1_base.log gpurun_out/l8_b1_tuned.log gpurun_out/l8_b1_base2.log | cut -c150-240
+rm -f /tmp/nls_bench/*.gguf
 exit $STEPS_RC
