@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--log", default="gpurun_out/tune_gemv.log")
     ap.add_argument("--only", default="", help="comma list of shape names (qkv,qkv6,o,gateup,down,down6,lm_head)")
     ap.add_argument("--dense", action="store_true", help="tune mode 4 (dense f16) at M > 64")
+    ap.add_argument("--base", default="q4_k", choices=("q4_k", "q5_k"),
+                    help="base tile type of the shapes (Q4_K_M models: q4_k; Q5_K_M, e.g. Mixtral: q5_k)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     spec = SPECS[args.model]
@@ -121,7 +123,8 @@ def main():
     os.makedirs(os.path.dirname(args.log) or ".", exist_ok=True)
     log = open(args.log, "a")
     Ms = [int(m) for m in args.ms.split(",")]
-    for name, segdef, K, epi in shapes(spec):
+    base = GGMLType.Q5_K if args.base == "q5_k" else GGMLType.Q4_K
+    for name, segdef, K, epi in shapes(spec, base=base):
         if args.only and name not in args.only.split(","):
             continue
         segs, col = [], 0
