@@ -6,7 +6,7 @@ step tunemx1 400 python3 -u tools/tune_gemv.py --model mixtral-8x7b --base q5_k 
 python3 - > gpurun_out/tunemx1_extra.json <<'PY'
 import json
 t = json.load(open("gpurun_out/tunemx1.json"))
-print(json.dumps({k: v for k, v in t.items() if not k.startswith("d:") and k.endswith(":1") and k.split(":")[0].startswith("13") and "28672" not in k and "14336" not in k}))
+print(json.dumps({k: v for k, v in t.items() if not k.startswith("d:") and k.endswith(":1") and (k.split(":")[0].startswith("13") or k.startswith("14:32000:")) and "28672" not in k and "14336" not in k}))
 PY
 cat gpurun_out/tunemx1_extra.json
 step mx_b1_base 300 python3 -u bench.py --no-rtt --serve-load 0 --tp-leg 0 --model mixtral-8x7b --ftype Q5_K_M --concurrency 1 --steps 60 --warmup 5
