@@ -17,10 +17,8 @@ grep -h '^{' gpurun_out/mx_b1_base.log gpurun_out/mx_b1_tuned.log gpurun_out/mx_
 run() { local n=$1; shift; step mx256_$n 400 env "$@" python3 -u bench.py --no-rtt --serve-load 0 --tp-leg 0 --model mixtral-8x7b --ftype Q5_K_M --concurrency 256 --steps 20 --warmup 3; }
 run base NLS_X=0
 run gu282 NLS_MOE_QCFG_GU=2,8,2
-run dn282 NLS_MOE_QCFG_DN=2,8,2
 run gu181 NLS_MOE_QCFG_GU=1,8,1
-run gu142 NLS_MOE_QCFG_GU=1,4,2
 run dn181 NLS_MOE_QCFG_DN=1,8,1
-for f in base gu282 dn282 gu181 gu142 dn181; do echo "$f $(grep -h '^{' gpurun_out/mx256_$f.log | cut -c150-230)"; done
+for f in base gu282 gu181 dn181; do echo "$f $(grep -h '^{' gpurun_out/mx256_$f.log | cut -c150-230)"; done
 rm -f /tmp/nls_bench/*.gguf
 exit $STEPS_RC
