@@ -593,6 +593,8 @@ class Engine:
     def _first_tokens(self, seqs: List[_Seq], toks: List[int]):
         now = time.monotonic()
         for s, t in zip(seqs, toks):
+            if s.done:                         # finished meanwhile (deadline, failed step): nothing to append
+                continue
             if s.t_first is None:
                 s.t_first = now
             self._append(s, t)
