@@ -469,6 +469,53 @@ __global__ __launch_bounds__(512) void moe_norm_route_kernel(
   if (wave < T) route_one(lg[wave], wave, lane, E, k, renorm, topw, counts, xrows, yrows, cap, sel);
 }
 
+// MoE router logits for many tokens (prefill chunks, decode batches > 4): logits[t][e] = h[t] . Wr[e] with Wr
+// the router's f16 copy [E][D]. The router is E (2-8) rows: the GEMV/GEMM tiles (128 weight rows per
+// workgroup, 128-row activation blocks) ran it on M / 128 workgroups with 15/16 of each MFMA idle -- ~50 us per
+// layer at 256 tokens (profiles/rocprof_mixtral_b256_quant_experts.txt). Here a workgroup takes TPB tokens:
+// each thread keeps its 8-value slices of the E router rows in registers per 16-byte chunk of D and dots them
+// with every token's slice (f32 accumulation), then one wave sum + an LDS sum per (token, expert).
+template <int E, int TPB>
+__global__ __launch_bounds__(256) void router_logits_kernel(const act_t* __restrict__ h, long ldh,
+                                                            const act_t* __restrict__ wr, int D,
+                                                            float* __restrict__ logits, int T) {
+  __shared__ float red[TPB][4][E];
+  typedef act_t act8 __attribute__((ext_vector_type(8)));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * TPB;
+  float acc[TPB][E];
+#pragma unroll
+  for (int t = 0; t < TPB; ++t)
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[t][e] = 0.f;
+  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+    act8 w[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) w[e] = *reinterpret_cast<const act8*>(wr + (size_t)e * D + c);
+#pragma unroll
+    for (int t = 0; t < TPB; ++t) {
+      if (t0 + t >= T) break;
+      const act8 x = *reinterpret_cast<const act8*>(h + (size_t)(t0 + t) * ldh + c);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[t][e] += (float)x[i] * (float)w[e][i];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TPB; ++t)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float a = wave_sum(acc[t][e]);
+      if (lane == 0) red[t][wave][e] = a;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TPB * E; i += 256) {
+    const int t = i / E, e = i % E;
+    if (t0 + t < T) logits[(size_t)(t0 + t) * E + e] = red[t][0][e] + red[t][1][e] + red[t][2][e] + red[t][3][e];
+  }
+}
+
 // SwiGLU pass after a library GEMM on the gate/up weights (ops "mode 7"): the GEMM's f16 output h keeps
 // the weights' [g0..g7, u0..u7] interleave per 16 columns, so out[m, 8j + i] = silu(alpha * h[m, 16j + i]) *
 // alpha * h[m, 16j + 8 + i]. One thread per 8 outputs: two 16-B loads, one 16-B store (HBM-bound).
@@ -610,6 +657,23 @@ int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* t
 }
 
 // x f32 [T][ldx] residual rows, nw f32 [D], wr f16 [E][D], h f16 [T][ldh] (out), logits f32 [T][E] (out)
+// router logits of T tokens (see router_logits_kernel): h f16 [T][ldh], wr f16 [E][D], logits f32 [T][E]
+int nls_router_logits(const void* h, long ldh, const void* wr, int D, int E, float* logits, int T, void* stream) {
+  if (T < 1 || D % 8 || ldh % 8) return -1;
+  constexpr int TPB = 4;
+  const dim3 grid((T + TPB - 1) / TPB);
+  hipStream_t st = (hipStream_t)stream;
+#define NLS_RL(EE)                                                                                             \
+  if (E == EE) {                                                                                               \
+    hipLaunchKernelGGL((router_logits_kernel<EE, TPB>), grid, dim3(256), 0, st, (const act_t*)h, ldh,            \
+                       (const act_t*)wr, D, logits, T);                                                        \
+    return (int)hipGetLastError();                                                                             \
+  }
+  NLS_RL(2) NLS_RL(4) NLS_RL(8)
+#undef NLS_RL
+  return -1;
+}
+
 int nls_moe_norm_route(const float* x, long ldx, const float* nw, float eps, int D, const void* wr, void* h, long ldh,
                        float* logits, int T, int E, int k, int renorm, float* topw, int* counts, int* xrows, int* yrows,
                        int cap, int* sel, void* stream) {

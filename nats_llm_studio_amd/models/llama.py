@@ -60,6 +60,8 @@ _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,
 # NLS_EP_A2A=0 keeps the combine-then-all-reduce everywhere
 _EP_A2A = os.environ.get("NLS_EP_A2A", "1")
 _EP_A2A_T = int(os.environ.get("NLS_EP_A2A_T", "64"))
+# MoE router logits through ops.router_logits (E-row kernel) rather than the GEMV/GEMM tiles; 0 = the GEMV
+_ROUTER_KERNEL = os.environ.get("NLS_ROUTER_KERNEL", "1") == "1"
 
 
 # device buffers superseded by larger ones; captured hipGraphs may still point at them
@@ -536,6 +538,14 @@ class LlamaModel:
             self.comm.row_parallel_add(w, xin, resid, T, alpha)
 
     @staticmethod
+    def _router(lw: LayerWeights, h: torch.Tensor, logits: torch.Tensor, T: int):
+        """Router logits of T tokens: the dedicated E-row kernel on the router's f16 copy (GPU), else the GEMV."""
+        if lw.router16 is not None and _ROUTER_KERNEL:
+            ops.router_logits(h, lw.router16, logits, T)
+        else:
+            ops.qgemv([Seg(lw.router)], h, logits, T)
+
+    @staticmethod
     def _moe_gemm_cfg(lw: LayerWeights, rows: int, n_exp: int):
         """Launch configs (gate/up, down, down split-K) of the grouped expert GEMMs for `rows` routed rows
         over `n_exp` experts."""
@@ -586,7 +596,7 @@ class LlamaModel:
         n = min(T, t0 + ts) - t0
         sel = m["sel"]
         if n:
-            ops.qgemv([Seg(lw.router)], b.h[t0:], m["rlogits"], n)
+            self._router(lw, b.h[t0:], m["rlogits"], n)
             ops.moe_route(m["rlogits"], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap, sel=sel)
         # dispatch: the slice's (token, slot) rows grouped by the rank owning the slot's expert
         eid = sel[:n * k].long()
@@ -648,7 +658,7 @@ class LlamaModel:
             if not routed:
                 ops.rmsnorm(b.x, in_norm, b.h, T, cfg.eps)
         if not routed:
-            ops.qgemv([Seg(lw.router)], b.h, m["rlogits"], T)
+            self._router(lw, b.h, m["rlogits"], T)
         # few tokens: path-A GEMV over each expert's gathered rows; many tokens: ONE route and the
         # LDS-dequant GEMM (mode 2) over all experts, each m-block of an expert gathering its rows
         # through xrows and exiting when it lies past the expert's device-side count

@@ -902,6 +902,21 @@ def moe_norm_route(x: torch.Tensor, nw: torch.Tensor, eps: float, wr: torch.Tens
     return True
 
 
+def router_logits(h: torch.Tensor, wr: torch.Tensor, logits: torch.Tensor, T: int) -> torch.Tensor:
+    """logits[:T] = h[:T] @ wr^T for a MoE router (wr: its f16 copy [E, D], E in {2, 4, 8}): one launch of
+    T / 4 workgroups (ops.hip router_logits_kernel) instead of a GEMM tiled for 128-row weight blocks."""
+    E, D = wr.shape
+    if h.is_cuda:
+        if h.dtype != ACT_DTYPE or wr.dtype != ACT_DTYPE or logits.dtype != torch.float32 or logits.shape[1] != E \
+                or not wr.is_contiguous() or logits.stride(0) != E or h.stride(1) != 1 or h.shape[1] < D:
+            raise ValueError("router_logits: f16 h / wr, f32 contiguous logits [>= T, E]")
+        _lib.check(_lib.lib().nls_router_logits(h.data_ptr(), h.stride(0), wr.data_ptr(), D, E, logits.data_ptr(), T,
+                                                _stream_ptr(h)), "nls_router_logits")
+        return logits
+    logits[:T] = h[:T, :D].float() @ wr.float().t()
+    return logits
+
+
 def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
               yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None):
     """Top-k routing: per-expert row lists (counts / xrows / yrows) and weights topw; `sel` (optional,

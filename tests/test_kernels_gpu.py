@@ -432,6 +432,23 @@ def test_moe_norm_route_fused(gpu, T, E, D):
                                   lgs.to(gpu), 5, k, topw, counts, xr, yr, cap)      # > 4 tokens: not taken
 
 
+@pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (5, 8, 4096), (257, 8, 4096), (2048, 8, 4096), (7, 4, 1024),
+                                   (33, 2, 768)])
+def test_router_logits(gpu, T, E, D):
+    """ops.router_logits (the E-row router kernel of MoE prefill / large decode batches) vs the fp32 product of
+    the same f16 operands; rows past T untouched."""
+    g = torch.Generator().manual_seed(T + E)
+    cap = T + 3
+    h = (torch.randn(cap, D, generator=g)).to(ops.ACT_DTYPE).to(gpu)
+    wr = (torch.randn(E, D, generator=g) * 0.05).to(torch.float16).to(gpu)
+    lg = torch.full((cap, E), 7.0, device=gpu)
+    ops.router_logits(h, wr, lg, T)
+    torch.cuda.synchronize()
+    ref = h[:T].float().cpu() @ wr.float().cpu().t()
+    _close(lg[:T], ref, 1e-3)
+    assert (lg[T:] == 7.0).all()
+
+
 def test_moe_route_nan_rows_stay_in_bounds(gpu):
     """A router row of NaN / inf logits must still pick k distinct valid experts (no index -1)."""
     T, E, k, cap = 6, 8, 2, 64
