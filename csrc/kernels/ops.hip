@@ -475,11 +475,16 @@ __global__ __launch_bounds__(512) void moe_norm_route_kernel(
 // layer at 256 tokens (profiles/rocprof_mixtral_b256_quant_experts.txt). Here a workgroup takes TPB tokens:
 // each thread keeps its 8-value slices of the E router rows in registers per 16-byte chunk of D and dots them
 // with every token's slice (f32 accumulation), then one wave sum + an LDS sum per (token, expert).
+// `zero` (optional, nz ints): the following route launch's expert counts, zeroed here by workgroup 0 (stream
+// order puts the previous layer's expert GEMMs, their last readers, before this launch) -- no memset launch.
 template <int E, int TPB>
 __global__ __launch_bounds__(256) void router_logits_kernel(const act_t* __restrict__ h, long ldh,
                                                             const act_t* __restrict__ wr, int D,
-                                                            float* __restrict__ logits, int T) {
+                                                            float* __restrict__ logits, int T, int* __restrict__ zero,
+                                                            int nz) {
   __shared__ float red[TPB][4][E];
+  if (zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < nz; i += 256) zero[i] = 0;
   typedef act_t act8 __attribute__((ext_vector_type(8)));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int t0 = blockIdx.x * TPB;
@@ -658,7 +663,8 @@ int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* t
 
 // x f32 [T][ldx] residual rows, nw f32 [D], wr f16 [E][D], h f16 [T][ldh] (out), logits f32 [T][E] (out)
 // router logits of T tokens (see router_logits_kernel): h f16 [T][ldh], wr f16 [E][D], logits f32 [T][E]
-int nls_router_logits(const void* h, long ldh, const void* wr, int D, int E, float* logits, int T, void* stream) {
+int nls_router_logits(const void* h, long ldh, const void* wr, int D, int E, float* logits, int T, int* zero, int nz,
+                      void* stream) {
   if (T < 1 || D % 8 || ldh % 8) return -1;
   constexpr int TPB = 4;
   const dim3 grid((T + TPB - 1) / TPB);
@@ -666,7 +672,7 @@ int nls_router_logits(const void* h, long ldh, const void* wr, int D, int E, flo
 #define NLS_RL(EE)                                                                                             \
   if (E == EE) {                                                                                               \
     hipLaunchKernelGGL((router_logits_kernel<EE, TPB>), grid, dim3(256), 0, st, (const act_t*)h, ldh,            \
-                       (const act_t*)wr, D, logits, T);                                                        \
+                       (const act_t*)wr, D, logits, T, zero, nz);                                              \
     return (int)hipGetLastError();                                                                             \
   }
   NLS_RL(2) NLS_RL(4) NLS_RL(8)

@@ -538,12 +538,15 @@ class LlamaModel:
             self.comm.row_parallel_add(w, xin, resid, T, alpha)
 
     @staticmethod
-    def _router(lw: LayerWeights, h: torch.Tensor, logits: torch.Tensor, T: int):
-        """Router logits of T tokens: the dedicated E-row kernel on the router's f16 copy (GPU), else the GEMV."""
+    def _router(lw: LayerWeights, h: torch.Tensor, logits: torch.Tensor, T: int,
+                counts: Optional[torch.Tensor] = None) -> bool:
+        """Router logits of T tokens: the dedicated E-row kernel on the router's f16 copy (GPU), else the GEMV.
+        True when the kernel also zeroed `counts` (the following moe_route can skip its memset)."""
         if lw.router16 is not None and _ROUTER_KERNEL:
-            ops.router_logits(h, lw.router16, logits, T)
-        else:
-            ops.qgemv([Seg(lw.router)], h, logits, T)
+            ops.router_logits(h, lw.router16, logits, T, zero=counts)
+            return counts is not None
+        ops.qgemv([Seg(lw.router)], h, logits, T)
+        return False
 
     @staticmethod
     def _moe_gemm_cfg(lw: LayerWeights, rows: int, n_exp: int):
@@ -596,8 +599,9 @@ class LlamaModel:
         n = min(T, t0 + ts) - t0
         sel = m["sel"]
         if n:
-            self._router(lw, b.h[t0:], m["rlogits"], n)
-            ops.moe_route(m["rlogits"], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap, sel=sel)
+            zeroed = self._router(lw, b.h[t0:], m["rlogits"], n, counts=m["counts"])
+            ops.moe_route(m["rlogits"], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap, sel=sel,
+                          counts_zeroed=zeroed)
         # dispatch: the slice's (token, slot) rows grouped by the rank owning the slot's expert
         eid = sel[:n * k].long()
         dest = torch.div(eid, per, rounding_mode="floor")
@@ -657,8 +661,9 @@ class LlamaModel:
                                         m["counts"], m["xrows"], m["yrows"], cap, sel=m["sel"] if use_sel else None)
             if not routed:
                 ops.rmsnorm(b.x, in_norm, b.h, T, cfg.eps)
+        zeroed = False
         if not routed:
-            self._router(lw, b.h, m["rlogits"], T)
+            zeroed = self._router(lw, b.h, m["rlogits"], T, counts=m["counts"])
         # few tokens: path-A GEMV over each expert's gathered rows; many tokens: ONE route and the
         # LDS-dequant GEMM (mode 2) over all experts, each m-block of an expert gathering its rows
         # through xrows and exiting when it lies past the expert's device-side count
@@ -691,7 +696,7 @@ class LlamaModel:
             use_sel = not gemm and self.device.type == "cuda" and n * k < len(self.experts)
             if not (routed and c0 == 0 and n == T):
                 ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap,
-                              sel=m["sel"] if use_sel else None)
+                              sel=m["sel"] if use_sel else None, counts_zeroed=zeroed and c0 == 0)
             loc = list(zip(self.experts, lw.exp_gateup, lw.exp_down))
             segs = [Seg(gu, 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, gu, _ in loc]
 

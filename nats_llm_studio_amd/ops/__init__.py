@@ -902,28 +902,37 @@ def moe_norm_route(x: torch.Tensor, nw: torch.Tensor, eps: float, wr: torch.Tens
     return True
 
 
-def router_logits(h: torch.Tensor, wr: torch.Tensor, logits: torch.Tensor, T: int) -> torch.Tensor:
+def router_logits(h: torch.Tensor, wr: torch.Tensor, logits: torch.Tensor, T: int,
+                  zero: Optional[torch.Tensor] = None) -> torch.Tensor:
     """logits[:T] = h[:T] @ wr^T for a MoE router (wr: its f16 copy [E, D], E in {2, 4, 8}): one launch of
-    T / 4 workgroups (ops.hip router_logits_kernel) instead of a GEMM tiled for 128-row weight blocks."""
+    T / 4 workgroups (ops.hip router_logits_kernel) instead of a GEMM tiled for 128-row weight blocks.
+    `zero` (int32, optional): zeroed in the same launch (the next moe_route's expert counts)."""
     E, D = wr.shape
     if h.is_cuda:
         if h.dtype != ACT_DTYPE or wr.dtype != ACT_DTYPE or logits.dtype != torch.float32 or logits.shape[1] != E \
                 or not wr.is_contiguous() or logits.stride(0) != E or h.stride(1) != 1 or h.shape[1] < D:
             raise ValueError("router_logits: f16 h / wr, f32 contiguous logits [>= T, E]")
+        if zero is not None and (zero.dtype != torch.int32 or not zero.is_contiguous()):
+            raise ValueError("router_logits: zero must be contiguous int32")
         _lib.check(_lib.lib().nls_router_logits(h.data_ptr(), h.stride(0), wr.data_ptr(), D, E, logits.data_ptr(), T,
-                                                _stream_ptr(h)), "nls_router_logits")
+                                                _p(zero), 0 if zero is None else zero.numel(), _stream_ptr(h)),
+                   "nls_router_logits")
         return logits
     logits[:T] = h[:T, :D].float() @ wr.float().t()
+    if zero is not None:
+        zero.zero_()
     return logits
 
 
 def moe_route(logits: torch.Tensor, T: int, k: int, topw: torch.Tensor, counts: torch.Tensor, xrows: torch.Tensor,
-              yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None):
+              yrows: torch.Tensor, cap: int, renorm: bool = True, sel: Optional[torch.Tensor] = None,
+              counts_zeroed: bool = False):
     """Top-k routing: per-expert row lists (counts / xrows / yrows) and weights topw; `sel` (optional,
-    int32 [>= T*k]) receives each (token, slot)'s expert id for device-selected expert launches."""
+    int32 [>= T*k]) receives each (token, slot)'s expert id for device-selected expert launches.
+    counts_zeroed: an earlier launch on the stream already zeroed `counts` (router_logits(zero=counts))."""
     E = logits.shape[1]
     if logits.is_cuda:
-        if T > 4:                  # one-workgroup launches (T <= 4) zero the counts in-kernel
+        if T > 4 and not counts_zeroed:   # one-workgroup launches (T <= 4) zero the counts in-kernel
             counts.zero_()
         _lib.check(_lib.lib().nls_moe_route(logits.data_ptr(), T, E, k, int(renorm), topw.data_ptr(),
                                             counts.data_ptr(), xrows.data_ptr(), yrows.data_ptr(), cap, _p(sel),

@@ -66,7 +66,7 @@ _SIGS = {
                       c_void_p, c_void_p],
     "nls_moe_norm_route": [c_void_p, c_long, c_void_p, c_float, c_int, c_void_p, c_void_p, c_long, c_void_p, c_int,
                            c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
-    "nls_router_logits": [c_void_p, c_long, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
+    "nls_router_logits": [c_void_p, c_long, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p],
     "nls_moe_combine": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p],
     "nls_moe_combine_norm": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p, c_float,
                              c_void_p, c_long, c_void_p],

@@ -442,11 +442,13 @@ def test_router_logits(gpu, T, E, D):
     h = (torch.randn(cap, D, generator=g)).to(ops.ACT_DTYPE).to(gpu)
     wr = (torch.randn(E, D, generator=g) * 0.05).to(torch.float16).to(gpu)
     lg = torch.full((cap, E), 7.0, device=gpu)
-    ops.router_logits(h, wr, lg, T)
+    counts = torch.full((E,), 5, dtype=torch.int32, device=gpu)
+    ops.router_logits(h, wr, lg, T, zero=counts)          # the next route's expert counts, zeroed in-launch
     torch.cuda.synchronize()
     ref = h[:T].float().cpu() @ wr.float().cpu().t()
     _close(lg[:T], ref, 1e-3)
     assert (lg[T:] == 7.0).all()
+    assert (counts.cpu() == 0).all()
 
 
 def test_moe_route_nan_rows_stay_in_bounds(gpu):
