@@ -474,17 +474,18 @@ __global__ __launch_bounds__(512) void moe_norm_route_kernel(
 // workgroup, 128-row activation blocks) ran it on M / 128 workgroups with 15/16 of each MFMA idle -- ~50 us per
 // layer at 256 tokens (profiles/rocprof_mixtral_b256_quant_experts.txt). Here a workgroup takes TPB tokens:
 // each thread keeps its 8-value slices of the E router rows in registers per 16-byte chunk of D and dots them
-// with every token's slice (f32 accumulation), then one wave sum + an LDS sum per (token, expert).
+// with every token's slice (f32 accumulation), then one wave sum + an LDS sum over the 8 waves per (token,
+// expert).
 // `zero` (optional, nz ints): the following route launch's expert counts, zeroed here by workgroup 0 (stream
 // order puts the previous layer's expert GEMMs, their last readers, before this launch) -- no memset launch.
 template <int E, int TPB>
-__global__ __launch_bounds__(256) void router_logits_kernel(const act_t* __restrict__ h, long ldh,
+__global__ __launch_bounds__(512) void router_logits_kernel(const act_t* __restrict__ h, long ldh,
                                                             const act_t* __restrict__ wr, int D,
                                                             float* __restrict__ logits, int T, int* __restrict__ zero,
                                                             int nz) {
-  __shared__ float red[TPB][4][E];
+  __shared__ float red[TPB][8][E];
   if (zero && blockIdx.x == 0)
-    for (int i = threadIdx.x; i < nz; i += 256) zero[i] = 0;
+    for (int i = threadIdx.x; i < nz; i += 512) zero[i] = 0;
   typedef act_t act8 __attribute__((ext_vector_type(8)));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int t0 = blockIdx.x * TPB;
@@ -493,7 +494,7 @@ __global__ __launch_bounds__(256) void router_logits_kernel(const act_t* __restr
   for (int t = 0; t < TPB; ++t)
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[t][e] = 0.f;
-  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+  for (int c = threadIdx.x * 8; c < D; c += 512 * 8) {
     act8 w[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) w[e] = *reinterpret_cast<const act8*>(wr + (size_t)e * D + c);
@@ -515,9 +516,12 @@ __global__ __launch_bounds__(256) void router_logits_kernel(const act_t* __restr
       if (lane == 0) red[t][wave][e] = a;
     }
   __syncthreads();
-  for (int i = threadIdx.x; i < TPB * E; i += 256) {
+  for (int i = threadIdx.x; i < TPB * E; i += 512) {
     const int t = i / E, e = i % E;
-    if (t0 + t < T) logits[(size_t)(t0 + t) * E + e] = red[t][0][e] + red[t][1][e] + red[t][2][e] + red[t][3][e];
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[t][w][e];
+    if (t0 + t < T) logits[(size_t)(t0 + t) * E + e] = v;
   }
 }
 
@@ -666,12 +670,14 @@ int nls_moe_route(const float* logits, int T, int E, int k, int renorm, float* t
 int nls_router_logits(const void* h, long ldh, const void* wr, int D, int E, float* logits, int T, int* zero, int nz,
                       void* stream) {
   if (T < 1 || D % 8 || ldh % 8) return -1;
-  constexpr int TPB = 4;
+  // one token per 8-wave workgroup: a 4096-wide row is one 16-byte chunk per thread, and the grid has T
+  // workgroups (4 tokens per 4-wave workgroup measured 11.2 us per launch at 256 tokens: 64 workgroups)
+  constexpr int TPB = 1;
   const dim3 grid((T + TPB - 1) / TPB);
   hipStream_t st = (hipStream_t)stream;
 #define NLS_RL(EE)                                                                                             \
   if (E == EE) {                                                                                               \
-    hipLaunchKernelGGL((router_logits_kernel<EE, TPB>), grid, dim3(256), 0, st, (const act_t*)h, ldh,            \
+    hipLaunchKernelGGL((router_logits_kernel<EE, TPB>), grid, dim3(512), 0, st, (const act_t*)h, ldh,            \
                        (const act_t*)wr, D, logits, T, zero, nz);                                              \
     return (int)hipGetLastError();                                                                             \
   }
