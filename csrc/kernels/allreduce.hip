@@ -75,6 +75,18 @@ __device__ __forceinline__ uint4 ar_load(const uint32_t* p) {
   const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
+// the same granule read by a read-modify-write (OR 0): performed where the memory's atomics are
+// performed, never answered from a cache line of this CU's or this XCD's hierarchy
+__device__ __forceinline__ uint4 ar_load_rmw(const uint32_t* p) {
+  gu64* q = (gu64*)p;
+  const unsigned long long a = __hip_atomic_fetch_or(q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long b = __hip_atomic_fetch_or(q + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+__device__ __forceinline__ uint32_t xcc_id() {
+  // HW_REG_XCC_ID (hwreg 20), bits [3:0]: the XCD this wave runs on (diagnostics only)
+  return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
+}
 // a float4 other workgroups of this launch read (the residual slice of the fused add+norm): write-through
 __device__ __forceinline__ void wt_store4(float* p, float4 v) {
   gu64* q = (gu64*)p;
@@ -103,6 +115,13 @@ __device__ __forceinline__ unsigned ep_load(const unsigned* p) {
 __device__ __forceinline__ void ep_store(unsigned* p, unsigned v) {
   __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// read-modify-write forms (AR_OPT_EP_RMW): the counter word is never answered from a cache line
+__device__ __forceinline__ unsigned ep_load_rmw(unsigned* p) {
+  return __hip_atomic_fetch_add((gu32*)p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void ep_store_rmw(unsigned* p, unsigned v) {
+  __hip_atomic_exchange((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // diagnostics of the first timed-out poll of a buffer set: words 1..7 of this rank's error area (a, b, epoch,
 // peer, the first dword seen -- its tag is the low 2 bits --, a marker, the kernel: 1 sum, 2 add+norm,
@@ -120,14 +139,47 @@ __device__ void ar_diag(uint32_t* mine, int world, long cap, int kid, long a, lo
   }
 }
 
+// more of the first add+norm timeout (words 8..18, written by the lane that recorded words 1..7): the four
+// dwords its last poll saw, its lane's column, its XCD, the epoch counter as read again at the timeout, and the
+// granule as an atomic read-modify-write sees it (memory's view, no cache line in between)
+__device__ void ar_diag2(uint32_t* mine, int world, long cap, uint4 seen, uint32_t col, unsigned ep_now, uint4 rmw) {
+  uint32_t* dw = ar_err_word(mine, world, cap);
+  if (atomicCAS(dw + 19, 0u, 0xB22u) == 0u) {
+    dw[8] = seen.x;
+    dw[9] = seen.y;
+    dw[10] = seen.z;
+    dw[11] = seen.w;
+    dw[12] = col;
+    dw[13] = xcc_id();
+    dw[14] = ep_now;
+    dw[15] = rmw.x;
+    dw[16] = rmw.y;
+    dw[17] = rmw.z;
+    dw[18] = rmw.w;
+  }
+}
+
 // launch-option bits carried above the spin budget (host: ar_opts(), env NLS_AR_POLL_INV / NLS_AR_RETAG)
 constexpr long AR_OPT_POLL_INV = 1L << 62;    // system-scope acquire (L2 invalidate) before every re-poll
 constexpr long AR_OPT_RETAG = 1L << 61;       // fused add+norm: re-tag consumed granules (the round-3 protocol)
+constexpr long AR_OPT_EP_RMW = 1L << 60;      // epoch counters read / written by atomic read-modify-writes
+constexpr long AR_OPT_POLL_RMW = 1L << 59;    // peer granules polled by atomic read-modify-writes (OR 0)
 constexpr long AR_SPIN_MASK = (1L << 48) - 1;
+
+__device__ __forceinline__ unsigned ep_get(unsigned* p, long opts) {
+  return (opts & AR_OPT_EP_RMW) ? ep_load_rmw(p) : ep_load(p);
+}
+__device__ __forceinline__ void ep_put(unsigned* p, unsigned v, long opts) {
+  if (opts & AR_OPT_EP_RMW)
+    ep_store_rmw(p, v);
+  else
+    ep_store(p, v);
+}
 
 // poll one 16-byte granule of peer data until every dword carries `tag` (bounded)
 __device__ __forceinline__ uint4 ar_poll(const uint32_t* src, uint32_t tag, long max_spins, bool& failed) {
-  uint4 g = ar_load(src);
+  const bool rmw = max_spins & AR_OPT_POLL_RMW;
+  uint4 g = rmw ? ar_load_rmw(src) : ar_load(src);
   long spins = 0;
   const long budget = max_spins & AR_SPIN_MASK;
   while (!failed && !ar_tagged(g, tag)) {
@@ -137,7 +189,7 @@ __device__ __forceinline__ uint4 ar_poll(const uint32_t* src, uint32_t tag, long
     }
     __builtin_amdgcn_s_sleep(2);
     if (max_spins & AR_OPT_POLL_INV) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    g = ar_load(src);
+    g = rmw ? ar_load_rmw(src) : ar_load(src);
   }
   return g;
 }
@@ -166,13 +218,15 @@ struct SlotBlocks {
 constexpr int AR_MAX_WG_BLOCKS = 64;   // slot blocks per workgroup at the largest message (host-checked)
 
 // this workgroup's block epochs -> LDS (advanced by one: the epoch of THIS call)
-__device__ __forceinline__ void blocks_begin(const unsigned* epochs, int first, int step, int mine, unsigned* s_ep) {
-  for (int j = threadIdx.x; j < mine; j += blockDim.x) s_ep[j] = ep_load(epochs + first + (long)j * step) + 1u;
+__device__ __forceinline__ void blocks_begin(unsigned* epochs, int first, int step, int mine, unsigned* s_ep,
+                                             long opts) {
+  for (int j = threadIdx.x; j < mine; j += blockDim.x) s_ep[j] = ep_get(epochs + first + (long)j * step, opts) + 1u;
   __syncthreads();
 }
-__device__ __forceinline__ void blocks_end(unsigned* epochs, int first, int step, int mine, const unsigned* s_ep) {
+__device__ __forceinline__ void blocks_end(unsigned* epochs, int first, int step, int mine, const unsigned* s_ep,
+                                           long opts) {
   __syncthreads();
-  for (int j = threadIdx.x; j < mine; j += blockDim.x) ep_store(epochs + first + (long)j * step, s_ep[j]);
+  for (int j = threadIdx.x; j < mine; j += blockDim.x) ep_put(epochs + first + (long)j * step, s_ep[j], opts);
 }
 
 // plain all-reduce (MoE expert outputs, generic decode-size sums): fixed grid, slot blocks of
@@ -186,7 +240,7 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
   const long n4 = n >> 2;
   const SlotBlocks<AR_THREADS> B(n4);
   if (threadIdx.x == 0) s_fail = 0;
-  blocks_begin(epochs, B.first, B.step, B.mine, s_ep);
+  blocks_begin(epochs, B.first, B.step, B.mine, s_ep, max_spins);
   // 1) push: my (rounded, tagged) values -> slot [par][rank] of every peer, 16 B per lane
   for (int j = 0; j < B.mine; ++j) {
     const unsigned ep = s_ep[j];
@@ -222,7 +276,7 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
     if (i < n4) reinterpret_cast<float4*>(data)[i] = acc;
   }
   if (failed) s_fail = 1;
-  blocks_end(epochs, B.first, B.step, B.mine, s_ep);
+  blocks_end(epochs, B.first, B.step, B.mine, s_ep, max_spins);
   if (threadIdx.x == 0 && s_fail) ar_raise(P, world, cap, err);
 }
 
@@ -261,7 +315,7 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     ssq += rank * sq;
   }
   const int eidx = b * nblk + c;
-  if (threadIdx.x == 0) s_ep = ep_load(epochs + eidx) + 1u;
+  if (threadIdx.x == 0) s_ep = ep_get(epochs + eidx, max_spins) + 1u;
   __syncthreads();
   const unsigned ep = s_ep;
   const uint32_t tag = ep & 3u;
@@ -290,7 +344,10 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
         uint32_t* src = mine + ((long)(par * world + p)) * cap + (long)b * D + col;
         const bool was = failed;
         const uint4 gv = ar_poll(src, tag, max_spins, failed);
-        if (failed && !was) ar_diag(mine, world, cap, 2, b, c, ep, p, gv.x);
+        if (failed && !was) {
+          ar_diag(mine, world, cap, 2, b, c, ep, p, gv.x);
+          ar_diag2(mine, world, cap, gv, (uint32_t)col, ep_get(epochs + eidx, max_spins), ar_load_rmw(src));
+        }
         v = ar_val4(gv);
         if (max_spins & AR_OPT_RETAG) {
           const uint32_t ct = (ep + 1u) & 3u;
@@ -318,7 +375,7 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) {
     __hip_atomic_store((gu32*)(ssq + eidx), __float_as_uint(ss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ep_store(epochs + eidx, ep);
+    ep_put(epochs + eidx, ep, max_spins);
     if (fm) ar_raise(P, world, cap, err);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -389,7 +446,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_gather_kernel(const uint32
   __shared__ int s_fail;
   const SlotBlocks<AG_THREADS> B(n2);
   if (threadIdx.x == 0) s_fail = 0;
-  blocks_begin(epochs, B.first, B.step, B.mine, s_ep);
+  blocks_begin(epochs, B.first, B.step, B.mine, s_ep, max_spins);
   auto out_at = [&](long w, int p) -> uint32_t* {
     const long a = w / per_arr, rem = w - a * per_arr, r = rem / C, c = rem - r * C;
     return dst + a * per_arr * world + r * (long)world * C + (long)p * C + c;
@@ -426,7 +483,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_gather_kernel(const uint32
     }
   }
   if (failed) s_fail = 1;
-  blocks_end(epochs, B.first, B.step, B.mine, s_ep);
+  blocks_end(epochs, B.first, B.step, B.mine, s_ep, max_spins);
   if (threadIdx.x == 0 && s_fail) ar_raise(P, world, cap, err);
 }
 
@@ -443,7 +500,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_argmax_kernel(unsigned lon
   __shared__ int s_fail;
   const SlotBlocks<AG_THREADS> B(n);
   if (threadIdx.x == 0) s_fail = 0;
-  blocks_begin(epochs, B.first, B.step, B.mine, s_ep);
+  blocks_begin(epochs, B.first, B.step, B.mine, s_ep, max_spins);
   for (int j = 0; j < B.mine; ++j) {
     const unsigned ep = s_ep[j];
     const long i = ((long)B.first + (long)j * B.step) * AG_THREADS + threadIdx.x;
@@ -474,7 +531,7 @@ __global__ __launch_bounds__(AG_THREADS) void oneshot_argmax_kernel(unsigned lon
     }
   }
   if (failed) s_fail = 1;
-  blocks_end(epochs, B.first, B.step, B.mine, s_ep);
+  blocks_end(epochs, B.first, B.step, B.mine, s_ep, max_spins);
   if (threadIdx.x == 0 && s_fail) ar_raise(P, world, cap, err);
 }
 
@@ -493,8 +550,12 @@ static long ar_opts(long max_spins) {
     long o = 0;
     const char* a = getenv("NLS_AR_POLL_INV");
     const char* b = getenv("NLS_AR_RETAG");
+    const char* c = getenv("NLS_AR_EP_RMW");
+    const char* d = getenv("NLS_AR_POLL_RMW");
     if (a && atoi(a)) o |= AR_OPT_POLL_INV;
     if (!b || atoi(b)) o |= AR_OPT_RETAG;      // default on: the simulated-rank tests need it (round 4)
+    if (c && atoi(c)) o |= AR_OPT_EP_RMW;
+    if (d && atoi(d)) o |= AR_OPT_POLL_RMW;
     return o;
   }();
   return (max_spins & AR_SPIN_MASK) | opts;
@@ -560,6 +621,10 @@ int nls_ar_err_fetch(void* buf, long cap, int world, void* host, void* stream) {
 int nls_ar_err_words(void* buf, long cap, int world, void* host, int n, void* stream) {
   return (int)hipMemcpyAsync(host, (char*)buf + 2L * world * cap * 4L, 4L * n, hipMemcpyDeviceToHost,
                              (hipStream_t)stream);
+}
+// n words at word offset `off` of a receive buffer (diagnostics: a timed-out slot as memory holds it)
+int nls_ar_peek(void* buf, long off, int n, void* host, void* stream) {
+  return (int)hipMemcpyAsync(host, (char*)buf + 4L * off, 4L * n, hipMemcpyDeviceToHost, (hipStream_t)stream);
 }
 int nls_ar_err_clear(void* buf, long cap, int world, void* stream) {
   hipLaunchKernelGGL(ar_err_clear_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,

@@ -98,7 +98,8 @@ class Spm {
   Spm(const std::vector<std::string>& tokens, const std::vector<float>& scores, std::vector<int32_t> byte_ids)
       : scores_(scores), byte_ids_(std::move(byte_ids)) {
     vocab_.reserve(tokens.size() * 2);
-    for (size_t i = 0; i < tokens.size(); ++i) vocab_.emplace(tokens[i], (int32_t)i);   // first id wins
+    for (size_t i = 0; i < tokens.size(); ++i) vocab_[tokens[i]] = (int32_t)i;   // last id wins, as the Python
+    // reference's {t: i} map and llama.cpp's token_to_id do for duplicate strings
   }
 
   // text: already "▁"-normalised (and prefixed) UTF-8

@@ -43,6 +43,7 @@ _HDR = 10
 # NLS_TP_TRACE=1: every rank logs each control op it sends / replays (stderr), to line up the ranks' op
 # sequences after a one-shot timeout
 _TP_TRACE = os.environ.get("NLS_TP_TRACE", "0") == "1"
+_NO_REPLAY = os.environ.get("NLS_GRAPH_NO_REPLAY", "0") == "1"
 # single-GPU prefill: the first tokens of finished prompts are read back once per engine step, not per chunk
 _ASYNC_FIRST = os.environ.get("NLS_ASYNC_FIRST", "1") == "1"
 _NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
@@ -1168,6 +1169,13 @@ class Engine:
         for s, t in zip(launch, out):
             if not s.done:
                 self._append(s, t)
+        if self.device_sampling:
+            # host-drawn tokens never reach the device penalty-history ring (the in-step sampler appends only
+            # its own draws): re-stage every sampling row still running, so a later in-step draw penalises
+            # the right tokens (the staged rows ship to followers with the next step)
+            for s in launch:
+                if not s.done and s.row >= 0 and not s.req.params.greedy:
+                    self._upload_sampling_row(s.row, s)
 
     def _step_forward(self, Bp: int, ns: int, need_logits: bool, dsamp: bool):
         self.model.forward(self.db, self.kc, self.vc, Bp, self.bs, ns, feed_prev=True,
@@ -1197,6 +1205,9 @@ class Engine:
             # that follows only records the kernels for the next steps
             self._step_forward(Bp, ns, need_logits, dsamp)
             self._capture(Bp, ns, need_logits, dsamp, warm=False)
+            return
+        if _NO_REPLAY:                          # (diagnostics: graphs captured, every step eager)
+            self._step_forward(Bp, ns, need_logits, dsamp)
             return
         g.replay()
         self.counters["graph_replays"] += 1

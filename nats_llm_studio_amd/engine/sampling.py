@@ -41,20 +41,26 @@ class SamplingParams:
                 and self.frequency_penalty == 0.0)
 
     @classmethod
-    def from_request(cls, req: dict, default_max: int = 256) -> "SamplingParams":
+    def from_request(cls, req: dict, default_max: int = 256, profile: Optional[str] = None) -> "SamplingParams":
+        """OpenAI / LM Studio chat fields -> params. Fields the request omits come from `profile`
+        (default: env NLS_SAMPLING_DEFAULTS, else "lmstudio"); see DEFAULT_PROFILES."""
         stop = req.get("stop") or []
         if isinstance(stop, str):
             stop = [stop]
         mt = req.get("max_tokens", req.get("max_completion_tokens"))
         if mt is None or int(mt) < 0:
             mt = default_max
-        temp = req.get("temperature")
+        d = defaults_for(req, profile)
+
+        def get(key, conv):
+            v = req.get(key)
+            return conv(d[key]) if v is None else conv(v)
         return cls(
-            temperature=0.0 if temp is None else float(temp),
-            top_k=int(req.get("top_k", 0) or 0),
-            top_p=float(req.get("top_p", 1.0) if req.get("top_p") is not None else 1.0),
-            min_p=float(req.get("min_p", 0.0) or 0.0),
-            repeat_penalty=float(req.get("repeat_penalty", 1.0) or 1.0),
+            temperature=get("temperature", float),
+            top_k=get("top_k", int),
+            top_p=get("top_p", float),
+            min_p=get("min_p", float),
+            repeat_penalty=get("repeat_penalty", float),
             presence_penalty=float(req.get("presence_penalty", 0.0) or 0.0),
             frequency_penalty=float(req.get("frequency_penalty", 0.0) or 0.0),
             seed=req.get("seed"),
@@ -62,6 +68,37 @@ class SamplingParams:
             stop=list(stop),
             ignore_eos=bool(req.get("ignore_eos", False)),
         )
+
+
+# Values of the sampling fields a chat request omits. The reference forwards the request verbatim to LM Studio
+# (`/root/reference/nats_llm_studio.go:348`), whose server fills omitted fields from its preset: temperature 0.8,
+# top-k 40, top-p 0.95, min-p 0.05, repeat penalty 1.1 [ext: LM Studio defaults; no fixture in the reference pins
+# them -- parity unpinned]. Decision (round 5):
+#   "lmstudio" (default): a request that SAMPLES (temperature > 0) gets LM Studio's top-k / top-p / min-p /
+#       repeat-penalty preset for the fields it omits -- the reference README's own payload `{"temperature":
+#       0.7}` (README.md:196-204) samples as LM Studio would sample it. A request that omits temperature, or sends
+#       0, decodes greedily with neutral penalties: deterministic output is this API's documented default (LM
+#       Studio would sample at 0.8 there -- the one deliberate deviation).
+#   "lmstudio-full": every omitted field from the preset, temperature 0.8 included (LM Studio's behaviour).
+#   "neutral": the round-4 behaviour: omitted fields are neutral (top-k 0, top-p 1, min-p 0, penalty 1).
+LMSTUDIO_PRESET = dict(temperature=0.8, top_k=40, top_p=0.95, min_p=0.05, repeat_penalty=1.1)
+NEUTRAL = dict(temperature=0.0, top_k=0, top_p=1.0, min_p=0.0, repeat_penalty=1.0)
+DEFAULT_PROFILES = ("lmstudio", "lmstudio-full", "neutral")
+
+
+def defaults_for(req: dict, profile: Optional[str] = None) -> dict:
+    import os
+    profile = profile or os.environ.get("NLS_SAMPLING_DEFAULTS", "lmstudio")
+    if profile == "lmstudio-full":
+        return LMSTUDIO_PRESET
+    if profile == "lmstudio":
+        t = req.get("temperature")
+        if t is not None and float(t) > 0.0:
+            return dict(LMSTUDIO_PRESET, temperature=0.0)
+        return NEUTRAL
+    if profile == "neutral":
+        return NEUTRAL
+    raise ValueError(f"NLS_SAMPLING_DEFAULTS: unknown profile {profile!r} (one of {DEFAULT_PROFILES})")
 
 
 _M64 = (1 << 64) - 1

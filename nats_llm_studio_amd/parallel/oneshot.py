@@ -150,10 +150,31 @@ class OneShotAllReduce:
         # per buffer set: [error, a, b, epoch, peer, first dword seen (tag = low 2 bits), marker, kernel]
         # (add+norm: a row, b slice; the others: a granule, b granules of the call)
         for name, buf in (("sum", self.buf), ("addnorm", self.nbuf), ("gather", self.gbuf)):
-            host = torch.zeros(8, dtype=torch.int32)
-            _lib.check(L.nls_ar_err_words(buf, self.cap, self.world, host.data_ptr(), 8, st), "nls_ar_err_words")
+            host = torch.zeros(20, dtype=torch.int32)
+            _lib.check(L.nls_ar_err_words(buf, self.cap, self.world, host.data_ptr(), 20, st), "nls_ar_err_words")
             torch.cuda.synchronize(self.device)
-            out[f"timeout_{name}"] = host.tolist()
+            w = host.tolist()
+            out[f"timeout_{name}"] = w[:8]
+            if name == "addnorm" and w[6] and w[19]:
+                # words 8..18: the granule the last poll saw, the lane's column, its XCD, the epoch counter
+                # re-read at the timeout and the granule read by an atomic RMW; plus the slot as memory holds
+                # it NOW (both parities) and this rank's epoch row -- compare with the peer's own dump
+                b, c, ep, peer, col = w[1], w[2], w[3], w[4], w[12]
+                out["addnorm_timeout_detail"] = dict(
+                    row=b, slice=c, epoch=ep, peer=peer, col=col, seen=[hex(v & 0xFFFFFFFF) for v in w[8:12]],
+                    xcc=w[13], epoch_counter_at_timeout=w[14], rmw_seen=[hex(v & 0xFFFFFFFF) for v in w[15:19]])
+                slots = {}
+                D = next(iter(self._norm)) if self._norm else 0
+                for par in (0, 1):
+                    pk = torch.zeros(4, dtype=torch.int32)
+                    off = (par * self.world + peer) * self.cap + b * D + col
+                    _lib.check(L.nls_ar_peek(buf, off, 4, pk.data_ptr(), st), "nls_ar_peek")
+                    torch.cuda.synchronize(self.device)
+                    slots[par] = [hex(v & 0xFFFFFFFF) for v in pk.tolist()]
+                out["addnorm_timeout_detail"]["slot_memory_now"] = slots
+        for D, (ep, tk, _sq) in self._norm.items():
+            nblk = ep.numel() // tk.numel()
+            out[f"addnorm{D}_epochs_rows0_23"] = ep.view(-1, nblk)[:24].tolist()
         return out
 
     def reset(self):

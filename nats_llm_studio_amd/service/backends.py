@@ -384,20 +384,21 @@ class HttpBackend:
         self.timeout = timeout
         self.requests = 0
 
-    def _do(self, method: str, path: str, body: Optional[bytes] = None):
+    def _do(self, method: str, path: str, body: Optional[bytes] = None, timeout: Optional[float] = None):
         import urllib.error
         import urllib.request
         req = urllib.request.Request(self.base + path, data=body, method=method)
         if body is not None:
             req.add_header("Content-Type", "application/json")
+        t = self.timeout if timeout is None else min(self.timeout, timeout)
         try:
-            with urllib.request.urlopen(req, timeout=self.timeout) as r:
+            with urllib.request.urlopen(req, timeout=t) as r:
                 return r.status, r.read()
         except urllib.error.HTTPError as e:       # non-2xx: body + status, not an error
             return e.code, e.read()
 
-    def list_models_raw(self):
-        return self._do("GET", "/api/v0/models")
+    def list_models_raw(self, timeout: Optional[float] = None):
+        return self._do("GET", "/api/v0/models", timeout=timeout)
 
     def chat_raw(self, payload: bytes):
         self.requests += 1

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -64,6 +65,8 @@ class Registry:
         self._entries: Dict[str, ModelEntry] = {}
         self._alias: Dict[str, str] = {}
         self._cache: Dict[str, tuple] = {}   # path -> (mtime, size, meta)
+        self.generation = 0                  # bumped whenever a scan finds a different set of entries
+        self._t_scan = -1e9                  # monotonic time of the last scan
 
     def scan(self) -> List[ModelEntry]:
         entries: Dict[str, ModelEntry] = {}
@@ -91,9 +94,13 @@ class Registry:
             entries.setdefault(e.id, e)
             for a in [e.id] + list(e.aliases):
                 alias.setdefault(a.lower(), e.id)
+        sig = lambda es: {k: (e.path, e.size_bytes, e.max_context_length) for k, e in es.items()}  # noqa: E731
         with self._lock:
+            if sig(entries) != sig(self._entries):
+                self.generation += 1
             self._entries = entries
             self._alias = alias
+            self._t_scan = time.monotonic()
         return list(entries.values())
 
     def _entry(self, pub, mdir, d, path, fname, idx, n) -> Optional[ModelEntry]:
@@ -132,6 +139,7 @@ class Registry:
                 self._alias.setdefault(a.lower(), e.id)
         self._extra = getattr(self, "_extra", {})
         self._extra[e.id] = e
+        self.generation += 1
 
     def resolve(self, ident: str) -> Optional[ModelEntry]:
         with self._lock:
@@ -144,8 +152,16 @@ class Registry:
         with self._lock:
             return list(self._entries.values())
 
-    def list_api(self, loaded_ids=()) -> dict:
-        self.scan()
+    # list_models re-reads the tree at most this often (pull / delete / sync re-scan at once): a model copied
+    # into MODELS_DIR by hand is listed within a second, and a burst of list requests costs one directory walk
+    RESCAN_S = 1.0
+
+    def refresh(self, max_age: float = None):
+        if time.monotonic() - self._t_scan > (self.RESCAN_S if max_age is None else max_age):
+            self.scan()
+
+    def list_api(self, loaded_ids=(), max_age: float = None) -> dict:
+        self.refresh(max_age)
         loaded = set(loaded_ids)
         return {"object": "list", "data": [e.to_api(e.id in loaded) for e in self.entries()]}
 

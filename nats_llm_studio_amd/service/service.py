@@ -26,13 +26,19 @@ from collections import defaultdict
 from typing import Optional
 
 from . import envelope
-from .backends import DeadlineExceeded, EngineBackend, HttpBackend, StubBackend
+from .backends import EngineBackend, HttpBackend, StubBackend
 from .config import WorkerConfig
 from .registry import Registry
 from .store import ModelStore, PullError
 from ..natsio import Client
 from ..utils.metrics import LatencyHistogram
 from ..utils.tracing import Tracer
+
+
+def _is_timeout(e: BaseException) -> bool:
+    import socket
+    return isinstance(e, (socket.timeout, TimeoutError)) or isinstance(getattr(e, "reason", None),
+                                                                         (socket.timeout, TimeoutError))
 
 
 class Service:
@@ -55,6 +61,8 @@ class Service:
         self.latency = defaultdict(LatencyHistogram)
         self.tracer = Tracer()
         self._lock = threading.Lock()
+        self._unloader = None         # persistent thread of the delete handler's bounded unload
+        self._list_cache = {}         # (registry generation, loaded ids) -> encoded list_models reply
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "Service":
@@ -101,28 +109,24 @@ class Service:
                 self.latency[name].add(time.perf_counter() - t0)
         return handler
 
-    @staticmethod
-    def _bounded(fn, seconds: float):
-        """fn() under a handler context of `seconds` (the reference's per-subject context.WithTimeout:
-        list 30 s, delete 2 min, `nats_llm_studio.go:229`, `:289`): the work runs on a helper thread and
-        DeadlineExceeded is raised when it has not finished in time (it may still complete afterwards, as
-        a Go RemoveAll does after its caller's context expired)."""
-        if seconds is None or seconds <= 0:
-            return fn()
-        box, ev = {}, threading.Event()
-
-        def run():
-            try:
-                box["v"] = fn()
-            except BaseException as e:        # noqa: BLE001 -- re-raised in the handler
-                box["e"] = e
-            ev.set()
-        threading.Thread(target=run, name="nls-handler-op", daemon=True).start()
-        if not ev.wait(seconds):
-            raise DeadlineExceeded("context deadline exceeded")
-        if "e" in box:
-            raise box["e"]
-        return box.get("v")
+    def _unload_bounded(self, model_id: str, deadline: Optional[float]) -> bool:
+        """The engine unload under the delete handler's context, like `lms unload` under
+        exec.CommandContext (`nats_llm_studio.go:87-97`): it runs on the service's one persistent unload
+        thread (no thread per request) and a call still running at the deadline is logged and left to
+        finish -- the unload is best effort in the reference too. True when it finished in time."""
+        if deadline is None:
+            self.backend.unload(model_id)
+            return True
+        if self._unloader is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._unloader = ThreadPoolExecutor(max_workers=1, thread_name_prefix="nls-unload")
+        fut = self._unloader.submit(self.backend.unload, model_id)
+        try:
+            fut.result(timeout=max(0.0, deadline - time.monotonic()))
+            return True
+        except Exception as e:                    # timeout, or the unload itself failed: logged, not fatal
+            print(f"warning: failed to unload model {model_id}: {e or 'context deadline exceeded'}", flush=True)
+            return False
 
     def respond(self, msg, body: bytes):
         """respondJSON (`nats_llm_studio.go:207-217`): log (not raise) when there is no reply subject."""
@@ -145,28 +149,37 @@ class Service:
     def on_list_models(self, msg):
         if isinstance(self.backend, HttpBackend):           # `nats_llm_studio.go:228-248`
             try:
-                status, body = self._bounded(self.backend.list_models_raw, self.cfg.timeout_list)
-            except DeadlineExceeded:
-                self.respond(msg, envelope.error("error calling LM Studio: context deadline exceeded",
-                                                 {"http_status": 0}))
-                return
+                # the 30 s context bounds the HTTP call itself (no helper thread)
+                status, body = self.backend.list_models_raw(timeout=self.cfg.timeout_list or None)
             except Exception as e:
+                if _is_timeout(e):
+                    e = "context deadline exceeded"
                 self.respond(msg, envelope.error(f"error calling LM Studio: {e}", {"http_status": 0}))
                 return
             raw = self._raw_json(body)
             self.respond(msg, envelope.FALLBACK if raw is None else
                          envelope.ok({"http_status": status, "models": raw}))
             return
+        # an in-memory registry snapshot: read inline on the handler thread (the RTT path of BASELINE config 1)
+        # and held to the 30 s context afterwards -- a thread per request cost ~0.1 ms of the ~0.08 ms RTT
+        t0 = time.monotonic()
         try:
-            models = self._bounded(lambda: self.registry.list_api(self.backend.loaded_ids()), self.cfg.timeout_list)
-        except DeadlineExceeded:
-            self.respond(msg, envelope.error("error reading model registry: context deadline exceeded",
-                                             {"http_status": 0}))
-            return
+            loaded = tuple(self.backend.loaded_ids())
+            self.registry.refresh()
+            key = (self.registry.generation, loaded)
+            body = self._list_cache.get(key)
+            if body is None:
+                # the encoded reply of an unchanged snapshot is reused (one per registry generation + loaded set)
+                body = envelope.ok({"http_status": 200, "models": self.registry.list_api(loaded)})
+                self._list_cache = {key: body}
         except Exception as e:
             self.respond(msg, envelope.error(f"error reading model registry: {e}", {"http_status": 0}))
             return
-        self.respond(msg, envelope.ok({"http_status": 200, "models": models}))
+        if self.cfg.timeout_list and time.monotonic() - t0 > self.cfg.timeout_list:
+            self.respond(msg, envelope.error("error reading model registry: context deadline exceeded",
+                                             {"http_status": 0}))
+            return
+        self.respond(msg, body)
 
     def on_pull_model(self, msg):
         err = envelope.go_json_error(msg.data, "PullModelRequest", {"identifier": "Identifier"})
@@ -212,35 +225,32 @@ class Service:
         if not mid:
             self.respond(msg, envelope.error("'model_id' is required"))
             return
-        replies = []
-        # unload + lookup + rmtree under the handler's 2-minute context (`nats_llm_studio.go:289`)
-        try:
-            self._bounded(lambda: self._delete(mid, replies.append), self.cfg.timeout_delete)
-        except DeadlineExceeded:
-            replies[:] = [envelope.failure("context deadline exceeded", {"model_id": mid, "dir": ""})]
-        self.respond(msg, replies[0] if replies else envelope.failure("delete failed", {"model_id": mid, "dir": ""}))
+        deadline = time.monotonic() + self.cfg.timeout_delete if self.cfg.timeout_delete > 0 else None
+        self.respond(msg, self._delete(mid, deadline))
 
-    def _delete(self, mid: str, reply):
+    def _delete(self, mid: str, deadline: Optional[float]) -> bytes:
+        """DeleteModel (`nats_llm_studio.go:99-133`) under the handler's 2-minute context (`:289`): the
+        context bounds the unload (`:104`) and the model lookup (`:106`); the directory check and removal
+        run to completion, so the reply always says what happened to the files."""
         self.registry.scan()
         ent = self.registry.resolve(mid)
         if ent is None:
-            reply(envelope.failure(f"model not found: {mid}", {"model_id": mid, "dir": ""}))
-            return
-        self.backend.unload(ent.id)                       # best effort, like `lms unload` (`:87-97`)
+            return envelope.failure(f"model not found: {mid}", {"model_id": mid, "dir": ""})
+        self._unload_bounded(ent.id, deadline)             # best effort, like `lms unload` (`:87-97`)
+        if deadline is not None and time.monotonic() > deadline:
+            # the reference's info lookup fails on the expired context (`:106-109`): nothing is removed
+            return envelope.failure("context deadline exceeded", {"model_id": mid, "dir": ""})
         d = ent.dir
         if not self.registry.safe_dir(d):
-            reply(envelope.failure(f"refusing to delete outside MODELS_DIR: {d}", {"model_id": mid, "dir": d}))
-            return
+            return envelope.failure(f"refusing to delete outside MODELS_DIR: {d}", {"model_id": mid, "dir": d})
         if not os.path.isdir(d):
-            reply(envelope.failure(f"model directory not found: {d}", {"model_id": mid, "dir": d}))
-            return
+            return envelope.failure(f"model directory not found: {d}", {"model_id": mid, "dir": d})
         try:
             ModelStore.remove_dir(d)
         except OSError as e:
-            reply(envelope.failure(f"error removing model directory {d}: {e}", {"model_id": mid, "dir": d}))
-            return
+            return envelope.failure(f"error removing model directory {d}: {e}", {"model_id": mid, "dir": d})
         self.registry.scan()
-        reply(envelope.ok({"model_id": mid, "deleted_dir": d}))
+        return envelope.ok({"model_id": mid, "deleted_dir": d})
 
     def on_chat_model(self, msg):
         t_recv = time.monotonic()

@@ -70,6 +70,17 @@ def _run(eng):
     while not all(f.done() for f in futs):
         eng.step()
     toks.append([f.result().token_ids for f in futs])
+    # mixed batch: a candidate-exact top-k row beside a row that forces the host-sampled path (repeat_penalty
+    # < 1). While both run, every TP step samples on the host; once the short one finishes, the long row goes
+    # back to the in-step sampler, whose penalty history ring must hold the tokens the host drew meanwhile.
+    mix_long = SamplingParams(max_tokens=12, temperature=0.9, top_k=40, repeat_penalty=3.0, presence_penalty=1.0,
+                              seed=21, ignore_eos=True)
+    mix_short = SamplingParams(max_tokens=4, temperature=0.8, top_k=10, repeat_penalty=0.7, seed=22,
+                               ignore_eos=True)
+    futs = [eng.submit(GenRequest(list(PROMPTS[0]), mix_long)), eng.submit(GenRequest(list(PROMPTS[1]), mix_short))]
+    while not all(f.done() for f in futs):
+        eng.step()
+    toks.append([f.result().token_ids for f in futs])
     return toks, lg
 
 

@@ -39,3 +39,22 @@ def test_masked_logits_and_seeded_reproducibility():
     assert toks == [sample_rows(lg.clone(), [p], [[]], [uniform01(42, i)])[0] for i in range(50)]
     top5 = set(torch.topk(lg[0], 5).indices.tolist())
     assert set(toks) <= top5 and all(t % 2 == 1 for t in toks)
+
+
+def test_omitted_fields_follow_the_documented_profile(monkeypatch):
+    """Parity unpinned (no reference fixture): omitted sampling fields of a SAMPLING request take LM Studio's
+    preset (top-k 40, top-p 0.95, min-p 0.05, repeat penalty 1.1); omitted / zero temperature stays greedy;
+    explicit fields always win; NLS_SAMPLING_DEFAULTS selects lmstudio-full / neutral."""
+    from nats_llm_studio_amd.engine.sampling import SamplingParams as S
+    monkeypatch.delenv("NLS_SAMPLING_DEFAULTS", raising=False)
+    p = S.from_request({"model": "m", "temperature": 0.7})          # the reference README's payload
+    assert (p.temperature, p.top_k, p.top_p, p.min_p, p.repeat_penalty) == (0.7, 40, 0.95, 0.05, 1.1)
+    assert S.from_request({"model": "m"}).greedy and S.from_request({"temperature": 0}).greedy
+    p = S.from_request({"temperature": 0.9, "top_k": 0, "top_p": 1.0, "min_p": 0, "repeat_penalty": 1.0})
+    assert (p.top_k, p.top_p, p.min_p, p.repeat_penalty) == (0, 1.0, 0.0, 1.0)
+    monkeypatch.setenv("NLS_SAMPLING_DEFAULTS", "lmstudio-full")
+    p = S.from_request({"model": "m"})
+    assert (p.temperature, p.top_k, p.repeat_penalty) == (0.8, 40, 1.1) and not p.greedy
+    monkeypatch.setenv("NLS_SAMPLING_DEFAULTS", "neutral")
+    p = S.from_request({"temperature": 0.7})
+    assert (p.top_k, p.top_p, p.min_p, p.repeat_penalty) == (0, 1.0, 0.0, 1.0)

@@ -90,3 +90,28 @@ def test_native_merge_loop_matches_python(tiny_models, name):
         finally:
             tok.native = keep
         assert nat == ref, (t, nat, ref)
+
+
+def test_spm_duplicate_token_strings_native_matches_python():
+    """A vocabulary that holds the same string twice (seen in converted GGUFs): the native SentencePiece core
+    keeps the LAST id, like the Python reference's {t: i} map and llama.cpp's token_to_id."""
+    from nats_llm_studio_amd.tokenizer import bpe
+    if bpe._tokcore is None:
+        pytest.skip("native tokenizer core not built")
+    toks = ["<unk>", "<s>", "</s>"] + [f"<0x{b:02X}>" for b in range(256)] + \
+        ["▁", "a", "b", "ab", "▁a", "ab", "▁ab", "b", "▁b", "ba"]
+    types = [bpe.TOKEN_TYPE_UNKNOWN, bpe.TOKEN_TYPE_CONTROL, bpe.TOKEN_TYPE_CONTROL] + \
+        [bpe.TOKEN_TYPE_BYTE] * 256 + [bpe.TOKEN_TYPE_NORMAL] * 10
+    scores = [0.0] * 259 + [-1.0, -2.0, -2.5, -0.5, -0.7, -0.4, -0.3, -2.2, -0.9, -1.5]
+    tok = bpe.SentencePieceBPE(toks, scores, types)
+    assert tok.native is not None
+    for t in ["ab", "a b", "abab ba", "bab", "b a ab ba ab", "xyz ab", "ababababab"]:
+        nat = tok.encode(t, add_bos=False)
+        keep, tok.native = tok.native, None
+        try:
+            ref = tok.encode(t, add_bos=False)
+        finally:
+            tok.native = keep
+        assert nat == ref, (t, nat, ref)
+    assert tok.encode("ab", add_bos=False) == [259 + 6]          # "▁ab": the only id of that string
+    assert tok.encode("bab", add_bos=False) == [259 + 8, 259 + 5]  # "▁b" + the duplicate "ab": its LAST id
