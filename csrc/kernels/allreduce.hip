@@ -17,8 +17,14 @@
 // call ahead of any peer (it cannot finish call c+1 without every peer's call-c+1 data, which a peer
 // writes only after finishing c). Epochs are kept per SLOT BLOCK (per row slice in the fused add+norm)
 // and a call writes every granule of every block it advances, so at epoch e a slot holds the peer's
-// epoch e - 2 granule or its epoch e granule -- a skipped block keeps its epoch too. The consumer never
-// writes its own receive slots (see SlotBlocks below for why that matters).
+// epoch e - 2 granule or its epoch e granule -- a skipped block keeps its epoch too. The plain all-reduce and
+// the gather never write their own receive slots (see SlotBlocks below); the fused add+norm DOES, by default:
+// it re-tags each consumed granule with the other parity's tag (AR_OPT_RETAG, NLS_AR_RETAG=0 disables), the
+// round-3 protocol, which the simulated-rank test measured as needed (cause not established).
+// Eager (non-captured) calls: on two ranks sharing ONE GPU, a peer's push into the parity-1 half of the
+// receive buffer was repeatedly never seen by the owner (profiles/tp_oneshot_eager_r04.txt,
+// profiles/tp_oneshot_eager_r05.txt); parallel/comm.py routes eager collectives to RCCL by default -- a
+// WORKAROUND, the one-shot kernels run inside captured decode graphs only (NLS_ONESHOT_EAGER=1 restores them).
 // Every rank uses the ROUNDED value of its own partial too, so the sums stay bit-identical.
 //
 // Element -> workgroup maps are fixed (the plain all-reduce runs a FIXED grid, grid-stride; the
@@ -164,6 +170,7 @@ constexpr long AR_OPT_POLL_INV = 1L << 62;    // system-scope acquire (L2 invali
 constexpr long AR_OPT_RETAG = 1L << 61;       // fused add+norm: re-tag consumed granules (the round-3 protocol)
 constexpr long AR_OPT_EP_RMW = 1L << 60;      // epoch counters read / written by atomic read-modify-writes
 constexpr long AR_OPT_POLL_RMW = 1L << 59;    // peer granules polled by atomic read-modify-writes (OR 0)
+constexpr long AR_OPT_PROBE = 1L << 58;       // fused add+norm: read every push back (RMW) and log a mismatch
 constexpr long AR_SPIN_MASK = (1L << 48) - 1;
 
 __device__ __forceinline__ unsigned ep_get(unsigned* p, long opts) {
@@ -330,6 +337,27 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     // 1) push this rank's partial slice to every peer
     for (int p = 0; p < world; ++p)
       if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + (long)b * D + col, g);
+    if (max_spins & AR_OPT_PROBE) {
+      // diagnostics: the pushed granule as memory holds it right after the store has completed; a mismatch is
+      // logged in THIS rank's error area (words 24..31: marker, row, slice, epoch, peer, written, read back, col)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int p = 0; p < world; ++p) {
+        if (p == rank) continue;
+        const uint4 rb = ar_load_rmw(P.buf[p] + ((long)(par * world + rank)) * cap + (long)b * D + col);
+        if (rb.x != g.x || rb.y != g.y || rb.z != g.z || rb.w != g.w) {
+          uint32_t* dw = ar_err_word(P.buf[rank], world, cap);
+          if (atomicCAS(dw + 24, 0u, 0xC33u) == 0u) {
+            dw[25] = (uint32_t)b;
+            dw[26] = (uint32_t)c;
+            dw[27] = ep;
+            dw[28] = (uint32_t)p;
+            dw[29] = g.x;
+            dw[30] = rb.x;
+            dw[31] = (uint32_t)col;
+          }
+        }
+      }
+    }
     // 2) rank-ordered sum + residual add (bit-identical on every rank); consumed granules get the other
     //    parity's tag (AR_OPT_RETAG, default on). Every call that advances eidx's epoch has the peer write
     //    ALL of the slice's granules, so the protocol itself does not need the re-tag; the simulated-rank
@@ -554,8 +582,10 @@ static long ar_opts(long max_spins) {
     const char* d = getenv("NLS_AR_POLL_RMW");
     if (a && atoi(a)) o |= AR_OPT_POLL_INV;
     if (!b || atoi(b)) o |= AR_OPT_RETAG;      // default on: the simulated-rank tests need it (round 4)
+    const char* e = getenv("NLS_AR_PROBE");
     if (c && atoi(c)) o |= AR_OPT_EP_RMW;
     if (d && atoi(d)) o |= AR_OPT_POLL_RMW;
+    if (e && atoi(e)) o |= AR_OPT_PROBE;
     return o;
   }();
   return (max_spins & AR_SPIN_MASK) | opts;

@@ -11,6 +11,7 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
 }
 namespace nls_hg10 {
 int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
+int launch_q11(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
 }
 namespace nls_q9 {
 int launch_q9(int kset, int waves, int rt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
@@ -55,6 +56,8 @@ struct NlsFuse {
 // mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
 // mode 10: dense f16 GEMM, 256 x 256 tiles, 4 phases per 64-deep K-tile with the two wave groups staggered
 //         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
+// mode 11: mode 10's schedule on the RAW Q4_K / Q6_K tile-blocks, dequantised once per workgroup into the f16
+//         LDS image (hgemm10.hip); rt 1 (256-row weight tiles, Q4_K only) or 2 (128-row), optional split-K.
 // mode 9: quantised GEMM on the raw tile-blocks (qgemm9.hip; Q4_K/Q5_K/Q6_K/Q8_0/Q51): 256-row activation
 //         blocks x 16*waves*rt weight rows ((waves, rt) = (4, 2) | (8, 2) | (8, 1)), the mode-8
 //         epilogues, optional split-K.
@@ -75,7 +78,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A or a dense GEMM without split-K; plain rows,
                            // contiguous Q|K|V segments
-    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10) && ks <= 1)) || argmax || !fz->pos || !fz->slot ||
+    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10 || mode == 11) && ks <= 1)) || argmax || !fz->pos || !fz->slot ||
         !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 || fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
       return -1;
     int c = 0;
@@ -99,8 +102,16 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
-  if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
+  if (mode < 0 || mode > 11 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode == 11) {     // rt 1: 256-row weight tiles (Q4_K), rt 2: 128-row (Q4_K / Q6_K)
+    if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
+        ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
+      return -1;
+    for (int i = 0; i < nseg; ++i)
+      if (!(segs[i].type == QT_Q4_K || (segs[i].type == QT_Q6_K && rt == 2)) || segs[i].xmap || segs[i].ymap ||
+          segs[i].mcount || segs[i].ycol % 4)
+        return -1;
+  } else if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
@@ -131,7 +142,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = (mode == 10 || mode == 11) ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -232,6 +243,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     int rc;
     if (mode == 10)
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
+    else if (mode == 11)
+      rc = nls_hg10::launch_q11(256 / rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode >= 4)

@@ -644,10 +644,10 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        if (mode in (4, 5, 10) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D and not neox and fuse_rope
-                and kc.dtype == torch.bfloat16):
-            # dense GEMM on the f16 copies with RoPE + KV append in its epilogue (no f32 qkv round trip,
-            # no RoPE launch)
+        if (mode in (4, 5, 10, 11) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D and not neox
+                and fuse_rope and kc.dtype == torch.bfloat16):
+            # large-M GEMM (dense f16 copies, or mode 11 on the quantised tile-blocks) with RoPE + KV append in
+            # its epilogue (no f32 qkv round trip, no RoPE launch)
             fz = _lib.NlsFuse(pos=pos.data_ptr(), slot=slot.data_ptr(), cs=cs.data_ptr(), bias=_p(bias),
                               q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
                               Hq=Hq, Hkv=Hkv, D=D)

@@ -150,11 +150,16 @@ class OneShotAllReduce:
         # per buffer set: [error, a, b, epoch, peer, first dword seen (tag = low 2 bits), marker, kernel]
         # (add+norm: a row, b slice; the others: a granule, b granules of the call)
         for name, buf in (("sum", self.buf), ("addnorm", self.nbuf), ("gather", self.gbuf)):
-            host = torch.zeros(20, dtype=torch.int32)
-            _lib.check(L.nls_ar_err_words(buf, self.cap, self.world, host.data_ptr(), 20, st), "nls_ar_err_words")
+            host = torch.zeros(32, dtype=torch.int32)
+            _lib.check(L.nls_ar_err_words(buf, self.cap, self.world, host.data_ptr(), 32, st), "nls_ar_err_words")
             torch.cuda.synchronize(self.device)
             w = host.tolist()
             out[f"timeout_{name}"] = w[:8]
+            if name == "addnorm" and w[24]:
+                # NLS_AR_PROBE: a push of THIS rank that memory did not hold right after the store completed
+                out["push_readback_mismatch"] = dict(row=w[25], slice=w[26], epoch=w[27], peer=w[28],
+                                                     written=hex(w[29] & 0xFFFFFFFF), read_back=hex(w[30] & 0xFFFFFFFF),
+                                                     col=w[31])
             if name == "addnorm" and w[6] and w[19]:
                 # words 8..18: the granule the last poll saw, the lane's column, its XCD, the epoch counter
                 # re-read at the timeout and the granule read by an atomic RMW; plus the slot as memory holds
@@ -175,6 +180,39 @@ class OneShotAllReduce:
         for D, (ep, tk, _sq) in self._norm.items():
             nblk = ep.numel() // tk.numel()
             out[f"addnorm{D}_epochs_rows0_23"] = ep.view(-1, nblk)[:24].tolist()
+        # the PUSHING side's view: for a peer whose add+norm poll timed out waiting for THIS rank, read that
+        # slot through this rank's IPC mapping of the peer's buffer (where this rank's kernel wrote) -- compare
+        # with the peer's own "slot_memory_now"; and whether an imported range overlaps this process's own
+        # allocations (a mapping shorter than the buffer would let later allocations land inside it)
+        D = next(iter(self._norm)) if self._norm else 0
+        for p in range(self.world):
+            if p == self.rank or not self.npeers[p]:
+                continue
+            host = torch.zeros(20, dtype=torch.int32)
+            _lib.check(L.nls_ar_err_words(self.npeers[p], self.cap, self.world, host.data_ptr(), 20, st),
+                       "nls_ar_err_words")
+            torch.cuda.synchronize(self.device)
+            w = host.tolist()
+            if w[6] and w[19] and w[4] == self.rank and D:
+                view = {}
+                for par in (0, 1):
+                    pk = torch.zeros(4, dtype=torch.int32)
+                    off = (par * self.world + self.rank) * self.cap + w[1] * D + w[12]
+                    _lib.check(L.nls_ar_peek(self.npeers[p], off, 4, pk.data_ptr(), st), "nls_ar_peek")
+                    torch.cuda.synchronize(self.device)
+                    view[par] = [hex(v & 0xFFFFFFFF) for v in pk.tolist()]
+                out[f"pusher_view_of_rank{p}"] = dict(row=w[1], col=w[12], epoch=w[3], slot_memory=view)
+        nbytes = L.nls_ar_buffer_bytes(self.cap, self.world)
+        imported = [(n, int(ptr)) for n, arr in (("sum", self.peers), ("addnorm", self.npeers), ("gather", self.gpeers))
+                    for r, ptr in enumerate(arr) if ptr and r != self.rank]
+        try:
+            segs = [(s["address"], s["total_size"]) for s in torch.cuda.memory_snapshot()]
+        except Exception:
+            segs = []
+        out["imported_overlaps"] = [dict(buf=n, ptr=hex(ptr), seg=hex(a), seg_bytes=sz) for n, ptr in imported
+                                    for a, sz in segs if a < ptr + nbytes and ptr < a + sz]
+        out["imported_ptrs"] = [(n, hex(ptr)) for n, ptr in imported]
+        out["own_ptrs"] = [hex(int(b)) for b in (self.buf, self.nbuf, self.gbuf)]
         return out
 
     def reset(self):

@@ -146,7 +146,9 @@ class ByteLevelBPE(_Base):
 
     def _encode_plain(self, text: str) -> List[int]:
         if self.native is not None:
-            return self.native.encode_pieces([p.encode("utf-8") for p in self.pretok.findall(text)])
+            # concurrent=True: the regex scan releases the GIL (handler threads of a request burst pre-tokenise in
+            # parallel; the merge loop below releases it too)
+            return self.native.encode_pieces([p.encode("utf-8") for p in self.pretok.findall(text, concurrent=True)])
         return self._encode_plain_py(text)
 
     def _encode_plain_py(self, text: str) -> List[int]:

@@ -1140,6 +1140,78 @@ def test_qgemm9_swiglu_multiseg(gpu, waves, rt, ks):
     _close(yq[:M], y2[:M], 1e-3)
 
 
+@pytest.mark.parametrize("t,M,rt,ks", [(GGMLType.Q4_K, 256, 1, 1), (GGMLType.Q4_K, 300, 1, 2), (GGMLType.Q4_K, 100, 2, 3),
+                                        (GGMLType.Q4_K, 512, 1, 1), (GGMLType.Q4_K, 520, 2, 2), (GGMLType.Q6_K, 256, 2, 1),
+                                        (GGMLType.Q6_K, 300, 2, 3), (GGMLType.Q6_K, 520, 2, 1), (GGMLType.Q4_K, 64, 1, 12)])
+def test_qgemm11_types(gpu, t, M, rt, ks):
+    """Mode 11 (hgemm10.hip q11_tile: mode 10's staggered schedule, the weight operand DMA'd as RAW Q4_K / Q6_K
+    bytes and dequantised once per workgroup into the f16 LDS image): a partial last weight tile (264 rows over
+    256 / 128-row tiles), partial activation blocks, k-slices down to one K-tile (ks 12 at K 768) through the
+    slab reduce; f32 store with arg-max keys, residual add with alpha -- against the fp32 torch reference."""
+    rows, K = 264, 768
+    w, Wd = _qw(rows, K, t, gpu)
+    x = _x(M, K, gpu)
+    pad = x.shape[0]
+    y = torch.zeros(pad, rows, device=gpu)
+    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, mode=11, waves=8, rt=rt, ks=ks, argmax=keys if ks == 1 else None)
+    ref = x[:M].float().cpu() @ Wd.t()
+    _close(y[:M], ref)
+    if M < pad:
+        assert float(y[M:].abs().max().cpu()) == 0.0
+    if ks == 1:
+        ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+        ops.argmax_unpack(keys, M, ids)
+        assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+    base = torch.randn(pad, rows, device=gpu)
+    y2 = base.clone()
+    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=11, waves=8, rt=rt, ks=ks)
+    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
+
+
+def test_qgemm11_rejects_q6k_256(gpu):
+    """Mode 11 runs Q6_K only on 128-row weight tiles (LDS budget): a 256-row launch is refused, not run."""
+    w, _ = _qw(256, 512, GGMLType.Q6_K, gpu)
+    x = _x(256, 512, gpu)
+    y = torch.zeros(x.shape[0], 256, device=gpu)
+    with pytest.raises(RuntimeError):
+        ops.qgemv([ops.Seg(w)], x, y, 256, mode=11, waves=8, rt=1, ks=1)
+
+
+@pytest.mark.parametrize("rt,ks", [(1, 1), (2, 1), (1, 2)])
+def test_qgemm11_swiglu_multiseg(gpu, rt, ks):
+    """Mode 11 SwiGLU epilogue on interleaved gate/up tile-blocks, and a Q|K|V-style launch mixing Q4_K and
+    Q6_K segments (128-row tiles: each workgroup dequantises its own segment's format) at column offsets."""
+    K, F = 512, 256
+    rng = np.random.default_rng(9)
+    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
+    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
+    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
+    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
+    M = 333
+    x = _x(M, K, gpu)
+    xf = x[:M].float().cpu()
+    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
+    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=11, waves=8, rt=rt, ks=ks)
+    _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
+    a, Ad = _qw(256, K, GGMLType.Q4_K, gpu, 1)
+    b, Bd = _qw(256, K, GGMLType.Q4_K, gpu, 2)
+    c, Cd = _qw(256, K, GGMLType.Q6_K, gpu, 3)
+    segs = [ops.Seg(a, 0), ops.Seg(b, 256), ops.Seg(c, 512)]
+    yq = torch.zeros(x.shape[0], 768, device=gpu)
+    ops.qgemv(segs, x, yq, M, mode=11, waves=8, rt=2, ks=ks)
+    _close(yq[:M], xf @ torch.cat([Ad, Bd, Cd]).t())
+
+
+@pytest.mark.parametrize("cfg", [(11, 8, 2, 1), (11, 8, 2, 2)])
+@pytest.mark.parametrize("M", [70, 300, 520])
+def test_qkv_rope_kv_quant11(gpu, cfg, M):
+    """Mode 11 on the quantised Q|K|V tile-blocks with the RoPE + KV-append epilogue (split-K 2: slabs summed by
+    the RoPE kernel): no f16 weight copies involved."""
+    _qkv_rope_case(gpu, cfg, M, False, dense=False)
+
+
 def test_hgemm_dense_add_rmsnorm_slabs(gpu):
     """Mode 4 split-K slabs feeding the fused reduce + residual + RMSNorm kernel (o / down projections)."""
     D, K, M = 512, 1024, 200

@@ -56,6 +56,8 @@ def configs(K, M=1, quant=True):
                     if M >= 128:   # mode 9 (qgemm9.hip): 256 activation rows x 128 / 256 weight rows (8 waves),
                         # 128 weight rows on 4 waves (one per SIMD, 512 registers)
                         c += [(9, 8, 1, ks), (9, 8, 2, ks), (9, 4, 2, ks)]
+                        # mode 11 (hgemm10.hip): mode 10's schedule on the raw tile-blocks, 256 / 128 weight rows
+                        c += [(11, 8, 1, ks), (11, 8, 2, ks)]
         return c
     c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
     for waves in (4, 8):
@@ -111,6 +113,7 @@ def main():
     ap.add_argument("--log", default="gpurun_out/tune_gemv.log")
     ap.add_argument("--only", default="", help="comma list of shape names (qkv,qkv6,o,gateup,down,down6,lm_head)")
     ap.add_argument("--dense", action="store_true", help="tune mode 4 (dense f16) at M > 64")
+    ap.add_argument("--modes", default="", help="comma list: time only these kernel modes (e.g. 9,11)")
     ap.add_argument("--base", default="q4_k", choices=("q4_k", "q5_k"),
                     help="base tile type of the shapes (Q4_K_M models: q4_k; Q5_K_M, e.g. Mixtral: q5_k)")
     args = ap.parse_args()
@@ -174,7 +177,10 @@ def main():
                 log.write(line + "\n")
                 log.flush()
                 continue
+            modes = {int(m) for m in args.modes.split(",")} if args.modes else None
             for cfg in configs(K, M, all(int(t) in (8, 12, 13, 14) for t, _ in segdef)):
+                if modes is not None and cfg[0] not in modes:
+                    continue
                 us = time_cfg(copies, x, y, M, epi, keys, cfg)
                 if us is not None:
                     res.append((us, cfg))
