@@ -295,46 +295,64 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
 // polls run on 32 CUs), adds it into the residual and leaves its share of sum(x^2); the slice that
 // arrives last at the row's ticket (agent-scope release / acquire, cdna_hip_programming.md Guideline
 // 16) sums the shares and normalises the whole row. Receive slots: [parity][rank][cap], row b at b * D.
+// NLS_AR_PROBE timing history of the fused add+norm (this process's launches only): per workgroup slot eidx, the
+// last 8 epochs as {epoch, xcc, t_start, t_pushed, t_polled} on the device-wide 100 MHz clock (wall_clock64), which
+// two ranks sharing one GPU read identically -- a timed-out poll is placed against the peer's push of that epoch
+#define AR_PROBE_SLOTS 4096
+#define AR_PROBE_DEPTH 8
+struct ArProbeRec {
+  unsigned ep, xcc;
+  unsigned long long t0, t1, t2;
+};
+__device__ ArProbeRec g_ar_probe[AR_PROBE_SLOTS * AR_PROBE_DEPTH];
+
+// Items (row-rank rr, slice c) of one launch: rows rr = xcd + 8 m sit on XCD xcd (their tickets, shares and
+// residual slices stay inside one L2: a row spread over XCDs normalised with stale shares, round 4); the k
+// workgroups of an XCD take items m * nblk + c = j, j + k, ...
+struct AnItem {
+  int rr, c;
+};
+__device__ __forceinline__ AnItem an_item(int xcd, int k, int j, int t, int nblk) {
+  const int idx = j + t * k;
+  return AnItem{xcd + 8 * (idx / nblk), idx % nblk};
+}
+
+// Bounded grid (round 5): a launch has at most nls_ar_norm_wgs() workgroups (default 128, NLS_AR_NORM_WGS), each
+// pushing ALL of its items before it polls for any. One workgroup per item (rows x D/256 of them) put 1,664
+// polling waves on the GPU for a 52-row eager prefill chunk at D=8192; on one MI355X shared by two ranks the
+// PEER rank's preceding GEMM could then not be scheduled, its push came only after the owner's bounded poll had
+// expired (device-clock timestamps of both ranks, profiles/tp_oneshot_eager_r05.txt) -- the eager timeout of
+// rounds 3-4. Half the CUs at most now wait in this kernel.
+#define ARN_MAX_ITEMS 64
 __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
-    const float* __restrict__ part, long ldp, float* __restrict__ x, long ldx, const float* __restrict__ nw,
-    _Float16* __restrict__ h, long ldh, int D, float eps, ArPeers P, int world, int rank, long cap,
-    unsigned* __restrict__ epochs, int* __restrict__ tickets, float* __restrict__ ssq, int* __restrict__ err,
+    const float* __restrict__ part0, long ldp, float* __restrict__ x0, long ldx, const float* __restrict__ nw,
+    _Float16* __restrict__ h0, long ldh, int D, float eps, ArPeers P, int world, int rank0, long cap,
+    unsigned* __restrict__ epochs0, int* __restrict__ tickets0, float* __restrict__ ssq0, int* __restrict__ err,
     long max_spins, int sim, long sp, long sx, long sh, long se, long st, long sq, int nblk, int nrr) {
-  __shared__ unsigned s_ep;
+  __shared__ unsigned s_ep[ARN_MAX_ITEMS];
   __shared__ int s_last;
-  // 1-D grid, XCD-aligned (workgroup L runs on XCD L % 8): every slice of row-rank r = b * sim + rank sits on
-  // XCD r % 8, whatever the row count of the launch -- the row's ticket, sum-of-squares shares and residual
-  // slices are exchanged inside one L2 (a row spread over XCDs normalised with stale shares: round 4), and a
-  // slice's epoch counter is always touched from the same XCD. Workgroups past the last row exit at once.
-  const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
-  const int c = q % nblk, rr = (q / nblk) * 8 + xcd;
-  if (rr >= nrr) return;
-  int b = rr;
-  if (sim > 1) {
-    // single-GPU simulation: ALL ranks in one grid (rr = row * sim + rank, per-rank operand strides)
-    rank = rr % sim;
-    b = rr / sim;
-    part += rank * sp;
-    x += rank * sx;
-    h += rank * sh;
-    epochs += rank * se;
-    tickets += rank * st;
-    ssq += rank * sq;
+  const int L = blockIdx.x, xcd = L & 7, j = L >> 3, k = gridDim.x >> 3;
+  const int mx = nrr > xcd ? (nrr - xcd + 7) / 8 : 0;           // rows of this XCD
+  const int nit = mx * nblk > j ? (mx * nblk - 1 - j) / k + 1 : 0;  // items of this workgroup (<= ARN_MAX_ITEMS)
+  if (nit == 0) return;
+  const bool probe_on = (max_spins & AR_OPT_PROBE) && sim == 1;
+  const unsigned long long t0 = probe_on ? (unsigned long long)wall_clock64() : 0ull;
+  // the epochs of this call, one per item (a slice's counter is only ever touched by its own item)
+  for (int t = threadIdx.x; t < nit; t += ARN_THREADS) {
+    const AnItem it = an_item(xcd, k, j, t, nblk);
+    const int r = sim > 1 ? it.rr % sim : 0, b = sim > 1 ? it.rr / sim : it.rr;
+    s_ep[t] = ep_get(epochs0 + r * se + b * nblk + it.c, max_spins) + 1u;
   }
-  const int eidx = b * nblk + c;
-  if (threadIdx.x == 0) s_ep = ep_get(epochs + eidx, max_spins) + 1u;
   __syncthreads();
-  const unsigned ep = s_ep;
-  const uint32_t tag = ep & 3u;
-  const int par = (int)(ep & 1u);
-  const int col = c * ARN_VPB + 4 * threadIdx.x;
-  const bool act = col < D;
-  bool failed = false;
-  float ss = 0.f;
-  if (act) {
-    const float4 pv = *reinterpret_cast<const float4*>(part + (size_t)b * ldp + col);
-    const uint4 g = ar_pack4(pv, tag);
-    // 1) push this rank's partial slice to every peer
+  // 1) push: every item's partial slice to every peer
+  for (int t = 0; t < nit; ++t) {
+    const AnItem it = an_item(xcd, k, j, t, nblk);
+    const int rank = sim > 1 ? it.rr % sim : rank0, b = sim > 1 ? it.rr / sim : it.rr;
+    const float* part = part0 + (sim > 1 ? rank * sp : 0);
+    const unsigned ep = s_ep[t];
+    const int par = (int)(ep & 1u), col = it.c * ARN_VPB + 4 * threadIdx.x;
+    if (col >= D) continue;
+    const uint4 g = ar_pack4(*reinterpret_cast<const float4*>(part + (size_t)b * ldp + col), ep & 3u);
     for (int p = 0; p < world; ++p)
       if (p != rank) ar_store(P.buf[p] + ((long)(par * world + rank)) * cap + (long)b * D + col, g);
     if (max_spins & AR_OPT_PROBE) {
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
           uint32_t* dw = ar_err_word(P.buf[rank], world, cap);
           if (atomicCAS(dw + 24, 0u, 0xC33u) == 0u) {
             dw[25] = (uint32_t)b;
-            dw[26] = (uint32_t)c;
+            dw[26] = (uint32_t)it.c;
             dw[27] = ep;
             dw[28] = (uint32_t)p;
             dw[29] = g.x;
@@ -358,87 +376,117 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
         }
       }
     }
-    // 2) rank-ordered sum + residual add (bit-identical on every rank); consumed granules get the other
-    //    parity's tag (AR_OPT_RETAG, default on). Every call that advances eidx's epoch has the peer write
-    //    ALL of the slice's granules, so the protocol itself does not need the re-tag; the simulated-rank
-    //    test (all ranks in one launch, after other launches on reused buffers) failed without it and
-    //    passed with it -- unexplained, kept as the measured-safe default.
-    uint32_t* mine = P.buf[rank];
-    const float4 own = ar_val4(g);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int p = 0; p < world; ++p) {
-      float4 v = own;
-      if (p != rank) {
-        uint32_t* src = mine + ((long)(par * world + p)) * cap + (long)b * D + col;
-        const bool was = failed;
-        const uint4 gv = ar_poll(src, tag, max_spins, failed);
-        if (failed && !was) {
-          ar_diag(mine, world, cap, 2, b, c, ep, p, gv.x);
-          ar_diag2(mine, world, cap, gv, (uint32_t)col, ep_get(epochs + eidx, max_spins), ar_load_rmw(src));
+  }
+  const unsigned long long t1 = probe_on ? (unsigned long long)wall_clock64() : 0ull;
+  // 2) per item: rank-ordered sum + residual add (bit-identical on every rank); consumed granules get the other
+  //    parity's tag (AR_OPT_RETAG, default on). Every call that advances an item's epoch has the peer write ALL
+  //    of the slice's granules, so the protocol itself does not need the re-tag; the simulated-rank test (all
+  //    ranks in one launch, after other launches on reused buffers) failed without it and passed with it --
+  //    unexplained, kept as the measured-safe default.
+  bool failed = false;   // after one timeout, stop waiting (the error words are raised below)
+  for (int t = 0; t < nit; ++t) {
+    const AnItem it = an_item(xcd, k, j, t, nblk);
+    const int rank = sim > 1 ? it.rr % sim : rank0, b = sim > 1 ? it.rr / sim : it.rr;
+    const int ro = sim > 1 ? rank : 0;
+    float* x = x0 + ro * sx;
+    _Float16* h = h0 + ro * sh;
+    unsigned* epochs = epochs0 + ro * se;
+    int* tickets = tickets0 + ro * st;
+    float* ssq = ssq0 + ro * sq;
+    const float* part = part0 + ro * sp;
+    const int c = it.c, eidx = b * nblk + c;
+    const unsigned ep = s_ep[t];
+    const uint32_t tag = ep & 3u;
+    const int par = (int)(ep & 1u), col = c * ARN_VPB + 4 * threadIdx.x;
+    float ss = 0.f;
+    if (col < D) {
+      uint32_t* mine = P.buf[rank];
+      const float4 own = ar_val4(ar_pack4(*reinterpret_cast<const float4*>(part + (size_t)b * ldp + col), tag));
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int p = 0; p < world; ++p) {
+        float4 v = own;
+        if (p != rank) {
+          uint32_t* src = mine + ((long)(par * world + p)) * cap + (long)b * D + col;
+          const bool was = failed;
+          const uint4 gv = ar_poll(src, tag, max_spins, failed);
+          if (failed && !was) {
+            ar_diag(mine, world, cap, 2, b, c, ep, p, gv.x);
+            ar_diag2(mine, world, cap, gv, (uint32_t)col, ep_get(epochs + eidx, max_spins), ar_load_rmw(src));
+          }
+          v = ar_val4(gv);
+          if (max_spins & AR_OPT_RETAG) {
+            const uint32_t ct = (ep + 1u) & 3u;
+            ar_store(src, make_uint4(ct, ct, ct, ct));
+          }
         }
-        v = ar_val4(gv);
-        if (max_spins & AR_OPT_RETAG) {
-          const uint32_t ct = (ep + 1u) & 3u;
-          ar_store(src, make_uint4(ct, ct, ct, ct));
-        }
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
       }
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
+      float4* xp = reinterpret_cast<float4*>(x + (size_t)b * ldx + col);
+      float4 xv = *xp;
+      xv.x += acc.x;
+      xv.y += acc.y;
+      xv.z += acc.z;
+      xv.w += acc.w;
+      wt_store4(reinterpret_cast<float*>(xp), xv);
+      ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
     }
-    float4* xp = reinterpret_cast<float4*>(x + (size_t)b * ldx + col);
-    float4 xv = *xp;
-    xv.x += acc.x;
-    xv.y += acc.y;
-    xv.z += acc.z;
-    xv.w += acc.w;
-    wt_store4(reinterpret_cast<float*>(xp), xv);
-    ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
-  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-  const unsigned long long fm = __ballot(failed);
-  // 3) publish the slice (x stores + share), then the row ticket: the last slice normalises the row
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (threadIdx.x == 0) {
-    __hip_atomic_store((gu32*)(ssq + eidx), __float_as_uint(ss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ep_put(epochs + eidx, ep, max_spins);
-    if (fm) ar_raise(P, world, cap, err);
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    const unsigned long long fm = __ballot(failed);
+    if (probe_on && threadIdx.x == 0 && eidx < AR_PROBE_SLOTS) {
+      ArProbeRec& r = g_ar_probe[eidx * AR_PROBE_DEPTH + (ep & (AR_PROBE_DEPTH - 1))];
+      r.ep = ep;
+      r.xcc = xcc_id() | (fm ? 0x100u : 0u);
+      r.t0 = t0;
+      r.t1 = t1;
+      r.t2 = (unsigned long long)wall_clock64();
+    }
+    // 3) publish the slice (x stores + share), then the row ticket: the last slice normalises the row
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(tickets + b), 1, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store((gu32*)(tickets + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  float tot = 0.f;
-  for (int i = threadIdx.x; i < nblk; i += ARN_THREADS)
-    tot += __uint_as_float(__hip_atomic_load((const gu32*)(ssq + (size_t)b * nblk + i), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
+    if (threadIdx.x == 0) {
+      __hip_atomic_store((gu32*)(ssq + eidx), __float_as_uint(ss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ep_put(epochs + eidx, ep, max_spins);
+      if (fm) ar_raise(P, world, cap, err);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s_last = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(tickets + b), 1, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((gu32*)(tickets + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      float tot = 0.f;
+      for (int i = threadIdx.x; i < nblk; i += ARN_THREADS)
+        tot += __uint_as_float(__hip_atomic_load((const gu32*)(ssq + (size_t)b * nblk + i), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  const float inv = rsqrtf(tot / (float)D + eps);
-  const float* xr = x + (size_t)b * ldx;
-  _Float16* hr = h + (size_t)b * ldh;
+      for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+      const float inv = rsqrtf(tot / (float)D + eps);
+      const float* xr = x + (size_t)b * ldx;
+      _Float16* hr = h + (size_t)b * ldh;
 #pragma unroll 4
-  for (int i = 4 * threadIdx.x; i < D; i += 4 * ARN_THREADS) {
-    const float4 xv = *reinterpret_cast<const float4*>(xr + i);
-    const float4 wv = *reinterpret_cast<const float4*>(nw + i);
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    h4 o;
-    o[0] = (_Float16)(xv.x * inv * wv.x);
-    o[1] = (_Float16)(xv.y * inv * wv.y);
-    o[2] = (_Float16)(xv.z * inv * wv.z);
-    o[3] = (_Float16)(xv.w * inv * wv.w);
-    *reinterpret_cast<h4*>(hr + i) = o;
+      for (int i = 4 * threadIdx.x; i < D; i += 4 * ARN_THREADS) {
+        const float4 xv = *reinterpret_cast<const float4*>(xr + i);
+        const float4 wv = *reinterpret_cast<const float4*>(nw + i);
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 o;
+        o[0] = (_Float16)(xv.x * inv * wv.x);
+        o[1] = (_Float16)(xv.y * inv * wv.y);
+        o[2] = (_Float16)(xv.z * inv * wv.z);
+        o[3] = (_Float16)(xv.w * inv * wv.w);
+        *reinterpret_cast<h4*>(hr + i) = o;
+      }
+    }
+    __syncthreads();     // s_last is reused by the next item
   }
 }
 
@@ -573,6 +621,17 @@ __global__ void ar_reinit_kernel(uint32_t* buf, long half) {
     buf[i] = i < half ? 0x01010101u : 0u;
 }
 
+// workgroups of one fused add+norm launch at most (multiple of 8, >= 8): NLS_AR_NORM_WGS, default 128
+static int nls_ar_norm_wgs() {
+  static const int n = [] {
+    const char* e = getenv("NLS_AR_NORM_WGS");
+    int v = e ? atoi(e) : 128;
+    v = v < 8 ? 8 : (v > 4096 ? 4096 : v);
+    return v & ~7;
+  }();
+  return n;
+}
+
 static long ar_opts(long max_spins) {
   static const long opts = [] {
     long o = 0;
@@ -656,6 +715,12 @@ int nls_ar_err_words(void* buf, long cap, int world, void* host, int n, void* st
 int nls_ar_peek(void* buf, long off, int n, void* host, void* stream) {
   return (int)hipMemcpyAsync(host, (char*)buf + 4L * off, 4L * n, hipMemcpyDeviceToHost, (hipStream_t)stream);
 }
+// NLS_AR_PROBE: the timing history of add+norm workgroup slot `eidx` (AR_PROBE_DEPTH records of 32 bytes)
+int nls_ar_probe_hist(int eidx, void* host) {
+  if (eidx < 0 || eidx >= AR_PROBE_SLOTS) return -1;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ar_probe), sizeof(ArProbeRec) * AR_PROBE_DEPTH,
+                                  sizeof(ArProbeRec) * AR_PROBE_DEPTH * (size_t)eidx, hipMemcpyDeviceToHost);
+}
 int nls_ar_err_clear(void* buf, long cap, int world, void* stream) {
   hipLaunchKernelGGL(ar_err_clear_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
                      (uint32_t*)((char*)buf + 2L * world * cap * 4L));
@@ -689,7 +754,11 @@ int nls_ar_addnorm_sim(const float* part, long ldp, float* x, long ldx, const fl
   if (sim_ranks > 1 && sim_ranks != world) return -1;
   const int sim = sim_ranks > 1 ? sim_ranks : 1;
   const int nblk = nls_ar_row_blocks(D), nrr = rows * sim;
-  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(8 * nblk * ((nrr + 7) / 8)), dim3(ARN_THREADS), 0,
+  // bounded grid: per XCD, k workgroups over its ceil(nrr / 8) rows x nblk slices (one item each when they fit)
+  const int per_xcd = nblk * ((nrr + 7) / 8);
+  int k = per_xcd < nls_ar_norm_wgs() / 8 ? per_xcd : nls_ar_norm_wgs() / 8;
+  if ((per_xcd + k - 1) / k > ARN_MAX_ITEMS) k = (per_xcd + ARN_MAX_ITEMS - 1) / ARN_MAX_ITEMS;
+  hipLaunchKernelGGL(oneshot_ar_addnorm_kernel, dim3(8 * k), dim3(ARN_THREADS), 0,
                      (hipStream_t)stream, part, ldp, x, ldx, nw, (_Float16*)h, ldh, D, eps, P, world, rank, cap, epochs,
                      tickets, ssq, err, ar_opts(max_spins), sim, sp, sx, sh, se, st, sq, nblk, nrr);
   return (int)hipGetLastError();

@@ -42,15 +42,15 @@ using namespace nls_gemv;
 using nls_dma::glds16;
 using nls_dma::lds_addr;
 
-constexpr int BM = 256;                  // activation rows per workgroup
-constexpr int XS = BM * 64;              // bytes of one activation stage [256][32] f16
 constexpr int LDS_MAX = 160 * 1024;
 
-// NWV waves x RT weight tiles: activation / raw-weight DMA instructions per wave per stage / super-block
-// (NWV*RT tile-blocks) and the ring depth
-template <int T, int RT, int NWV>
+// NWV waves x RT weight tiles over BM activation rows (256; mode 12: 64, the MoE experts' routed rows):
+// activation / raw-weight DMA instructions per wave per stage / super-block (NWV*RT tile-blocks), the ring depth
+template <int T, int RT, int NWV, int BM = 256>
 struct Geo {
+  static constexpr int XS = BM * 64;                             // bytes of one activation stage [BM][32] f16
   static constexpr int XI = XS / 1024 / NWV;
+  static_assert(XI >= 1 && XS % (1024 * NWV) == 0, "one stage must split evenly over the waves");
   static constexpr int TB = TileBytes<T>::v;
   static constexpr int NW = (RT * TB + 1023) / 1024;
   static constexpr int WL = NWV * NW * 1024;                     // weight buffer incl. pad lanes
@@ -118,10 +118,11 @@ struct Cnt {
   static constexpr int v = (NS - 3) * XI + ((P >= 2 && P <= NS - 1) ? NW : 0);
 };
 
-template <int T, int RT, int NWV>
-DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
-  typedef Geo<T, RT, NWV> G;
-  constexpr int NS = G::NS, NW = G::NW, TB = G::TB, XI = G::XI;
+template <int T, int RT, int NWV, int BM = 256>
+DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
+                  const int* xm = nullptr, const int* ym = nullptr) {
+  typedef Geo<T, RT, NWV, BM> G;
+  constexpr int NS = G::NS, NW = G::NW, TB = G::TB, XI = G::XI, XS = G::XS;
   constexpr int MT = BM / 16;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -141,7 +142,8 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
     const int row = min(16 * (XI * wave + i) + (lane >> 2), M - 1);   // rows >= M: clamped, never stored
-    xsrc[i] = a.x + (size_t)row * a.ldx + (size_t)sb0 * 256 + lc * 8;
+    const int xr = xm ? xm[row] : row;                                 // mapped rows: the routed token's row
+    xsrc[i] = a.x + (size_t)xr * a.ldx + (size_t)sb0 * 256 + lc * 8;
   }
   // raw weights: byte b of the packed buffer <- tile-block b / TB (clamped to the segment), byte b % TB;
   // the sources are recomputed per super-block (registers are the scarce resource here, not VALU)
@@ -245,6 +247,24 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 #pragma unroll
     for (int i = 0; i < RT; ++i) wf[i] = wn[i];
   };
+  // BM 64 (one group of 4 activation tiles per stage): the stages alternate between XA and XB, each stage
+  // requesting the next one's fragments before its MFMAs, and its MFMAs carry ALL the next stage's weight
+  // dequantisation
+  auto stage64 = [&](int j, int pn, auto ODD) __attribute__((always_inline)) {
+    constexpr bool odd = decltype(ODD)::value;
+    f16x8* cur = odd ? XB : XA;
+    f16x8* nxt = odd ? XA : XB;
+    __builtin_amdgcn_s_setprio(1);
+    rdg(nxt, j + 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mmv(cur, 0, [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i) wn[i] = frag(i, pn);
+    });
+    __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 0; i < RT; ++i) wf[i] = wn[i];
+  };
 
   if (nst > 0) {
     dma_w(0);
@@ -281,7 +301,10 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 #pragma unroll
           for (int i = 0; i < RT; ++i) prep_sc<T>(raw[i], g, sc[i]);
         }
-        stage(j0 + p, (p + 1) & 7);
+        if constexpr (BM == 64)
+          stage64(j0 + p, (p + 1) & 7, std::integral_constant<bool, (p & 1) != 0>{});
+        else
+          stage(j0 + p, (p + 1) & 7);
       };
       step(std::integral_constant<int, 0>{});
       step(std::integral_constant<int, 1>{});
@@ -297,9 +320,11 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- epilogue: lane holds weight rows nb0 + 16i + 4g + e and activation row 16m + r
+  // ---- epilogue: lane holds weight rows nb0 + 16i + 4g + e and activation row 16m + r (mapped: output row
+  // ym[16m + r]; mapped split-K slabs are indexed by the output row, one shared segment column range)
   const int g4 = 4 * g;
   const int nb0 = row0 + wave * RT * 16;
+  auto yrow = [&](int mm) __attribute__((always_inline)) { return ym ? ym[mm] : mm; };
   if (ks > 1 || a.epi == EPI_SLABS) {
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
@@ -309,7 +334,9 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
       for (int m = 0; m < MT; ++m) {
         const int mm = 16 * m + r;
         if (mm >= M) continue;
-        *reinterpret_cast<f32x4*>(ws + ((size_t)kslice * a.mtot + a.m0 + mm) * a.pad + S.tile_begin_col + n) = acc[i][m];
+        const size_t srow = ym ? (size_t)ym[mm] : (size_t)(a.m0 + mm);
+        const int scol = ym ? n : S.tile_begin_col + n;
+        *reinterpret_cast<f32x4*>(ws + ((size_t)kslice * a.mtot + srow) * a.pad + scol) = acc[i][m];
       }
     }
     return;
@@ -330,7 +357,7 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
           h4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (_Float16)(silu(acc[i][m][e] * al) * u[e]);
-          *reinterpret_cast<h4*>(reinterpret_cast<act_t*>(a.y) + (size_t)mm * a.ldy + S.ycol + (n16 >> 1) + g4) = o;
+          *reinterpret_cast<h4*>(reinterpret_cast<act_t*>(a.y) + (size_t)yrow(mm) * a.ldy + S.ycol + (n16 >> 1) + g4) = o;
         }
       }
     }
@@ -348,10 +375,10 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
         const f32x4 v = acc[i][m] * al;
         if (a.epi == EPI_ACT) {
           typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-          *reinterpret_cast<h4*>(reinterpret_cast<act_t*>(a.y) + (size_t)mm * a.ldy + S.ycol + n) =
+          *reinterpret_cast<h4*>(reinterpret_cast<act_t*>(a.y) + (size_t)yrow(mm) * a.ldy + S.ycol + n) =
               h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
         } else {
-          f32x4* q = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + (size_t)mm * a.ldy + S.ycol + n);
+          f32x4* q = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + (size_t)yrow(mm) * a.ldy + S.ycol + n);
           *q = a.epi == EPI_ADD_F32 ? *q + v : v;
         }
       }
@@ -382,16 +409,19 @@ DEVI void q9_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
 
 // the formats of one kernel type-set (dispatcher's kset: 0 = Q4_K/Q6_K, 1 = Q5_K/Q6_K/Q8_0,
 // 3 = Q51/Q6_K/Q8_0) and the LDS they need
-template <int KSET, int RT, int NWV>
+template <int KSET, int RT, int NWV, int BM>
 constexpr int kset_lds() {
-  return KSET == 0 ? (Geo<QT_Q4_K, RT, NWV>::LDS > Geo<QT_Q6_K, RT, NWV>::LDS ? Geo<QT_Q4_K, RT, NWV>::LDS
-                                                                              : Geo<QT_Q6_K, RT, NWV>::LDS)
+  return KSET == 0 ? (Geo<QT_Q4_K, RT, NWV, BM>::LDS > Geo<QT_Q6_K, RT, NWV, BM>::LDS ? Geo<QT_Q4_K, RT, NWV, BM>::LDS
+                                                                                      : Geo<QT_Q6_K, RT, NWV, BM>::LDS)
                    : LDS_MAX;
 }
 
 // NWV = 8: two waves per SIMD (256 registers); NWV = 4: one wave per SIMD with up to 512 registers, so a
-// wave holds 4 weight tiles x 16 activation tiles of accumulators (half the LDS reads per MFMA)
-template <int KSET, int RT, int NWV>
+// wave holds 4 weight tiles x 16 activation tiles of accumulators (half the LDS reads per MFMA).
+// BM = 64 (mode 12, the MoE experts' grouped GEMM): segments may be mapped -- each expert's routed rows are
+// gathered through xmap and scattered through ymap, and m-blocks past the expert's device-side row count
+// exit before reading any weights (the grid is sized for every token on one expert)
+template <int KSET, int RT, int NWV, int BM>
 __global__ __launch_bounds__(64 * NWV, 1) void qgemm9_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                           int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t q9lds[];
@@ -405,58 +435,71 @@ __global__ __launch_bounds__(64 * NWV, 1) void qgemm9_kernel(SegList segs, GemvA
 #pragma unroll
   for (int s = 1; s < 8; ++s)
     if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
+  // mapped rows only at BM 64 (the dispatcher refuses them for mode 9): the 256-row build keeps mode 9's code
+  const int mrows = (BM == 64 && S.mcount) ? min(*S.mcount, a.M) : a.M;
+  if (m0 >= mrows) return;
+  const int* xm = (BM == 64 && S.xmap) ? S.xmap + m0 : nullptr;
+  const int* ym = (BM == 64 && S.ymap) ? S.ymap + m0 : nullptr;
   a.m0 = m0;
-  a.x += (size_t)m0 * a.ldx;
+  if (!xm) a.x += (size_t)m0 * a.ldx;
   const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-  a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
   if (a.argmax) a.argmax += m0;
-  a.M = min(BM, a.M - m0);
+  a.M = min(BM, mrows - m0);
   const int row0 = (tile - S.tile_begin) * 16 * RT * NWV;
   if constexpr (KSET == 0) {
-    if (S.type == QT_Q4_K) q9_tile<QT_Q4_K, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
-    else q9_tile<QT_Q6_K, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
+    if (S.type == QT_Q4_K) q9_tile<QT_Q4_K, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
+    else q9_tile<QT_Q6_K, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
   } else if constexpr (KSET == 1) {
-    if (S.type == QT_Q5_K) q9_tile<QT_Q5_K, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
-    else if (S.type == QT_Q8_0) q9_tile<QT_Q8_0, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
-    else q9_tile<QT_Q6_K, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
+    if (S.type == QT_Q5_K) q9_tile<QT_Q5_K, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
+    else if (S.type == QT_Q8_0) q9_tile<QT_Q8_0, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
+    else q9_tile<QT_Q6_K, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
   } else {
-    if (S.type == QT_Q51) q9_tile<QT_Q51, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
-    else if (S.type == QT_Q8_0) q9_tile<QT_Q8_0, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
-    else q9_tile<QT_Q6_K, RT, NWV>(S, row0, kslice, ks, a, ws, q9lds);
+    if (S.type == QT_Q51) q9_tile<QT_Q51, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
+    else if (S.type == QT_Q8_0) q9_tile<QT_Q8_0, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
+    else q9_tile<QT_Q6_K, RT, NWV, BM>(S, row0, kslice, ks, a, ws, q9lds, xm, ym);
   }
 }
 
-template <int KSET, int RT, int NWV>
+template <int KSET, int RT, int NWV, int BM>
 int launch_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  constexpr int lds = kset_lds<KSET, RT, NWV>();
+  constexpr int lds = kset_lds<KSET, RT, NWV, BM>();
   const int nmb = (a.M + BM - 1) / BM;
   const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
-    if (hipFuncSetAttribute((const void*)qgemm9_kernel<KSET, RT, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)qgemm9_kernel<KSET, RT, NWV, BM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds) != hipSuccess)
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL((qgemm9_kernel<KSET, RT, NWV>), dim3(grid), dim3(64 * NWV), lds, st, sl, a, ks, ws, ntiles, nmb);
+  hipLaunchKernelGGL((qgemm9_kernel<KSET, RT, NWV, BM>), dim3(grid), dim3(64 * NWV), lds, st, sl, a, ks, ws, ntiles,
+                     nmb);
   return (int)hipGetLastError();
 }
 
 template <int KSET>
-int launch_k(int waves, int rt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  if (waves == 4 && rt == 2) return launch_t<KSET, 2, 4>(sl, ntiles, ks, ws, a, st);
-  if (waves == 8 && rt == 2) return launch_t<KSET, 2, 8>(sl, ntiles, ks, ws, a, st);
-  if (waves == 8 && rt == 1) return launch_t<KSET, 1, 8>(sl, ntiles, ks, ws, a, st);
+int launch_k(int waves, int rt, int bm, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
+             hipStream_t st) {
+  if (bm == 64) {                      // mode 12: 4 waves (one 16-row activation tile group per stage)
+    if (waves == 4 && rt == 2) return launch_t<KSET, 2, 4, 64>(sl, ntiles, ks, ws, a, st);
+    if (waves == 4 && rt == 4) return launch_t<KSET, 4, 4, 64>(sl, ntiles, ks, ws, a, st);
+    return -1;
+  }
+  if (waves == 4 && rt == 2) return launch_t<KSET, 2, 4, 256>(sl, ntiles, ks, ws, a, st);
+  if (waves == 8 && rt == 2) return launch_t<KSET, 2, 8, 256>(sl, ntiles, ks, ws, a, st);
+  if (waves == 8 && rt == 1) return launch_t<KSET, 1, 8, 256>(sl, ntiles, ks, ws, a, st);
   return -1;
 }
 
 // waves x rt weight tiles of 16 rows per workgroup: (4, 2) | (8, 2) | (8, 1) (4 x 4 spills: 256 accumulators
-// plus the pipelined fragments exceed 512 registers); kset as the dispatcher's
+// plus the pipelined fragments exceed 512 registers) over 256 activation rows; bm 64 (mode 12): (4, 2) | (4, 4);
+// kset as the dispatcher's
 int launch_q9(int kset, int waves, int rt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
-              hipStream_t st) {
-  if (kset == 0) return launch_k<0>(waves, rt, sl, ntiles, ks, ws, a, st);
-  if (kset == 1) return launch_k<1>(waves, rt, sl, ntiles, ks, ws, a, st);
-  if (kset == 3) return launch_k<3>(waves, rt, sl, ntiles, ks, ws, a, st);
+              hipStream_t st, int bm) {
+  if (kset == 0) return launch_k<0>(waves, rt, bm, sl, ntiles, ks, ws, a, st);
+  if (kset == 1) return launch_k<1>(waves, rt, bm, sl, ntiles, ks, ws, a, st);
+  if (kset == 3) return launch_k<3>(waves, rt, bm, sl, ntiles, ks, ws, a, st);
   return -1;
 }
 

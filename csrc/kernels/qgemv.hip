@@ -15,7 +15,7 @@ int launch_q11(int bn, const SegList& sl, int ntiles, int ks, float* ws, const G
 }
 namespace nls_q9 {
 int launch_q9(int kset, int waves, int rt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
-              hipStream_t st);
+              hipStream_t st, int bm);
 }
 
 
@@ -58,6 +58,8 @@ struct NlsFuse {
 //         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
 // mode 11: mode 10's schedule on the RAW Q4_K / Q6_K tile-blocks, dequantised once per workgroup into the f16
 //         LDS image (hgemm10.hip); rt 1 (256-row weight tiles, Q4_K only) or 2 (128-row), optional split-K.
+// mode 12: mode 9 over 64-row activation blocks (4 waves, rt 2 | 4) with mapped rows: the MoE experts' grouped
+//         GEMM (each expert's routed rows gathered through xmap / scattered through ymap, device row counts).
 // mode 9: quantised GEMM on the raw tile-blocks (qgemm9.hip; Q4_K/Q5_K/Q6_K/Q8_0/Q51): 256-row activation
 //         blocks x 16*waves*rt weight rows ((waves, rt) = (4, 2) | (8, 2) | (8, 1)), the mode-8
 //         epilogues, optional split-K.
@@ -102,8 +104,14 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 11 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
-  if (mode == 11) {     // rt 1: 256-row weight tiles (Q4_K), rt 2: 128-row (Q4_K / Q6_K)
+  if (mode < 0 || mode > 12 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode == 12) {
+    if (waves != 4 || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE || argmax || ldx % 8 ||
+        ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
+      return -1;
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].ycol % 4) return -1;
+  } else if (mode == 11) {     // rt 1: 256-row weight tiles (Q4_K), rt 2: 128-row (Q4_K / Q6_K)
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
@@ -137,12 +145,12 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0 && ks > 1 && !ws) return -1;
   if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
   // mapped split-K (MoE down projection at many tokens): slabs indexed by the y row, one reduce
-  bool mks = (mode == 1 || mode == 2 || mode == 4 || mode == 5) && ks > 1 && epi == EPI_F32 && !argmax;
+  bool mks = (mode == 1 || mode == 2 || mode == 4 || mode == 5 || mode == 12) && ks > 1 && epi == EPI_F32 && !argmax;
   for (int i = 0; i < nseg && mks; ++i)
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = (mode == 10 || mode == 11) ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = (mode == 10 || mode == 11) ? 256 / rt : (mode == 9 || mode == 12) ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -150,7 +158,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     // arg-max; split-K only as "mapped split-K" (every segment an expert writing the same output
     // columns of its own y rows, f32 store)
     if ((segs[i].xmap || segs[i].ymap || segs[i].mcount) && mode != 0 &&
-        (!(mode == 1 || mode == 2 || mode == 4 || mode == 5) || argmax || epi == EPI_SLABS || (ks > 1 && !mks)))
+        (!(mode == 1 || mode == 2 || mode == 4 || mode == 5 || mode == 12) || argmax || epi == EPI_SLABS ||
+         (ks > 1 && !mks)))
       return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;
@@ -234,7 +243,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   hipStream_t st = (hipStream_t)stream;
   auto launch = kset == 0 ? launch_k0 : (kset == 1 ? launch_k1 : (kset == 2 ? launch_k2 : launch_k3));
   if (mode >= 2 && mode <= 3 && kset >= 2) return -1;   // tiled float / Q51 weights: paths A and B only
-  if (mode == 9 && kset == 2) return -1;                // mode 9: quantised formats only
+  if ((mode == 9 || mode == 12) && kset == 2) return -1;   // modes 9 / 12: quantised formats only
   if (mode == 3)
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type == QT_Q8_0) return -1;   // raw Q8_0 tiles do not fit the DMA LDS budget
@@ -245,8 +254,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 11)
       rc = nls_hg10::launch_q11(256 / rt, sl, tiles, ks, (float*)ws, a, st);
-    else if (mode == 9)
-      rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st);
+    else if (mode == 9 || mode == 12)
+      rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st, mode == 12 ? 64 : 256);
     else if (mode >= 4)
       rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : 3, sl, tiles, ks, (float*)ws, a,
                                    st);

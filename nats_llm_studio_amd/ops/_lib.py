@@ -108,6 +108,7 @@ _SIGS = {
     "nls_ar_err_clear": [c_void_p, c_long, c_int, c_void_p],
     "nls_ar_err_words": [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p],
     "nls_ar_peek": [c_void_p, c_long, c_int, c_void_p, c_void_p],
+    "nls_ar_probe_hist": [c_int, c_void_p],
     "nls_ar_buffer_bytes": [c_long, c_int],
     "nls_ag_blocks": [],
     "nls_ag_run": [c_void_p, c_long, c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p,

@@ -53,16 +53,9 @@ def heuristic(segs, M: int):
             return (1, 4, 2, 2) if rows >= 16 * K and K >= 1024 else (1, 4, 2, 1)
         return (0, 4, 2, 1) if len(segs) > 1 else (0, 4, 1, 1)
     if M > 64:
-        types = [int(s.w.type) for s in segs]
-        if M >= 128 and all(t in (12, 14) for t in types):
-            # mode 11 (hgemm10.hip): mode 10's staggered schedule on the raw Q4_K / Q6_K tile-blocks, 256 x 256
-            # tiles for Q4_K-only launches (128-row weight tiles with Q6_K); split K until ~256 workgroups
-            rt = 1 if all(t == 12 for t in types) else 2
-            tiles = sum((s.w.rows + 256 // rt - 1) // (256 // rt) for s in segs) * ((M + 255) // 256)
-            ks, nkt = 1, K // 64
-            while tiles * ks * 2 <= 320 and nkt // (ks * 2) >= 8:
-                ks *= 2
-            return (11, 8, rt, ks)
+        # mode 11 (hgemm10.hip's staggered schedule on raw Q4_K / Q6_K tile-blocks) is a tuner candidate only:
+        # it lost every measured Llama-3-8B shape to modes 2 / 9 (LM head M=256: 489 vs 320 us, profiles/
+        # qgemm11_r05.txt)
         if all(int(s.w.type) in (12, 13, 14) for s in segs):
             # LDS-dequant GEMM (mode 2): 128 weight rows x 256 (or 128) activation rows per workgroup;
             # split K until the grid covers the 256 CUs (the measured winners on the 8B shapes)

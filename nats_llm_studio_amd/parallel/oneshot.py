@@ -177,6 +177,8 @@ class OneShotAllReduce:
                     torch.cuda.synchronize(self.device)
                     slots[par] = [hex(v & 0xFFFFFFFF) for v in pk.tolist()]
                 out["addnorm_timeout_detail"]["slot_memory_now"] = slots
+                if D:
+                    out["probe_hist_self"] = self._probe_hist(b * L.nls_ar_row_blocks(D) + c)
         for D, (ep, tk, _sq) in self._norm.items():
             nblk = ep.numel() // tk.numel()
             out[f"addnorm{D}_epochs_rows0_23"] = ep.view(-1, nblk)[:24].tolist()
@@ -201,7 +203,9 @@ class OneShotAllReduce:
                     _lib.check(L.nls_ar_peek(self.npeers[p], off, 4, pk.data_ptr(), st), "nls_ar_peek")
                     torch.cuda.synchronize(self.device)
                     view[par] = [hex(v & 0xFFFFFFFF) for v in pk.tolist()]
-                out[f"pusher_view_of_rank{p}"] = dict(row=w[1], col=w[12], epoch=w[3], slot_memory=view)
+                out[f"pusher_view_of_rank{p}"] = dict(row=w[1], col=w[12], epoch=w[3], slot_memory=view,
+                                                      probe_hist_pusher=self._probe_hist(
+                                                          w[1] * L.nls_ar_row_blocks(D) + w[2]))
         nbytes = L.nls_ar_buffer_bytes(self.cap, self.world)
         imported = [(n, int(ptr)) for n, arr in (("sum", self.peers), ("addnorm", self.npeers), ("gather", self.gpeers))
                     for r, ptr in enumerate(arr) if ptr and r != self.rank]
@@ -214,6 +218,24 @@ class OneShotAllReduce:
         out["imported_ptrs"] = [(n, hex(ptr)) for n, ptr in imported]
         out["own_ptrs"] = [hex(int(b)) for b in (self.buf, self.nbuf, self.gbuf)]
         return out
+
+    @staticmethod
+    def _probe_hist(eidx: int):
+        """NLS_AR_PROBE: this process's last 8 add+norm launches of workgroup slot `eidx`, oldest first, as
+        (epoch, xcc, failed, t_start, t_pushed, t_polled) -- times in the device-wide 100 MHz clock, which two
+        ranks sharing one GPU read identically (compare a timed-out poll with the peer's push)."""
+        import numpy as np
+        host = np.zeros(8 * 8, dtype=np.uint32)
+        if _lib.lib().nls_ar_probe_hist(int(eidx), host.ctypes.data) != 0:
+            return None
+        recs = []
+        for i in range(8):
+            w = host[8 * i:8 * i + 8]
+            if not w[0]:
+                continue
+            t = [int(w[2 + 2 * k]) | (int(w[3 + 2 * k]) << 32) for k in range(3)]
+            recs.append((int(w[0]), int(w[1] & 0xFF), int(w[1] >> 8), *t))
+        return sorted(recs)
 
     def reset(self):
         """After a timed-out poll: put every rank's receive slots, epochs and tickets back to the freshly
