@@ -21,14 +21,15 @@
 // the gather never write their own receive slots (see SlotBlocks below); the fused add+norm DOES, by default:
 // it re-tags each consumed granule with the other parity's tag (AR_OPT_RETAG, NLS_AR_RETAG=0 disables), the
 // round-3 protocol, which the simulated-rank test measured as needed (cause not established).
-// Eager (non-captured) calls: on two ranks sharing ONE GPU, a peer's push into the parity-1 half of the
-// receive buffer was repeatedly never seen by the owner (profiles/tp_oneshot_eager_r04.txt,
-// profiles/tp_oneshot_eager_r05.txt); parallel/comm.py routes eager collectives to RCCL by default -- a
-// WORKAROUND, the one-shot kernels run inside captured decode graphs only (NLS_ONESHOT_EAGER=1 restores them).
+// Eager (non-captured) calls timed out in rounds 3-4 on two ranks sharing ONE GPU: the fused add+norm launched one
+// workgroup per (row, slice), its polling waves filled the GPU and the PEER rank's preceding kernels could not be
+// scheduled until the poll expired (device-clock timestamps of both ranks, profiles/tp_oneshot_eager_r05.txt). The
+// add+norm now runs on a bounded grid (every workgroup pushes all of its items before polling), and eager calls
+// take these kernels again (parallel/comm.py).
 // Every rank uses the ROUNDED value of its own partial too, so the sums stay bit-identical.
 //
 // Element -> workgroup maps are fixed (the plain all-reduce runs a FIXED grid, grid-stride; the
-// fused add+norm maps row b, 256-column slice c to workgroup (b, c) for a given D), so the per-
+// fused add+norm maps row b, 256-column slice c to a workgroup on XCD b % 8 for a given D), so the per-
 // workgroup epoch counters (device memory, advanced by the workgroup itself) stay in lock-step
 // across ranks and across hipGraph replays (no per-launch argument is frozen into a graph).
 // Spins are bounded: on timeout a workgroup raises the error word of EVERY rank (an extra 256-byte

@@ -545,6 +545,24 @@ __global__ __launch_bounds__(256) void swiglu16_kernel(const act_t* __restrict__
   *reinterpret_cast<f16x8*>(out + (size_t)m * ldo + 8 * j) = o;
 }
 
+// Touch `bytes` of device memory (16-B loads, grid-stride over the whole grid) so that a later kernel finds them
+// in the memory-side Infinity Cache (MALL, 256 MB) / L2 instead of HBM -- the batch-1 decode experiment: stream
+// the NEXT projection's weights while a latency-bound kernel (attention, a GEMV's tail) leaves HBM idle. The
+// loaded words feed a sum that is stored only if it equals a value it never takes (keeps the loads alive).
+__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ p, long n16, uint32_t never,
+                                                       uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  const long stride = (long)gridDim.x * 256 * 4;
+  for (long i = (long)blockIdx.x * 256 * 4 + threadIdx.x; i < n16; i += stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < n16 ? p[i + u * 256] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (acc == never && sink) sink[threadIdx.x] = acc;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -552,6 +570,13 @@ __global__ __launch_bounds__(256) void swiglu16_kernel(const act_t* __restrict__
 // ===========================================================================
 
 extern "C" {
+
+int nls_prefetch(const void* p, long bytes, int blocks, void* stream) {
+  if (bytes <= 0) return 0;
+  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const uint4*)p, bytes / 16,
+                     0x9E3779B9u, (uint32_t*)nullptr);
+  return (int)hipGetLastError();
+}
 
 int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, int M, int D, float eps,
                 int out_f32, void* stream) {

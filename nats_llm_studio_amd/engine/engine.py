@@ -1218,10 +1218,22 @@ class Engine:
         if warm:
             self._step_forward(Bp, ns, need_logits, dsamp)
         torch.cuda.synchronize(self.dev)
-        g = torch.cuda.CUDAGraph()
+        dump = os.environ.get("NLS_GRAPH_DUMP")
+        g = torch.cuda.CUDAGraph(keep_graph=True) if dump else torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._step_forward(Bp, ns, need_logits, dsamp)
         torch.cuda.synchronize(self.dev)
+        if dump:
+            # (diagnostics) the captured graph's kernel nodes by name, one file per graph: proves e.g. that a TP
+            # decode graph holds no RCCL call (parallel/rehearsal.py summarises the dumps)
+            import ctypes
+            os.makedirs(dump, exist_ok=True)
+            buf = ctypes.create_string_buffer(1 << 20)
+            n = ops._lib.lib().nls_graph_kernel_names(g.raw_cuda_graph(), buf, len(buf))
+            with open(os.path.join(dump, f"w{self.model.shard.size}_r{self.rank}_B{Bp}_logits{int(need_logits)}_dsamp{int(dsamp)}.nodes"),
+                      "w") as f:
+                f.write(f"# {n} nodes\n" + buf.value.decode(errors="replace"))
+            g.instantiate()
         self.graphs[(Bp, need_logits, dsamp) if dsamp else (Bp, need_logits)] = g
         return g
 

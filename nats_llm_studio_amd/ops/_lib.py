@@ -47,6 +47,8 @@ _SIGS = {
     "nls_fuse_size": [],
     "nls_qgemv_norm": [ctypes.POINTER(NlsSeg), c_int, c_void_p, c_long, c_void_p, c_float, c_void_p, c_long, c_int,
                        c_float, c_int, c_void_p, c_int, c_int, c_void_p],
+    "nls_prefetch": [c_void_p, c_long, c_int, c_void_p],
+    "nls_graph_kernel_names": [c_void_p, c_void_p, c_long],
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
     "nls_splitk_add_rmsnorm": [c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int,
                                c_float, c_void_p],

@@ -39,13 +39,14 @@ class Comm:
         self.src = dist.get_global_rank(group, 0) if group is not None else 0
         self.device = torch.device(device) if device is not None else None
         self.oneshot = None          # optional small-message all-reduce (parallel/oneshot.py)
-        # The IPC one-shot kernels run only inside captured (decode-graph) launches; eager calls (prefill
-        # chunks, capture warm-ups, first-use steps) take RCCL. Measured on one MI355X shared by two ranks
-        # (profiles/tp_oneshot_eager_r04.txt): eager one-shot calls interleaved with graph replays timed out
-        # waiting for a granule the peer had pushed (any buffer kind, with or without per-poll invalidate),
-        # while graph-only one-shot traffic -- also across bucket changes -- never did. NLS_ONESHOT_EAGER=1
-        # restores eager one-shot calls.
-        self.oneshot_eager = os.environ.get("NLS_ONESHOT_EAGER", "0") == "1"
+        # Eager calls (prefill chunks, capture warm-ups, first-use steps) take the IPC one-shot kernels too when
+        # the message fits `cap` (round 5). Rounds 3-4 routed them to RCCL after eager add+norm calls timed out on
+        # one MI355X shared by two ranks; the cause was scheduling, not visibility: one workgroup per (row, slice)
+        # put ~1,700 polling waves on the GPU for a 52-row prefill chunk, the PEER rank's preceding GEMM could not
+        # be scheduled, and its push came only after the bounded poll had expired (device-clock timestamps of both
+        # ranks, profiles/tp_oneshot_eager_r05.txt). The fused add+norm now runs on a bounded grid (allreduce.hip).
+        # NLS_ONESHOT_EAGER=0 sends eager calls to RCCL again.
+        self.oneshot_eager = os.environ.get("NLS_ONESHOT_EAGER", "1") == "1"
         self.stats = dict(all_reduce=0, all_reduce_bytes=0, ctrl=0, ctrl_s=0.0)
         self.ring = None             # shared-memory control ring (ranks on one host), else gloo broadcasts
         if self.size > 1 and os.environ.get("NLS_SHM_CTRL", "1") == "1":

@@ -37,7 +37,13 @@ def _requests(new_tokens: int, greedy_only: bool = False):
     greedy = SamplingParams(max_tokens=new_tokens, ignore_eos=True)
     topk = SamplingParams(max_tokens=new_tokens, temperature=0.8, top_k=40, top_p=0.95, repeat_penalty=1.1,
                           seed=7, ignore_eos=True)
-    return [(p, greedy) for p in PROMPTS] + ([] if greedy_only else [(p, topk) for p in PROMPTS])
+    # the reference's canonical payload (`/root/reference/README.md:196-204`: temperature only, plus a seed so TP=1
+    # and TP=2 draw the same stream): the omitted fields take LM Studio's preset (engine/sampling.py), top_k 40
+    # included, so these rows are sampled in-graph like the explicit top-k ones
+    canon = SamplingParams.from_request({"temperature": 0.7, "seed": 11, "max_tokens": new_tokens,
+                                         "ignore_eos": True})
+    return [(p, greedy) for p in PROMPTS] + ([] if greedy_only else [(p, topk) for p in PROMPTS]
+                                             + [(p, canon) for p in PROMPTS[:2]])
 
 
 def _sync(dev):
@@ -83,6 +89,21 @@ def _kernel_profile(eng, futs, steps: int) -> Dict:
     rows = sorted(([v[0] / max(1, n), round(v[1] / max(1, n), 1), k] for k, v in kern.items()), key=lambda r: -r[1])
     return dict(steps=n, per_step=[[round(c, 2), us, nm[:90]] for c, us, nm in rows],
                 rccl_kernels=[nm for _, _, nm in rows if "nccl" in nm.lower() or "rccl" in nm.lower()])
+
+
+def graph_dump_summary(d: str) -> Dict:
+    """NLS_GRAPH_DUMP=<d>: per captured graph (engine._capture: one `.nodes` file of kernel-node names), its
+    kernel count by name and the nodes naming RCCL / NCCL -- the evidence that TP decode graphs are RCCL-free."""
+    import collections
+    import glob
+    out = {}
+    for f in sorted(glob.glob(os.path.join(d, "*.nodes"))):
+        names = collections.Counter(ln.strip()[:100] for ln in open(f, errors="replace")
+                                    if ln.strip() and not ln.startswith("#"))
+        out[os.path.basename(f)] = dict(nodes=sum(names.values()), kernels=dict(names.most_common()),
+                                        rccl_nodes=sum(c for k, c in names.items()
+                                                       if "nccl" in k.lower() or "rccl" in k.lower()))
+    return out
 
 
 def _drive(eng, new_tokens: int, profile_steps: int = 0, greedy_only: bool = False) -> Dict:
@@ -253,6 +274,8 @@ def run(path: str, world: int = 2, ep: bool = False, new_tokens: int = 8, ref: b
     res = _collect(procs, q, world, timeout)
     out["tp"] = res.get(0)
     out["followers"] = [res.get(r) for r in range(1, world)]
+    if os.environ.get("NLS_GRAPH_DUMP"):
+        out["graph_dump"] = graph_dump_summary(os.environ["NLS_GRAPH_DUMP"])
     return out
 
 

@@ -20,10 +20,20 @@ def models(tmp_path_factory):
 
 @pytest.mark.parametrize("name,ep", [("llama-3-70b-2layer", False), ("mixtral-8x7b-1layer", True),
                                      ("mixtral-8x7b-1layer", False)])
-def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep):
+def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep, tmp_path):
+    import os
     from nats_llm_studio_amd.parallel import rehearsal
-    r = rehearsal.run(models[name], world=2, ep=ep, new_tokens=8, timeout=300)
+    os.environ["NLS_GRAPH_DUMP"] = str(tmp_path)       # kernel-node list of every captured graph (spawned ranks)
+    try:
+        r = rehearsal.run(models[name], world=2, ep=ep, new_tokens=8, timeout=300)
+    finally:
+        os.environ.pop("NLS_GRAPH_DUMP", None)
     ref, tp, fol = r["ref"], r["tp"], r["followers"][0]
+    # every captured TP / EP decode graph of both ranks: no collective-library kernel among its nodes
+    dumps = {f: v for f, v in r["graph_dump"].items() if f.startswith("w2_")}
+    assert {f.split("_")[1] for f in dumps} == {"r0", "r1"}, sorted(r["graph_dump"])
+    for f, v in dumps.items():
+        assert v["nodes"] > 0 and v["rccl_nodes"] == 0, (f, v)
     for v in (ref, tp, fol):
         assert "exception" not in v, v
     c = tp["counters"]
@@ -42,9 +52,10 @@ def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep):
 def test_tp2_greedy_prefill_after_graph_replays(gpu, models, name, ep):
     """Greedy-only batches (every step on the vocab-parallel arg-max), waves of requests that end at different
     lengths (the decode batch walks down and back up the graph buckets, rows idle for many steps return),
-    then a second round of requests whose eager prefill follows the graph replays (eager one-shot calls timed
-    out here on a shared GPU; eager collectives now take RCCL / gloo: round-4 regression). Mixtral EP also
-    runs the plain one-shot all-reduce of the expert outputs."""
+    then a second round of requests whose eager prefill follows the graph replays. Eager collectives take the
+    IPC one-shot kernels: in rounds 3-4 an eager add+norm here timed out (its one-workgroup-per-slice grid kept
+    the peer rank's GEMM off the shared GPU, profiles/tp_oneshot_eager_r05.txt). Mixtral EP also runs the
+    plain one-shot all-reduce of the expert outputs."""
     from nats_llm_studio_amd.parallel import rehearsal
     import os
     os.environ["NLS_REHEARSAL_WAVES"] = "1"      # + batch churn through the graph buckets (spawned ranks inherit)
