@@ -55,16 +55,18 @@ struct HG {
 };
 
 template <int WM, int BN, int NWV, int NST>
-DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
-                     const int* xm, const int* ym) {
+using HGAcc = f32x4[HG<WM, BN, NWV, NST>::MTW][HG<WM, BN, NWV, NST>::NTW];
+
+// acc += the tile's product over K-steps [kt0, kt1) (64 columns each); LDS is free again on return
+template <int WM, int BN, int NWV, int NST>
+DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, uint8_t* lds, const int* xm,
+                  HGAcc<WM, BN, NWV, NST>& acc) {
   typedef HG<WM, BN, NWV, NST> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, NX = G::NX, NW = G::NW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave / WN, wn = wave % WN;
-  const int nkt = S.K >> 6;
-  const int kt0 = (nkt * kslice) / ks, kt1 = (nkt * (kslice + 1)) / ks;
   const int nq = kt1 - kt0;
   const int M = a.M;
 
@@ -101,12 +103,6 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
 #pragma unroll
     for (int i = 0; i < NW; ++i) glds16(wsrc[i] + koff, wl + so + i * 1024);
   };
-
-  f32x4 acc[MTW][NTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one K-step (two 32-deep MFMA K-slices): each slice's fragments are requested together (the LDS
   // latency is exposed once per slice), then its MTW * NTW MFMAs
@@ -184,8 +180,20 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
   }
   wait_vm_lgkm0<0>();                           // drain the clamped tail DMAs before LDS reuse / exit
   __syncthreads();
+}
 
-  // ---- epilogue: lane holds weight rows rbase + 16j + r and activation rows 16i + 4g + e
+// epilogue of a finished tile: split-K slab (ks > 1) or the launch's epilogue
+template <int WM, int BN, int NWV, int NST>
+DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
+                 const int* ym, HGAcc<WM, BN, NWV, NST>& acc) {
+  typedef HG<WM, BN, NWV, NST> G;
+  constexpr int MTW = G::MTW, NTW = G::NTW, WN = G::WN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave / WN, wn = wave % WN;
+  const int M = a.M;
+  // ---- lane holds weight rows rbase + 16j + r and activation rows 16i + 4g + e
   const int rbase = row0 + wn * NTW * 16, mbase = wm * 64;
   if (ks > 1) {
     const int ntot = a.pad;
@@ -270,6 +278,20 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
 }
 
 template <int WM, int BN, int NWV, int NST>
+DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
+                     const int* xm, const int* ym) {
+  typedef HG<WM, BN, NWV, NST> G;
+  HGAcc<WM, BN, NWV, NST> acc;
+#pragma unroll
+  for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nkt = S.K >> 6;
+  hg_main<WM, BN, NWV, NST>(S, row0, (nkt * kslice) / ks, (nkt * (kslice + 1)) / ks, a, lds, xm, acc);
+  hg_epi<WM, BN, NWV, NST>(S, row0, kslice, ks, a, ws, lds, ym, acc);
+}
+
+template <int WM, int BN, int NWV, int NST>
 __global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                        int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
@@ -298,6 +320,168 @@ __global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegLi
   if (a.argmax) a.argmax += m0;
   a.M = min(BM, mrows - m0);
   hgemm_tile<WM, BN, NWV, NST>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds, xm, ym);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stream-K (mode 13): the narrow-N shapes of a decode batch (Llama-3-8B Q|K|V and o at M = 512: 192 / 128 tiles
+// of 128 x 128 for 256 CUs) spread their (tile, K-step) work evenly over a persistent grid. Each XCD owns the weight
+// tiles x, x + 8, ... with all their m-blocks (a weight tile stays in one L2) and cuts that work into equal
+// K-step ranges, one per workgroup of the XCD; a tile split between workgroups is finished by the workgroup that
+// holds its FIRST K-steps (the owner): the others store their fp32 partial accumulators to a slot of `part`
+// (system-scope stores, never left in an L2) and raise a per-workgroup flag carrying the launch generation; the
+// owner adds the partials in K order and runs the launch's epilogue (RoPE / KV append included). An owner whose
+// partner has not delivered within a bounded wait computes that K-range itself (a partner that is not resident --
+// e.g. another process's kernel holds the CUs -- can never hang the owner; a late partial is simply ignored).
+// Generations: workgroup g advances its counter once per launch, and launches of one grid size share a counter set
+// (grids 64 << c, class c), so all workgroups of a launch agree on the generation without a host argument
+// (hipGraph replays stay valid). Launches of one process never overlap (one compute stream).
+#define HG_SK_MAX_WG 1024
+#define HG_SK_CLASSES 5
+__device__ unsigned sk_gen[HG_SK_CLASSES * HG_SK_MAX_WG];
+__device__ unsigned sk_flag[HG_SK_CLASSES * HG_SK_MAX_WG];
+__device__ __forceinline__ int sk_class(int grid) { return grid <= 64 ? 0 : grid <= 128 ? 1 : grid <= 256 ? 2 : grid <= 512 ? 3 : 4; }
+
+struct SkRange {
+  long u0, u1;
+};
+// K-step range of workgroup w of the nw on an XCD that owns U units
+__device__ __forceinline__ SkRange sk_range(long U, int w, int nw) { return SkRange{U * w / nw, U * (w + 1) / nw}; }
+
+template <int WM, int BN, int NWV, int NST>
+__global__ __launch_bounds__(64 * NWV, 1) void hgemm_sk_kernel(SegList segs, GemvArgs a0, float* __restrict__ part,
+                                                             int ntiles, int nmb, long max_spins) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
+  typedef HG<WM, BN, NWV, NST> G;
+  constexpr int BM = G::BM, NACC = G::MTW * G::NTW * 4;
+  __shared__ unsigned s_gen;
+  __shared__ int s_ok;
+  const int gid = blockIdx.x, xcd = gid & 7, w = gid >> 3, nw = gridDim.x >> 3;
+  const int tx = ntiles > xcd ? (ntiles - xcd + 7) / 8 : 0;      // weight tiles of this XCD
+  const int nkt = segs.s[0].K >> 6;                              // every segment has the same K (host-checked)
+  const long U = (long)tx * nmb * nkt;
+  unsigned* const gens = sk_gen + sk_class(gridDim.x) * HG_SK_MAX_WG;
+  unsigned* const flags = sk_flag + sk_class(gridDim.x) * HG_SK_MAX_WG;
+  if (threadIdx.x == 0) {
+    const unsigned gen = __hip_atomic_load(gens + gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_store(gens + gid, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_gen = gen;
+  }
+  __syncthreads();
+  const unsigned gen = s_gen;
+  const SkRange R = sk_range(U, w, nw);
+  for (long u = R.u0; u < R.u1;) {
+    const long lt = u / nkt;                                     // this XCD's (tile, m-block) unit
+    const int ka = (int)(u % nkt);
+    const int kb = (int)min((long)nkt, ka + (R.u1 - u));
+    u += kb - ka;
+    const int tile = (int)(lt / nmb) * 8 + xcd, mb = (int)(lt % nmb);
+    Seg S = segs.s[0];
+#pragma unroll
+    for (int s = 1; s < 8; ++s)
+      if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
+    GemvArgs a = a0;
+    const int m0 = mb * BM;
+    a.m0 = m0;
+    a.x += (size_t)m0 * a.ldx;
+    const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+    a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+    if (a.argmax) a.argmax += m0;
+    a.M = min(BM, a0.M - m0);
+    const int row0 = (tile - S.tile_begin) * BN;
+    HGAcc<WM, BN, NWV, NST> acc;
+#pragma unroll
+    for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    hg_main<WM, BN, NWV, NST>(S, row0, ka, kb, a, hlds, nullptr, acc);
+    if (ka > 0) {
+      // a later piece of the tile: partial -> slot gid ([element][thread], coalesced), then the flag
+      float* slot = part + (size_t)gid * NACC * G::NT;
+#pragma unroll
+      for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NTW; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __hip_atomic_store((unsigned*)slot + ((i * G::NTW + j) * 4 + e) * G::NT + threadIdx.x,
+                               __float_as_uint(acc[i][j][e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(flags + gid, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      continue;
+    }
+    // the owner: the pieces [kb, nkt) belong to the next workgroups of this XCD, in order
+    int k = kb;
+    for (int ww = w + 1; k < nkt && ww < nw; ++ww) {
+      const SkRange P = sk_range(U, ww, nw);
+      if (P.u1 == P.u0) continue;                                   // an empty range (U < workgroups)
+      const int pe = (int)min((long)nkt, (long)k + (P.u1 - P.u0));   // P.u0 == lt * nkt + k
+      const int pg = ww * 8 + xcd;
+      if (threadIdx.x == 0) {
+        long spins = 0;
+        bool ok;
+        while (!(ok = __hip_atomic_load(flags + pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == gen) &&
+               ++spins < max_spins)
+          __builtin_amdgcn_s_sleep(8);
+        s_ok = ok;
+      }
+      __syncthreads();
+      if (s_ok) {
+        const float* slot = part + (size_t)pg * NACC * G::NT;
+#pragma unroll
+        for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+          for (int j = 0; j < G::NTW; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[i][j][e] += __uint_as_float(__hip_atomic_load(
+                  (const unsigned*)slot + ((i * G::NTW + j) * 4 + e) * G::NT + threadIdx.x, __ATOMIC_RELAXED,
+                  __HIP_MEMORY_SCOPE_SYSTEM));
+      } else {
+        hg_main<WM, BN, NWV, NST>(S, row0, k, pe, a, hlds, nullptr, acc);   // partner absent: compute it here
+      }
+      __syncthreads();
+      k = pe;
+    }
+    if (k < nkt) hg_main<WM, BN, NWV, NST>(S, row0, k, nkt, a, hlds, nullptr, acc);   // (unreachable: ranges tile U)
+    hg_epi<WM, BN, NWV, NST>(S, row0, 0, 1, a, nullptr, hlds, nullptr, acc);
+    __syncthreads();      // the epilogue's LDS (arg-max) before the next piece's DMA
+  }
+}
+
+// fp32 workspace of a stream-K launch: one BM x 128 partial slot per workgroup
+long sk_part_floats(int wm, int grid) { return (long)grid * 64 * wm * 128; }
+
+// the owner's wait for a partner's partial, in polls of ~0.2 us (nls_sk_set_spins: 0 = always compute it itself)
+static long g_sk_spins = 1L << 14;
+
+template <int WM, int BN, int NWV, int NST>
+int launch_sk_t(const SegList& sl, int ntiles, int grid, float* part, const GemvArgs& a, hipStream_t st) {
+  typedef HG<WM, BN, NWV, NST> G;
+  const int nmb = (a.M + G::BM - 1) / G::BM;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)hgemm_sk_kernel<WM, BN, NWV, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)G::LDS) != hipSuccess)
+      return -1;
+    attr = true;
+  }
+  hipLaunchKernelGGL((hgemm_sk_kernel<WM, BN, NWV, NST>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, part, ntiles, nmb,
+                     g_sk_spins);
+  return (int)hipGetLastError();
+}
+
+// mode 13: wm 2 (128-row activation blocks), 128 weight rows, 8 | 16 waves; grid = workgroups (a multiple
+// of 8, <= HG_SK_MAX_WG); part: sk_part_floats(wm, grid) floats
+int launch_sk(int wm, int waves, const SegList& sl, int ntiles, int grid, float* part, const GemvArgs& a,
+              hipStream_t st) {
+  if (grid < 8 || grid % 8 || grid > HG_SK_MAX_WG) return -1;
+  for (int i = 1; i < sl.nseg; ++i)
+    if (sl.s[i].K != sl.s[0].K) return -1;
+  // wm 4 (256-row blocks) spills 70-130 registers with the owner's fallback main loop: not instantiated
+  if (wm == 2 && waves == 16) return launch_sk_t<2, 128, 16, 3>(sl, ntiles, grid, part, a, st);
+  if (wm == 2 && waves == 8) return launch_sk_t<2, 128, 8, 3>(sl, ntiles, grid, part, a, st);
+  return -1;
 }
 
 template <int WM, int BN, int NWV, int NST>
@@ -331,3 +515,5 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
 }
 
 }  // namespace nls_hgemm
+
+extern "C" void nls_sk_set_spins(long n) { nls_hgemm::g_sk_spins = n < 0 ? (1L << 14) : n; }

@@ -8,6 +8,8 @@ using namespace nls_gemv;
 namespace nls_hgemm {
 int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
                  const GemvArgs& a, hipStream_t st);
+int launch_sk(int wm, int waves, const SegList& sl, int ntiles, int grid, float* part, const GemvArgs& a,
+              hipStream_t st);
 }
 namespace nls_hg10 {
 int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
@@ -80,7 +82,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A or a dense GEMM without split-K; plain rows,
                            // contiguous Q|K|V segments
-    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10 || mode == 11) && ks <= 1)) || argmax || !fz->pos || !fz->slot ||
+    if (!(mode == 0 || mode == 13 || ((mode == 4 || mode == 5 || mode == 10 || mode == 11) && ks <= 1)) || argmax ||
+        !fz->pos || !fz->slot ||
         !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 || fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
       return -1;
     int c = 0;
@@ -104,8 +107,16 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 12 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
-  if (mode == 12) {
+  if (mode < 0 || mode > 13 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode == 13) {            // stream-K dense GEMM (hgemm.hip): 128 weight rows x 128 activation rows (rt 2), 32 * ks
+                               // persistent workgroups (a power of two, 64..1024), partial slots in ws
+    const int grid = 32 * ks;
+    if ((waves != 8 && waves != 16) || rt != 2 || grid < 64 || grid > 1024 || (grid & (grid - 1)) ||
+        !ws || fz->xf || fz->onw || epi == EPI_SLABS)
+      return -1;
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].K != segs[0].K) return -1;
+  } else if (mode == 12) {
     if (waves != 4 || (rt != 2 && rt != 4) || fz->xf || fz->onw || epi == EPI_ROPE || argmax || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
@@ -150,7 +161,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = (mode == 10 || mode == 11) ? 256 / rt : (mode == 9 || mode == 12) ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = (mode == 10 || mode == 11) ? 256 / rt : (mode == 9 || mode == 12) ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));   // mode 13: 128
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -250,6 +261,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0) {
     if (ks < 1) ks = 1;
     int rc;
+    if (mode == 13) return nls_hgemm::launch_sk(rt, waves, sl, tiles, 32 * ks, (float*)ws, a, st);
     if (mode == 10)
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 11)

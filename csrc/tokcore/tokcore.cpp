@@ -12,18 +12,154 @@
 //              "▁"-normalised text; the adjacent pair whose concatenation is the highest-scoring
 //              vocabulary entry is merged first (leftmost on ties); unknown symbols fall back to <0xXX>
 //              byte tokens -- identical to bpe.py SentencePieceBPE._encode_plain.
+//
+//   Pretok:    the regex pre-tokenisers of bpe.py (LLAMA3_PRETOK, QWEN2_PRETOK, GPT2_PRETOK) as hand-written
+//              scanners over code points, with \p{L} / \p{N} / \s from tables generated out of the same
+//              `regex` module (tools/gen_unicode_tables.py); leftmost-first alternation and the greedy /
+//              backtracking outcome of each alternative are reproduced case by case (comments below), and
+//              tests/test_tokenizer.py fuzzes them against the regex module. ByteLevel.encode_text runs the
+//              pre-tokeniser and the merges of a whole text without the GIL.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <queue>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
+#include "unicode_tables.h"
+
 namespace py = pybind11;
 
 namespace {
+
+bool in_ranges(const CpRange* r, int n, uint32_t cp) {
+  int lo = 0, hi = n - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cp < r[mid].lo) hi = mid - 1;
+    else if (cp > r[mid].hi) lo = mid + 1;
+    else return true;
+  }
+  return false;
+}
+bool is_L(uint32_t c) { return c < 0x80 ? ((c | 0x20) - 'a' < 26u) : in_ranges(kLetter, kLetter_N, c); }
+bool is_N(uint32_t c) { return c < 0x80 ? (c - '0' < 10u) : in_ranges(kNumber, kNumber_N, c); }
+bool is_S(uint32_t c) { return c < 0x80 ? (c == ' ' || (c >= 9 && c <= 13)) : in_ranges(kSpace, kSpace_N, c); }
+bool is_rn(uint32_t c) { return c == '\r' || c == '\n'; }
+
+// UTF-8 -> code points with the byte offset of each (invalid bytes pass through as themselves: Python strings
+// given to encode_text are always valid UTF-8)
+void decode_utf8(const std::string& s, std::vector<uint32_t>& cp, std::vector<uint32_t>& off) {
+  cp.clear();
+  off.clear();
+  for (size_t i = 0; i < s.size();) {
+    const uint8_t c = (uint8_t)s[i];
+    uint32_t v = c;
+    size_t len = 1;
+    if (c >= 0xF0 && i + 3 < s.size() + 0) {
+      len = 4;
+      v = ((c & 7u) << 18) | (((uint8_t)s[i + 1] & 63u) << 12) | (((uint8_t)s[i + 2] & 63u) << 6) | ((uint8_t)s[i + 3] & 63u);
+    } else if (c >= 0xE0 && i + 2 < s.size()) {
+      len = 3;
+      v = ((c & 15u) << 12) | (((uint8_t)s[i + 1] & 63u) << 6) | ((uint8_t)s[i + 2] & 63u);
+    } else if (c >= 0xC0 && i + 1 < s.size()) {
+      len = 2;
+      v = ((c & 31u) << 6) | ((uint8_t)s[i + 1] & 63u);
+    }
+    cp.push_back(v);
+    off.push_back((uint32_t)i);
+    i += len;
+  }
+  off.push_back((uint32_t)s.size());
+}
+
+enum PreMode { PRE_LLAMA3 = 0, PRE_QWEN2 = 1, PRE_GPT2 = 2 };
+
+// length (in code points) of the match at i, >= 1 (every code point matches some alternative)
+size_t pretok_match(const std::vector<uint32_t>& c, size_t i, int mode) {
+  const size_t n = c.size();
+  auto at = [&](size_t k) -> uint32_t { return k < n ? c[k] : 0xFFFFFFFFu; };
+  auto other = [&](size_t k) { return k < n && !is_S(c[k]) && !is_L(c[k]) && !is_N(c[k]); };
+  // contractions: (?i:'s|'t|'re|'ve|'m|'ll|'d) (llama3 / qwen2; case folding: s <-> S <-> U+017F), or the
+  // case-sensitive list (gpt2)
+  if (c[i] == '\'') {
+    const bool ci = mode != PRE_GPT2;
+    auto eq = [&](size_t k, char lc) {
+      const uint32_t v = at(k);
+      if (v == (uint32_t)lc) return true;
+      if (!ci) return false;
+      return v == (uint32_t)(lc - 32) || (lc == 's' && v == 0x17F);
+    };
+    if (eq(i + 1, 's') || eq(i + 1, 't') || eq(i + 1, 'm') || eq(i + 1, 'd')) return 2;
+    if (eq(i + 1, 'r') && eq(i + 2, 'e')) return 3;
+    if (eq(i + 1, 'v') && eq(i + 2, 'e')) return 3;
+    if (eq(i + 1, 'l') && eq(i + 2, 'l')) return 3;
+  }
+  if (mode == PRE_GPT2) {
+    // ' ?\p{L}+', ' ?\p{N}+', ' ?[^\s\p{L}\p{N}]+': an optional space belongs to the run after it
+    const size_t j = (c[i] == ' ' && i + 1 < n) ? i + 1 : i;
+    for (int kind = 0; kind < 3; ++kind) {
+      auto ok = [&](size_t k) {
+        return k < n && (kind == 0 ? is_L(c[k]) : kind == 1 ? is_N(c[k]) : other(k));
+      };
+      size_t s0 = ok(j) ? j : (ok(i) ? i : n);
+      if (s0 == n) continue;
+      size_t e = s0;
+      while (ok(e)) ++e;
+      return e - i;
+    }
+  } else {
+    // [^\r\n\p{L}\p{N}]?\p{L}+
+    if (!is_rn(c[i]) && !is_L(c[i]) && !is_N(c[i]) && i + 1 < n && is_L(c[i + 1])) {
+      size_t e = i + 1;
+      while (e < n && is_L(c[e])) ++e;
+      return e - i;
+    }
+    if (is_L(c[i])) {
+      size_t e = i;
+      while (e < n && is_L(c[e])) ++e;
+      return e - i;
+    }
+    // \p{N}{1,3} (llama3) / \p{N} (qwen2)
+    if (is_N(c[i])) {
+      const size_t cap = mode == PRE_QWEN2 ? 1 : 3;
+      size_t e = i;
+      while (e < n && e - i < cap && is_N(c[e])) ++e;
+      return e - i;
+    }
+    // ' ?[^\s\p{L}\p{N}]+[\r\n]*'
+    {
+      const size_t s0 = (c[i] == ' ' && other(i + 1)) ? i + 1 : (other(i) ? i : n);
+      if (s0 != n) {
+        size_t e = s0;
+        while (other(e)) ++e;
+        while (e < n && is_rn(c[e])) ++e;
+        return e - i;
+      }
+    }
+    // '\s*[\r\n]+': up to and including the LAST \r / \n of the whitespace run at i
+    {
+      size_t w = i, last = n;
+      while (w < n && is_S(c[w])) {
+        if (is_rn(c[w])) last = w;
+        ++w;
+      }
+      if (last != n) return last + 1 - i;
+    }
+  }
+  // '\s+(?!\S)' then '\s+': the whitespace run, minus its last character when a non-space follows it
+  size_t w = i;
+  while (w < n && is_S(c[w])) ++w;
+  if (w > i) {
+    if (w == n) return w - i;
+    if (w - i >= 2) return w - 1 - i;
+    return 1;                                   // '\s+' of a single space before a non-space
+  }
+  return 1;                                     // (unreachable: every code point is L, N, \s or other)
+}
 
 struct PairHash {
   size_t operator()(uint64_t k) const { return std::hash<uint64_t>()(k * 0x9E3779B97F4A7C15ull); }
@@ -40,6 +176,17 @@ class ByteLevel {
       const auto& m = merges[i];
       const uint64_t k = key(std::get<0>(m), std::get<1>(m));
       if (rank_.find(k) == rank_.end()) rank_.emplace(k, std::make_pair((int32_t)i, std::get<2>(m)));
+    }
+  }
+
+  // the whole text: pre-tokenise (mode: PreMode) and merge every piece
+  void encode_text(const std::string& text, int mode, std::vector<int32_t>& out) const {
+    std::vector<uint32_t> cp, off;
+    decode_utf8(text, cp, off);
+    for (size_t i = 0; i < cp.size();) {
+      const size_t len = pretok_match(cp, i, mode);
+      encode_piece(text.data() + off[i], off[i + len] - off[i], out);
+      i += len;
     }
   }
 
@@ -186,12 +333,34 @@ PYBIND11_MODULE(_tokcore, m) {
         }
         return out;
       })
+      // text (UTF-8) -> ids: the native pre-tokeniser (mode 0 llama3, 1 qwen2, 2 gpt2) + merges, GIL released
+      .def("encode_text", [](const ByteLevel& b, const std::string& text, int mode) {
+        std::vector<int32_t> out;
+        {
+          py::gil_scoped_release r;
+          out.reserve(text.size() / 3 + 4);
+          b.encode_text(text, mode, out);
+        }
+        return out;
+      })
       .def("encode_piece", [](const ByteLevel& b, const py::bytes& piece) {
         std::string s = piece;
         std::vector<int32_t> out;
         b.encode_piece(s.data(), s.size(), out);
         return out;
       });
+  // the pre-tokeniser alone (tests): text -> the matched pieces as UTF-8 byte strings
+  m.def("pretokenize", [](const std::string& text, int mode) {
+    std::vector<uint32_t> cp, off;
+    decode_utf8(text, cp, off);
+    std::vector<py::bytes> out;
+    for (size_t i = 0; i < cp.size();) {
+      const size_t len = pretok_match(cp, i, mode);
+      out.emplace_back(text.substr(off[i], off[i + len] - off[i]));
+      i += len;
+    }
+    return out;
+  });
   py::class_<Spm>(m, "Spm")
       .def(py::init<const std::vector<std::string>&, const std::vector<float>&, std::vector<int32_t>>())
       .def("encode", [](const Spm& s, const std::string& text) {

@@ -241,6 +241,11 @@ _WS = {}
 _WS_OLD = []   # superseded workspaces stay alive: captured hipGraphs may still point at them
 
 
+def sk_floats(rt: int, ks: int) -> int:
+    """Partial-slot floats of a stream-K launch (mode 13): 32 * ks workgroups x (64 * rt) x 128."""
+    return 32 * ks * 64 * rt * 128
+
+
 def _workspace(dev, n: int) -> torch.Tensor:
     """Split-K partial-slab workspace (64 MiB minimum; only grows, never freed)."""
     w = _WS.get(dev)
@@ -281,9 +286,9 @@ def _seg_arr(segs: Sequence[Seg], mode: int):
     included: the dense GEMM gathers/scatters mapped rows like mode 2)."""
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
-        if mode in (4, 5, 6, 10):
+        if mode in (4, 5, 6, 10, 13):
             if s.w.d16 is None:
-                raise ValueError(f"{s.w.name}: dense modes (4-6, 8, 10) need QWeight.expand_dense()")
+                raise ValueError(f"{s.w.name}: dense modes (4-6, 10, 13) need QWeight.expand_dense()")
             arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, s.w.rows, s.w.K,
                                  s.ycol)
         else:
@@ -378,7 +383,9 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
             return y
         arr = _seg_arr(segs, mode)
         ws = None
-        if mode != 0 and ks > 1:
+        if mode == 13:
+            ws = _workspace(x.device, sk_floats(rt, ks)).data_ptr()
+        elif mode != 0 and ks > 1:
             width = segs[0].w.rows if mapped else sum(s.w.rows for s in segs)   # mapped split-K: shared columns
             ws = _workspace(x.device, ks * M * width).data_ptr()
         rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
@@ -464,7 +471,7 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
                                                x.stride(0), M, float(alpha), EPI["add"], None, waves, rt, 0, 1, None,
                                                _stream_ptr(x), ctypes.byref(fz)), "nls_qgemv_ex(addnorm)")
             return h
-        if mode != 0 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
+        if mode not in (0, 13) and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
             L = _lib.lib()
             ws = _workspace(x.device, ks * M * seg.w.rows)
             arr = _seg_arr([seg], mode)
@@ -644,19 +651,20 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        if (mode in (4, 5, 10, 11) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D and not neox
-                and fuse_rope and kc.dtype == torch.bfloat16):
-            # large-M GEMM (dense f16 copies, or mode 11 on the quantised tile-blocks) with RoPE + KV append in
-            # its epilogue (no f32 qkv round trip, no RoPE launch)
+        if (((mode in (4, 5, 10, 11) and ks == 1) or mode == 13) and contiguous and ncol == (Hq + 2 * Hkv) * D
+                and not neox and fuse_rope and kc.dtype == torch.bfloat16):
+            # large-M GEMM (dense f16 copies, stream-K, or mode 11 on the quantised tile-blocks) with RoPE + KV
+            # append in its epilogue (no f32 qkv round trip, no RoPE launch)
             fz = _lib.NlsFuse(pos=pos.data_ptr(), slot=slot.data_ptr(), cs=cs.data_ptr(), bias=_p(bias),
                               q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
                               Hq=Hq, Hkv=Hkv, D=D)
+            ws = _workspace(h.device, sk_floats(rt, ks)).data_ptr() if mode == 13 else None
             _lib.check(_lib.lib().nls_qgemv_ex(_seg_arr(segs, mode), len(segs), h.data_ptr(), h.stride(0),
                                                qkv.data_ptr(), qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt,
-                                               mode, 1, None, _stream_ptr(h), ctypes.byref(fz)),
+                                               mode, ks if mode == 13 else 1, ws, _stream_ptr(h), ctypes.byref(fz)),
                        "nls_qgemv_ex(dense rope)")
             return
-        if mode != 0 and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
+        if mode not in (0, 13) and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
             L = _lib.lib()
             ws = _workspace(h.device, ks * T * ncol)
             arr = _seg_arr(segs, mode)

@@ -49,6 +49,7 @@ _SIGS = {
                        c_float, c_int, c_void_p, c_int, c_int, c_void_p],
     "nls_prefetch": [c_void_p, c_long, c_int, c_void_p],
     "nls_graph_kernel_names": [c_void_p, c_void_p, c_long],
+    "nls_sk_set_spins": [c_long],
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
     "nls_splitk_add_rmsnorm": [c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int,
                                c_float, c_void_p],

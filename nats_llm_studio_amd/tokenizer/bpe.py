@@ -109,6 +109,8 @@ class ByteLevelBPE(_Base):
         self.u2b = {v: k for k, v in self.b2u.items()}
         self.pretok = re.compile(GPT2_PRETOK if pre in ("gpt2", "default") else
                                  QWEN2_PRETOK if pre == "qwen2" else LLAMA3_PRETOK)
+        # the same pattern in the native pre-tokeniser (csrc/tokcore Pretok: 0 llama3, 1 qwen2, 2 gpt2)
+        self.pre_mode = 2 if pre in ("gpt2", "default") else 1 if pre == "qwen2" else 0
         self._cache: Dict[str, List[int]] = {}
         self.native = self._native_core()
 
@@ -146,8 +148,10 @@ class ByteLevelBPE(_Base):
 
     def _encode_plain(self, text: str) -> List[int]:
         if self.native is not None:
-            # concurrent=True: the regex scan releases the GIL (handler threads of a request burst pre-tokenise in
-            # parallel; the merge loop below releases it too)
+            if hasattr(self.native, "encode_text"):
+                # pre-tokeniser + merges natively, the GIL released for the whole text: a burst of requests
+                # tokenises in parallel on the handler threads
+                return self.native.encode_text(text, self.pre_mode)
             return self.native.encode_pieces([p.encode("utf-8") for p in self.pretok.findall(text, concurrent=True)])
         return self._encode_plain_py(text)
 

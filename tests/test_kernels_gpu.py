@@ -784,12 +784,14 @@ def test_qkv_rope_kv_fused(gpu, cfg, M, bias):
     _qkv_rope_case(gpu, cfg, M, bias, dense=False)
 
 
-@pytest.mark.parametrize("cfg", [(4, 16, 2, 1), (4, 16, 4, 1), (5, 8, 4, 1), (10, 8, 1, 1), (10, 8, 1, 2), (10, 8, 2, 1)])
+@pytest.mark.parametrize("cfg", [(4, 16, 2, 1), (4, 16, 4, 1), (5, 8, 4, 1), (10, 8, 1, 1), (10, 8, 1, 2), (10, 8, 2, 1),
+                                 (13, 16, 2, 2), (13, 8, 2, 4), (13, 16, 2, 8)])
 @pytest.mark.parametrize("M", [70, 300, 520])
 @pytest.mark.parametrize("bias", [False, True])
 def test_qkv_rope_kv_dense(gpu, cfg, M, bias):
-    """The dense GEMMs on the weights' f16 copies (modes 4/5/10) with the RoPE + KV-append epilogue
-    (split-K 1: lane pairs rotated in registers; split-K 2: slabs summed by the RoPE kernel)."""
+    """The dense GEMMs on the weights' f16 copies (modes 4/5/10, stream-K mode 13) with the RoPE + KV-append
+    epilogue (split-K 1 and stream-K owners: lane pairs rotated in registers; split-K 2: slabs summed by the
+    RoPE kernel)."""
     _qkv_rope_case(gpu, cfg, M, bias, dense=True)
 
 
@@ -984,6 +986,53 @@ def test_hgemm_dense(gpu, t, M, mode, wm, ks, wv):
     y3 = torch.zeros(pad, rows, device=gpu)
     ops.qgemv([ops.Seg(w)], x, y3, M, mode=2, waves=8, rt=wm, ks=1)
     _close(y3[:M], y[:M], 1e-3)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("M", [65, 300, 520])
+@pytest.mark.parametrize("wm,ks,wv", [(2, 2, 16), (2, 4, 8), (2, 8, 8), (2, 8, 16), (2, 16, 16)])
+@pytest.mark.parametrize("spins", [-1, 0])
+def test_hgemm_streamk(gpu, t, M, wm, ks, wv, spins):
+    """Stream-K dense GEMM (mode 13): 32 * ks persistent workgroups cut each XCD's (tile, K-step) work evenly, so
+    tiles are split over 2-3 workgroups (3 weight tiles of a 264-row matrix: most XCDs idle, the rest split 12
+    K-steps x up to 5 m-blocks); the owner sums the partials -- or, with a zero wait budget (spins 0), computes
+    every missing piece itself. Store with arg-max keys, residual add; repeated launches (generation flags) and
+    replays of a captured graph with new activations."""
+    L = ops._lib.lib()
+    L.nls_sk_set_spins(spins)
+    try:
+        rows, K = 264, 768
+        w, Wd = _qw(rows, K, t, gpu)
+        w.expand_dense()
+        x = _x(M, K, gpu)
+        pad = x.shape[0]
+        y = torch.zeros(pad, rows, device=gpu)
+        keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
+        for rep in range(3):
+            x[:M] = (torch.randn(M, K, device=gpu) * 0.5).to(x.dtype)
+            keys.zero_()
+            ops.qgemv([ops.Seg(w)], x, y, M, mode=13, waves=wv, rt=wm, ks=ks, argmax=keys)
+            ref = x[:M].float().cpu() @ Wd.t()
+            _close(y[:M], ref)
+        ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
+        ops.argmax_unpack(keys, M, ids)
+        assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
+        base = torch.randn(pad, rows, device=gpu)
+        y2 = base.clone()
+        ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=13, waves=wv, rt=wm, ks=ks)
+        _close(y2[:M], base[:M].cpu() + 0.5 * (x[:M].float().cpu() @ Wd.t()))
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            ops.qgemv([ops.Seg(w)], x, y, M, mode=13, waves=wv, rt=wm, ks=ks)
+        for rep in range(3):
+            x[:M] = (torch.randn(M, K, device=gpu) * 0.5).to(x.dtype)
+            y.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            _close(y[:M], x[:M].float().cpu() @ Wd.t())
+    finally:
+        L.nls_sk_set_spins(-1)
 
 
 @pytest.mark.parametrize("mode,ks,wv", [(4, 1, 8), (4, 2, 8), (5, 1, 8), (5, 2, 8), (5, 1, 16), (4, 2, 16)])

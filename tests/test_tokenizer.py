@@ -115,3 +115,28 @@ def test_spm_duplicate_token_strings_native_matches_python():
         assert nat == ref, (t, nat, ref)
     assert tok.encode("ab", add_bos=False) == [259 + 6]          # "▁ab": the only id of that string
     assert tok.encode("bab", add_bos=False) == [259 + 8, 259 + 5]  # "▁b" + the duplicate "ab": its LAST id
+
+
+def test_native_pretokenizer_matches_regex():
+    """csrc/tokcore's hand-written pre-tokenisers (llama3 / qwen2 / gpt2) split random texts exactly as the regex
+    module does with bpe.py's patterns: letters, digits, Unicode whitespace, CR/LF runs, contractions in both
+    cases (and U+017F, which case-folds to 's'), combining marks, CJK, emoji, punctuation runs."""
+    import random
+
+    import regex
+
+    from nats_llm_studio_amd.tokenizer import bpe
+    tc = pytest.importorskip("nats_llm_studio_amd.tokenizer._tokcore")
+    alphabet = (list("abcXYZ sStTrReEvVmMlLdD'") + list("0123456789") + [" ", " ", "  ", "\n", "\r", "\t", "\r\n"]
+                + list("!?.,;:-_()[]{}\"'`~@#$%^&*+=/\\|<>") + ["é", "ß", "Ω", "ж", "ſ", "ǅ", "́", "̀",
+                "中", "文", "日本", "한", "😀", "👍🏽", "٣", "Ⅻ", "½", "²", " ", " ", "　", " ",
+                "\u0085", "\x0b", "\x0c", "\x1c", "​", "﻿", "'S", "'LL", "'Re", "'ve", "'D", "'ſ"])
+    rng = random.Random(5)
+    pats = {0: bpe.LLAMA3_PRETOK, 1: bpe.QWEN2_PRETOK, 2: bpe.GPT2_PRETOK}
+    for mode, pat in pats.items():
+        rx = regex.compile(pat)
+        for _ in range(3000):
+            text = "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 40)))
+            want = [p.encode("utf-8") for p in rx.findall(text)]
+            got = tc.pretokenize(text.encode("utf-8").decode("utf-8"), mode)
+            assert got == want, (mode, text, got, want)

@@ -69,7 +69,12 @@ def candidates(M, K, epi):
     if epi == "argmax":
         out = [c for c in out if c[3] == 1]
     nkt = K // 64
-    return [c for c in out if nkt // c[3] >= 8]
+    out = [c for c in out if nkt // c[3] >= 8]
+    # mode 13: stream-K over 32 * ks persistent workgroups (ks is the grid, not a K split)
+    for waves in (16, 8):
+        for ks in (4, 8):
+            out.append((13, waves, 2, ks))
+    return out
 
 
 def main():
@@ -79,6 +84,7 @@ def main():
     ap.add_argument("--roles", default="qkv,o,gateup,down,lm_head")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--emit", action="store_true")
+    ap.add_argument("--modes", default="", help="comma list: time only these modes (e.g. 4,13)")
     a = ap.parse_args()
     spec = SPECS[a.model]
     dev = torch.device("cuda:0")
@@ -134,6 +140,8 @@ def main():
                 return fn
             res = []
             for cfg in candidates(M, K, epi):
+                if a.modes and cfg[0] not in {int(m) for m in a.modes.split(",")}:
+                    continue
                 try:
                     res.append((timed(graph_of(launch(cfg)), a.rounds), cfg))
                 except Exception as e:

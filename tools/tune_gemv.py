@@ -72,7 +72,9 @@ def dense_configs(K):
     nkt = K // 64
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
-            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
+            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
+            # mode 13: stream-K over 32 * ks persistent workgroups (hgemm.hip hgemm_sk_kernel)
+            + [(13, wv, 2, ks) for wv in (16, 8) for ks in (4, 8, 16)])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
@@ -161,7 +163,10 @@ def main():
             if args.dense:
                 qcfg = tuning.select(segs, M)
                 qus = time_cfg(copies, x, y, M, epi, keys, tuple(qcfg))
+                modes = {int(m) for m in args.modes.split(",")} if args.modes else None
                 for cfg in dense_configs(K):
+                    if modes is not None and cfg[0] not in modes:
+                        continue
                     us = time_cfg(copies, x, y, M, epi, keys, cfg)
                     if us is not None:
                         res.append((us, cfg))
