@@ -60,6 +60,8 @@ _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,
 # NLS_EP_A2A=0 keeps the combine-then-all-reduce everywhere
 _EP_A2A = os.environ.get("NLS_EP_A2A", "1")
 _EP_A2A_T = int(os.environ.get("NLS_EP_A2A_T", "64"))
+# tokens per step the EP decode exchange covers (receive buffers: 2 x tokens x top-k x d_model floats per rank)
+_EPX_TOKENS = int(os.environ.get("NLS_EPX_TOKENS", "512"))
 # MoE router logits through ops.router_logits (E-row kernel) rather than the GEMV/GEMM tiles; 0 = the GEMV
 _ROUTER_KERNEL = os.environ.get("NLS_ROUTER_KERNEL", "1") == "1"
 
@@ -175,6 +177,14 @@ class LlamaModel:
         self.vocab_lo, self.vocab_hi = self._vocab_range()
         self.weight_bytes = 0
         self._load()
+        # expert parallelism on GPUs: decode-size MoE steps exchange the experts' output rows over the IPC buffers
+        # (parallel/oneshot.py ep_exchange) instead of all-reducing [T, d] partial combines (NLS_EP_EXCHANGE=0: off)
+        self.ep_exchange = False
+        os_ = getattr(comm, "oneshot", None) if comm is not None else None
+        if (self.ep and os_ is not None and self.device.type == "cuda"
+                and os.environ.get("NLS_EP_EXCHANGE", "1") == "1"):
+            os_.ep_setup(_EPX_TOKENS * cfg.n_expert_used, cfg.d_model)
+            self.ep_exchange = True
         ff = reader.dequantized("rope_freqs.weight") if "rope_freqs.weight" in reader.tensors else None
         self.cs = ops.rope_table(cfg.ctx, self.D, cfg.rope_base, self.device, ff, cfg.rope_pos_scale)
 
@@ -454,7 +464,7 @@ class LlamaModel:
             nxt = self.layers[L + 1].attn_norm if L + 1 < len(self.layers) else self.out_norm
             fused_prev = False
             if cfg.n_expert:
-                fused_prev = self._moe(lw, b, T, nxt if fused else None,
+                fused_prev = self._moe(lw, b, T, nxt if (fused or self.ep_exchange) else None,
                                        lw.ffn_norm if moe_norm and not moe_routed else None, routed=moe_routed)
             else:
                 ops.qgemv([Seg(lw.gateup)], b.h, b.act, T, epi="swiglu")
@@ -694,9 +704,11 @@ class LlamaModel:
             # few tokens: the route kernel also lists each (token, slot)'s expert and the expert GEMVs
             # launch only those experts' tiles (k of E; the rest would be launched just to exit)
             use_sel = not gemm and self.device.type == "cuda" and n * k < len(self.experts)
+            # the EP exchange needs every (token, slot)'s expert: its owner rank pushes the row
+            exch = self.ep_exchange and self.comm.oneshot.ep_ok(n * k, cfg.d_model)
             if not (routed and c0 == 0 and n == T):
                 ops.moe_route(m["rlogits"][c0:], n, k, m["topw"], m["counts"], m["xrows"], m["yrows"], cap,
-                              sel=m["sel"] if use_sel else None, counts_zeroed=zeroed and c0 == 0)
+                              sel=m["sel"] if (use_sel or exch) else None, counts_zeroed=zeroed and c0 == 0)
             loc = list(zip(self.experts, lw.exp_gateup, lw.exp_down))
             segs = [Seg(gu, 0, m["xrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, gu, _ in loc]
 
@@ -704,14 +716,24 @@ class LlamaModel:
                 return (m["sel"], n * k, self.experts[0] + s0) if use_sel else None
             for s0 in range(0, len(segs), 8):
                 ops.qgemv(segs[s0:s0 + 8], b.h[c0:], b.act, n, epi="swiglu", sel=sel(s0), **gu)
-            if self.ep:                        # rows routed to other ranks' experts stay zero
+            if self.ep and not exch:           # rows routed to other ranks' experts stay zero
                 m["yexp"][:n * k].zero_()
             segs = [Seg(dn, 0, m["yrows"][e * cap:], m["yrows"][e * cap:], m["counts"][e:e + 1]) for e, _, dn in loc]
             for s0 in range(0, len(segs), 8):
                 ops.qgemv(segs[s0:s0 + 8], b.act, m["yexp"], dn_rows if dn.get("ks", 1) > 1 else n, epi="f32",
                           sel=sel(s0), **dn)
             xs = b.x[c0:c0 + n]
-            if self.shard.size > 1:
+            if exch:
+                # every rank ends with all n * k expert rows (its own pushed, the peers' received): the single-GPU
+                # combine, identical on every rank, no all-reduce
+                self.comm.oneshot.ep_exchange(m["yexp"], n * k, m["sel"], len(self.experts))
+                self.comm.stats["ep_exchange"] = self.comm.stats.get("ep_exchange", 0) + 1
+                if next_norm is not None and n == T:
+                    ops.moe_combine_norm(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale, next_norm, cfg.eps, b.h)
+                    normed = True
+                else:
+                    ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale)
+            elif self.shard.size > 1:
                 # combine locally first, then ONE all-reduce of the combined [n, d] rows (k x fewer bytes
                 # than reducing the per-slot expert outputs): rank 0 adds into the residual, the others
                 # contribute their partial combine from zero (EP: own experts; TP: own FFN slice)

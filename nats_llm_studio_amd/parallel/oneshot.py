@@ -61,13 +61,45 @@ class OneShotAllReduce:
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._norm = {}               # D -> (epochs, tickets, ssq) of the fused add+norm
         self.resets = 0
+        self.ebuf = None              # expert-parallel decode exchange (ep_setup)
+        self.ERR_WORDS = 3
         comm.barrier()
 
-    def _exchange(self, L, hs, comm):
+    def ep_setup(self, rows: int, D: int):
+        """Receive buffers of the expert-parallel decode exchange (csrc/kernels/ep_exchange.hip) for up to `rows`
+        (token, slot) rows of D floats; collective (every rank calls it, in the same order as the others)."""
+        L = _lib.lib()
+        need = L.nls_epx_bytes(rows, D)
+        ar_cap = -(-(need - 256) // (8 * self.world)) + 4
+        ar_cap += (-ar_cap) % 4
+        bufs_before = len(self._owned)
+        buf, peers = self._exchange(L, L.nls_ar_handle_size(), self.comm, cap=ar_cap)
+        if self.comm.min_int(int(self.ok and len(self._owned) > bufs_before)) == 0:
+            raise RuntimeError("expert-parallel exchange: IPC buffer setup failed on some rank")
+        self.ebuf, self.epeers, self.e_rows, self.e_D = buf, peers, int(rows), int(D)
+        self.egen = torch.zeros(L.nls_epx_wgs(), dtype=torch.int32, device=self.device)
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(L.nls_epx_init(buf, self.e_rows, self.e_D, st), "nls_epx_init")
+        torch.cuda.synchronize(self.device)
+        self.ERR_WORDS = 4
+        self.comm.barrier()
+
+    def ep_ok(self, n: int, D: int) -> bool:
+        return self.ebuf is not None and n <= self.e_rows and D == self.e_D
+
+    def ep_exchange(self, y: torch.Tensor, n: int, sel: torch.Tensor, per: int):
+        """y[:n] (f32, [n, D]): rows whose expert (sel[j], global id) belongs to this rank (sel // per == rank)
+        are pushed to every peer; the other rows are filled with the peers' -- every rank ends with all n rows."""
+        rc = _lib.lib().nls_epx_run(y.data_ptr(), y.stride(0), n, y.shape[1], sel.data_ptr(), per, self.rank,
+                                    self.world, self.epeers, self.e_rows, self.egen.data_ptr(), self.err.data_ptr(),
+                                    self.max_spins, _stream(y))
+        _lib.check(rc, "nls_epx_run")
+
+    def _exchange(self, L, hs, comm, cap: Optional[int] = None):
         buf = ctypes.c_void_p()
         handle = (ctypes.c_char * hs)()
         mine = b""
-        if self.ok and L.nls_ar_alloc(self.cap, self.world, ctypes.byref(buf), handle) == 0:
+        if self.ok and L.nls_ar_alloc(self.cap if cap is None else cap, self.world, ctypes.byref(buf), handle) == 0:
             self._owned.append(buf.value)
             mine = bytes(handle)
         else:
@@ -114,7 +146,7 @@ class OneShotAllReduce:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= self.cap
                 and t.numel() % 4 == 0)
 
-    ERR_WORDS = 3      # one error word per buffer set (sum, fused add+norm, gather / arg-max)
+    ERR_WORDS = 3      # one error word per buffer set (sum, fused add+norm, gather / arg-max[, EP exchange: 4])
 
     def err_fetch(self, host: torch.Tensor):
         """Enqueue the copy of this rank's error words (raised by ANY rank's timed-out poll, one per buffer
@@ -123,12 +155,17 @@ class OneShotAllReduce:
         st = torch.cuda.current_stream(self.device).cuda_stream
         for i, b in enumerate((self.buf, self.nbuf, self.gbuf)):
             _lib.check(L.nls_ar_err_fetch(b, self.cap, self.world, host.data_ptr() + 4 * i, st), "nls_ar_err_fetch")
+        if self.ebuf is not None:
+            _lib.check(L.nls_epx_err_fetch(self.ebuf, self.e_rows, self.e_D, host.data_ptr() + 12, st),
+                       "nls_epx_err_fetch")
 
     def err_clear(self):
         L = _lib.lib()
         st = torch.cuda.current_stream(self.device).cuda_stream
         for b in (self.buf, self.nbuf, self.gbuf):
             _lib.check(L.nls_ar_err_clear(b, self.cap, self.world, st), "nls_ar_err_clear")
+        if self.ebuf is not None:
+            _lib.check(L.nls_epx_err_clear(self.ebuf, self.e_rows, self.e_D, st), "nls_epx_err_clear")
         self.err.zero_()
 
     def debug_state(self, rows: int = 48) -> dict:
@@ -249,6 +286,9 @@ class OneShotAllReduce:
         st = torch.cuda.current_stream(self.device).cuda_stream
         for b in (self.buf, self.nbuf, self.gbuf):
             _lib.check(L.nls_ar_reinit(b, self.cap, self.world, st), "nls_ar_reinit")
+        if self.ebuf is not None:
+            _lib.check(L.nls_epx_init(self.ebuf, self.e_rows, self.e_D, st), "nls_epx_init")
+            self.egen.zero_()
         for t in [self.epochs, self.gepochs, self.err] + [x for st_ in self._norm.values() for x in st_]:
             t.zero_()
         torch.cuda.synchronize(self.device)

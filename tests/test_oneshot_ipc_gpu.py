@@ -84,6 +84,20 @@ def _worker(rank, world, port, q):
                            for r in range(world)], dim=1)
         d = dst.cpu()
         out["gather_bad"] = float(not (torch.equal(d[0].view(torch.float32), exp_v) and torch.equal(d[1], exp_i)))
+        # expert-parallel decode exchange: rows whose expert lives on rank r are computed (here: filled) by rank r
+        # only; after the exchange every rank holds every row, bit-exact (random routing, repeated calls / parities)
+        E, per, D, n = 4 * world, 4, 256, 40
+        ar.ep_setup(64, D)
+        bad = 0.0
+        for it in range(4):
+            sel = torch.randint(0, E, (n,), generator=g.manual_seed(900 + it), dtype=torch.int32)
+            full = torch.randn(n, D, generator=g.manual_seed(950 + it))
+            mine = (sel // per) == rank
+            y = torch.where(mine.unsqueeze(1), full, torch.full_like(full, float("nan"))).to(dev)
+            ar.ep_exchange(y, n, sel.to(dev), per)
+            torch.cuda.synchronize()
+            bad += float(not torch.equal(y.cpu(), full))
+        out["ep_exchange_bad"] = bad
         out["err"] = int(ar.err.item())
         ar.close()
         dist.barrier()

@@ -43,6 +43,8 @@ def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep, tmp_path):
     assert fol["counters"]["device_sampled_steps"] == c["device_sampled_steps"], (fol["counters"], c)
     assert sorted(map(tuple, fol["graphs"])) == sorted(map(tuple, tp["graphs"]))
     assert tp["oneshot_resets"] == 0
+    if ep:      # decode MoE steps exchanged the experts' rows over IPC instead of all-reducing partial combines
+        assert tp["comm"].get("ep_exchange", 0) > 0, tp["comm"]
     n = len(rehearsal.PROMPTS)
     assert tp["tokens"][:n] == ref["tokens"][:n], (tp["tokens"], ref["tokens"])      # greedy
     assert tp["tokens"][n:] == ref["tokens"][n:], (tp["tokens"], ref["tokens"])      # seeded top-k
