@@ -24,7 +24,10 @@ import torch.distributed as dist
 
 from ..ops import _lib
 
-DEFAULT_CAP = 64 * 4096 * 4          # floats: B=64 x d=16384 fp32 (8 MiB message), 2 slots x world
+# floats per message (2 parity slots x world per buffer set): a 256-row prefill chunk of d = 8192 (Llama-3-70B) fits,
+# so every tensor-parallel all-reduce of the engine runs on the IPC kernels (8 MiB; 384 MiB of buffers at TP=8)
+DEFAULT_CAP = 256 * 8192
+AG_MAX_WORDS = 16 * 64 * 256 * 2       # the gather kernel's fixed grid: AG_BLOCKS x AR_MAX_WG_BLOCKS x AG_THREADS granules
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -306,7 +309,7 @@ class OneShotAllReduce:
         _lib.check(rc, "nls_ag_argmax")
 
     def gather_ok(self, words: int) -> bool:
-        return 2 * words <= self.cap
+        return 2 * words <= self.cap and words <= AG_MAX_WORDS
 
     def gather(self, src: torch.Tensor, dst: torch.Tensor):
         """Lossless all-gather: src [A, rows, C] of 32-bit words (this rank) -> dst [A, rows, world * C] with
