@@ -71,6 +71,7 @@ class Comm:
         self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
         if op == dist.ReduceOp.SUM and self._os(t) is not None and self.oneshot.eligible(t):
             self.oneshot.all_reduce(t)
+            self.stats["oneshot_all_reduce"] = self.stats.get("oneshot_all_reduce", 0) + 1
             return t
         dist.all_reduce(t, op=op, group=self.group)
         return t

@@ -58,7 +58,11 @@ def _engine(path: str, dev, shard=None, comm=None, graphs: bool = True):
     from ..models.llama import LlamaModel, ShardSpec
     m = LlamaModel(GGUFReader(path), dev, shard or ShardSpec(), comm)
     graphs = graphs and dev.type == "cuda" and os.environ.get("NLS_REHEARSAL_GRAPHS", "1") == "1"
-    return Engine(m, None, max_batch=8, max_prefill_tokens=256, num_blocks=256, use_graphs=graphs, ctx=512)
+    # NLS_REHEARSAL_PREFILL: a larger prefill chunk (long-prompt case: row-parallel prefill all-reduces in 256-row
+    # chunks on the comm side stream, comm.row_parallel_add)
+    mp = int(os.environ.get("NLS_REHEARSAL_PREFILL", "256"))
+    return Engine(m, None, max_batch=8, max_prefill_tokens=mp, num_blocks=max(256, 2 * mp // 16 + 64),
+                  use_graphs=graphs, ctx=max(512, mp + 64))
 
 
 def _kernel_profile(eng, futs, steps: int) -> Dict:
@@ -122,6 +126,16 @@ def _drive(eng, new_tokens: int, profile_steps: int = 0, greedy_only: bool = Fal
     wall = time.perf_counter() - t0
     out = dict(tokens=[f.result().token_ids for f in futs], steps=steps, wall_s=round(wall, 3),
                counters=dict(eng.counters), graphs=[list(k) for k in sorted(eng.graphs)])
+    long_len = int(os.environ.get("NLS_REHEARSAL_LONG", "0"))
+    if long_len:
+        # one long greedy prompt prefilled in ONE chunk (NLS_REHEARSAL_PREFILL >= its length)
+        from ..engine.sampling import SamplingParams
+        f = eng.submit(GenRequest([1] + [(37 * i) % 5000 + 10 for i in range(long_len - 1)],
+                                  SamplingParams(max_tokens=4, ignore_eos=True)))
+        while not f.done():
+            eng.step()
+        _sync(eng.dev)
+        out["long_tokens"] = f.result().token_ids
     if os.environ.get("NLS_REHEARSAL_WAVES", "0") == "1":
         # batch-size churn: a wave whose requests end at different lengths (the decode batch shrinks through
         # the graph buckets 8 -> 4 -> 2 -> 1), then a second wave joining (back up to 8): rows idle for many

@@ -75,6 +75,25 @@ def test_tp2_greedy_prefill_after_graph_replays(gpu, models, name, ep):
     assert tp["waves_tokens"] == ref["waves_tokens"]
 
 
+def test_tp2_long_prompt_prefill_chunks(gpu, models):
+    """A 700-token prompt prefilled in one chunk: its row-parallel projections run comm.row_parallel_add -- the
+    GEMM in 256-row chunks, each chunk's all-reduce on the comm side stream through the IPC one-shot kernel
+    (d = 8192: 2M floats, inside the buffer) while the next chunk's GEMM computes. Greedy tokens equal TP=1."""
+    from nats_llm_studio_amd.parallel import rehearsal
+    import os
+    os.environ.update(NLS_REHEARSAL_LONG="700", NLS_REHEARSAL_PREFILL="1024")
+    try:
+        r = rehearsal.run(models["llama-3-70b-2layer"], world=2, new_tokens=4, timeout=300, greedy_only=True)
+    finally:
+        os.environ.pop("NLS_REHEARSAL_LONG", None)
+        os.environ.pop("NLS_REHEARSAL_PREFILL", None)
+    ref, tp, fol = r["ref"], r["tp"], r["followers"][0]
+    for v in (ref, tp, fol):
+        assert "exception" not in v, v
+    assert tp["long_tokens"] == ref["long_tokens"], (tp["long_tokens"], ref["long_tokens"])
+    assert tp["comm"].get("oneshot_all_reduce", 0) >= 12, tp["comm"]   # 2 layers x 2 projections x 3 chunks
+
+
 def test_sample_decode_cand_matches_cpu_twin(gpu):
     """The in-graph candidate sampler (sample.hip) against its CPU twin (ops.sample_decode_cand)."""
     import numpy as np
