@@ -42,7 +42,6 @@ struct NlsFuse {
   const int* sel; int sel_slots, sel_base, pad1;                             // device-selected segments
   const void* wr; int E, topk, renorm, rcap;                                 // MoE route after the norm (onw)
   float* rlogits; float* topw; int* counts; int* xrows; int* yrows; int* rsel;
-  const int* dep; int dep_n, pad2; int* dep_pass; int* done;               // overlapped decode chain (path A)
 };
 
 // mode 0: path A (waves split K, LDS reduce; mapped rows / MoE capable)
@@ -100,12 +99,6 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (fz->wr && (!fz->onw || M > 4 || fz->E < 1 || fz->E > 64 || fz->topk < 1 || fz->topk > fz->E || fz->topk > 8 ||
                  !fz->rlogits || !fz->topw || !fz->counts || !fz->xrows || !fz->yrows || segs[0].rows % 4))
     return -1;
-  // overlapped decode chain: path A, or path B's staged batch-1 launch; plain rows (no selected / mapped segments)
-  if ((fz->dep || fz->done) && (!(mode == 0 || (mode == 1 && ks <= 1)) || fz->sel ||
-                                (fz->dep && (!fz->dep_pass || fz->dep_n < 1))))
-    return -1;
-  for (int i = 0; i < nseg && (fz->dep || fz->done); ++i)
-    if (segs[i].xmap || segs[i].ymap || segs[i].mcount) return -1;
   if (fz->sel) {           // path A over routed experts only: identical segment shapes
     if (mode != 0 || fz->sel_slots < 1 || fz->sel_slots > 256 || argmax) return -1;
     for (int i = 1; i < nseg; ++i)
@@ -254,10 +247,6 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   a.rsel = fz->rsel;
   a.ssq_out = fz->ssq_out;
   a.ssq_in = fz->ssq_in;
-  a.dep = fz->dep;
-  a.dep_n = fz->dep_n;
-  a.dep_pass = fz->dep_pass;
-  a.done = fz->done;
   a.ldss = fz->ldss;
   a.nss_in = fz->nss_in;
   const int mt = M > 64 ? 8 : (M + 15) / 16;

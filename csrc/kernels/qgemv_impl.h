@@ -70,25 +70,7 @@ struct GemvArgs {
   // norm + router + route launch folded away. counts [E] are zeroed here first.
   const act_t* wr; int E, topk, renorm, rcap;
   float* rlogits; float* topw; int* counts; int* xrows; int* yrows; int* rsel;
-  // overlapped decode chain (path A, batch 1): this launch runs concurrently with its predecessor (a parallel
-  // branch of the decode graph). Each workgroup issues its weight prologue, then waits until the predecessor's
-  // dep_n workgroups have all bumped *dep (they wrote their outputs first), then stages its activations; the last
-  // of this launch's workgroups (ticket dep_pass) re-arms *dep. `done`: this launch's own counter, bumped by every
-  // workgroup after its outputs (agent-scope release), for the next link of the chain.
-  const int* dep; int dep_n; int* dep_pass; int* done;
 };
-
-// overlapped chain: wait for the predecessor (bounded: a missing producer costs a wrong step, never a hang;
-// the chain is only built where every producer workgroup is dispatched independently of this launch)
-DEVI void dep_wait(const GemvArgs& a) {
-  if (threadIdx.x == 0) {
-    long spins = 0;
-    while (__hip_atomic_load(a.dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.dep_n && ++spins < (1L << 22))
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
 
 // inv[m] = 1 / rms of rows m < M from producer partial sums of squares (see GemvArgs::ssq_in); one
 // wave per row, lanes sum the shares in a fixed order; ends with a workgroup barrier
@@ -365,8 +347,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   const int sbl = max(sb1 - 1, sb0);
   XPre xp;
   bool xfast = false;
-  if constexpr (XL)
-    if (!a.dep) xfast = xpre<WAVES * 64>(xp, a, mcount, S.K, 0, S.K);
+  if constexpr (XL) xfast = xpre<WAVES * 64>(xp, a, mcount, S.K, 0, S.K);
   if (sb0 < sb1) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) wA[rt] = load_raw<T, true>(W, rowc[rt], sb0, g);
@@ -381,11 +362,7 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
   }
   // (the prologue weight loads above are issued BEFORE the activation rows are staged: at batch 1 the
   // x round trip -- and the fused RMSNorm's reduction -- then overlaps the first weight fetch instead of
-  // preceding it on the critical path; in an overlapped chain the weights stream while the predecessor runs)
-  if (a.dep) {
-    dep_wait(a);
-    if constexpr (XL) xfast = xpre<WAVES * 64>(xp, a, mcount, S.K, 0, S.K);
-  }
+  // preceding it on the critical path)
   // Activation rows (A operand row = batch row r of tile mt). Padded / unmapped rows load a
   // valid row (row 0: broadcast, cache-resident) and are zeroed with a select after the load:
   // a lane-conditional load would compile to a branch + vmcnt(0) per K-step that drains the
@@ -632,32 +609,9 @@ DEVI void gemv_tile(const Seg& S, int row0, const GemvArgs& a, float* lds) {
 // KSET 0: Q4_K/Q6_K (the Q4_K_M mix); KSET 1: Q5_K/Q6_K/Q8_0; KSET 2: plain F16/BF16/F32. Splitting the format
 // switch keeps the register budget of the quantised kernels small (a switch case's
 // VGPR demand is paid by every case).
-template <int WAVES, int RT, int MT, int KSET, bool XL>
-DEVI void qgemv_body(const SegList& segs, const GemvArgs& a, float* lds);
-
-// overlapped chain, end of a workgroup: publish (every wave's stores drained, barrier, agent-scope release,
-// bump `done`) and, in the last workgroup of a consumer launch, re-arm the predecessor's counter
-DEVI void dep_finish(const GemvArgs& a, float* lds) {
-  if (!a.done && !a.dep) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (a.done && threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (a.dep && last_arriver(a.dep_pass, gridDim.x, reinterpret_cast<int*>(lds)) && threadIdx.x == 0)
-    __hip_atomic_store(const_cast<int*>(a.dep), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int WAVES, int RT, int MT, int KSET, bool XL = false>
 __global__ __launch_bounds__(WAVES * 64) void qgemv_kernel(SegList segs, GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  qgemv_body<WAVES, RT, MT, KSET, XL>(segs, a, lds);
-  dep_finish(a, lds);
-}
-
-template <int WAVES, int RT, int MT, int KSET, bool XL>
-DEVI void qgemv_body(const SegList& segs, const GemvArgs& a, float* lds) {
   int tile = blockIdx.x;
   Seg S = segs.s[0];
   if (a.sel) {
@@ -768,16 +722,12 @@ DEVI void mm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a,
     Raw wb[DEPTH][RT];
     const int sbl = max(sb1 - 1, sb0);
     XPre xp;              // batch 1: the x slice's loads go out first (xpre), the weight prologue after them
-    bool xfast = !a.dep && xpre<NT>(xp, a, M, S.K, sb0 * 256, (sb1 - sb0) * 256);
+    const bool xfast = xpre<NT>(xp, a, M, S.K, sb0 * 256, (sb1 - sb0) * 256);
     if (sb0 < sb1) {      // weight prologue: the x staging below overlaps its latency
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) wb[d][rt] = load_raw<T, true>(W, rowc[rt], min(sb0 + d, sbl), g);
-    }
-    if (a.dep) {          // overlapped chain: the weights stream while the producer finishes
-      dep_wait(a);
-      xfast = xpre<NT>(xp, a, M, S.K, sb0 * 256, (sb1 - sb0) * 256);
     }
     // x slice -> LDS [sb - sb0][M][256] (XOR-swizzled 16-B chunks)
     const int kc = (sb1 - sb0) * 32;
@@ -1056,19 +1006,10 @@ DEVI void mm_tile_na(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
   }
 }
 
-template <int WAVES, int RT, int MT, int KSET, bool XL>
-DEVI void qmm_body(const SegList& segs, GemvArgs a, int ks, float* ws, int ntiles, int nmb, act_t* xlds);
-
 template <int WAVES, int RT, int MT, int KSET, bool XL = false>
 __global__ __launch_bounds__(WAVES * 64) void qmm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                          int nmb) {
   extern __shared__ __attribute__((aligned(16))) act_t xlds[];
-  qmm_body<WAVES, RT, MT, KSET, XL>(segs, a, ks, ws, ntiles, nmb, xlds);
-  if constexpr (XL) dep_finish(a, reinterpret_cast<float*>(xlds));
-}
-
-template <int WAVES, int RT, int MT, int KSET, bool XL>
-DEVI void qmm_body(const SegList& segs, GemvArgs a, int ks, float* ws, int ntiles, int nmb, act_t* xlds) {
   int tile, kslice = 0, mb = 0;
   if (nmb > 1) {
     // Large M (prefill / big decode batches): blocks of MT*16 activation rows. The workgroups
@@ -1238,7 +1179,7 @@ int launch_b(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a
       return (int)hipGetLastError();
     }
   }
-  if (a.xf || a.dep || a.done) return -1;   // fused input norm / overlapped chain: the staged (XL) path only
+  if (a.xf) return -1;          // fused input norm: the staged (XL) path only
   if constexpr (WAVES == 7) {   // (the 7-wave instance exists for the staged batch-1 path only)
     return -1;
   } else {

@@ -305,20 +305,10 @@ def norm_fusable(M: int, K: int) -> bool:
     return M <= 16 and M * K * 2 <= NORM_FUSE_LDS
 
 
-def gemv_grid(segs: Sequence[Seg], rt: int, mode: int = 0, waves: int = 4) -> int:
-    """Workgroups of a batch-1 GEMV launch: path A (mode 0) one per RT*16-row tile of every segment, path B
-    (mode 1, split-K 1) one per WAVES*RT*16 rows."""
-    rows = 16 * rt * (waves if mode == 1 else 1)
-    return sum(-(-s.w.rows // rows) for s in segs)
-
-
 def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
           argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1,
-          norm=None, sel=None, dep=None, done: Optional[torch.Tensor] = None):
+          norm=None, sel=None):
     """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K].
-    dep = (counter, producer_workgroups, pass_counter) / done = counter (int32 device words, zeroed once): an
-    overlapped decode chain on path A (mode 0) -- this launch may run concurrently with its producer and waits on
-    the device for it after issuing its weight prologue (GemvArgs::dep); `done` is this launch's own counter.
     norm = (xf f32 [M, K], w f32 [K], eps[, ssq, ldss, nparts]): the GEMV input is f16(rmsnorm(xf) * w),
     computed inside the kernel (batch <= a few rows; `x` is then ignored on the GPU). With the partial
     sums of squares a qgemv_add_ssq producer left in `ssq`, the kernel skips the reduction pass and the
@@ -390,16 +380,6 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
                 mm = min(64, M - m0)
                 qgemv(segs, x[m0:], y[m0:], mm, alpha, epi, None if argmax is None else argmax[m0:], waves, rt,
                       mode, ks)
-            return y
-        if dep is not None or done is not None:
-            fz = _lib.NlsFuse()
-            if dep is not None:
-                fz.dep, fz.dep_n, fz.dep_pass = dep[0].data_ptr(), int(dep[1]), dep[2].data_ptr()
-            if done is not None:
-                fz.done = done.data_ptr()
-            _lib.check(L.nls_qgemv_ex(_segs(segs), len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M,
-                                      float(alpha), EPI[epi], _p(argmax), waves, rt, mode, ks, None, _stream_ptr(x),
-                                      ctypes.byref(fz)), "nls_qgemv_ex(dep)")
             return y
         arr = _seg_arr(segs, mode)
         ws = None

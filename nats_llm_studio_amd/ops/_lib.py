@@ -36,8 +36,7 @@ class NlsFuse(ctypes.Structure):
                 ("sel", c_void_p), ("sel_slots", c_int), ("sel_base", c_int), ("pad1", c_int),
                 ("wr", c_void_p), ("E", c_int), ("topk", c_int), ("renorm", c_int), ("rcap", c_int),
                 ("rlogits", c_void_p), ("topw", c_void_p), ("counts", c_void_p), ("xrows", c_void_p),
-                ("yrows", c_void_p), ("rsel", c_void_p),
-                ("dep", c_void_p), ("dep_n", c_int), ("pad2", c_int), ("dep_pass", c_void_p), ("done", c_void_p)]
+                ("yrows", c_void_p), ("rsel", c_void_p)]
 
 
 _SIGS = {

@@ -124,7 +124,7 @@ class EngineBackend:
         self._lock = threading.RLock()
         self._build_lock = threading.Lock()   # one model build at a time (device memory is sized at build)
         self._loaded: "collections.OrderedDict[str, dict]" = collections.OrderedDict()
-        self._loading: Dict[str, "Future"] = {}
+        self._loading: Dict[str, list] = {}    # model id -> [build Future, chats waiting on it]
         self._ids: tuple = ()          # lock-free snapshot of the loaded model ids
         self._device = None
         self.pinned = False          # tensor-parallel worker: serves only its preloaded model
@@ -201,13 +201,17 @@ class EngineBackend:
                     return st
                 if self.pinned:
                     raise RuntimeError(f"this tensor-parallel worker serves only {list(self._loaded)}")
-                fut = self._loading.get(entry.id)
-                owner = fut is None
+                slot = self._loading.get(entry.id)
+                owner = slot is None
                 if owner:
-                    fut = self._loading[entry.id] = Future()
+                    slot = self._loading[entry.id] = [Future(), 0]
+                else:
+                    slot[1] += 1        # the owner pins the state for this waiter when the build lands
+                fut = slot[0]
             if not owner:
-                fut.result()            # another chat is loading this model; then pin it (loop)
-                continue
+                # another chat is loading this model: the state arrives already pinned for this chat, so a
+                # build of another model that evicts right after this one cannot take it away in between
+                return fut.result()
             try:
                 with self._build_lock:
                     with self._lock:    # evict under the build mutex: the slot this build takes is free
@@ -223,7 +227,7 @@ class EngineBackend:
             with self._lock:
                 idle = self._evict_locked(max(1, self.cfg.max_loaded_models) - 1)
                 self._loaded[entry.id] = st
-                st["inflight"] += 1
+                st["inflight"] += 1 + slot[1]       # this chat and every chat waiting on the build
                 self._publish()
                 self._loading.pop(entry.id, None)
             for old in idle:
