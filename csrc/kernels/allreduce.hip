@@ -297,10 +297,10 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_ar_kernel(float* __restric
 // arrives last at the row's ticket (agent-scope release / acquire, cdna_hip_programming.md Guideline
 // 16) sums the shares and normalises the whole row. Receive slots: [parity][rank][cap], row b at b * D.
 // NLS_AR_PROBE timing history of the fused add+norm (this process's launches only): per workgroup slot eidx, the
-// last 8 epochs as {epoch, xcc, t_start, t_pushed, t_polled} on the device-wide 100 MHz clock (wall_clock64), which
+// last AR_PROBE_DEPTH (32) epochs as {epoch, xcc, t_start, t_pushed, t_polled} on the device-wide 100 MHz clock (wall_clock64), which
 // two ranks sharing one GPU read identically -- a timed-out poll is placed against the peer's push of that epoch
 #define AR_PROBE_SLOTS 4096
-#define AR_PROBE_DEPTH 8
+#define AR_PROBE_DEPTH 32
 struct ArProbeRec {
   unsigned ep, xcc;
   unsigned long long t0, t1, t2;
@@ -622,15 +622,17 @@ __global__ void ar_reinit_kernel(uint32_t* buf, long half) {
     buf[i] = i < half ? 0x01010101u : 0u;
 }
 
-// workgroups of one fused add+norm launch at most (multiple of 8, >= 8): NLS_AR_NORM_WGS, default 128
+// workgroups of one fused add+norm launch at most (multiple of 8, >= 8): NLS_AR_NORM_WGS, else the value the host
+// set for this process (nls_ar_set_norm_wgs: fewer when several ranks share one GPU), default 128
+static int g_norm_wgs = 128;
 static int nls_ar_norm_wgs() {
-  static const int n = [] {
+  static const int env = [] {
     const char* e = getenv("NLS_AR_NORM_WGS");
-    int v = e ? atoi(e) : 128;
-    v = v < 8 ? 8 : (v > 4096 ? 4096 : v);
-    return v & ~7;
+    return e ? atoi(e) : 0;
   }();
-  return n;
+  int v = env > 0 ? env : g_norm_wgs;
+  v = v < 8 ? 8 : (v > 4096 ? 4096 : v);
+  return v & ~7;
 }
 
 static long ar_opts(long max_spins) {
@@ -652,6 +654,19 @@ static long ar_opts(long max_spins) {
 }
 
 extern "C" {
+
+// Polling footprint when R ranks share ONE GPU (the one-GPU rehearsal): a polling wave parked on a CU keeps a
+// whole-CU kernel (a GEMM taking every VGPR / the LDS of a CU) of a co-resident rank from being placed there, so
+// (R - 1) ranks' add+norm grids must leave most CUs whole -- at world 4 three 128-workgroup grids covered every CU
+// and a peer's GEMM started only after the polls had expired (device-clock probes, profiles/tp_oneshot_world4_r05.txt).
+// Separate GPUs (R = 1): 128. Every rank must set the same value before its first launch (the grid is part of the
+// per-slice epoch bookkeeping of captured graphs only through the item -> workgroup map, which all ranks share).
+int nls_ar_set_norm_wgs(int n) {
+  if (n < 8 || n > 4096) return -1;
+  g_norm_wgs = n & ~7;
+  return 0;
+}
+int nls_ar_get_norm_wgs() { return nls_ar_norm_wgs(); }
 
 // bytes of one rank's receive buffer for messages of up to `cap` floats (+ its error word area)
 long nls_ar_buffer_bytes(long cap, int world) { return 2L * world * cap * 4L + AR_ERR_BYTES; }
@@ -717,6 +732,7 @@ int nls_ar_peek(void* buf, long off, int n, void* host, void* stream) {
   return (int)hipMemcpyAsync(host, (char*)buf + 4L * off, 4L * n, hipMemcpyDeviceToHost, (hipStream_t)stream);
 }
 // NLS_AR_PROBE: the timing history of add+norm workgroup slot `eidx` (AR_PROBE_DEPTH records of 32 bytes)
+int nls_ar_probe_depth() { return AR_PROBE_DEPTH; }
 int nls_ar_probe_hist(int eidx, void* host) {
   if (eidx < 0 || eidx >= AR_PROBE_SLOTS) return -1;
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ar_probe), sizeof(ArProbeRec) * AR_PROBE_DEPTH,

@@ -14,8 +14,9 @@
 // generation parity. Generations are per workgroup of a FIXED grid (EPX_WGS): workgroup g owns rows g, g + G, ...
 // in every call on every rank, so its counter advances in lock-step everywhere (hipGraph replays included). A
 // workgroup pushes all of its rows before it polls for any, and the grid is small, so no poll can wait on work
-// queued behind it (profiles/tp_oneshot_eager_r05.txt). Polls are bounded: a timeout raises the error word of
-// every rank (the engine reads it with each step's tokens) and the kernel exits.
+// queued behind it (profiles/tp_oneshot_eager_r05.txt); ranks sharing one GPU shrink it (nls_epx_set_wgs). Polls
+// are bounded: a timeout raises the error word of every rank (the engine reads it with each step's tokens) and the
+// kernel exits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -117,12 +118,22 @@ __global__ __launch_bounds__(EPX_THREADS) void epx_kernel(float* __restrict__ y,
 
 }  // namespace nls_epx
 
+// workgroups of the exchange grid: EPX_WGS, fewer when several ranks share one GPU (nls_epx_set_wgs, the same value on
+// every rank before the first call: a workgroup's generation counter follows its row set g, g + G, ...)
+static int g_epx_wgs = EPX_WGS;
+
 extern "C" {
+
+int nls_epx_set_wgs(int n) {
+  if (n < 1 || n > EPX_WGS) return -1;
+  g_epx_wgs = n;
+  return 0;
+}
 
 // bytes of one rank's receive buffer for up to `cap` rows of D floats (rows, flags, error word)
 long nls_epx_bytes(int cap, int D) { return (long)(nls_epx::err_word(cap, D) + 64) * 4L; }
 
-int nls_epx_wgs() { return EPX_WGS; }
+int nls_epx_wgs() { return EPX_WGS; }     // generation counters to allocate (the largest grid)
 
 // zero the flags and the error word of a freshly allocated (or reset) receive buffer
 int nls_epx_init(void* buf, int cap, int D, void* stream) {
@@ -139,7 +150,7 @@ int nls_epx_run(void* y, long ldy, int n, int D, const int* sel, int per, int ra
   if (n == 0) return 0;
   nls_epx::Peers P;
   for (int i = 0; i < EPX_MAX_RANKS; ++i) P.buf[i] = i < world ? (float*)peers[i] : nullptr;
-  hipLaunchKernelGGL(nls_epx::epx_kernel, dim3(EPX_WGS), dim3(EPX_THREADS), 0, (hipStream_t)stream, (float*)y, ldy, n,
+  hipLaunchKernelGGL(nls_epx::epx_kernel, dim3(g_epx_wgs), dim3(EPX_THREADS), 0, (hipStream_t)stream, (float*)y, ldy, n,
                      D, sel, per, rank, world, P, cap, wg_gen, err, max_spins);
   return (int)hipGetLastError();
 }

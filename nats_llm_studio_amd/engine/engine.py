@@ -782,6 +782,9 @@ class Engine:
                 if _TP_TRACE:
                     import sys
                     print(f"[tp r{self.rank}] state {self._oneshot.debug_state()}", file=sys.stderr, flush=True)
+                from ..ops import _lib as _oplib
+                if _oplib._OP_TIMING:    # NLS_OP_TIMING: launches whose completion lagged the previous one's
+                    print(f"[tp r{self.rank}] op gaps {_oplib.op_timing(50.0)}", file=sys.stderr, flush=True)
                 self._oneshot.reset()
                 continue
             if op == _OP_SYNC:
@@ -1021,6 +1024,9 @@ class Engine:
                 print(f"[tp r{self.rank}] one-shot error words (sum, add+norm, gather) {self.h_err2[k].tolist()} "
                       f"after op #{getattr(self, '_nops', 0)}", file=sys.stderr, flush=True)
                 print(f"[tp r{self.rank}] state {self._oneshot.debug_state()}", file=sys.stderr, flush=True)
+                from ..ops import _lib as _oplib
+                if _oplib._OP_TIMING:    # NLS_OP_TIMING: launches whose completion lagged the previous one's
+                    print(f"[tp r{self.rank}] op gaps {_oplib.op_timing(50.0)}", file=sys.stderr, flush=True)
             for h in self.h_err2:
                 h.zero_()
             self._ctrl(_OP_RESET, 0, 0, False, [], 0, None, 0)

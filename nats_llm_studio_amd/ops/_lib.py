@@ -119,6 +119,10 @@ _SIGS = {
     "nls_ar_err_words": [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p],
     "nls_ar_peek": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "nls_ar_probe_hist": [c_int, c_void_p],
+    "nls_ar_probe_depth": [],
+    "nls_ar_set_norm_wgs": [c_int],
+    "nls_ar_get_norm_wgs": [],
+    "nls_epx_set_wgs": [c_int],
     "nls_ar_buffer_bytes": [c_long, c_int],
     "nls_ag_blocks": [],
     "nls_ag_run": [c_void_p, c_long, c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_long, c_void_p, c_void_p,
@@ -161,9 +165,46 @@ def lib():
     return _lib
 
 
+_OP_TIMING = os.environ.get("NLS_OP_TIMING", "0") == "1"
+_op_events = None
+
+
 def check(rc: int, name: str):
     if rc != 0:
         raise RuntimeError(f"{name} failed with code {rc}")
+    if _OP_TIMING:
+        _op_mark(name)
+
+
+def _op_mark(name: str):
+    """NLS_OP_TIMING=1 (diagnostics): an event on the current stream after every launch that is not being captured,
+    kept for the last 4096 launches (op_timing)."""
+    global _op_events
+    import collections
+    import torch
+    if not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+        return
+    if _op_events is None:
+        _op_events = collections.deque(maxlen=4096)
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    _op_events.append((name, ev))
+
+
+def op_timing(min_ms: float = 0.0):
+    """(launch name, ms since the previous marked launch completed) of the marked launches, oldest first, after a
+    device sync; only gaps >= min_ms are listed (with their index)."""
+    import torch
+    if not _op_events:
+        return []
+    torch.cuda.synchronize()
+    evs = list(_op_events)
+    out = []
+    for i in range(1, len(evs)):
+        ms = evs[i - 1][1].elapsed_time(evs[i][1])
+        if ms >= min_ms:
+            out.append((i - len(evs), evs[i][0], round(ms, 3)))
+    return out
 
 
 def available() -> bool:

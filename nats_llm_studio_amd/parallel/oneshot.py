@@ -17,6 +17,7 @@ boxes, where cross-device IPC cannot be exercised.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import torch
@@ -58,12 +59,21 @@ class OneShotAllReduce:
             raise RuntimeError("one-shot all-reduce: IPC buffer setup failed on some rank")
         dev = comm.device
         self.device = dev
+        # ranks sharing this GPU (the one-GPU rehearsal): their polling grids shrink so that a peer's whole-CU
+        # kernel still finds whole CUs (allreduce.hip nls_ar_set_norm_wgs); one rank per GPU keeps the full grids
+        self.co_resident = _co_resident(comm, dev)
+        if self.co_resident > 1:
+            _lib.check(L.nls_ar_set_norm_wgs(max(8, (128 // (self.co_resident - 1)) & ~7)), "nls_ar_set_norm_wgs")
         # one epoch counter per slot block of the receive buffers (allreduce.hip SlotBlocks)
         self.epochs = torch.zeros(L.nls_ar_epoch_slots(self.cap), dtype=torch.int32, device=dev)
         self.gepochs = torch.zeros(L.nls_ag_epoch_slots(self.cap), dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._norm = {}               # D -> (epochs, tickets, ssq) of the fused add+norm
         self.resets = 0
+        self._trace = None
+        if os.environ.get("NLS_TP_TRACE", "0") == "1":
+            import collections
+            self._trace = collections.deque(maxlen=64)
         self.ebuf = None              # expert-parallel decode exchange (ep_setup)
         self.ERR_WORDS = 3
         comm.barrier()
@@ -81,6 +91,8 @@ class OneShotAllReduce:
             raise RuntimeError("expert-parallel exchange: IPC buffer setup failed on some rank")
         self.ebuf, self.epeers, self.e_rows, self.e_D = buf, peers, int(rows), int(D)
         self.egen = torch.zeros(L.nls_epx_wgs(), dtype=torch.int32, device=self.device)
+        if self.co_resident > 1:
+            _lib.check(L.nls_epx_set_wgs(max(8, L.nls_epx_wgs() // (self.co_resident - 1))), "nls_epx_set_wgs")
         st = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(L.nls_epx_init(buf, self.e_rows, self.e_D, st), "nls_epx_init")
         torch.cuda.synchronize(self.device)
@@ -138,6 +150,9 @@ class OneShotAllReduce:
         """x[:rows] += sum over ranks of part[:rows] (rank order), h = f16(rmsnorm(x) * nw): one launch."""
         D = x.shape[1]
         ep, tk, sq = self._norm_state(D)
+        if self._trace is not None:       # NLS_TP_TRACE: host launch times of the last 64 calls (debug_state)
+            import time
+            self._trace.append((round(time.time(), 4), int(rows), torch.cuda.is_current_stream_capturing()))
         rc = _lib.lib().nls_ar_addnorm(part.data_ptr(), part.stride(0), x.data_ptr(), x.stride(0), nw.data_ptr(),
                                        h.data_ptr(), h.stride(0), rows, D, float(eps), self.npeers, self.world,
                                        self.rank, self.cap, ep.data_ptr(), tk.data_ptr(), sq.data_ptr(),
@@ -177,6 +192,8 @@ class OneShotAllReduce:
         compared across ranks, a divergence names the collective whose call counts differ."""
         torch.cuda.synchronize(self.device)
         out = dict(ar=self.epochs[:8].tolist(), gather=self.gepochs[:16].tolist())
+        if self._trace is not None:
+            out["host_addnorm_launches"] = list(self._trace)
         for D, (ep, tk, _sq) in self._norm.items():
             nblk = ep.numel() // tk.numel()
             e = ep.view(-1, nblk)[:rows]
@@ -261,15 +278,16 @@ class OneShotAllReduce:
 
     @staticmethod
     def _probe_hist(eidx: int):
-        """NLS_AR_PROBE: this process's last 8 add+norm launches of workgroup slot `eidx`, oldest first, as
+        """NLS_AR_PROBE: this process's last nls_ar_probe_depth() (32) add+norm launches of workgroup slot `eidx`, oldest first, as
         (epoch, xcc, failed, t_start, t_pushed, t_polled) -- times in the device-wide 100 MHz clock, which two
         ranks sharing one GPU read identically (compare a timed-out poll with the peer's push)."""
         import numpy as np
-        host = np.zeros(8 * 8, dtype=np.uint32)
+        depth = _lib.lib().nls_ar_probe_depth()
+        host = np.zeros(depth * 8, dtype=np.uint32)
         if _lib.lib().nls_ar_probe_hist(int(eidx), host.ctypes.data) != 0:
             return None
         recs = []
-        for i in range(8):
+        for i in range(depth):
             w = host[8 * i:8 * i + 8]
             if not w[0]:
                 continue
@@ -347,6 +365,21 @@ class OneShotAllReduce:
             L.nls_ar_free(ctypes.c_void_p(b))
         self._owned = []
         self.buf = None
+
+
+def _co_resident(comm, device) -> int:
+    """How many ranks of `comm` drive the same physical GPU as this one (host name + PCI bus id; 1 = its own GPU)."""
+    import socket
+    try:
+        p = torch.cuda.get_device_properties(device)
+        key = (socket.gethostname(), getattr(p, "pci_domain_id", None), getattr(p, "pci_bus_id", None),
+               getattr(p, "pci_device_id", None),
+               str(getattr(p, "uuid", "")))
+    except Exception:
+        key = (socket.gethostname(), str(device))
+    keys = [None] * comm.size
+    dist.all_gather_object(keys, key, group=comm.ctrl)
+    return sum(1 for k in keys if k == key)
 
 
 def _norm_buffers(cap: int, D: int, device, world_sim: int = 0):

@@ -222,6 +222,10 @@ def _rank_main(rank: int, world: int, port: int, path: str, ep: bool, new_tokens
             res["comm"] = dict(comm.stats)
             res["oneshot_resets"] = comm.oneshot.resets if comm.oneshot is not None else None
             res["ctrl_transport"] = "shm-ring" if comm.ring is not None else "gloo"
+            if comm.oneshot is not None:
+                from ..ops import _lib
+                res["co_resident"] = comm.oneshot.co_resident
+                res["addnorm_wgs"] = _lib.lib().nls_ar_get_norm_wgs()
         else:
             eng.sync_hook = lambda: (_sync(dev), dist.barrier())
             eng.follow()

@@ -94,6 +94,36 @@ def test_tp2_long_prompt_prefill_chunks(gpu, models):
     assert tp["comm"].get("oneshot_all_reduce", 0) >= 12, tp["comm"]   # 2 layers x 2 projections x 3 chunks
 
 
+@pytest.mark.parametrize("name,ep", [("llama-3-70b-2layer", False), ("mixtral-8x7b-1layer", True)])
+def test_tp4_one_gpu_matches_tp1(gpu, models, name, ep):
+    """Four ranks on the one GPU: every one-shot kernel (fused add+norm, arg-max, candidate gather, the EP row
+    exchange with two experts per rank) with three peers instead of one, eager prefill and captured decode
+    graphs; greedy + seeded top-k tokens equal TP=1. With the 128-workgroup add+norm grid of one rank per GPU, three
+    ranks' polling waves covered every CU and the fourth rank's GEMM started only after their polls expired (about
+    every other run timed out, profiles/tp_oneshot_world4_r05.txt): co-resident ranks shrink the grid to 40."""
+    from nats_llm_studio_amd.parallel import rehearsal
+    r = rehearsal.run(models[name], world=4, ep=ep, new_tokens=8, timeout=400)
+    ref, tp = r["ref"], r["tp"]
+    for v in [ref, tp] + r["followers"]:
+        assert v is not None and "exception" not in v, v
+    assert tp["oneshot_resets"] == 0
+    assert tp["co_resident"] == 4 and tp["addnorm_wgs"] == 40, tp     # 3 peers' polling grids leave whole CUs
+    c = tp["counters"]
+    assert c["graph_replays"] > 0 and c["device_sampled_steps"] > 0 and c["candidate_sampled_steps"] == 0, c
+    assert tp["comm"]["all_reduce"] > 0, tp["comm"]
+    if ep:
+        assert tp["comm"].get("ep_exchange", 0) > 0, tp["comm"]
+    n = len(rehearsal.PROMPTS)
+    assert tp["tokens"][:n] == ref["tokens"][:n], (tp["tokens"], ref["tokens"])      # greedy: exact
+    # seeded sampled rows: TP changes the order of the row-parallel sums (4 rank-ordered partials instead of one
+    # GEMM), so logits differ from TP=1 in the last bits; a kept-set boundary (top-p 0.95 / min-p over the top 40 of a
+    # random-init model's nearly flat distribution) can then move and the draw lands elsewhere. Measured: Llama-70B
+    # 2-layer request 9 draws 15304 instead of 15453 at TP=4 on every run, with the candidate gather AND with the
+    # full-logit gather (NLS_TP_CANDIDATES=0), so not the candidate path. At most one sampled request may differ.
+    diff = [i for i in range(n, len(ref["tokens"])) if tp["tokens"][i] != ref["tokens"][i]]
+    assert len(diff) <= 1, (diff, tp["tokens"], ref["tokens"])
+
+
 def test_sample_decode_cand_matches_cpu_twin(gpu):
     """The in-graph candidate sampler (sample.hip) against its CPU twin (ops.sample_decode_cand)."""
     import numpy as np
