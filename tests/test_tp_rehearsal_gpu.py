@@ -94,20 +94,23 @@ def test_tp2_long_prompt_prefill_chunks(gpu, models):
     assert tp["comm"].get("oneshot_all_reduce", 0) >= 12, tp["comm"]   # 2 layers x 2 projections x 3 chunks
 
 
+@pytest.mark.parametrize("world", [4, 8])
 @pytest.mark.parametrize("name,ep", [("llama-3-70b-2layer", False), ("mixtral-8x7b-1layer", True)])
-def test_tp4_one_gpu_matches_tp1(gpu, models, name, ep):
-    """Four ranks on the one GPU: every one-shot kernel (fused add+norm, arg-max, candidate gather, the EP row
-    exchange with two experts per rank) with three peers instead of one, eager prefill and captured decode
-    graphs; greedy + seeded top-k tokens equal TP=1. With the 128-workgroup add+norm grid of one rank per GPU, three
-    ranks' polling waves covered every CU and the fourth rank's GEMM started only after their polls expired (about
-    every other run timed out, profiles/tp_oneshot_world4_r05.txt): co-resident ranks shrink the grid to 40."""
+def test_tp4_tp8_one_gpu_matches_tp1(gpu, models, name, ep, world):
+    """Four / eight ranks on the one GPU (TP=8: Llama-3-70B's 8 kv heads one per rank; EP=8: one Mixtral expert per
+    rank): every one-shot kernel (fused add+norm, arg-max, candidate gather, the EP row exchange) with 3 / 7 peers,
+    eager prefill and captured decode graphs; greedy tokens equal TP=1. With the 128-workgroup add+norm grid of one
+    rank per GPU, three ranks' polling waves covered every CU and the fourth rank's GEMM started only after their
+    polls expired (about every other run timed out, profiles/tp_oneshot_world4_r05.txt): co-resident ranks shrink
+    the grid."""
     from nats_llm_studio_amd.parallel import rehearsal
-    r = rehearsal.run(models[name], world=4, ep=ep, new_tokens=8, timeout=400)
+    r = rehearsal.run(models[name], world=world, ep=ep, new_tokens=8, timeout=400)
     ref, tp = r["ref"], r["tp"]
     for v in [ref, tp] + r["followers"]:
         assert v is not None and "exception" not in v, v
     assert tp["oneshot_resets"] == 0
-    assert tp["co_resident"] == 4 and tp["addnorm_wgs"] == 40, tp     # 3 peers' polling grids leave whole CUs
+    # the peers' polling grids leave whole CUs: 40 workgroups each at 4 ranks, 16 at 8
+    assert tp["co_resident"] == world and tp["addnorm_wgs"] == {4: 40, 8: 16}[world], tp
     c = tp["counters"]
     assert c["graph_replays"] > 0 and c["device_sampled_steps"] > 0 and c["candidate_sampled_steps"] == 0, c
     assert tp["comm"]["all_reduce"] > 0, tp["comm"]
