@@ -56,12 +56,15 @@ _MOE_GEMV_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_GEMV_DN", "").split
 # MoE expert GEMMs on the experts' f16 copies: (mode, waves, rt[, ks]) of gate/up and down
 _MOE_DENSE_GU = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_GU", "5,8,2").split(","))
 _MOE_DENSE_DN = tuple(int(v) for v in os.environ.get("NLS_MOE_DENSE_DN", "5,8,2,4").split(","))
-# expert parallelism: eager steps of >= NLS_EP_A2A_T tokens dispatch / combine over all-to-all (LlamaModel._moe_a2a);
-# NLS_EP_A2A=0 keeps the combine-then-all-reduce everywhere
+# expert parallelism: eager steps of >= NLS_EP_A2A_T tokens that the IPC row exchange does not cover dispatch /
+# combine over all-to-all (LlamaModel._moe_a2a); NLS_EP_A2A=0 keeps the combine-then-all-reduce everywhere
 _EP_A2A = os.environ.get("NLS_EP_A2A", "1")
 _EP_A2A_T = int(os.environ.get("NLS_EP_A2A_T", "64"))
-# tokens per step the EP decode exchange covers (receive buffers: 2 x tokens x top-k x d_model floats per rank)
-_EPX_TOKENS = int(os.environ.get("NLS_EPX_TOKENS", "512"))
+# tokens per step the EP row exchange covers (receive buffers: 2 x tokens x top-k x d_model floats per rank; 2048 =
+# the engine's default prefill chunk: 134 MB per rank for Mixtral), decode AND prefill: no host-side split sizes, no
+# RCCL call. NLS_EP_PREFILL=a2a sends eager steps of >= NLS_EP_A2A_T tokens to the all-to-all instead.
+_EPX_TOKENS = int(os.environ.get("NLS_EPX_TOKENS", "2048"))
+_EP_PREFILL = os.environ.get("NLS_EP_PREFILL", "exchange")
 # MoE router logits through ops.router_logits (E-row kernel) rather than the GEMV/GEMM tiles; 0 = the GEMV
 _ROUTER_KERNEL = os.environ.get("NLS_ROUTER_KERNEL", "1") == "1"
 
@@ -581,10 +584,14 @@ class LlamaModel:
 
     def _ep_a2a(self, T: int) -> bool:
         """Take the all-to-all dispatch / combine (_moe_a2a) for this MoE step? Eager EP steps of
-        >= NLS_EP_A2A_T tokens (prefill chunks, large eager batches); captured decode graphs keep the
-        host-sync-free combine-then-all-reduce (the all-to-all needs its split sizes on the host)."""
+        >= NLS_EP_A2A_T tokens (prefill chunks, large eager batches) that the IPC row exchange does not cover
+        (no exchange: CPU / no IPC, or more than NLS_EPX_TOKENS tokens); captured decode graphs never (the
+        all-to-all needs its split sizes on the host)."""
         if not self.ep or _EP_A2A == "0" or T < _EP_A2A_T:
             return False
+        if (self.ep_exchange and _EP_PREFILL != "a2a"
+                and self.comm.oneshot.ep_ok(T * self.cfg.n_expert_used, self.cfg.d_model)):
+            return False                     # the row exchange covers this step (_moe, exch)
         if self.device.type == "cuda":
             # grouped-GEMM path only (the path-A GEMVs take <= 64 rows) and never inside a capture
             return T > _MOE_GEMM_T and not torch.cuda.is_current_stream_capturing()

@@ -127,6 +127,27 @@ def test_tp4_tp8_one_gpu_matches_tp1(gpu, models, name, ep, world):
     assert len(diff) <= 1, (diff, tp["tokens"], ref["tokens"])
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_ep_long_prompt_prefill_row_exchange(gpu, models, world):
+    """Mixtral EP: a 300-token prompt prefilled in 256-token chunks -- eager MoE steps of 256 tokens (512 routed rows)
+    -- runs through the IPC row exchange like decode (no host-side split sizes, no all-to-all, no RCCL call);
+    greedy tokens equal TP=1."""
+    from nats_llm_studio_amd.parallel import rehearsal
+    import os
+    os.environ["NLS_REHEARSAL_LONG"] = "300"
+    try:
+        r = rehearsal.run(models["mixtral-8x7b-1layer"], world=world, ep=True, new_tokens=4, timeout=300,
+                          greedy_only=True)
+    finally:
+        os.environ.pop("NLS_REHEARSAL_LONG", None)
+    ref, tp = r["ref"], r["tp"]
+    for v in [ref, tp] + r["followers"]:
+        assert v is not None and "exception" not in v, v
+    assert tp["comm"].get("all_to_all", 0) == 0 and tp["comm"].get("ep_exchange", 0) > 0, tp["comm"]
+    assert tp["long_tokens"] == ref["long_tokens"], (tp["long_tokens"], ref["long_tokens"])
+    assert tp["tokens"] == ref["tokens"]
+
+
 def test_sample_decode_cand_matches_cpu_twin(gpu):
     """The in-graph candidate sampler (sample.hip) against its CPU twin (ops.sample_decode_cand)."""
     import numpy as np
@@ -172,11 +193,12 @@ def test_ep2_alltoall_prefill_matches_tp1(gpu, models):
     decode graphs keep the combine-then-all-reduce. Tokens must equal TP=1."""
     from nats_llm_studio_amd.parallel import rehearsal
     import os
-    os.environ["NLS_EP_A2A_T"] = "17"            # (spawned ranks inherit)
+    os.environ.update(NLS_EP_A2A_T="17", NLS_EP_PREFILL="a2a")     # (spawned ranks inherit)
     try:
         r = rehearsal.run(models["mixtral-8x7b-1layer"], world=2, ep=True, new_tokens=8, timeout=300)
     finally:
         os.environ.pop("NLS_EP_A2A_T", None)
+        os.environ.pop("NLS_EP_PREFILL", None)
     ref, tp, fol = r["ref"], r["tp"], r["followers"][0]
     for v in (ref, tp, fol):
         assert "exception" not in v, v
