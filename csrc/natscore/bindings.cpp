@@ -160,6 +160,15 @@ PYBIND11_MODULE(_natscore, m) {
           py::arg("sid"), py::arg("timeout_ms") = -1)
       .def("pending", &Client::pending)
       .def(
+          "set_auto_reply",
+          [](Client& c, int64_t sid, py::object body) {
+            std::shared_ptr<const std::string> b;
+            if (!body.is_none()) b = std::make_shared<const std::string>(std::string(body.cast<py::bytes>()));
+            c.set_auto_reply(sid, std::move(b));
+          },
+          py::arg("sid"), py::arg("body"))
+      .def("auto_replied", &Client::auto_replied)
+      .def(
           "request",
           [](Client& c, const std::string& subj, py::bytes data, int timeout_ms, py::bytes hdr) {
             std::string d = data, h = hdr;

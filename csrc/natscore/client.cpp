@@ -300,6 +300,19 @@ Msg Client::next_msg(int64_t sid, int timeout_ms) {
   return m;
 }
 
+void Client::set_auto_reply(int64_t sid, std::shared_ptr<const std::string> body) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = subs_.find(sid);
+  if (it == subs_.end()) throw std::runtime_error("nats: unknown subscription");
+  it->second->auto_reply = std::move(body);
+}
+
+uint64_t Client::auto_replied(int64_t sid) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = subs_.find(sid);
+  return it == subs_.end() ? 0 : it->second->auto_replied;
+}
+
 int Client::pending(int64_t sid) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = subs_.find(sid);
@@ -386,24 +399,38 @@ void Client::on_op(Op& op) {
       m.hdr = std::move(op.hdr);
       m.sid = std::atoll(op.sid.c_str());
       if (!m.hdr.empty()) m.status = parse_headers(m.hdr).status;
-      std::lock_guard<std::mutex> g(mu_);
-      if (m.sid == resp_sid_ && resp_sid_ != 0) {
-        auto tok = m.subject.substr(resp_prefix_.size());
-        auto it = pending_.find(tok);
-        if (it != pending_.end()) {
-          it->second->msg = std::move(m);
-          it->second->done = true;
-          resp_cv_.notify_all();
+      std::shared_ptr<const std::string> auto_body;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (m.sid == resp_sid_ && resp_sid_ != 0) {
+          auto tok = m.subject.substr(resp_prefix_.size());
+          auto it = pending_.find(tok);
+          if (it != pending_.end()) {
+            it->second->msg = std::move(m);
+            it->second->done = true;
+            resp_cv_.notify_all();
+          }
+          break;
         }
-        break;
+        auto it = subs_.find(m.sid);
+        if (it == subs_.end() || it->second->closed) break;
+        auto& s = it->second;
+        if (s->auto_reply && !m.reply.empty()) {
+          auto_body = s->auto_reply;        // answered below, outside the subscription lock
+          s->auto_replied++;
+        } else {
+          s->delivered++;
+          s->q.push_back(std::move(m));
+          s->cv.notify_one();
+          if (s->max > 0 && s->delivered >= s->max) s->closed = true;   // queued messages stay drainable
+        }
       }
-      auto it = subs_.find(m.sid);
-      if (it == subs_.end() || it->second->closed) break;
-      auto& s = it->second;
-      s->delivered++;
-      s->q.push_back(std::move(m));
-      s->cv.notify_one();
-      if (s->max > 0 && s->delivered >= s->max) s->closed = true;   // queued messages stay drainable
+      if (auto_body) {
+        try {
+          publish(m.reply, *auto_body);
+        } catch (...) {       // a reply that cannot be written is the requester's timeout, as for any responder
+        }
+      }
       break;
     }
     case Op::INFO: {

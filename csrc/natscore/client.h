@@ -66,6 +66,12 @@ class Client {
   // Blocks up to timeout_ms (<0 = forever). Throws TimeoutError / ConnectionClosedError.
   Msg next_msg(int64_t sid, int timeout_ms);
   int pending(int64_t sid);
+  // Static responder: every message of `sid` that carries a reply subject is answered with `body` from the
+  // reader thread -- no next_msg consumer, no Python on the path (a cached read-only reply such as the
+  // list_models registry listing, kept current by its owner). A null body turns it off; messages without a
+  // reply subject still queue.
+  void set_auto_reply(int64_t sid, std::shared_ptr<const std::string> body);
+  uint64_t auto_replied(int64_t sid);
   Msg request(const std::string& subject, const std::string& data, int timeout_ms, const std::string& hdr = "");
   void flush(int timeout_ms);
   std::string new_inbox() { return "_INBOX." + nuid_next(); }
@@ -87,6 +93,8 @@ class Client {
     std::condition_variable cv;
     long max = 0, delivered = 0;
     bool closed = false;
+    std::shared_ptr<const std::string> auto_reply;   // set_auto_reply
+    uint64_t auto_replied = 0;
   };
   struct Pending {
     Msg msg;

@@ -68,6 +68,15 @@ class Subscription:
     def next_msg(self, timeout: float = 1.0):
         return self.client._c.next_msg(self.sid, int(timeout * 1000))
 
+    def set_auto_reply(self, body: Optional[bytes]):
+        """Answer this subscription's requests with `body` from the native reader thread (None: hand them to
+        the callback again). For cached read-only replies; the owner keeps `body` current."""
+        self.client._c.set_auto_reply(self.sid, body)
+
+    @property
+    def auto_replied(self) -> int:
+        return self.client._c.auto_replied(self.sid)
+
     def unsubscribe(self):
         self._stop = True
         try:

@@ -59,6 +59,10 @@ class WorkerConfig:
     timeout_delete: float = 120.0
     timeout_chat: float = 120.0
     handler_workers: int = 4
+    # list_models answered by the NATS client's reader thread from the cached registry reply (kept current on every
+    # reply the service sends and every list_refresh_ms): BASELINE config 1's RTT path without Python. 0 = handler
+    native_list_models: bool = True
+    list_refresh_ms: float = 50.0
     lmstudio_base_url: str = "http://127.0.0.1:1234"   # used by the `http` backend only
     # NATS authentication (nats.go options): token, user/password, nkey seed or a .creds file
     nats_token: str = ""
@@ -102,6 +106,8 @@ class WorkerConfig:
         c.max_ctx = int(e.get("MAX_CTX", c.max_ctx))
         c.kv_mem_fraction = float(e.get("KV_MEM_FRACTION", c.kv_mem_fraction))
         c.lmstudio_base_url = e.get("LMSTUDIO_BASE_URL", c.lmstudio_base_url)
+        c.native_list_models = e.get("NATIVE_LIST_MODELS", "1") not in ("0", "false", "no")
+        c.list_refresh_ms = float(e.get("LIST_REFRESH_MS", c.list_refresh_ms))
         c.subject_prefix = e.get("SUBJECT_PREFIX", c.subject_prefix)
         c.embedded_server = e.get("EMBEDDED_NATS", "0") in ("1", "true", "yes")
         c.store_dir = e.get("NATS_STORE_DIR", c.store_dir)

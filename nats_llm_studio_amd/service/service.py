@@ -63,6 +63,11 @@ class Service:
         self._lock = threading.Lock()
         self._unloader = None         # persistent thread of the delete handler's bounded unload
         self._list_cache = {}         # (registry generation, loaded ids) -> encoded list_models reply
+        self._list_sub = None         # the list_models subscription while its replies are native (auto-reply)
+        self._list_key = None         # cache key of the body the native responder holds
+        self._list_stop = threading.Event()
+        self._list_thread = None
+        self._list_lock = threading.Lock()   # orders body updates against native_list(False)
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "Service":
@@ -84,10 +89,74 @@ class Service:
         ]
         for name, fn, workers in routes:
             self.subs.append(self.client.subscribe(self.cfg.subject(name), q, self._wrap(name, fn), workers))
+            if name == "list_models" and self.cfg.native_list_models and not isinstance(self.backend, HttpBackend):
+                self._list_sub = self.subs[-1]
+        if self._list_sub is not None:
+            # the registry listing is a cached read: the client's reader thread answers it (no Python on the RTT
+            # path), the body refreshed before every reply this service sends (a pull / delete / chat reply is
+            # followed by a listing that shows it) and every list_refresh_ms (loads, unloads, rescans)
+            self._publish_list_reply()
+            self._list_stop.clear()
+            self._list_thread = threading.Thread(target=self._list_refresher, name="nls-list-reply", daemon=True)
+            self._list_thread.start()
         self.client.flush()
         return self
 
+    def native_list(self, enabled: bool):
+        """Switch list_models between the native responder and the Python handler at run time (the handler keeps
+        the reference's 30 s read deadline; the native reply is the last snapshot, refreshed every list_refresh_ms)."""
+        sub = next((x for x in self.subs if x.subject == self.cfg.subject("list_models")), None)
+        if sub is None or isinstance(self.backend, HttpBackend):
+            return
+        if enabled:
+            with self._list_lock:
+                self._list_sub, self._list_key = sub, None
+            self._publish_list_reply()
+        else:
+            with self._list_lock:
+                self._list_sub = None
+                sub.set_auto_reply(None)
+
+    def _list_body(self):
+        """(cache key, encoded list_models reply) of the current registry snapshot and loaded set."""
+        loaded = tuple(self.backend.loaded_ids())
+        self.registry.refresh()
+        key = (self.registry.generation, loaded)
+        body = self._list_cache.get(key)
+        if body is None:
+            # the encoded reply of an unchanged snapshot is reused (one per registry generation + loaded set)
+            body = envelope.ok({"http_status": 200, "models": self.registry.list_api(loaded)})
+            self._list_cache = {key: body}
+        return key, body
+
+    def _publish_list_reply(self):
+        if self._list_sub is None:
+            return
+        try:
+            key, body = self._list_body()
+        except Exception:
+            key, body = None, None      # a registry read that fails goes back to the handler (its error reply)
+        with self._list_lock:
+            sub = self._list_sub
+            if sub is None or (key is not None and key == self._list_key):
+                return
+            try:
+                sub.set_auto_reply(body)
+                self._list_key = key
+            except Exception:
+                self._list_key = None
+
+    def _list_refresher(self):
+        period = max(0.005, self.cfg.list_refresh_ms / 1e3)
+        while not self._list_stop.wait(period):
+            self._publish_list_reply()
+
     def stop(self):
+        self._list_stop.set()
+        if self._list_thread is not None:
+            self._list_thread.join(timeout=2)
+            self._list_thread = None
+        self._list_sub = None
         for s in self.subs:
             s.unsubscribe()
         self.subs.clear()
@@ -133,6 +202,8 @@ class Service:
         if not msg.reply:
             print(f"error responding to NATS message: nats: message does not have a reply", flush=True)
             return
+        if self._list_sub is not None:
+            self._publish_list_reply()       # a listing requested after this reply sees what this request changed
         try:
             self.client.publish(msg.reply, body)
         except Exception as e:
@@ -164,14 +235,7 @@ class Service:
         # and held to the 30 s context afterwards -- a thread per request cost ~0.1 ms of the ~0.08 ms RTT
         t0 = time.monotonic()
         try:
-            loaded = tuple(self.backend.loaded_ids())
-            self.registry.refresh()
-            key = (self.registry.generation, loaded)
-            body = self._list_cache.get(key)
-            if body is None:
-                # the encoded reply of an unchanged snapshot is reused (one per registry generation + loaded set)
-                body = envelope.ok({"http_status": 200, "models": self.registry.list_api(loaded)})
-                self._list_cache = {key: body}
+            _, body = self._list_body()
         except Exception as e:
             self.respond(msg, envelope.error(f"error reading model registry: {e}", {"http_status": 0}))
             return
@@ -337,7 +401,7 @@ class Service:
     def on_metrics(self, msg):
         data = {
             "uptime_s": round(time.time() - self.t_start, 3),
-            "requests": dict(self.counters),
+            "requests": self._request_counts(),
             "latency_ms": {k: v.summary_ms() for k, v in self.latency.items()},
             "trace": self.tracer.summary(),
             "backend": self.backend.stats(),
@@ -346,6 +410,15 @@ class Service:
             "queue_group": self.cfg.queue_group,
         }
         self.respond(msg, envelope.ok(data))
+
+    def _request_counts(self) -> dict:
+        out = dict(self.counters)
+        sub = next((x for x in self.subs if x.subject == self.cfg.subject("list_models")), None)
+        native = sub.auto_replied if sub is not None else 0
+        if native:              # answered by the native responder (no handler latency recorded for them)
+            out["list_models_native"] = native
+            out["list_models"] = out.get("list_models", 0) + native
+        return out
 
     def on_health(self, msg):
         self.respond(msg, envelope.ok({"status": "ok", "pid": os.getpid(), "backend": self.backend.name,

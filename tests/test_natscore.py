@@ -114,6 +114,31 @@ def test_request_reply_and_no_responders(server):
     srv.close(); cli.close()
 
 
+def test_auto_reply_static_responder(server):
+    """set_auto_reply: requests on the subscription are answered by the reader thread with the stored body (the
+    callback never runs); None hands them back to the callback; plain publishes still reach it."""
+    srv, cli = client(server), client(server)
+    seen = []
+    sub = srv.subscribe("svc.static", "g", cb=lambda m: (seen.append(m.data),
+                                                          m.reply and srv.publish(m.reply, b"cb")))
+    srv.flush()
+    sub.set_auto_reply(b"cached")
+    assert [cli.request("svc.static", b"q", 2).data for _ in range(3)] == [b"cached"] * 3
+    assert sub.auto_replied == 3 and seen == []
+    sub.set_auto_reply(b"v2")
+    assert cli.request("svc.static", b"q", 2).data == b"v2"
+    cli.publish("svc.static", b"no-reply")
+    cli.flush()
+    for _ in range(100):
+        if seen:
+            break
+        time.sleep(0.01)
+    assert seen == [b"no-reply"]
+    sub.set_auto_reply(None)
+    assert cli.request("svc.static", b"q", 2).data == b"cb" and sub.auto_replied == 4
+    srv.close(); cli.close()
+
+
 def test_concurrent_requests(server):
     srv, cli = client(server), client(server)
     srv.subscribe("add", "", cb=lambda m: srv.publish(m.reply, str(int(m.data) + 1).encode()), workers=4)

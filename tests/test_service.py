@@ -72,16 +72,42 @@ def test_chat_stub_echo(env):
 
 
 def test_metrics_health(env):
-    _, _, _, cli = env
-    req(cli, "list_models", {})
+    _, _, svc, cli = env
+    req(cli, "list_models", {})                      # native responder
+    svc.native_list(False)
+    req(cli, "list_models", {})                      # the Python handler
     for _ in range(50):   # the handler records its latency just after it has replied
         m = req(cli, "metrics", {})
         if "list_models" in m["data"]["latency_ms"]:
             break
         time.sleep(0.01)
-    assert m["ok"] and m["data"]["requests"]["list_models"] >= 1 and "p50" in m["data"]["latency_ms"]["list_models"]
+    r = m["data"]["requests"]
+    assert m["ok"] and r["list_models"] == 2 and r["list_models_native"] == 1, r
+    assert "p50" in m["data"]["latency_ms"]["list_models"]
     h = req(cli, "health", {})
     assert h["data"]["status"] == "ok" and h["data"]["backend"] == "stub"
+
+
+def test_list_models_native_matches_handler(env, tiny_models):
+    """The native list_models reply (client reader thread, cached registry body) is byte-identical to the
+    handler's, and a listing requested right after a pull / delete reply already shows the change (the body is
+    refreshed before the service sends any reply)."""
+    srv, cfg, svc, cli = env
+    raw = lambda: cli.request("lmstudio.list_models", b"{}", 10).data
+    empty = raw()
+    svc.native_list(False)
+    assert raw() == empty
+    svc.native_list(True)
+    _push_tiny(srv.url, tiny_models["tiny-llama"], "synthetic/tiny-llama-GGUF/tiny-llama-Q4_K_M.gguf")
+    assert req(cli, "pull_model", {"identifier": "synthetic/tiny-llama"}, timeout=60)["ok"]
+    one = raw()
+    assert [m["id"] for m in json.loads(one)["data"]["models"]["data"]] == ["tiny-llama"]
+    svc.native_list(False)
+    assert raw() == one
+    svc.native_list(True)
+    n0 = svc._list_sub.auto_replied
+    assert req(cli, "delete_model", {"model_id": "tiny-llama"})["ok"]
+    assert raw() == empty and svc._list_sub.auto_replied == n0 + 1
 
 
 def _push_tiny(srv_url, tiny_path, name):
@@ -143,8 +169,8 @@ def test_queue_group_scale_out(env):
     try:
         for _ in range(200):
             assert req(cli, "list_models", {})["ok"]
-        assert svc.counters["list_models"] > 20 and svc2.counters["list_models"] > 20
-        assert svc.counters["list_models"] + svc2.counters["list_models"] == 200
+        n1, n2 = svc._request_counts()["list_models"], svc2._request_counts()["list_models"]
+        assert n1 > 20 and n2 > 20 and n1 + n2 == 200, (n1, n2)
     finally:
         svc2.stop()
         svc2.client.close()
@@ -328,8 +354,10 @@ def test_list_and_delete_deadlines(env):
     from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
     write_synthetic_gguf(os.path.join(d, "slow-Q4_K_M.gguf"), "tiny-llama", "Q4_K_M")
     real_list = svc.registry.list_api
+    svc.native_list(False)                # the handler path holds the 30 s context (the native reply never waits)
     cfg.timeout_list = 0.3
     svc.registry.list_api = lambda *a, **k: (time.sleep(2.0), real_list(*a, **k))[1]
+    svc._list_cache = {}                  # a registry snapshot not encoded yet (the slow read runs)
     r = req(cli, "list_models", {})
     assert r == {"ok": False, "error": "error reading model registry: context deadline exceeded",
                  "data": {"http_status": 0}}
