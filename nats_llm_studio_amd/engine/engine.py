@@ -46,6 +46,9 @@ _TP_TRACE = os.environ.get("NLS_TP_TRACE", "0") == "1"
 _NO_REPLAY = os.environ.get("NLS_GRAPH_NO_REPLAY", "0") == "1"
 # single-GPU prefill: the first tokens of finished prompts are read back once per engine step, not per chunk
 _ASYNC_FIRST = os.environ.get("NLS_ASYNC_FIRST", "1") == "1"
+# single-GPU prefill of ONE prompt chunk of <= 64 tokens (a chat request's prompt): a captured graph per token bucket
+# instead of ~230 eager launches, whose host time (~2.5 ms on the 8B) exceeded the GPU time
+_PREFILL_GRAPHS = os.environ.get("NLS_PREFILL_GRAPHS", "1") == "1"
 _NSEG = 6        # int32 step metadata segments: ids | pos | slot | tok_seq | ctx_len | use_prev (+ block tables)
 
 
@@ -285,6 +288,7 @@ class Engine:
         self.async_decode = async_decode
         self.use_graphs = use_graphs and self.dev.type == "cuda"
         self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}     # (bucket, logits needed) -> graph
+        self.pf_graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}  # (token bucket, logits needed) -> prefill graph
         self.eos = set(int(e) for e in eos_ids)
         if tokenizer is not None and getattr(tokenizer, "eos_id", None) is not None:
             self.eos.add(int(tokenizer.eos_id))
@@ -301,6 +305,7 @@ class Engine:
         self._ids = itertools.count()
         self.host_ms = defaultdict(float)
         self.counters = dict(steps=0, decode_tokens=0, prefill_tokens=0, requests=0, graph_replays=0,
+                             prefill_graph_replays=0,
                              device_sampled_steps=0, preemptions=0, recompute_tokens=0, candidate_sampled_steps=0,
                              candidate_sampled_prefills=0)
         self.full_logits: Optional[torch.Tensor] = None
@@ -423,6 +428,7 @@ class Engine:
             return
         self.shutdown()
         self.graphs.clear()
+        self.pf_graphs.clear()
         self.kc = self.vc = None
         self.db = self.pb = None
         self.model = None
@@ -632,21 +638,60 @@ class Engine:
             self._first_tokens(seqs, toks)
             self._first_pool.append(pin)
 
-    def _exec_prefill(self, T: int, rows: List[int], need_logits: bool):
-        b = self.pb
-        cuda = self.dev.type == "cuda"
-        b.meta.copy_(self.h_meta_p, non_blocking=cuda and self.rank == 0)
-        pad = b.pad
-        h = self.h_meta_p.numpy()
-        qb = ops.prefill_blocks(h[3 * pad:4 * pad], h[pad:2 * pad], T) if self.prefill_attn else None
-        # logit rows and query blocks through pinned staging (async, stream-ordered: pageable uploads block
-        # the host until the decode step in flight has drained), one set per prefill metadata buffer
+    PREFILL_GRAPH_T = (16, 32, 64)      # token buckets of the captured single-prompt prefill graphs
+
+    def _pf_buffers(self):
+        """Pinned staging (two sets) and the device copies of the prefill logit rows and query blocks."""
         if not hasattr(self, "_pf_pin"):
+            cuda = self.dev.type == "cuda"
             nq = (self.max_prefill + 15) // 16 + self.max_batch
             self._pf_pin = [(torch.zeros(self.max_batch, dtype=torch.int32, pin_memory=cuda),
                              torch.zeros(nq, 4, dtype=torch.int32, pin_memory=cuda)) for _ in range(2)]
             self._pf_dev = (torch.zeros(self.max_batch, dtype=torch.int32, device=self.dev),
                             torch.zeros(nq, 4, dtype=torch.int32, device=self.dev))
+
+    def _pf_graph_key(self, T: int, rows: List[int], qb, need_logits: bool):
+        """The prefill graph of this chunk, if any: single GPU, one contiguous run of <= 64 tokens of one
+        sequence (one query block, one logit row) -- the shape of a chat request's prompt."""
+        if not (self.use_graphs and _PREFILL_GRAPHS and self.tp is None and qb is not None and len(qb) == 1
+                and len(rows) == 1 and self.model.cfg.n_expert == 0):
+            return None
+        for Tb in self.PREFILL_GRAPH_T:
+            if T <= Tb <= self.max_prefill:
+                return (Tb, bool(need_logits))
+        return None
+
+    def _pf_forward(self, Tb: int, need_logits: bool):
+        ld, qd = self._pf_dev
+        return self.model.forward(self.pb, self.kc, self.vc, Tb, self.bs, LlamaModel.attn_splits(Tb, self.model.Hkv),
+                                  logit_rows=ld[:1], n_logits=1, qblocks=qd[:1], nqb=1, need_logits=need_logits)
+
+    def _capture_prefill(self, key):
+        """Capture the prefill graph `key` on the current metadata (the caller ran the same forward eagerly)."""
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._pf_forward(*key)
+        torch.cuda.synchronize(self.dev)
+        self.pf_graphs[key] = g
+
+    def _exec_prefill(self, T: int, rows: List[int], need_logits: bool):
+        b = self.pb
+        cuda = self.dev.type == "cuda"
+        pad = b.pad
+        h = self.h_meta_p.numpy()
+        qb = ops.prefill_blocks(h[3 * pad:4 * pad], h[pad:2 * pad], T) if self.prefill_attn else None
+        key = self._pf_graph_key(T, rows, qb, need_logits)
+        if key is not None:
+            # rows T .. Tb-1 of the token bucket: no KV writes (slot -1), position 0 (the RoPE table), no attention
+            # (the one query block covers [0, T)); their GEMV rows compute on stale activations and are never read
+            Tb = key[0]
+            for seg, v in ((0, 0), (1, 0), (2, -1), (3, 0), (4, 0)):
+                h[seg * pad + T:seg * pad + Tb] = v
+        b.meta.copy_(self.h_meta_p, non_blocking=cuda and self.rank == 0)
+        # logit rows and query blocks through pinned staging (async, stream-ordered: pageable uploads block
+        # the host until the decode step in flight has drained), one set per prefill metadata buffer
+        self._pf_buffers()
         # (set _pfk's previous uploads have executed: _next_prefill_buf waited on their event)
         lp, qp = self._pf_pin[self._pfk]
         ld, qd = self._pf_dev
@@ -663,9 +708,19 @@ class Engine:
                 qbt.copy_(qp[:len(qb)], non_blocking=cuda)
         if self._pf_ev[self._pfk] is not None:
             self._pf_ev[self._pfk].record()
-        n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
-                               logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb),
-                               need_logits=need_logits)
+        if key is not None:
+            g = self.pf_graphs.get(key)
+            if g is not None:
+                g.replay()
+                self.counters["prefill_graph_replays"] += 1
+                n = 1
+            else:                       # first chunk of this bucket: run it eagerly, then capture for the next
+                n = self._pf_forward(*key)
+                self._capture_prefill(key)
+        else:
+            n = self.model.forward(b, self.kc, self.vc, T, self.bs, LlamaModel.attn_splits(T, self.model.Hkv),
+                                   logit_rows=lr, n_logits=len(rows), qblocks=qbt, nqb=0 if qbt is None else len(qb),
+                                   need_logits=need_logits)
         self._gather(b, n, need_logits)
 
     CAND = 128           # TP sampling: candidates per rank and row
@@ -1243,11 +1298,39 @@ class Engine:
         self.graphs[(Bp, need_logits, dsamp) if dsamp else (Bp, need_logits)] = g
         return g
 
+    def _precapture_prefill(self):
+        """Capture every single-prompt prefill graph on dummy metadata: every row slot -1 (no KV writes), one query
+        block over the whole bucket at position 0 of sequence 0 (its reads land in valid blocks, the outputs are
+        discarded)."""
+        if not (self.use_graphs and _PREFILL_GRAPHS and self.tp is None and self.model.cfg.n_expert == 0
+                and self.prefill_attn):
+            return
+        self._pf_buffers()
+        b, pad = self.pb, self.pb.pad
+        h = self.h_meta_p.numpy()
+        ld, qd = self._pf_dev
+        for Tb in self.PREFILL_GRAPH_T:
+            if Tb > self.max_prefill:
+                continue
+            h[:_NSEG * pad] = 0
+            h[2 * pad:3 * pad] = -1
+            h[_NSEG * pad:] = 0
+            b.meta.copy_(self.h_meta_p)
+            ld.zero_()
+            qd[0] = torch.tensor([0, Tb, 0, 0], dtype=torch.int32)
+            for need in (False, True):
+                if (Tb, need) not in self.pf_graphs:
+                    self._pf_forward(Tb, need)
+                    self._capture_prefill((Tb, need))
+        torch.cuda.synchronize(self.dev)
+
     def capture_all(self, buckets: Seq[int] = None):
-        """Pre-capture decode graphs (padded rows have ctx 0 / slot -1: no KV writes)."""
+        """Pre-capture decode graphs (padded rows have ctx 0 / slot -1: no KV writes) and the single-prompt
+        prefill graphs."""
         if not self.use_graphs:
             return
         self._drain()
+        self._precapture_prefill()
         pad = self.db.pad
         h = self.h_meta_d2[0].numpy()
         h[:_NSEG * pad] = 0

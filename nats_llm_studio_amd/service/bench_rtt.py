@@ -87,6 +87,8 @@ def measure_engine_chat_rtt(engine, metadata: dict, model_id: str = "llama-3-8b"
                 raise RuntimeError(f"chat_model failed: {str(r)[:300]}")
             cli._c.bench_requests("lmstudio.chat_model", body, warmup, 60000)
             us = cli._c.bench_requests("lmstudio.chat_model", body, n, 60000)
+            # where one request's time goes (service tracer, p50 per phase over the timed requests)
+            phases = {k: v.get("p50") for k, v in svc.tracer.summary(last=0)["phases_ms"].items()}
         finally:
             cli.close()
             for sub in svc.subs:
@@ -97,7 +99,7 @@ def measure_engine_chat_rtt(engine, metadata: dict, model_id: str = "llama-3-8b"
                 engine.shutdown()
     return {"p50_ms": round(_pct(us, 50) / 1e3, 4), "p99_ms": round(_pct(us, 99) / 1e3, 4),
             "mean_ms": round(statistics.mean(us) / 1e3, 4), "n": n, "max_tokens": max_tokens,
-            "prompt_tokens": r["data"]["response"]["usage"]["prompt_tokens"]}
+            "prompt_tokens": r["data"]["response"]["usage"]["prompt_tokens"], "phases_p50_ms": phases}
 
 
 def measure_engine_chat_load(engine, metadata: dict, model_id: str = "llama-3-8b", n: int = 512,

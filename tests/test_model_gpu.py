@@ -182,6 +182,43 @@ def test_engine_fp8_kv_cache(gpu, tiny_models, name, monkeypatch):
     assert eng.counters["graph_replays"] > 0
 
 
+@pytest.mark.parametrize("precapture", [False, True])
+def test_prefill_graphs_match_eager(gpu, tiny_models, monkeypatch, precapture):
+    """Single-prompt prefill chunks of <= 64 tokens replay a captured graph of their token bucket (16 / 32 / 64;
+    padded rows write no KV and are never read): greedy and seeded-sampled tokens equal the eager prefill, the
+    first greedy token equals the fp32 reference, and a second prompt of a bucket replays its graph."""
+    from nats_llm_studio_amd.engine import engine as E
+    r = GGUFReader(tiny_models["tiny-llama"])
+    m = LlamaModel(r, gpu)
+    ref = ReferenceModel(r)
+    rng = np.random.default_rng(11)
+    lens = (5, 16, 17, 33, 64, 65, 9, 30)
+    prompts = [[int(t) for t in rng.integers(0, 900, n)] for n in lens]
+    params = [SamplingParams(max_tokens=5, ignore_eos=True) if i % 2 == 0 else
+              SamplingParams(max_tokens=5, temperature=0.8, top_k=20, seed=i, ignore_eos=True) for i in range(len(lens))]
+    outs, counters = [], []
+    for flag in (False, True):
+        monkeypatch.setattr(E, "_PREFILL_GRAPHS", flag)
+        eng = Engine(m, None, max_batch=4, max_prefill_tokens=128, use_graphs=True)
+        if precapture:
+            eng.capture_all()
+        res = []
+        for p, sp in zip(prompts, params):           # one prompt at a time: each prefill is its own chunk
+            f = eng.submit(GenRequest(list(p), sp))
+            while not f.done():
+                eng.step()
+            res.append(f.result().token_ids)
+        outs.append(res)
+        counters.append(dict(eng.counters))
+    assert outs[0] == outs[1]
+    assert counters[0]["prefill_graph_replays"] == 0
+    # keys (bucket 16 / 32 / 64, logits): lazily, only the 9-token greedy prompt finds its (16, greedy) graph; precaptured, all 7 <= 64 do
+    assert counters[1]["prefill_graph_replays"] >= (7 if precapture else 1), counters[1]
+    for p, sp, toks in zip(prompts, params, outs[1]):
+        if sp.greedy:
+            assert toks[0] == ref.greedy(p, 1)[0]
+
+
 def test_graph_equals_eager(gpu, tiny_models):
     r = GGUFReader(tiny_models["tiny-llama"])
     m = LlamaModel(r, gpu)
