@@ -190,16 +190,25 @@ def _run_tp_leg(args, world: int, cuda: bool) -> dict:
                         "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE",
                         "ROLE_NAME", "TORCH_NCCL_ASYNC_ERROR_HANDLING")}
     t0 = time.time()
+    # its own session: at the time limit the WHOLE process group goes (the launcher and every rank it started),
+    # so no rank of an abandoned leg keeps a GPU for the runs after this one
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True)
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.tp_leg_timeout, env=env,
-                           start_new_session=True)
+        out, err = p.communicate(timeout=args.tp_leg_timeout)
     except subprocess.TimeoutExpired:
+        import signal
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.communicate()
         return {"model": f"{tmodel} Q4_K_M", "parallelism": f"tp{world}",
-                "error": f"no result within {args.tp_leg_timeout} s (killed)"}
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"model": f"{tmodel} Q4_K_M", "parallelism": f"tp{world}", "error": f"rc {r.returncode}",
-                "stderr_tail": r.stderr[-600:]}
+                "error": f"no result within {args.tp_leg_timeout} s (process group killed)"}
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"model": f"{tmodel} Q4_K_M", "parallelism": f"tp{world}", "error": f"rc {p.returncode}",
+                "stderr_tail": err[-600:]}
     d = json.loads(lines[-1])
     return {"model": d["config"]["model"], "parallelism": d["config"]["parallelism"],
             "concurrency": args.tp_leg_concurrency, "value": d["value"], "unit": d["unit"],

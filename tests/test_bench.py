@@ -50,6 +50,14 @@ def test_bench_dp_run_adds_tp_leg(tmp_path):
     assert c["oneshot"] is False and c["ctrl_transport"] == "shm-ring"
 
 
+def test_bench_tp_leg_time_limit(tmp_path):
+    """A TP leg that overruns its limit costs the leg only: its whole process group (launcher + ranks) is killed
+    and the headline line still comes out."""
+    out = _bench(tmp_path, "--gpus", "2", "--model", "tiny-llama-tp", "--tp-leg-timeout", "1")
+    assert out["config"]["parallelism"] == "dp2" and out["value"] > 0
+    assert "process group killed" in out["tp_leg"]["error"], out["tp_leg"]
+
+
 def test_bench_rejects_mismatched_world(tmp_path):
     env = dict(os.environ, WORLD_SIZE="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu"],
