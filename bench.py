@@ -273,6 +273,7 @@ def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, step
     eng = Engine(model, None, max_batch=B, max_prefill_tokens=max_prefill, use_graphs=cuda and not args.no_graphs,
                  ctx=ctx, num_blocks=None if cuda else B * ((need_tokens + 15) // 16 + 1))
     marks = []
+    info_mem = dict(dense_gb=round(eng.dense_bytes / 1e9, 2), kv_pool_gb=round(eng.kv_pool_bytes / 1e9, 2))
 
     def barrier_hook():                 # both sides of the timed region, on every rank
         sync()
@@ -282,7 +283,7 @@ def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, step
         marks.append(time.perf_counter())
 
     info = dict(B=B, tp=tp, weights_gb=round(model.weight_bytes / 1e9, 3), n_expert=model.cfg.n_expert,
-                timings={"gguf_write": round(t_gen, 1), "load": round(t_load, 1)})
+                timings={"gguf_write": round(t_gen, 1), "load": round(t_load, 1)}, **info_mem)
     out = dict(elapsed=0.0, tokens=0.0, info=info, extra={})
     leader = tp_rank == 0
     if not leader:                      # follower: replay the leader's steps until STOP
@@ -441,6 +442,8 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
         "rtt_chat_model_engine": chat_rtt,
         "rtt": rtt,
         "weights_gb_per_rank": info["weights_gb"],
+        "dense_weight_copies_gb": info.get("dense_gb"),
+        "kv_pool_gb": info.get("kv_pool_gb"),
         "comm": info["comm_stats"],
         "timings_s": info["timings"],
         "kernels_stamp_current": _kernels_current(),

@@ -217,16 +217,29 @@ class Engine:
         self.max_blocks = math.ceil(self.ctx / block_size)
         # f16 copies of the projection weights for the large-M dense GEMM (prefill chunks, decode
         # batches >= ops.DENSE_MIN_M): NLS_DENSE_WEIGHTS=auto (default: when the copies take at most
-        # 60 % of free HBM -- Llama-3-8B: 15 GB of 288, Llama-3-70B: 140 GB of ~245 (B=512 86.3 vs
+        # 60 % of free HBM and leave the KV pool room for max_batch x ctx -- Llama-3-8B: 15 GB of 288;
+        # Llama-3-70B: 140 GB of ~245 only at small batch x context (B=512 86.3 vs
         # 96.8 ms/step with mode 7; at <= 256 rows its launches keep the quantised GEMMs, tuning "d:" -1
         # entries: B=256 51.4 vs 58.4, profiles/bench_70b_mode7.txt); the rest stays for the KV pool), 1 (always),
         # 0 (never). NLS_DENSE_EXPERTS=1 adds the MoE experts (Mixtral-8x7B: 90 GB) as a second tier
         dense = os.environ.get("NLS_DENSE_WEIGHTS", "auto")
         self.dense_bytes = 0
+        self.dense_policy = dense
         if self.dev.type == "cuda" and dense != "0" and hasattr(model, "expand_dense"):
             free, _ = torch.cuda.mem_get_info(self.dev)
-            self.dense_bytes = model.expand_dense(None if dense == "1" else int(0.60 * free),
-                                                  experts=os.environ.get("NLS_DENSE_EXPERTS", "0") == "1")
+            budget = None
+            if dense != "1":
+                # auto: at most 60 % of free HBM, and never so much that the KV pool (kv_mem_fraction of what is
+                # left) could not hold every row of a full batch at full context -- the copies buy ~10 % of
+                # large-batch step time, a squeezed pool costs admissions (Llama-3-70B at 512 x 480 tokens:
+                # 79 GB of KV, no copies; Llama-3-8B: 31 GB, copies kept)
+                esz = torch.finfo(getattr(model, "kv_dtype", torch.bfloat16)).bits // 8
+                kv_need = (self.max_batch * self.ctx * 2 * self.cfg.n_layer * model.Hkv * model.D * esz
+                           if num_blocks is None else 0)
+                budget = max(0, min(int(0.60 * free), int(free - kv_need / max(kv_mem_fraction, 1e-3))))
+            self.dense_bytes = model.expand_dense(budget, experts=os.environ.get("NLS_DENSE_EXPERTS", "0") == "1")
+            if dense != "1" and self.dense_bytes == 0:
+                self.dense_policy = "auto: no copies (KV pool for max_batch x ctx first)"
         if num_blocks is None:
             # every row at full context, plus the admission watermark (below) on top: a pool sized to the
             # worst case never preempts
@@ -243,6 +256,7 @@ class Engine:
             num_blocks = self.tp.min_int(num_blocks)
         self.num_blocks = num_blocks
         self.kc, self.vc = model.kv_cache(num_blocks, block_size)
+        self.kv_pool_bytes = 2 * self.kc.numel() * self.kc.element_size()
         self.alloc = BlockAllocator(num_blocks, cache=prefix_cache)
         # admission keeps this many blocks free for the running sequences to grow into (fewer
         # preemptions right after a burst of admissions); NLS_KV_RESERVE=full restores worst-case
@@ -1420,4 +1434,7 @@ class Engine:
                     kv_blocks_free=self.alloc.n_free, kv_blocks_total=self.num_blocks,
                     kv_reserve="full" if self.reserve_full else "ondemand", gen_ratio=round(self.gen_ratio, 3),
                     prefix_cache_hit_tokens=self.alloc.hits, prefix_cache_blocks=len(self.alloc.block_of),
-                    graphs=sorted(self.graphs), host_ms={k: round(v, 1) for k, v in self.host_ms.items()})
+                    graphs=sorted(self.graphs), prefill_graphs=sorted(self.pf_graphs),
+                    dense_weight_gb=round(self.dense_bytes / 1e9, 2), dense_policy=self.dense_policy,
+                    kv_pool_gb=round(self.kv_pool_bytes / 1e9, 2),
+                    host_ms={k: round(v, 1) for k, v in self.host_ms.items()})
