@@ -57,6 +57,16 @@ def heuristic(segs, M: int):
         # it lost every measured Llama-3-8B shape to modes 2 / 9 (LM head M=256: 489 vs 320 us, profiles/
         # qgemm11_r05.txt)
         if all(int(s.w.type) in (12, 13, 14) for s in segs):
+            if M >= 256 and (rows >= 4 * K or K >= 2 * rows):
+                # wide (gate|up, LM head) and down-projection shapes: the quantised GEMM on the raw tile-blocks
+                # (mode 9, 256 weight rows x 256 activation rows) won every measured one at M >= 256 -- Llama-3-8B
+                # gate|up / LM head, Llama-3-70B gate|up / down / LM head by 10-20 % over mode 2
+                # (profiles/tune_quant_70b_r05.txt); split K until the grid covers the 256 CUs
+                tiles = sum((s.w.rows + 255) // 256 for s in segs) * ((M + 255) // 256)
+                ks, nb = 1, K // 256
+                while tiles * ks < 256 and ks * 2 <= min(8, max(1, nb // 4)):    # (ks <= 8: the tuned range)
+                    ks *= 2
+                return (9, 8, 2, ks)
             # LDS-dequant GEMM (mode 2): 128 weight rows x 256 (or 128) activation rows per workgroup;
             # split K until the grid covers the 256 CUs (the measured winners on the 8B shapes)
             tiles = sum((s.w.rows + 127) // 128 for s in segs) * ((M + 255) // 256)
