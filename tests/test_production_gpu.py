@@ -31,9 +31,10 @@ _DENSE = sorted({k.rsplit(":", 1)[0] for k, v in _TABLE.items() if k.startswith(
 
 
 def _weights(types, rows, K, dev, rng):
-    """Segments of a fused launch: Q|K|V (3 types) splits rows 4:1:1 as in Llama-3-8B."""
+    """Segments of a fused launch: Q|K|V (3 types) as in the Llama family, n_head x head_dim = d_model = K query
+    rows and the rest split evenly between K and V (Llama-3-8B 4096:1024:1024, -70B 8192:1024:1024)."""
     if len(types) == 3:
-        kv = rows // 6
+        kv = (rows - K) // 2
         parts = [(types[0], rows - 2 * kv), (types[1], kv), (types[2], kv)]
     else:
         parts = [(types[0], rows)]
