@@ -44,6 +44,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ctx", default="128,512,2048")
     ap.add_argument("--kv", default="bf16")
+    ap.add_argument("--splits", type=int, default=0, help="override the split count (0: the production policy)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     kvt = torch.bfloat16 if a.kv == "bf16" else torch.float8_e4m3fn
@@ -55,7 +56,7 @@ def main():
     out = torch.zeros(1, Hq * D, dtype=ops.ACT_DTYPE, device=dev)
     ts = torch.zeros(1, dtype=torch.int32, device=dev)
     dummy = torch.zeros(256, device=dev)
-    ns = llama.LlamaModel.attn_splits(1, Hkv)
+    ns = a.splits or llama.LlamaModel.attn_splits(1, Hkv)
     ws = torch.zeros(Hq * ns * (D + 2), dtype=torch.float32, device=dev)
     cnt = torch.zeros(Hkv, dtype=torch.int32, device=dev)
     for ctx in [int(c) for c in a.ctx.split(",")]:
@@ -74,6 +75,7 @@ def main():
             attn(i)
         t_attn, t_triv, t_both = timed(attn), timed(triv), timed(both)
         print(json.dumps(dict(ctx=ctx, kv=a.kv, n_split=ns, waves_env=os.environ.get("NLS_ATTN_MFMA_WAVES"),
+                              mfma_env=os.environ.get("NLS_ATTN_MFMA"),
                               attn_us=round(t_attn, 2), trivial_us=round(t_triv, 2), pair_us=round(t_both, 2),
                               attn_after_kernel_us=round(t_both - t_triv, 2))), flush=True)
 

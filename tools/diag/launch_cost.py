@@ -4,7 +4,10 @@ stream, captured once and replayed; per-link time of
   * M=1 Q4_K GEMVs x_{i+1} = f16(W_i x_i) with the tuned batch-1 config, W_i [R, 4096], R = 256 .. 14336
     (x_{i+1} takes the first 4096 outputs; rows beyond are written to a scratch tail),
 and the least-squares line t = a + bytes / bw through the GEMV points: `a` is the per-launch cost a fused
-(fewer-launch) decode layer could remove, `bw` the streaming rate."""
+(fewer-launch) decode layer could remove, `bw` the streaming rate.
+Then the same chains with the weights held in the Infinity Cache (a few distinct weights cycled, > the 32 MiB of
+L2, < its 256 MiB): how much of the per-link streaming time a read from the die-level cache instead of HBM saves
+(the case for prefetching the next GEMV's weights into it while the current one runs)."""
 import os
 import sys
 
@@ -73,6 +76,20 @@ def main(N=24, D=4096):
     A = np.stack([np.ones_like(b), b], 1)
     (a, s), *_ = np.linalg.lstsq(A, u, rcond=None)
     print(f"fit: t = {a:.2f} us + bytes / {1 / s / 1e6:.2f} TB/s", flush=True)
+    for R, nw in ((4096, 8), (6144, 6), (14336, 4)):
+        ws = [ops.QWeight(Q.random_blocks(GGMLType.Q4_K, R * D, 0.02, rng), GGMLType.Q4_K, R, D, dev) for _ in range(nw)]
+        ys = [torch.zeros(16, max(R, D), dtype=ops.ACT_DTYPE, device=dev) for _ in range(N + 1)]
+        ys[0][0, :D] = (torch.randn(D, device=dev) * 0.5).to(ops.ACT_DTYPE)
+
+        def chain():
+            for i in range(N):
+                ops.qgemv([ops.Seg(ws[i % nw])], ys[i][:, :D], ys[i + 1], 1, epi="act")
+        us = per_link(chain, N)
+        nbytes = R * D * 144 // 256
+        print(f"gemv R={R:6d} resident ({nw} weights, {nw * nbytes / 2**20:.0f} MiB cycled): {us:.2f} us per link, "
+              f"{nbytes / us / 1e6:.2f} TB/s, streaming part {us - a:.2f} us", flush=True)
+        del ws, ys
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
