@@ -50,6 +50,12 @@ enum QType : int {
 
 #define DEVI __device__ __forceinline__
 
+// Q4_K nibbles -> f16 through the scaled fp8 conversion (frag8_nib) instead of the magic-number subtract;
+// -DNLS_Q4_FP8CVT=1 builds it (A/B builds, tools/gemm_ab.py; default off until measured on the GPU)
+#ifndef NLS_Q4_FP8CVT
+#define NLS_Q4_FP8CVT 0
+#endif
+
 DEVI float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 DEVI float bf2f(uint16_t b) { return __builtin_bit_cast(float, ((uint32_t)b) << 16); }
 DEVI uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
@@ -118,6 +124,23 @@ DEVI f16x8 frag8(uint32_t n0, uint32_t n1, f16x2 off, f16x2 a, f16x2 c) {
   u[1] = as_u32(__builtin_elementwise_fma(mag_hi(n0) - off, a, c));
   u[2] = as_u32(__builtin_elementwise_fma(mag_lo(n1) - off, a, c));
   u[3] = as_u32(__builtin_elementwise_fma(mag_hi(n1) - off, a, c));
+  return __builtin_bit_cast(f16x8, u);
+}
+// 8 nibble values (bytes of n0, n1, each < 16) -> f16x8 of a*b + c, two values per conversion: a byte b < 16
+// read as OCP fp8 e4m3 is exactly b * 2^-9 (0..7 subnormal, 8..15 exponent field 1), so gfx950's scaled
+// fp8 -> f16 conversion with scale 2^9 yields b itself and the FMA follows directly -- the magic-number
+// path's exact (1024 + b) - 1024 subtract is gone (4 of its 12 VALU ops per 8 values). Same single rounding,
+// bit-identical to frag8 with off = 1024.
+DEVI f16x2 nib_h2(uint32_t w, bool hi) {
+  return hi ? __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, 512.f, true)
+            : __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, 512.f, false);
+}
+DEVI f16x8 frag8_nib(uint32_t n0, uint32_t n1, f16x2 a, f16x2 c) {
+  u32x4 u;
+  u[0] = as_u32(__builtin_elementwise_fma(nib_h2(n0, false), a, c));
+  u[1] = as_u32(__builtin_elementwise_fma(nib_h2(n0, true), a, c));
+  u[2] = as_u32(__builtin_elementwise_fma(nib_h2(n1, false), a, c));
+  u[3] = as_u32(__builtin_elementwise_fma(nib_h2(n1, true), a, c));
   return __builtin_bit_cast(f16x8, u);
 }
 // 4 bytes -> two f16 pairs (b - off) (exact small integers), e.g. 6-bit scales
@@ -273,7 +296,11 @@ DEVI f16x8 frag_q4k(const RawQ4K& r, const ScK& s, int t) {
   const u32x4 p = t < 4 ? r.p0 : r.p1;
   const int wi = 2 * ((t >> 1) & 1), sh = 4 * (t & 1);
   const uint32_t n0 = (p[wi] >> sh) & 0x0F0F0F0Fu, n1 = (p[wi + 1] >> sh) & 0x0F0F0F0Fu;
+#if NLS_Q4_FP8CVT
+  return frag8_nib(n0, n1, bcast(s.a2, t), bcast(s.c2, t));
+#else
   return frag8(n0, n1, h2((_Float16)1024.f), bcast(s.a2, t), bcast(s.c2, t));
+#endif
 }
 // Q5_K: plus the 5th bit = bit t of the lane's 8 qh bytes
 DEVI f16x8 frag_q5k(const RawQ5K& r, const ScK& s, int t) {

@@ -480,8 +480,13 @@ DEVI void q11_deq_store(const RawRegs<T>& R, int c, int lane, uint8_t* a0, uint8
     const f16x2 d = h2(__builtin_bit_cast(_Float16, (uint16_t)(h[0] & 0xFFFF)));
     const f16x2 nd = -h2(__builtin_bit_cast(_Float16, (uint16_t)(h[0] >> 16)));
     const f16x2 a2 = (mag_lo(scp) - k1024) * d, c2 = (mag_lo(mp) - k1024) * nd;
+#if NLS_Q4_FP8CVT
+    f0 = frag8_nib(w0 & 0x0F0F0F0Fu, w1 & 0x0F0F0F0Fu, bcast(&a2, 0), bcast(&c2, 0));
+    f1 = frag8_nib((w0 >> 4) & 0x0F0F0F0Fu, (w1 >> 4) & 0x0F0F0F0Fu, bcast(&a2, 1), bcast(&c2, 1));
+#else
     f0 = frag8(w0 & 0x0F0F0F0Fu, w1 & 0x0F0F0F0Fu, k1024, bcast(&a2, 0), bcast(&c2, 0));
     f1 = frag8((w0 >> 4) & 0x0F0F0F0Fu, (w1 >> 4) & 0x0F0F0F0Fu, k1024, bcast(&a2, 1), bcast(&c2, 1));
+#endif
   } else {   // Q6_K: k-step s of chunk c = K-step t = 2c + s of frag_q6k
     const u32x4 ql = R.q;
     const uint32_t h0 = R.e0, h1 = R.e1;

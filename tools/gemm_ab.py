@@ -84,9 +84,11 @@ def main():
             g.replay()
             torch.cuda.synchronize()
             graphs.append(g)
+        diffs = []
         for o in outs[1:]:
             err = (o - outs[0]).abs().max().item() / (outs[0].abs().max().item() + 1e-9)
             assert err < 1e-2, f"{name}: variant output differs ({err:.3g})"
+            diffs.append("bit-equal" if torch.equal(o, outs[0]) else f"max rel diff {err:.2e}")
         ts = [[] for _ in libs]
         for _ in range(a.rounds):
             for li, g in enumerate(graphs):
@@ -101,7 +103,7 @@ def main():
         for (path, _), t in zip(libs, ts):
             med = sorted(t)[len(t) // 2]
             line += f" | {os.path.basename(path)} {med:8.2f}us {flops / med / 1e6:6.1f}TF"
-        print(line, flush=True)
+        print(line + (" | " + ", ".join(diffs) if diffs else ""), flush=True)
         del graphs, copies, segs
         torch.cuda.empty_cache()
 
