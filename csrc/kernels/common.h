@@ -51,9 +51,9 @@ enum QType : int {
 #define DEVI __device__ __forceinline__
 
 // Q4_K nibbles -> f16 through the scaled fp8 conversion (frag8_nib) instead of the magic-number subtract;
-// -DNLS_Q4_FP8CVT=1 builds it (A/B builds, tools/gemm_ab.py; default off until measured on the GPU)
+// -DNLS_Q4_FP8CVT=0 builds the previous form (A/B builds, tools/gemm_ab.py; profiles/q4_fp8cvt_ab_r05.txt)
 #ifndef NLS_Q4_FP8CVT
-#define NLS_Q4_FP8CVT 0
+#define NLS_Q4_FP8CVT 1
 #endif
 
 DEVI float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
