@@ -27,7 +27,9 @@
 // dequantised with the f16 "magic number" trick: v_perm_b32 places byte b under the
 // exponent byte 0x64 -> f16 (1024 + b) exactly, then one packed subtract (exact) and one
 // packed FMA with the sub-block scale (single rounding) give d*sc*q - dmin*m, two values
-// per instruction. The residual stream and all accumulators stay fp32.
+// per instruction. Q4_K's 4-bit values skip the subtract: read as fp8 e4m3 a byte < 16 is
+// exactly b * 2^-9, so one scaled fp8 -> f16 conversion per pair yields b (frag8_nib).
+// The residual stream and all accumulators stay fp32.
 #pragma once
 #include <type_traits>
 #include <hip/hip_runtime.h>
