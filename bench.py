@@ -318,7 +318,6 @@ def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, step
 
     wait = [0.0]
     orig = eng._process
-    extra = out["extra"]
     if args.step_breakdown and cuda and headline:    # time the host spends blocked on step N's event
         def timed_outer(infl):
             t = time.perf_counter()
@@ -326,11 +325,21 @@ def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, step
             wait[0] += time.perf_counter() - t
             orig(infl)
         eng._process = timed_outer
+    extra = out["extra"]
     st0 = dict(comm.stats) if comm is not None else None
+    telem = None
+    if cuda and headline:      # GFX clock / power / temperature at both brackets and in between
+        from nats_llm_studio_amd.utils.telemetry import GpuTelemetry
+        telem = GpuTelemetry(local)
     eng.sync(barrier_hook) if tp > 1 else barrier_hook()
+    if telem is not None:
+        telem.start()
     for _ in range(steps):
         eng.step()
     eng.sync(barrier_hook) if tp > 1 else barrier_hook()
+    if telem is not None:
+        telem.stop()
+        extra["gpu_telemetry"] = telem.summary()
     elapsed = marks[1] - marks[0]
     eng._process = orig
     comm_stats = None

@@ -55,12 +55,15 @@ class SamplingParams:
         def get(key, conv):
             v = req.get(key)
             return conv(d[key]) if v is None else conv(v)
+        rp = get("repeat_penalty", float)
+        if not rp > 0.0:        # 0 / negative / NaN: clients send 0 for "off"; v / 0 would make the logits inf
+            rp = 1.0
         return cls(
             temperature=get("temperature", float),
             top_k=get("top_k", int),
             top_p=get("top_p", float),
             min_p=get("min_p", float),
-            repeat_penalty=get("repeat_penalty", float),
+            repeat_penalty=rp,
             presence_penalty=float(req.get("presence_penalty", 0.0) or 0.0),
             frequency_penalty=float(req.get("frequency_penalty", 0.0) or 0.0),
             seed=req.get("seed"),

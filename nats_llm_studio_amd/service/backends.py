@@ -389,17 +389,55 @@ class HttpBackend:
         self.requests = 0
 
     def _do(self, method: str, path: str, body: Optional[bytes] = None, timeout: Optional[float] = None):
+        """One HTTP exchange under a TOTAL deadline (the reference's context / http.Client timeout bound the whole
+        request, `nats_llm_studio.go:36`, `:229`): urllib's `timeout` is per socket operation, so a slow-dripping
+        server could run past it. The exchange runs on a daemon thread and the caller waits at most `t`; the
+        thread itself re-arms the socket timeout to what is left before every read, so it ends soon after."""
         import urllib.error
         import urllib.request
         req = urllib.request.Request(self.base + path, data=body, method=method)
         if body is not None:
             req.add_header("Content-Type", "application/json")
         t = self.timeout if timeout is None else min(self.timeout, timeout)
-        try:
-            with urllib.request.urlopen(req, timeout=t) as r:
-                return r.status, r.read()
-        except urllib.error.HTTPError as e:       # non-2xx: body + status, not an error
-            return e.code, e.read()
+        deadline = time.monotonic() + t
+        box = {}
+
+        def read_all(r):
+            sock = getattr(getattr(getattr(r, "fp", None), "raw", None), "_sock", None)
+            parts = []
+            while True:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise TimeoutError("context deadline exceeded")
+                if sock is not None:
+                    try:
+                        sock.settimeout(left)
+                    except OSError:
+                        pass
+                b = r.read(1 << 16)
+                if not b:
+                    return b"".join(parts)
+                parts.append(b)
+
+        def run():
+            try:
+                with urllib.request.urlopen(req, timeout=t) as r:
+                    box["v"] = (r.status, read_all(r))
+            except urllib.error.HTTPError as e:       # non-2xx: body + status, not an error
+                try:
+                    box["v"] = (e.code, read_all(e))
+                except BaseException as e2:
+                    box["e"] = e2
+            except BaseException as e:
+                box["e"] = e
+        th = threading.Thread(target=run, name="nls-http", daemon=True)
+        th.start()
+        th.join(max(0.0, deadline - time.monotonic()))
+        if th.is_alive() or not box:
+            raise TimeoutError("context deadline exceeded")
+        if "e" in box:
+            raise box["e"]
+        return box["v"]
 
     def list_models_raw(self, timeout: Optional[float] = None):
         return self._do("GET", "/api/v0/models", timeout=timeout)

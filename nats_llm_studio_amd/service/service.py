@@ -61,7 +61,7 @@ class Service:
         self.latency = defaultdict(LatencyHistogram)
         self.tracer = Tracer()
         self._lock = threading.Lock()
-        self._unloader = None         # persistent thread of the delete handler's bounded unload
+        self._unloads = {}            # model id -> daemon thread of the delete handler's bounded unload
         self._list_cache = {}         # (registry generation, loaded ids) -> encoded list_models reply
         self._list_sub = None         # the list_models subscription while its replies are native (auto-reply)
         self._list_key = None         # cache key of the body the native responder holds
@@ -93,8 +93,9 @@ class Service:
                 self._list_sub = self.subs[-1]
         if self._list_sub is not None:
             # the registry listing is a cached read: the client's reader thread answers it (no Python on the RTT
-            # path), the body refreshed before every reply this service sends (a pull / delete / chat reply is
-            # followed by a listing that shows it) and every list_refresh_ms (loads, unloads, rescans)
+            # path), the body rebuilt before a reply whose request changed the registry or the loaded set (a pull /
+            # delete / JIT-loading chat reply is followed by a listing that shows it; see respond()) and every
+            # list_refresh_ms on the refresher thread (rescans of MODELS_DIR, loads, unloads)
             self._publish_list_reply()
             self._list_stop.clear()
             self._list_thread = threading.Thread(target=self._list_refresher, name="nls-list-reply", daemon=True)
@@ -117,10 +118,12 @@ class Service:
                 self._list_sub = None
                 sub.set_auto_reply(None)
 
-    def _list_body(self):
-        """(cache key, encoded list_models reply) of the current registry snapshot and loaded set."""
+    def _list_body(self, rescan: bool = True):
+        """(cache key, encoded list_models reply) of the current registry snapshot and loaded set. `rescan`
+        lets the registry re-walk MODELS_DIR when its last scan is stale; reply paths pass False."""
         loaded = tuple(self.backend.loaded_ids())
-        self.registry.refresh()
+        if rescan:
+            self.registry.refresh()
         key = (self.registry.generation, loaded)
         body = self._list_cache.get(key)
         if body is None:
@@ -129,22 +132,38 @@ class Service:
             self._list_cache = {key: body}
         return key, body
 
-    def _publish_list_reply(self):
+    def _publish_list_reply(self, rescan: bool = True):
+        """Install the current listing in the native responder. The snapshot is built and stored under ONE
+        lock, so a refresher snapshot taken before a pull / delete can never overwrite the newer one a reply
+        path installed after it (the last writer always holds the newest registry state)."""
         if self._list_sub is None:
             return
-        try:
-            key, body = self._list_body()
-        except Exception:
-            key, body = None, None      # a registry read that fails goes back to the handler (its error reply)
         with self._list_lock:
             sub = self._list_sub
-            if sub is None or (key is not None and key == self._list_key):
+            if sub is None:
+                return
+            try:
+                key, body = self._list_body(rescan)
+            except Exception:
+                key, body = None, None      # a registry read that fails goes back to the handler (its error reply)
+            if key is not None and key == self._list_key:
                 return
             try:
                 sub.set_auto_reply(body)
                 self._list_key = key
             except Exception:
                 self._list_key = None
+
+    def _listing_stale(self) -> bool:
+        """Cheap check on the reply path: did the loaded set or the registry generation move since the
+        installed body was built? (No directory walk: rescans belong to the refresher thread.)"""
+        k = self._list_key
+        if k is None:
+            return True
+        try:
+            return k[0] != self.registry.generation or k[1] != tuple(self.backend.loaded_ids())
+        except Exception:
+            return True
 
     def _list_refresher(self):
         period = max(0.005, self.cfg.list_refresh_ms / 1e3)
@@ -182,28 +201,47 @@ class Service:
         """The engine unload under the delete handler's context, like `lms unload` under
         exec.CommandContext (`nats_llm_studio.go:87-97`): it runs on the service's one persistent unload
         thread (no thread per request) and a call still running at the deadline is logged and left to
-        finish -- the unload is best effort in the reference too. True when it finished in time."""
+        finish -- the unload is best effort in the reference too. True when it finished in time.
+
+        Each call gets its own daemon thread (like each `lms unload` being its own process): an unload that
+        hangs never queues later deletes behind it and never blocks interpreter exit. While a previous unload
+        of the SAME model is still running, no second one is started (it would only wait on the first)."""
         if deadline is None:
             self.backend.unload(model_id)
             return True
-        if self._unloader is None:
-            from concurrent.futures import ThreadPoolExecutor
-            self._unloader = ThreadPoolExecutor(max_workers=1, thread_name_prefix="nls-unload")
-        fut = self._unloader.submit(self.backend.unload, model_id)
-        try:
-            fut.result(timeout=max(0.0, deadline - time.monotonic()))
-            return True
-        except Exception as e:                    # timeout, or the unload itself failed: logged, not fatal
-            print(f"warning: failed to unload model {model_id}: {e or 'context deadline exceeded'}", flush=True)
-            return False
+        with self._lock:
+            prev = self._unloads.get(model_id)
+            if prev is None or not prev.is_alive():
+                box = {}
 
-    def respond(self, msg, body: bytes):
-        """respondJSON (`nats_llm_studio.go:207-217`): log (not raise) when there is no reply subject."""
+                def run(_m=model_id, _b=box):
+                    try:
+                        self.backend.unload(_m)
+                    except BaseException as e:
+                        _b["e"] = e
+                prev = threading.Thread(target=run, name="nls-unload", daemon=True)
+                prev.box = box
+                self._unloads[model_id] = prev
+                prev.start()
+        prev.join(max(0.0, deadline - time.monotonic()))
+        err = "context deadline exceeded" if prev.is_alive() else prev.box.get("e")
+        if err is not None:                       # timeout, or the unload itself failed: logged, not fatal
+            print(f"warning: failed to unload model {model_id}: {err}", flush=True)
+            return False
+        return True
+
+    def respond(self, msg, body: bytes, changed: bool = False):
+        """respondJSON (`nats_llm_studio.go:207-217`): log (not raise) when there is no reply subject.
+
+        A listing requested after this reply sees what this request changed: handlers that change the
+        registry (pull, delete, sync) pass `changed` and the native listing is rebuilt before the reply goes
+        out; any other reply only compares the installed body's key with the registry generation and the
+        loaded set (a chat's JIT load) -- no directory walk on the chat reply path."""
         if not msg.reply:
             print(f"error responding to NATS message: nats: message does not have a reply", flush=True)
             return
-        if self._list_sub is not None:
-            self._publish_list_reply()       # a listing requested after this reply sees what this request changed
+        if self._list_sub is not None and (changed or self._listing_stale()):
+            self._publish_list_reply(rescan=False)
         try:
             self.client.publish(msg.reply, body)
         except Exception as e:
@@ -278,7 +316,7 @@ class Service:
                     data["load_seconds"] = round(time.time() - t0, 3)
                 except Exception as e:
                     data["load_error"] = str(e)
-        self.respond(msg, envelope.ok(data))
+        self.respond(msg, envelope.ok(data), changed=True)
 
     def on_delete_model(self, msg):
         err = envelope.go_json_error(msg.data, "DeleteModelRequest", {"model_id": "ModelID"})
@@ -290,7 +328,7 @@ class Service:
             self.respond(msg, envelope.error("'model_id' is required"))
             return
         deadline = time.monotonic() + self.cfg.timeout_delete if self.cfg.timeout_delete > 0 else None
-        self.respond(msg, self._delete(mid, deadline))
+        self.respond(msg, self._delete(mid, deadline), changed=True)
 
     def _delete(self, mid: str, deadline: Optional[float]) -> bytes:
         """DeleteModel (`nats_llm_studio.go:99-133`) under the handler's 2-minute context (`:289`): the
@@ -396,7 +434,7 @@ class Service:
             self.respond(msg, envelope.failure(str(e), {"bucket": bucket, "object_name": req["object_name"]}))
             return
         self.registry.scan()          # the `lms import` step of README.md:305-308
-        self.respond(msg, envelope.ok(res))
+        self.respond(msg, envelope.ok(res), changed=True)
 
     def on_metrics(self, msg):
         data = {

@@ -52,6 +52,11 @@ def test_omitted_fields_follow_the_documented_profile(monkeypatch):
     assert S.from_request({"model": "m"}).greedy and S.from_request({"temperature": 0}).greedy
     p = S.from_request({"temperature": 0.9, "top_k": 0, "top_p": 1.0, "min_p": 0, "repeat_penalty": 1.0})
     assert (p.top_k, p.top_p, p.min_p, p.repeat_penalty) == (0, 1.0, 0.0, 1.0)
+    # repeat_penalty 0 ("off" for some clients) or negative is the neutral 1.0, never a division by zero
+    for rp in (0, 0.0, -1.5):
+        p = S.from_request({"temperature": 0.7, "repeat_penalty": rp})
+        assert p.repeat_penalty == 1.0
+    assert S.from_request({"repeat_penalty": 0}).greedy
     monkeypatch.setenv("NLS_SAMPLING_DEFAULTS", "lmstudio-full")
     p = S.from_request({"model": "m"})
     assert (p.temperature, p.top_k, p.repeat_penalty) == (0.8, 40, 1.1) and not p.greedy

@@ -273,6 +273,41 @@ class _FakeLMStudio:
         self.srv.shutdown()
 
 
+def test_http_backend_total_deadline_against_a_dripping_server():
+    """The reference's context bounds the WHOLE request (`nats_llm_studio.go:36`, `:229`): a server that drips
+    one byte every 50 ms (each socket read well inside urllib's per-operation timeout) is cut at the deadline."""
+    import http.server
+    import time as _t
+    from nats_llm_studio_amd.service.backends import HttpBackend
+
+    class Drip(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            self.send_response(200)
+            self.send_header("Content-Length", "1000")
+            self.end_headers()
+            try:
+                for _ in range(1000):
+                    self.wfile.write(b" ")
+                    self.wfile.flush()
+                    _t.sleep(0.05)
+            except OSError:
+                pass
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), Drip)
+    srv.daemon_threads = True
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        be = HttpBackend(f"http://127.0.0.1:{srv.server_address[1]}", timeout=120)
+        t0 = _t.monotonic()
+        with pytest.raises(TimeoutError):
+            be.list_models_raw(timeout=0.6)
+        assert _t.monotonic() - t0 < 2.0
+    finally:
+        srv.shutdown()
+
+
 def test_http_backend_proxy_semantics(tmp_path):
     """backend=http reproduces nats_llm_studio.go:136-179/228-364: raw bodies embedded, status
     NOT checked (404 -> ok:true + http_status 404), payload forwarded verbatim as JSON, a
