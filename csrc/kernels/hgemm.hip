@@ -36,11 +36,13 @@ using nls_dma::glds16;
 using nls_dma::lds_addr;
 using nls_dma::wait_vm_lgkm0;
 
-template <int WM, int BN, int NWV, int NST = 3>
+template <int WM, int BN, int NWV, int NST = 3, int KG = 1>
 struct HG {
-  static constexpr int NT = 64 * NWV;         // threads per workgroup (8 or 16 waves)
+  static constexpr int NT = 64 * NWV;         // threads per workgroup (4, 8 or 16 waves)
   static constexpr int BM = 64 * WM;          // activation rows per workgroup
-  static constexpr int WN = NWV / WM;         // waves along N
+  static constexpr int NWC = NWV / KG;        // waves per K-group (KG 2: waves >= NWC take the second 32-deep
+                                              // half of every K-step; the halves are summed through LDS at the end)
+  static constexpr int WN = NWC / WM;         // waves along N
   static constexpr int NTW = BN / 16 / WN;    // 16-row weight tiles per wave
   static constexpr int MTW = 4;               // 16-row activation tiles per wave
   static constexpr int XS = BM * 128;         // bytes of one activation stage [BM][64] f16
@@ -50,23 +52,31 @@ struct HG {
   static constexpr int NSW = NST == 2 ? 2 : ((NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2);
   static constexpr int NX = BM / 8 / NWV;     // activation DMA instructions per wave per stage
   static constexpr int NW = BN / 8 / NWV;     // weight DMA instructions per wave per stage
-  static_assert(NX >= 1 && NW >= 1 && NTW >= 1, "tile too small for the wave count");
-  static constexpr size_t LDS = (size_t)NSX * XS + (size_t)NSW * WSB;
+  static_assert(NX >= 1 && NW >= 1 && NTW >= 1 && NX * 8 * NWV == BM && NW * 8 * NWV == BN &&
+                NTW * 16 * WN == BN && WN * WM == NWC && (KG == 1 || KG == 2), "tile geometry");
+  static constexpr size_t RING = (size_t)NSX * XS + (size_t)NSW * WSB;
+  // K-group partial sums (KG 2) and the epilogue's scratch reuse the drained ring
+  static_assert(KG == 1 || (size_t)NWC * MTW * NTW * 1024 <= RING, "K-group reduce area");
+  // + rinv[BM] (dense RMSNorm consumer, RinvPre) where it fits (not at BM 256 x BN 256: 160 KiB of rings)
+  static constexpr bool RIN = RING + BM * 4 <= 160 * 1024;
+  static constexpr size_t LDS = RING + (RIN ? BM * 4 : 0);
 };
 
-template <int WM, int BN, int NWV, int NST>
-using HGAcc = f32x4[HG<WM, BN, NWV, NST>::MTW][HG<WM, BN, NWV, NST>::NTW];
+template <int WM, int BN, int NWV, int NST, int KG = 1>
+using HGAcc = f32x4[HG<WM, BN, NWV, NST, KG>::MTW][HG<WM, BN, NWV, NST, KG>::NTW];
 
-// acc += the tile's product over K-steps [kt0, kt1) (64 columns each); LDS is free again on return
-template <int WM, int BN, int NWV, int NST>
+// acc += the tile's product over K-steps [kt0, kt1) (64 columns each); LDS is free again on return. `pre` runs
+// once after the prologue's counted wait, before its barrier (the dense RMSNorm consumer's rinv, RinvPre).
+template <int WM, int BN, int NWV, int NST, int KG, class Pre>
 DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, uint8_t* lds, const int* xm,
-                  HGAcc<WM, BN, NWV, NST>& acc) {
-  typedef HG<WM, BN, NWV, NST> G;
+                  HGAcc<WM, BN, NWV, NST, KG>& acc, Pre&& pre) {
+  typedef HG<WM, BN, NWV, NST, KG> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, NX = G::NX, NW = G::NW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
-  const int wm = wave / WN, wn = wave % WN;
+  const int wl = wave % G::NWC, kg = wave / G::NWC;   // compute layout within the K-group; K-group
+  const int wm = wl / WN, wn = wl % WN;
   const int nq = kt1 - kt0;
   const int M = a.M;
 
@@ -90,7 +100,7 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
   uint8_t* const Wl = lds + G::NSX * G::XS;
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint32_t xl = base + (uint32_t)(NX * wave) * 1024u;
-  const uint32_t wl = base + G::NSX * G::XS + (uint32_t)(NW * wave) * 1024u;
+  const uint32_t wl_lds = base + G::NSX * G::XS + (uint32_t)(NW * wave) * 1024u;
   auto dma_x = [&](int j) __attribute__((always_inline)) {    // K-step j (clamped) -> x slot j % NSX
     const int koff = min(j, nq - 1) * 64;
     const uint32_t so = (uint32_t)(j % G::NSX) * G::XS;
@@ -101,16 +111,17 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
     const int koff = min(j, nq - 1) * 64;
     const uint32_t so = (uint32_t)(j % G::NSW) * G::WSB;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) glds16(wsrc[i] + koff, wl + so + i * 1024);
+    for (int i = 0; i < NW; ++i) glds16(wsrc[i] + koff, wl_lds + so + i * 1024);
   };
 
-  // one K-step (two 32-deep MFMA K-slices): each slice's fragments are requested together (the LDS
-  // latency is exposed once per slice), then its MTW * NTW MFMAs
+  // one K-step (two 32-deep MFMA K-slices; with KG 2 each K-group takes one of them): each slice's fragments
+  // are requested together (the LDS latency is exposed once per slice), then its MTW * NTW MFMAs
   auto step = [&](int j) __attribute__((always_inline)) {
     const uint8_t* xb = lds + (j % G::NSX) * G::XS;
     const uint8_t* wb = Wl + (j % G::NSW) * G::WSB;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      if (KG == 2 && t != kg) continue;
       const int co = ((4 * t + g) ^ (r & 7)) << 4;
       f16x8 A[MTW], B[NTW];
 #pragma unroll
@@ -133,6 +144,7 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
       dma_w(1);
       dma_x(1);
       wait_vm_lgkm0<NX + NW>();                 // step 0 landed (step 1 in flight)
+      pre();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       for (int j = 0; j < nq; ++j) {
@@ -149,6 +161,7 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
       dma_w(0);
       dma_x(0);
       wait_vm_lgkm0<0>();
+      pre();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       for (int j = 0; j < nq; ++j) {
@@ -166,6 +179,7 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
       dma_x(0);
       dma_x(1);
       wait_vm_lgkm0<NX>();                      // W(0), X(0) landed (X(1) in flight)
+      pre();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       for (int j = 0; j < nq; ++j) {
@@ -177,25 +191,42 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
         asm volatile("" ::: "memory");
       }
     }
+  } else {
+    pre();
   }
   wait_vm_lgkm0<0>();                           // drain the clamped tail DMAs before LDS reuse / exit
   __syncthreads();
 }
 
-// epilogue of a finished tile: split-K slab (ks > 1) or the launch's epilogue
-template <int WM, int BN, int NWV, int NST>
+// epilogue of a finished tile: split-K slab (ks > 1) or the launch's epilogue. Only the waves of K-group 0
+// hold results (`act`); every wave of the workgroup calls this (the arg-max / EPI_ADDX reductions barrier).
+// rin: LDS rinv[BM] of a dense RMSNorm consumer (the output row m is scaled by rin[m]), or null.
+template <int WM, int BN, int NWV, int NST, int KG>
 DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
-                 const int* ym, HGAcc<WM, BN, NWV, NST>& acc) {
-  typedef HG<WM, BN, NWV, NST> G;
+                 const int* ym, HGAcc<WM, BN, NWV, NST, KG>& acc, const float* rin) {
+  typedef HG<WM, BN, NWV, NST, KG> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
-  const int wm = wave / WN, wn = wave % WN;
+  const int wl = wave % G::NWC;
+  const bool act = wave < G::NWC;
+  const int wm = wl / WN, wn = wl % WN;
   const int M = a.M;
   // ---- lane holds weight rows rbase + 16j + r and activation rows 16i + 4g + e
   const int rbase = row0 + wn * NTW * 16, mbase = wm * 64;
+  if (rin && act) {             // fold the per-row inverse RMS into the accumulators (every epilogue is linear in them)
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float s = rin[mbase + 16 * i + 4 * g + e];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j][e] *= s;
+      }
+  }
   if (ks > 1) {
+    if (!act) return;
     const int ntot = a.pad;
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
@@ -215,35 +246,85 @@ DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, 
     }
     return;
   }
+  if (a.epi == EPI_ADDX) {
+    // x[b, n] += alpha * acc; hout[b, n] = f16(x); this workgroup's share of sum(x^2) over its BN columns per row
+    // b -> ssq_out[(m0 + b) * ldss + (ycol + row0) / BN] (16 lanes of a row group, then the WN waves via LDS)
+    float* red = reinterpret_cast<float*>(lds);      // [WN][BM] (the ring is drained)
+    if (act) {
+      float ss[MTW][4];
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int row = rbase + 16 * j + r;
+      for (int i = 0; i < MTW; ++i)
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) {
+        for (int e = 0; e < 4; ++e) ss[i][e] = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int b = mbase + 16 * i + 4 * g + e;
-        const float v = acc[i][j][e] * a.alpha;
-        if (a.epi == EPI_ROPE) {
-          // RoPE pair (row, row ^ 1) = lanes r, r ^ 1 (same b)
-          const float pv = __shfl_xor(v, 1, 64);
-          if (b < M && row < S.rows) rope_store1(a, S.ycol + row, a.m0 + b, v, pv);
-          continue;
-        }
-        if (a.epi == EPI_SWIGLU) {
-          // interleaved [g0..g7, u0..u7] per 16 weight rows: the partner row is lane ^ 8 (same b)
-          const float u = __shfl_xor(v, 8, 64);
-          if (r < 8 && b < M && row < S.rows) {
-            const int n = S.ycol + ((row & ~15) >> 1) + (row & 7);
-            reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
+      for (int j = 0; j < NTW; ++j) {
+        const int row = rbase + 16 * j + r;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int b = mbase + 16 * i + 4 * g + e;
+            if (b < M && row < S.rows) {
+              const size_t off = (size_t)b * a.ldy + S.ycol + row;
+              float* p = reinterpret_cast<float*>(a.y) + off;
+              const float v = *p + acc[i][j][e] * a.alpha;
+              *p = v;
+              a.hout[(size_t)b * a.ldh + S.ycol + row] = (act_t)v;
+              ss[i][e] += v * v;
+            }
           }
-          continue;
+      }
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = ss[i][e];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+          if (r == 0) red[wn * G::BM + mbase + 16 * i + 4 * g + e] = v;
         }
-        if (b < M && row < S.rows) {
-          const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
-          if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
-          else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-          else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
+    }
+    __syncthreads();
+    const int tile = (S.ycol + row0) / BN;
+    for (int b = threadIdx.x; b < M; b += G::NT) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WN; ++w) v += red[w * G::BM + b];
+      a.ssq_out[(size_t)(a.m0 + b) * a.ldss + tile] = v;
+    }
+    return;
+  }
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int row = rbase + 16 * j + r;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int b = mbase + 16 * i + 4 * g + e;
+          const float v = acc[i][j][e] * a.alpha;
+          if (a.epi == EPI_ROPE) {
+            // RoPE pair (row, row ^ 1) = lanes r, r ^ 1 (same b)
+            const float pv = __shfl_xor(v, 1, 64);
+            if (b < M && row < S.rows) rope_store1(a, S.ycol + row, a.m0 + b, v, pv);
+            continue;
+          }
+          if (a.epi == EPI_SWIGLU) {
+            // interleaved [g0..g7, u0..u7] per 16 weight rows: the partner row is lane ^ 8 (same b)
+            const float u = __shfl_xor(v, 8, 64);
+            if (r < 8 && b < M && row < S.rows) {
+              const int n = S.ycol + ((row & ~15) >> 1) + (row & 7);
+              reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
+            }
+            continue;
+          }
+          if (b < M && row < S.rows) {
+            const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
+            if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
+            else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
+            else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
+          }
         }
       }
     }
@@ -254,48 +335,91 @@ DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, 
     unsigned long long* red = reinterpret_cast<unsigned long long*>(lds);
     for (int idx = threadIdx.x; idx < G::BM; idx += G::NT) red[idx] = 0ull;
     __syncthreads();
+    if (act) {
 #pragma unroll
-    for (int i = 0; i < MTW; ++i)
+      for (int i = 0; i < MTW; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        unsigned long long k = 0ull;
+        for (int e = 0; e < 4; ++e) {
+          unsigned long long k = 0ull;
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int row = rbase + 16 * j + r;
-          const unsigned long long kj = (row < S.rows) ? argmax_key(acc[i][j][e] * a.alpha, S.ycol + row) : 0ull;
-          k = kj > k ? kj : k;
+          for (int j = 0; j < NTW; ++j) {
+            const int row = rbase + 16 * j + r;
+            const unsigned long long kj = (row < S.rows) ? argmax_key(acc[i][j][e] * a.alpha, S.ycol + row) : 0ull;
+            k = kj > k ? kj : k;
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            const unsigned long long ok = __shfl_xor(k, o, 64);
+            k = ok > k ? ok : k;
+          }
+          if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          const unsigned long long ok = __shfl_xor(k, o, 64);
-          k = ok > k ? ok : k;
-        }
-        if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
-      }
+    }
     __syncthreads();
     for (int idx = threadIdx.x; idx < M; idx += G::NT) atomicMax(a.argmax + idx, red[idx]);
   }
 }
 
-template <int WM, int BN, int NWV, int NST>
+struct NoPre {
+  DEVI void operator()() const {}
+};
+
+template <int WM, int BN, int NWV, int NST, int KG>
 DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
                      const int* xm, const int* ym) {
-  typedef HG<WM, BN, NWV, NST> G;
-  HGAcc<WM, BN, NWV, NST> acc;
+  typedef HG<WM, BN, NWV, NST, KG> G;
+  HGAcc<WM, BN, NWV, NST, KG> acc;
 #pragma unroll
   for (int i = 0; i < G::MTW; ++i)
 #pragma unroll
     for (int j = 0; j < G::NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nkt = S.K >> 6;
-  hg_main<WM, BN, NWV, NST>(S, row0, (nkt * kslice) / ks, (nkt * (kslice + 1)) / ks, a, lds, xm, acc);
-  hg_epi<WM, BN, NWV, NST>(S, row0, kslice, ks, a, ws, lds, ym, acc);
+  const int kt0 = (nkt * kslice) / ks, kt1 = (nkt * (kslice + 1)) / ks;
+  float* rin = nullptr;
+  if constexpr (G::RIN) {
+    if (a.ssq_in && !a.xf) {      // dense RMSNorm consumer: rinv of the block's rows, loads issued ahead of the DMA
+      rin = reinterpret_cast<float*>(lds + G::RING);
+      RinvPre<G::NT, G::BM> rp;
+      rp.issue(a, a.m0, a.M);
+      hg_main<WM, BN, NWV, NST, KG>(S, row0, kt0, kt1, a, lds, xm, acc, [&]() __attribute__((always_inline)) {
+        rp.finish(a, rin, S.K);
+      });
+    } else {
+      hg_main<WM, BN, NWV, NST, KG>(S, row0, kt0, kt1, a, lds, xm, acc, NoPre{});
+    }
+  } else {
+    hg_main<WM, BN, NWV, NST, KG>(S, row0, kt0, kt1, a, lds, xm, acc, NoPre{});
+  }
+  if constexpr (KG == 2) {
+    // K-group 1 hands its partial sums to K-group 0 through the drained ring ([wave][tile][lane] f32x4)
+    constexpr int NACC = G::MTW * G::NTW;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    f32x4* red = reinterpret_cast<f32x4*>(lds);
+    const int wl = wave % G::NWC;
+    if (wave >= G::NWC) {
+#pragma unroll
+      for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NTW; ++j) red[(wl * NACC + i * G::NTW + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (wave < G::NWC) {
+#pragma unroll
+      for (int i = 0; i < G::MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NTW; ++j) acc[i][j] += red[(wl * NACC + i * G::NTW + j) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  hg_epi<WM, BN, NWV, NST, KG>(S, row0, kslice, ks, a, ws, lds, ym, acc, rin);
 }
 
-template <int WM, int BN, int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
-                                                       int nmb) {
+template <int WM, int BN, int NWV, int NST, int KG>
+__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws,
+                                                                          int ntiles, int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
-  constexpr int BM = HG<WM, BN, NWV, NST>::BM;
+  constexpr int BM = HG<WM, BN, NWV, NST, KG>::BM;
   // (tile, m-block, k-slice) with all m-blocks and k-slices of a tile on one XCD
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
   const int kslice = j % ks;
@@ -315,198 +439,40 @@ __global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegLi
   const int* ym = S.ymap ? S.ymap + m0 : nullptr;
   a.m0 = m0;
   if (!xm) a.x += (size_t)m0 * a.ldx;
-  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX || a.epi == EPI_ADDX) ? 4 : 2;
   if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (a.hout) a.hout += (size_t)m0 * a.ldh;
   if (a.argmax) a.argmax += m0;
   a.M = min(BM, mrows - m0);
-  hgemm_tile<WM, BN, NWV, NST>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds, xm, ym);
+  hgemm_tile<WM, BN, NWV, NST, KG>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds, xm, ym);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Stream-K (mode 13): the narrow-N shapes of a decode batch (Llama-3-8B Q|K|V and o at M = 512: 192 / 128 tiles
-// of 128 x 128 for 256 CUs) spread their (tile, K-step) work evenly over a persistent grid. Each XCD owns the weight
-// tiles x, x + 8, ... with all their m-blocks (a weight tile stays in one L2) and cuts that work into equal
-// K-step ranges, one per workgroup of the XCD; a tile split between workgroups is finished by the workgroup that
-// holds its FIRST K-steps (the owner): the others store their fp32 partial accumulators to a slot of `part`
-// (system-scope stores, never left in an L2) and raise a per-workgroup flag carrying the launch generation; the
-// owner adds the partials in K order and runs the launch's epilogue (RoPE / KV append included). An owner whose
-// partner has not delivered within a bounded wait computes that K-range itself (a partner that is not resident --
-// e.g. another process's kernel holds the CUs -- can never hang the owner; a late partial is simply ignored).
-// Generations: workgroup g advances its counter once per launch, and launches of one grid size share a counter set
-// (grids 64 << c, class c), so all workgroups of a launch agree on the generation without a host argument
-// (hipGraph replays stay valid). Launches of one process never overlap (one compute stream).
-#define HG_SK_MAX_WG 1024
-#define HG_SK_CLASSES 5
-__device__ unsigned sk_gen[HG_SK_CLASSES * HG_SK_MAX_WG];
-__device__ unsigned sk_flag[HG_SK_CLASSES * HG_SK_MAX_WG];
-__device__ __forceinline__ int sk_class(int grid) { return grid <= 64 ? 0 : grid <= 128 ? 1 : grid <= 256 ? 2 : grid <= 512 ? 3 : 4; }
-
-struct SkRange {
-  long u0, u1;
-};
-// K-step range of workgroup w of the nw on an XCD that owns U units
-__device__ __forceinline__ SkRange sk_range(long U, int w, int nw) { return SkRange{U * w / nw, U * (w + 1) / nw}; }
-
-template <int WM, int BN, int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, 1) void hgemm_sk_kernel(SegList segs, GemvArgs a0, float* __restrict__ part,
-                                                             int ntiles, int nmb, long max_spins) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
-  typedef HG<WM, BN, NWV, NST> G;
-  constexpr int BM = G::BM, NACC = G::MTW * G::NTW * 4;
-  __shared__ unsigned s_gen;
-  __shared__ int s_ok;
-  const int gid = blockIdx.x, xcd = gid & 7, w = gid >> 3, nw = gridDim.x >> 3;
-  const int tx = ntiles > xcd ? (ntiles - xcd + 7) / 8 : 0;      // weight tiles of this XCD
-  const int nkt = segs.s[0].K >> 6;                              // every segment has the same K (host-checked)
-  const long U = (long)tx * nmb * nkt;
-  unsigned* const gens = sk_gen + sk_class(gridDim.x) * HG_SK_MAX_WG;
-  unsigned* const flags = sk_flag + sk_class(gridDim.x) * HG_SK_MAX_WG;
-  if (threadIdx.x == 0) {
-    const unsigned gen = __hip_atomic_load(gens + gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    __hip_atomic_store(gens + gid, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_gen = gen;
-  }
-  __syncthreads();
-  const unsigned gen = s_gen;
-  const SkRange R = sk_range(U, w, nw);
-  for (long u = R.u0; u < R.u1;) {
-    const long lt = u / nkt;                                     // this XCD's (tile, m-block) unit
-    const int ka = (int)(u % nkt);
-    const int kb = (int)min((long)nkt, ka + (R.u1 - u));
-    u += kb - ka;
-    const int tile = (int)(lt / nmb) * 8 + xcd, mb = (int)(lt % nmb);
-    Seg S = segs.s[0];
-#pragma unroll
-    for (int s = 1; s < 8; ++s)
-      if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
-    GemvArgs a = a0;
-    const int m0 = mb * BM;
-    a.m0 = m0;
-    a.x += (size_t)m0 * a.ldx;
-    const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-    a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-    if (a.argmax) a.argmax += m0;
-    a.M = min(BM, a0.M - m0);
-    const int row0 = (tile - S.tile_begin) * BN;
-    HGAcc<WM, BN, NWV, NST> acc;
-#pragma unroll
-    for (int i = 0; i < G::MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < G::NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    hg_main<WM, BN, NWV, NST>(S, row0, ka, kb, a, hlds, nullptr, acc);
-    if (ka > 0) {
-      // a later piece of the tile: partial -> slot gid ([element][thread], coalesced), then the flag
-      float* slot = part + (size_t)gid * NACC * G::NT;
-#pragma unroll
-      for (int i = 0; i < G::MTW; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NTW; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            __hip_atomic_store((unsigned*)slot + ((i * G::NTW + j) * 4 + e) * G::NT + threadIdx.x,
-                               __float_as_uint(acc[i][j][e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(flags + gid, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      continue;
-    }
-    // the owner: the pieces [kb, nkt) belong to the next workgroups of this XCD, in order
-    int k = kb;
-    for (int ww = w + 1; k < nkt && ww < nw; ++ww) {
-      const SkRange P = sk_range(U, ww, nw);
-      if (P.u1 == P.u0) continue;                                   // an empty range (U < workgroups)
-      const int pe = (int)min((long)nkt, (long)k + (P.u1 - P.u0));   // P.u0 == lt * nkt + k
-      const int pg = ww * 8 + xcd;
-      if (threadIdx.x == 0) {
-        long spins = 0;
-        bool ok;
-        while (!(ok = __hip_atomic_load(flags + pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == gen) &&
-               ++spins < max_spins)
-          __builtin_amdgcn_s_sleep(8);
-        s_ok = ok;
-      }
-      __syncthreads();
-      if (s_ok) {
-        const float* slot = part + (size_t)pg * NACC * G::NT;
-#pragma unroll
-        for (int i = 0; i < G::MTW; ++i)
-#pragma unroll
-          for (int j = 0; j < G::NTW; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              acc[i][j][e] += __uint_as_float(__hip_atomic_load(
-                  (const unsigned*)slot + ((i * G::NTW + j) * 4 + e) * G::NT + threadIdx.x, __ATOMIC_RELAXED,
-                  __HIP_MEMORY_SCOPE_SYSTEM));
-      } else {
-        hg_main<WM, BN, NWV, NST>(S, row0, k, pe, a, hlds, nullptr, acc);   // partner absent: compute it here
-      }
-      __syncthreads();
-      k = pe;
-    }
-    if (k < nkt) hg_main<WM, BN, NWV, NST>(S, row0, k, nkt, a, hlds, nullptr, acc);   // (unreachable: ranges tile U)
-    hg_epi<WM, BN, NWV, NST>(S, row0, 0, 1, a, nullptr, hlds, nullptr, acc);
-    __syncthreads();      // the epilogue's LDS (arg-max) before the next piece's DMA
-  }
-}
-
-// fp32 workspace of a stream-K launch: one BM x 128 partial slot per workgroup
-long sk_part_floats(int wm, int grid) { return (long)grid * 64 * wm * 128; }
-
-// the owner's wait for a partner's partial, in polls of ~0.2 us (nls_sk_set_spins: 0 = always compute it itself)
-static long g_sk_spins = 1L << 14;
-
-template <int WM, int BN, int NWV, int NST>
-int launch_sk_t(const SegList& sl, int ntiles, int grid, float* part, const GemvArgs& a, hipStream_t st) {
-  typedef HG<WM, BN, NWV, NST> G;
-  const int nmb = (a.M + G::BM - 1) / G::BM;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)hgemm_sk_kernel<WM, BN, NWV, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)G::LDS) != hipSuccess)
-      return -1;
-    attr = true;
-  }
-  hipLaunchKernelGGL((hgemm_sk_kernel<WM, BN, NWV, NST>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, part, ntiles, nmb,
-                     g_sk_spins);
-  return (int)hipGetLastError();
-}
-
-// mode 13: wm 2 (128-row activation blocks), 128 weight rows, 8 | 16 waves; grid = workgroups (a multiple
-// of 8, <= HG_SK_MAX_WG); part: sk_part_floats(wm, grid) floats
-int launch_sk(int wm, int waves, const SegList& sl, int ntiles, int grid, float* part, const GemvArgs& a,
-              hipStream_t st) {
-  if (grid < 8 || grid % 8 || grid > HG_SK_MAX_WG) return -1;
-  for (int i = 1; i < sl.nseg; ++i)
-    if (sl.s[i].K != sl.s[0].K) return -1;
-  // wm 4 (256-row blocks) spills 70-130 registers with the owner's fallback main loop: not instantiated
-  if (wm == 2 && waves == 16) return launch_sk_t<2, 128, 16, 3>(sl, ntiles, grid, part, a, st);
-  if (wm == 2 && waves == 8) return launch_sk_t<2, 128, 8, 3>(sl, ntiles, grid, part, a, st);
-  return -1;
-}
-
-template <int WM, int BN, int NWV, int NST>
+template <int WM, int BN, int NWV, int NST, int KG>
 int launch_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  typedef HG<WM, BN, NWV, NST> G;
+  typedef HG<WM, BN, NWV, NST, KG> G;
+  if (a.ssq_in && !a.xf && !G::RIN) return -1;        // no room for the rinv rows
   const int nmb = (a.M + G::BM - 1) / G::BM;
   const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
-    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV, NST, KG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)G::LDS) != hipSuccess)
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV, NST>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles, nmb);
+  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV, NST, KG>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles,
+                     nmb);
   return (int)hipGetLastError();
 }
 
-// bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at
-// wm 4); nst 2: 2-deep rings (64 KiB at wm 2, bn 128: two workgroups per CU); waves: 8 (2 per SIMD, 64 x 16*bn/128 accumulator tile per wave) or 16 (4 per SIMD, half
-// the tile per wave: more waves to cover each other's LDS and barrier waits)
+// modes 4/5/6: bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at
+// wm 4); nst 2: 2-deep rings (64 KiB at wm 2, bn 128: two workgroups per CU); waves: 8 (2 per SIMD, 64 x 16*bn/128
+// accumulator tile per wave) or 16 (4 per SIMD, half the tile per wave: more waves to cover each other's LDS and
+// barrier waits)
 int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
                  const GemvArgs& a, hipStream_t st) {
 #define NLS_HG(W, B, V, S) \
-  if (wm == W && bn == B && waves == V && nst == S) return launch_t<W, B, V, S>(sl, ntiles, ks, ws, a, st);
+  if (wm == W && bn == B && waves == V && nst == S) return launch_t<W, B, V, S, 1>(sl, ntiles, ks, ws, a, st);
   NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
   NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
   NLS_HG(2, 128, 8, 2)
@@ -514,6 +480,26 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
   return -1;
 }
 
-}  // namespace nls_hgemm
+// mode 14: the narrow-N shapes of a decode batch (Llama-3-8B Q|K|V, o and down at M = 256..512: 48 / 32 weight
+// tiles of 128 rows leave most of the 256 CUs idle at 256-row activation blocks, and split-K pays slab traffic plus
+// a reduce pass). 128-row activation blocks x bn = 64 | 96 | 128 weight rows, so Q|K|V (6,144 rows) and o / down
+// (4,096) fill the chip with ONE workgroup per CU and no split-K:
+//   waves 4: one wave per SIMD, each 64 activation rows x bn/2 weight rows (bn 64 | 96 | 128);
+//   waves 8: two K-groups of 4 waves (kg = wave / 4) take the two 32-deep halves of every K-step -- the same
+//            64 x bn/2 register tile per wave and fragment reads per MFMA as 4 waves, with a partner wave on every
+//            SIMD to cover LDS latency -- summed through LDS before the epilogue (bn 64 | 128).
+// The dense RMSNorm consumer (RinvPre) and the EPI_ADDX producer run on every variant.
+int launch_dense14(int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
+                   hipStream_t st) {
+  if (waves == 4) {
+    if (bn == 64) return launch_t<2, 64, 4, 3, 1>(sl, ntiles, ks, ws, a, st);
+    if (bn == 96) return launch_t<2, 96, 4, 3, 1>(sl, ntiles, ks, ws, a, st);
+    if (bn == 128) return launch_t<2, 128, 4, 3, 1>(sl, ntiles, ks, ws, a, st);
+  } else if (waves == 8) {
+    if (bn == 64) return launch_t<2, 64, 8, 3, 2>(sl, ntiles, ks, ws, a, st);
+    if (bn == 128) return launch_t<2, 128, 8, 3, 2>(sl, ntiles, ks, ws, a, st);
+  }
+  return -1;
+}
 
-extern "C" void nls_sk_set_spins(long n) { nls_hgemm::g_sk_spins = n < 0 ? (1L << 14) : n; }
+}  // namespace nls_hgemm

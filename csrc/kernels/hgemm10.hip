@@ -44,7 +44,7 @@ template <int BN>
 struct H10 {
   static constexpr int AB = BN * KT * 2;     // weight half of a K-tile buffer (32 or 16 KiB)
   static constexpr int TB = AB + BM * KT * 2;
-  static constexpr int LDS = 2 * TB;
+  static constexpr int LDS = 2 * TB + BM * 4;  // + rinv[BM] of a dense RMSNorm consumer (RinvPre)
   static constexpr int RTG = BN / 32;        // 16-row weight tiles per wave group (wr)
   static constexpr int NQH = RTG / 2;        // ... per quadrant half (nq)
   static constexpr int NA = BN / 128;        // DMA instructions per lane of a weight unit (B units: 2)
@@ -79,8 +79,8 @@ DEVI int unit_rt(int u, int idx) {           // idx: row-tile slot of the unit
 // ---- epilogue (mode 8's; shared by modes 10 and 11): lane holds weight rows nb + 16i + 4(l >> 4) + e, activation
 // row mb + 16j + (l & 15)
 template <int BN>
-DEVI void h10_epilogue(const f32x4 (&acc)[2 * H10<BN>::NQH][4], const Seg& S, int row0, int kslice, int ks,
-                       const GemvArgs& a, float* ws) {
+DEVI void h10_epilogue(f32x4 (&acc)[2 * H10<BN>::NQH][4], const Seg& S, int row0, int kslice, int ks,
+                       const GemvArgs& a, float* ws, const float* rin) {
   constexpr int NQH = H10<BN>::NQH;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -88,6 +88,14 @@ DEVI void h10_epilogue(const f32x4 (&acc)[2 * H10<BN>::NQH][4], const Seg& S, in
   const int M = a.M;
   const int g4 = 4 * (lane >> 4), r16 = lane & 15;
   const int nb = row0 + wr * (BN / 2), mb = wc * 64;
+  if (rin) {             // dense RMSNorm consumer: activation row m of acc[.][j] scaled by rinv[m]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float sc = rin[mb + 16 * j + r16];
+#pragma unroll
+      for (int i = 0; i < 2 * NQH; ++i) acc[i][j] *= sc;
+    }
+  }
   if (ks > 1 || a.epi == EPI_SLABS) {
 #pragma unroll
     for (int i = 0; i < 2 * NQH; ++i) {
@@ -197,6 +205,10 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   const int nkt = t1 - t0;
   const int M = a.M;
   const act_t* Wd = reinterpret_cast<const act_t*>(S.w);
+  // dense RMSNorm consumer (GemvArgs::ssq_in without xf): the rows' share loads go out ahead of the prologue DMA
+  float* const rin = (a.ssq_in && !a.xf) ? reinterpret_cast<float*>(lds + 2 * TB) : nullptr;
+  RinvPre<512, BM> rp;
+  if (rin) rp.issue(a, a.m0, M);
 
   // ---- DMA: unit u of K-tile T -> buffer T & 1. This wave issues subtiles idx = n * wave + j (j < n; n = 2,
   // or NA for a weight unit) of every unit: row-tile unit_rt(u, idx >> 1), k-step idx & 1. Lane L -> row
@@ -272,6 +284,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     dma(0, 1);
     dma(1, 1);
     wait_vm<C::VM_PRO>();
+    if (rin) rp.finish(a, rin, S.K);
     bar();
     if (wr == 1) bar();
     for (int T = 0; T < nkt; ++T) {
@@ -316,12 +329,14 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       bar();
     }
     if (wr == 0) bar();                         // barrier counts even again
+  } else if (rin) {
+    rp.finish(a, rin, S.K);
   }
   wait_vm<0>();                                 // drain the clamped tail DMAs
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  h10_epilogue<BN>(acc, S, row0, kslice, ks, a, ws);
+  h10_epilogue<BN>(acc, S, row0, kslice, ks, a, ws, rin);
 }
 
 template <int BN>
@@ -371,362 +386,5 @@ int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, con
   return -1;
 }
 
-
-// =============================================================================================================
-// Mode 11: mode 10's schedule with the weight operand streamed as the RAW K-quant tile-blocks (common.h layout)
-// and dequantised ONCE per workgroup into the f16 A image that mode 10 would have DMA'd -- no f16 weight
-// copies (weights stay quantised on the device), 3.5x (Q4_K) / 2.7x (Q6_K) fewer weight bytes
-// through L2 and LDS-DMA per MFMA.
-//   * per K-tile T every wave DMAs (global_load_lds) the raw bytes of ITS row-tiles (BN 256: w and w + 8; BN 128:
-//     w) for chunk c = T % 4 of super-block T / 4 into a 2-slot raw ring -- Q4_K: the lane's 8 nibble bytes (2
-//     dword DMAs) + the 256-B header; Q6_K: the ql piece (1 KiB) + 8 qh bytes + sc + d -- and, one K-tile ahead
-//     of its use, dequantises them (magic-number f16, common.h) into the A image with one ds_write_b128 per
-//     8-value fragment: 2-4 fragments per wave per K-tile instead of mode 10's 4 A-unit DMA instructions;
-//   * issue points (mode 10's U0 / U3 slots are free): Q0(T) act U2(T+1); Q1(T) dequantise K-tile T + 1 (raw
-//     slot (T+1) & 1 -> A image of buffer (T+1) & 1, whose previous contents were last read at Q2(T-1));
-//     Q3(T) act U1(T+2) + raw(T+3) into the raw slot last read at Q1(T). Counted waits: end of Q0 / Q1 leave
-//     {U1(T+1), raw(T+2), U2(T+1)} in flight, Q2 retires U1(T+1), Q3 retires raw(T+2) and U2(T+1) (each
-//     retired >= one phase before its first read, as mode 10);
-//   * LDS: mode 10's two K-tile buffers (128 KiB at BN 256) + 2 raw slots + 2 header slots (Q4_K BN 256:
-//     152 KiB; Q6_K runs at BN 128 only: 128 KiB).
-template <int T>
-struct RawK {
-  static constexpr int RAWB = T == QT_Q4_K ? 512 : 1536;    // raw bytes per row-tile per K-tile
-  static constexpr int HDRB = T == QT_Q4_K ? 256 : 512;     // header bytes per row-tile (Q6_K: sc | d)
-  static constexpr int NDMA = T == QT_Q4_K ? 3 : 5;         // DMA instructions per row-tile per K-tile
-};
-template <int T, int BN>
-struct Q11 {
-  static constexpr int RTS = BN / 16;                       // weight row-tiles per workgroup tile
-  static constexpr int RPW = RTS / 8;                       // ... per wave
-  static constexpr int RING = RTS * RawK<T>::RAWB;
-  static constexpr int HSL = RTS * RawK<T>::HDRB;
-  static constexpr int TB = H10<BN>::TB;
-  static constexpr int LDS = 2 * TB + 2 * RING + 2 * HSL;
-  static constexpr int NR = RPW * RawK<T>::NDMA;           // raw + header DMA instructions per wave per K-tile
-  static_assert(RPW >= 1 && LDS <= 160 * 1024, "mode 11 geometry");
-};
-
-// 4 B per lane global -> LDS (dst = wave-uniform `lds_dst` + 4 * lane), inline asm as glds16
-DEVI void glds4(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-
-// raw bytes of row-tile `gt` (global 16-row tile), K-tile chunk c of super-block sb -> raw / header slots
-template <int T>
-DEVI void q11_dma_rt(const uint8_t* w, int gt, int nsb, int sb, int c, int lane, uint32_t rdst, uint32_t hdst) {
-  const uint8_t* b = w + ((size_t)gt * nsb + sb) * TileBytes<T>::v;
-  if constexpr (T == QT_Q4_K) {
-    const uint8_t* p = b + 256 + (c >> 1) * 1024 + 16 * lane + 8 * (c & 1);
-    glds4(p, rdst);
-    glds4(p + 4, rdst + 256);
-    glds4(b + 4 * lane, hdst);                                  // hdr[16 rows][16 B]
-  } else {   // Q6_K
-    glds16(b + (c >> 1) * 1024 + 16 * lane, rdst);               // QL_n piece: both runs
-    const uint8_t* h = b + 2048 + 16 * lane + 8 * (c >> 1);     // QH words 2n, 2n + 1
-    glds4(h, rdst + 1024);
-    glds4(h + 4, rdst + 1280);
-    glds4(b + 3072 + 4 * lane, hdst);                           // sc[16 rows][16]
-    glds4(b + 3328 + 4 * min(lane, 7), hdst + 256);             // d[16 rows] (f16)
-  }
-}
-
-// raw registers of one row-tile's K-tile (read from the raw / header slots one phase before they are dequantised)
-template <int T>
-struct RawRegs {
-  u32x4 q;        // Q4_K: nibble dwords in q[0], q[1]; Q6_K: the ql piece
-  u32x4 h;        // Q4_K: hdr[r]; Q6_K: sc[r]
-  uint32_t e0, e1;   // Q6_K: qh dwords
-  uint32_t d;        // Q6_K: d[r]
-};
-template <int T>
-DEVI void q11_deq_load(RawRegs<T>& R, const uint8_t* raw, const uint8_t* hdr, int lane) {
-  const int r = lane & 15;
-  if constexpr (T == QT_Q4_K) {
-    R.q[0] = *reinterpret_cast<const uint32_t*>(raw + 4 * lane);
-    R.q[1] = *reinterpret_cast<const uint32_t*>(raw + 256 + 4 * lane);
-    R.h = ld16(hdr + 16 * r);
-  } else {
-    R.q = ld16(raw + 16 * lane);
-    R.e0 = *reinterpret_cast<const uint32_t*>(raw + 1024 + 4 * lane);
-    R.e1 = *reinterpret_cast<const uint32_t*>(raw + 1280 + 4 * lane);
-    R.h = ld16(hdr + 16 * r);
-    R.d = *reinterpret_cast<const uint16_t*>(hdr + 256 + 2 * r);
-  }
-}
-// dequantise (chunk c) into the f16 A image: k-steps 0 / 1 of the K-tile
-template <int T>
-DEVI void q11_deq_store(const RawRegs<T>& R, int c, int lane, uint8_t* a0, uint8_t* a1, int fro) {
-  const int g = lane >> 4;
-  f16x8 f0, f1;
-  if constexpr (T == QT_Q4_K) {
-    const u32x4 h = R.h;
-    const uint32_t w0 = R.q[0], w1 = R.q[1];
-    // get_scale_min_k4 of sub-blocks 2c, 2c + 1 (bytes 0 / 1 of the pairs below)
-    const int sh = 16 * (c & 1);
-    uint32_t scp, mp;
-    if (c < 2) {
-      scp = (h[1] >> sh) & 0x3F3Fu;
-      mp = (h[2] >> sh) & 0x3F3Fu;
-    } else {
-      scp = ((h[3] >> sh) & 0x0F0Fu) | (((h[1] >> sh) >> 2) & 0x3030u);
-      mp = (((h[3] >> sh) >> 4) & 0x0F0Fu) | (((h[2] >> sh) >> 2) & 0x3030u);
-    }
-    const f16x2 k1024 = h2((_Float16)1024.f);
-    const f16x2 d = h2(__builtin_bit_cast(_Float16, (uint16_t)(h[0] & 0xFFFF)));
-    const f16x2 nd = -h2(__builtin_bit_cast(_Float16, (uint16_t)(h[0] >> 16)));
-    const f16x2 a2 = (mag_lo(scp) - k1024) * d, c2 = (mag_lo(mp) - k1024) * nd;
-#if NLS_Q4_FP8CVT
-    f0 = frag8_nib(w0 & 0x0F0F0F0Fu, w1 & 0x0F0F0F0Fu, bcast(&a2, 0), bcast(&c2, 0));
-    f1 = frag8_nib((w0 >> 4) & 0x0F0F0F0Fu, (w1 >> 4) & 0x0F0F0F0Fu, bcast(&a2, 1), bcast(&c2, 1));
-#else
-    f0 = frag8(w0 & 0x0F0F0F0Fu, w1 & 0x0F0F0F0Fu, k1024, bcast(&a2, 0), bcast(&c2, 0));
-    f1 = frag8((w0 >> 4) & 0x0F0F0F0Fu, (w1 >> 4) & 0x0F0F0F0Fu, k1024, bcast(&a2, 1), bcast(&c2, 1));
-#endif
-  } else {   // Q6_K: k-step s of chunk c = K-step t = 2c + s of frag_q6k
-    const u32x4 ql = R.q;
-    const uint32_t h0 = R.e0, h1 = R.e1;
-    const uint32_t v = R.h[c] >> (8 * (g >> 1));               // int8 sc[4c + (g >> 1)], sc[4c + 2 + (g >> 1)]
-    const uint32_t e = ((v & 0xFFu) | ((v >> 8) & 0xFF00u)) ^ 0x8080u;
-    const f16x2 a2 = (mag_lo(e) - h2((_Float16)1152.f)) * h2(__builtin_bit_cast(_Float16, (uint16_t)R.d));
-    const int sh = 4 * (c & 1), hs = 4 * (c & 1);
-    const uint32_t n00 = ((ql[0] >> sh) & 0x0F0F0F0Fu) | (((h0 >> hs) & 0x03030303u) << 4);
-    const uint32_t n01 = ((ql[1] >> sh) & 0x0F0F0F0Fu) | (((h1 >> hs) & 0x03030303u) << 4);
-    const uint32_t n10 = ((ql[2] >> sh) & 0x0F0F0F0Fu) | (((h0 >> (hs + 2)) & 0x03030303u) << 4);
-    const uint32_t n11 = ((ql[3] >> sh) & 0x0F0F0F0Fu) | (((h1 >> (hs + 2)) & 0x03030303u) << 4);
-    f0 = frag8(n00, n01, h2((_Float16)1056.f), bcast(&a2, 0), h2((_Float16)0.f));
-    f1 = frag8(n10, n11, h2((_Float16)1056.f), bcast(&a2, 1), h2((_Float16)0.f));
-  }
-  *reinterpret_cast<f16x8*>(a0 + fro) = f0;
-  *reinterpret_cast<f16x8*>(a1 + fro) = f1;
-}
-
-template <int T, int BN>
-DEVI void q11_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
-  typedef H10<BN> C;
-  typedef Q11<T, BN> Q;
-  constexpr int TB = C::TB, NQH = C::NQH, NR = Q::NR, RPW = Q::RPW;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nkt_all = S.K / KT;
-  const int t0 = (nkt_all * kslice) / ks, t1 = (nkt_all * (kslice + 1)) / ks;
-  const int nkt = t1 - t0;
-  const int M = a.M;
-  const int nsb = S.K >> 8;
-  const int ntile = (S.rows + 15) >> 4, tile0 = row0 >> 4;
-  const int lc = (lane & 3) ^ swz(lane >> 2);
-  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-  const uint32_t rawb = base + 2 * TB, hdrb = rawb + 2 * Q::RING;
-
-  // activation units U1 / U2 exactly as mode 10
-  auto dma = [&](int u, int Tt) __attribute__((always_inline)) {
-    const int Tc = t0 + min(Tt, nkt - 1);
-    const uint32_t buf = base + (uint32_t)(Tt & 1) * TB + (uint32_t)C::AB;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int idx = 2 * wave + j;
-      const int rt = unit_rt<BN>(u, idx >> 1), kstep = idx & 1;
-      const int row = min(16 * rt + (lane >> 2), M - 1);
-      glds16(a.x + (size_t)row * a.ldx + (size_t)Tc * KT + kstep * 32 + lc * 8, buf + (uint32_t)(rt * 2 + kstep) * 1024u);
-    }
-  };
-  // this wave's weight row-tiles (rt = wave + 8 j): raw bytes of K-tile Tt -> raw / header slot Tt & 1
-  auto rawdma = [&](int Tt) __attribute__((always_inline)) {
-    const int Tc = t0 + min(Tt, nkt - 1);
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      const int rt = wave + 8 * j;
-      q11_dma_rt<T>(S.w, min(tile0 + rt, ntile - 1), nsb, Tc >> 2, Tc & 3, lane,
-                    rawb + (uint32_t)(Tt & 1) * Q::RING + (uint32_t)rt * RawK<T>::RAWB,
-                    hdrb + (uint32_t)(Tt & 1) * Q::HSL + (uint32_t)rt * RawK<T>::HDRB);
-    }
-  };
-  const int fro = (lane & 15) * 64 + (((lane >> 4) ^ swz(lane & 15)) << 4);
-  // dequantisation of K-tile Tt (this wave's row-tiles): raw slot Tt & 1 -> registers (one phase early), then
-  // registers -> the A image of buffer Tt & 1, split over two phases (row-tile j = 0 at Q1, j = 1 at Q2)
-  RawRegs<T> RR[RPW];
-  auto deq_load = [&](int Tt) __attribute__((always_inline)) {
-    const uint8_t* rs = lds + 2 * TB + (Tt & 1) * Q::RING;
-    const uint8_t* hs = lds + 2 * TB + 2 * Q::RING + (Tt & 1) * Q::HSL;
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      const int rt = wave + 8 * j;
-      q11_deq_load<T>(RR[j], rs + rt * RawK<T>::RAWB, hs + rt * RawK<T>::HDRB, lane);
-    }
-  };
-  auto deq_store = [&](int Tt, int j) __attribute__((always_inline)) {
-    const int rt = wave + 8 * j;
-    uint8_t* A = lds + (Tt & 1) * TB;
-    q11_deq_store<T>(RR[j], (t0 + Tt) & 3, lane, A + (rt * 2) * 1024, A + (rt * 2 + 1) * 1024, fro);
-  };
-  auto deq = [&](int Tt) __attribute__((always_inline)) {
-    deq_load(Tt);
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) deq_store(Tt, j);
-  };
-
-  f16x8 FA[NQH][2], FB0[2][2], FB1[2][2];
-  auto rdA = [&](int Tt, int nq) __attribute__((always_inline)) {
-    const uint8_t* p = lds + (Tt & 1) * TB + fro;
-#pragma unroll
-    for (int i = 0; i < NQH; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        FA[i][s] = *reinterpret_cast<const f16x8*>(p + ((wr * C::RTG + nq * NQH + i) * 2 + s) * 1024);
-  };
-  auto rdB = [&](f16x8 (&F)[2][2], int Tt, int mh) __attribute__((always_inline)) {
-    const uint8_t* p = lds + (Tt & 1) * TB + C::AB + fro;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) F[i][s] = *reinterpret_cast<const f16x8*>(p + ((wc * 4 + mh * 2 + i) * 2 + s) * 1024);
-  };
-  f32x4 acc[2 * NQH][4];
-#pragma unroll
-  for (int i = 0; i < 2 * NQH; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](int nq, int mh, const f16x8 (&F)[2][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < NQH; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[nq * NQH + i][mh * 2 + j] = mfma16(FA[i][s], F[j][s], acc[nq * NQH + i][mh * 2 + j]);
-  };
-  auto bar = []() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  if (nkt > 0) {
-    // prologue: raw(0), U1(0), U2(0), raw(1); K-tile 0 dequantised; then the steady state's Q3(-1) issues
-    // (U1(1), raw(2)) with U1(0) / U2(0) / raw(1) retired
-    rawdma(0);
-    dma(1, 0);
-    dma(2, 0);
-    rawdma(1);
-    wait_vm<NR + 4>();
-    deq(0);
-    dma(1, 1);
-    rawdma(2);
-    wait_vm<NR + 2>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    if (wr == 1) bar();
-    for (int Tt = 0; Tt < nkt; ++Tt) {
-      // ---- Q0: (nq0, mh0); stage U2(T+1); K-tile T + 1's raw bytes -> registers
-      const bool more = Tt + 1 < nkt;
-      rdA(Tt, 0);
-      rdB(FB0, Tt, 0);
-      dma(2, Tt + 1);
-      if (more) deq_load(Tt + 1);
-      bar();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-      mma(0, 0, FB0);
-      __builtin_amdgcn_s_setprio(0);
-      wait_vm<NR + 4>();
-      bar();
-      // ---- Q1: (nq0, mh1); dequantise row-tile 0 of K-tile T + 1 into the other buffer's A image
-      rdB(FB1, Tt, 1);
-      if (more) deq_store(Tt + 1, 0);
-      bar();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-      mma(0, 1, FB1);
-      __builtin_amdgcn_s_setprio(0);
-      wait_vm<NR + 4>();
-      bar();
-      // ---- Q2: (nq1, mh1); row-tile 1 of K-tile T + 1 (BN 256)
-      rdA(Tt, 1);
-      if constexpr (RPW > 1)
-        if (more) deq_store(Tt + 1, 1);
-      bar();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-      mma(1, 1, FB1);
-      __builtin_amdgcn_s_setprio(0);
-      wait_vm<NR + 2>();
-      bar();
-      // ---- Q3: (nq1, mh0) from registers; stage U1(T+2), raw(T+3)
-      dma(1, Tt + 2);
-      rawdma(Tt + 3);
-      bar();
-      __builtin_amdgcn_s_setprio(1);
-      mma(1, 0, FB0);
-      __builtin_amdgcn_s_setprio(0);
-      wait_vm<NR + 2>();
-      bar();
-    }
-    if (wr == 0) bar();
-  }
-  wait_vm<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  h10_epilogue<BN>(acc, S, row0, kslice, ks, a, ws);
-}
-
-template <int BN>
-__global__ __launch_bounds__(512, 1) void qgemm11_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
-                                                          int nmb) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t q11lds[];
-  const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
-  const int kslice = j % ks;
-  const int mb = (j / ks) % nmb;
-  const int tile = (j / ks / nmb) * 8 + xcd;
-  if (tile >= ntiles) return;
-  const int m0 = mb * BM;
-  Seg S = segs.s[0];
-#pragma unroll
-  for (int s = 1; s < 8; ++s)
-    if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
-  a.m0 = m0;
-  a.x += (size_t)m0 * a.ldx;
-  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-  a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-  if (a.argmax) a.argmax += m0;
-  a.M = min(BM, a.M - m0);
-  const int row0 = (tile - S.tile_begin) * BN;
-  // one weight format per tile (a tile never spans two segments); Q6_K only at BN 128 (LDS budget)
-  if (S.type == QT_Q4_K) {
-    q11_tile<QT_Q4_K, BN>(S, row0, kslice, ks, a, ws, q11lds);
-  } else {
-    if constexpr (BN == 128) q11_tile<QT_Q6_K, BN>(S, row0, kslice, ks, a, ws, q11lds);
-  }
-}
-
-template <int BN>
-int launch_q11_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  constexpr int LDS = BN == 256 ? Q11<QT_Q4_K, 256>::LDS
-                                : (Q11<QT_Q4_K, 128>::LDS > Q11<QT_Q6_K, 128>::LDS ? Q11<QT_Q4_K, 128>::LDS
-                                                                                   : Q11<QT_Q6_K, 128>::LDS);
-  const int nmb = (a.M + BM - 1) / BM;
-  const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)qgemm11_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
-        hipSuccess)
-      return -1;
-    attr = true;
-  }
-  hipLaunchKernelGGL(qgemm11_kernel<BN>, dim3(grid), dim3(512), LDS, st, sl, a, ks, ws, ntiles, nmb);
-  return (int)hipGetLastError();
-}
-
-// mode 11: bn 256 (Q4_K segments only) or 128 (Q4_K / Q6_K)
-int launch_q11(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  for (int i = 0; i < sl.nseg; ++i)
-    if (!(sl.s[i].type == QT_Q4_K || (sl.s[i].type == QT_Q6_K && bn == 128))) return -1;
-  if (bn == 256) return launch_q11_t<256>(sl, ntiles, ks, ws, a, st);
-  if (bn == 128) return launch_q11_t<128>(sl, ntiles, ks, ws, a, st);
-  return -1;
-}
 
 }  // namespace nls_hg10

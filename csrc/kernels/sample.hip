@@ -550,7 +550,144 @@ __global__ __launch_bounds__(NT) void sample_decode_cand_kernel(float* __restric
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Tensor-parallel sampling: per row, the C largest logits of this rank's vocab shard in VOCABULARY order, written as
+// (f32 value bits, global token id) straight into the [2][n][C] int32 source buffer of the candidate all-gather
+// (parallel/comm.py gather_candidates) -- the round-5 graph ran PyTorch's radix top-k + sort + gather + fill + stack
+// here (profiles/tp_graph_nodes_r05.txt). One 256-thread workgroup per row:
+//   * radix select of the k-th largest order-preserving key (k = min(C, valid)): four 8-bit histogram passes over
+//     the row (L2-resident after the first), each bin found by a wave-0 suffix scan; T = that key, need_eq = how many
+//     keys equal to T belong to the top k (the lowest indices first: deterministic, ties never exceed k);
+//   * compaction in index order: each thread owns a contiguous chunk, counts its keys > T and == T, a block
+//     exclusive scan gives every thread its output offset, and it writes its selected entries in order.
+// Shards with fewer than C tokens pad with (-inf, -1), as the host reference does.
+constexpr int TCT = 256;
+
+DEVI uint32_t okey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// exclusive prefix sums over the workgroup of two per-thread counts (TCT threads); returns via refs
+DEVI void block_excl2(int a, int b, int& ea, int& eb, int* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int ia = a, ib = b;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int ta = __shfl_up(ia, o, 64), tb = __shfl_up(ib, o, 64);
+    if (lane >= o) {
+      ia += ta;
+      ib += tb;
+    }
+  }
+  if (lane == 63) {
+    red[w] = ia;
+    red[4 + w] = ib;
+  }
+  __syncthreads();
+  int oa = 0, ob = 0;
+#pragma unroll
+  for (int i = 0; i < TCT / 64; ++i)
+    if (i < w) {
+      oa += red[i];
+      ob += red[4 + i];
+    }
+  ea = oa + ia - a;
+  eb = ob + ib - b;
+}
+
+__global__ __launch_bounds__(TCT) void topc_kernel(const float* __restrict__ logits, long ld, int valid, int C,
+                                                   int vocab_lo, int* __restrict__ out, long plane) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_bin, s_above;
+  __shared__ int red[8];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float* x = logits + (size_t)row * ld;
+  int* ov = out + (size_t)row * C;
+  int* oi = out + plane + (size_t)row * C;
+  const int k = min(C, max(valid, 0));
+  for (int j = k + tid; j < C; j += TCT) {          // padding of a short shard
+    ov[j] = (int)0xFF800000u;
+    oi[j] = -1;
+  }
+  if (k <= 0) return;
+  uint32_t prefix = 0u, mask = 0u;
+  int need = k;                                       // keys still to take at the current prefix
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[tid] = 0u;
+    __syncthreads();
+    for (int i = tid; i < valid; i += TCT) {
+      const uint32_t key = okey(x[i]);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {                                   // wave 0: lane l holds bins 4l..4l+3; suffix sums over lanes
+      const uint32_t h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
+      const uint32_t ls = h0 + h1 + h2 + h3;
+      uint32_t sfx = ls;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_down(sfx, o, 64);
+        if (tid + o < 64) sfx += t;
+      }
+      uint32_t above = sfx - ls;                      // keys in bins above this lane's four
+      const uint32_t hh[4] = {h0, h1, h2, h3};
+#pragma unroll
+      for (int e = 3; e >= 0; --e) {
+        const uint32_t c = above + hh[e];
+        if (above < (uint32_t)need && c >= (uint32_t)need) {
+          s_bin = 4u * tid + e;
+          s_above = above;
+        }
+        above = c;
+      }
+    }
+    __syncthreads();
+    prefix |= s_bin << shift;
+    mask |= 255u << shift;
+    need -= (int)s_above;
+    __syncthreads();                                  // s_bin / hist reused by the next pass
+  }
+  // keys > prefix: k - need of them, all taken; keys == prefix: the first `need` in index order
+  const int chunk = (valid + TCT - 1) / TCT;
+  const int c0 = min(valid, tid * chunk), c1 = min(valid, c0 + chunk);
+  int ngt = 0, neq = 0;
+  for (int i = c0; i < c1; ++i) {
+    const uint32_t key = okey(x[i]);
+    ngt += key > prefix;
+    neq += key == prefix;
+  }
+  int gt, eq;
+  block_excl2(ngt, neq, gt, eq, red);
+  for (int i = c0; i < c1; ++i) {
+    const float v = x[i];
+    const uint32_t key = okey(v);
+    int pos = -1;
+    if (key > prefix) {
+      pos = gt + min(eq, need);
+      ++gt;
+    } else if (key == prefix) {
+      if (eq < need) pos = gt + eq;
+      ++eq;
+    }
+    if (pos >= 0) {
+      ov[pos] = __float_as_int(v);
+      oi[pos] = vocab_lo + i;
+    }
+  }
+}
+
 }  // namespace
+
+// per row r < n: the C largest of logits[r][0, valid) in vocabulary order -> out[0][r][:] (f32 bits), out[1][r][:]
+// (vocab_lo + index); plane = n * C (the offset of the id plane)
+extern "C" int nls_topc(const float* logits, long ld, int n, int valid, int C, int vocab_lo, int* out, void* stream) {
+  if (n < 1 || C < 1 || C > (1 << 16)) return -1;
+  hipLaunchKernelGGL(topc_kernel, dim3(n), dim3(TCT), 0, (hipStream_t)stream, logits, ld, valid, C, vocab_lo, out,
+                     (long)n * C);
+  return (int)hipGetLastError();
+}
 
 extern "C" int nls_sample_decode_cand(void* cand, long ld, int n, int M, const int* ids, long ldi, const void* params,
                                       const void* seeds, const int* pos, const int* ctx_len, int* hist, int hist_stride,

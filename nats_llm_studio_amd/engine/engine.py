@@ -1096,10 +1096,13 @@ class Engine:
                 from ..ops import _lib as _oplib
                 if _oplib._OP_TIMING:    # NLS_OP_TIMING: launches whose completion lagged the previous one's
                     print(f"[tp r{self.rank}] op gaps {_oplib.op_timing(50.0)}", file=sys.stderr, flush=True)
+            words = self.h_err2[k].tolist()
             for h in self.h_err2:
                 h.zero_()
             self._ctrl(_OP_RESET, 0, 0, False, [], 0, None, 0)
             self._oneshot.reset()
+            if len(words) > 3 and words[3] == 2:
+                raise RuntimeError("expert-parallel row exchange: a received row failed its payload checksum")
             raise RuntimeError("tensor-parallel all-reduce timed out waiting for a peer rank")
 
     def _process(self, infl):

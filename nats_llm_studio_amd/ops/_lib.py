@@ -49,15 +49,15 @@ _SIGS = {
                        c_float, c_int, c_void_p, c_int, c_int, c_void_p],
     "nls_prefetch": [c_void_p, c_long, c_int, c_void_p],
     "nls_graph_kernel_names": [c_void_p, c_void_p, c_long],
-    "nls_sk_set_spins": [c_long],
     "nls_epx_bytes": [c_int, c_int],
     "nls_epx_wgs": [],
     "nls_epx_init": [c_void_p, c_int, c_int, c_void_p],
     "nls_epx_run": [c_void_p, c_long, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
-                    c_long, c_void_p],
+                    c_long, c_int, c_void_p],
     "nls_epx_err_clear": [c_void_p, c_int, c_int, c_void_p],
     "nls_epx_err_fetch": [c_void_p, c_int, c_int, c_void_p, c_void_p],
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
+    "nls_xprep": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nls_splitk_add_rmsnorm": [c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int,
                                c_float, c_void_p],
     "nls_rope_kv": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
@@ -96,6 +96,7 @@ _SIGS = {
                              c_int, c_int, c_float, c_void_p, c_long, c_void_p],
     "nls_sample": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "nls_sample_params_size": [],
+    "nls_topc": [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "nls_sample_decode": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                           c_void_p, c_void_p],
     "nls_sample_decode_cand": [c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p,

@@ -152,7 +152,9 @@ class Comm:
             # lossless IPC all-gather of (values | ids) in one launch, rows already in vocabulary order
             self.stats["all_reduce"] += 1
             self.stats["all_reduce_bytes"] += 8 * n * C * self.size
-            src = torch.stack([vals.contiguous().view(torch.int32), idx.contiguous().view(torch.int32)])
+            src = getattr(vals, "_packed", None)       # ops.topc_candidates' [2, n, C] block: gathered as it is
+            if src is None or getattr(idx, "_packed", None) is not src:
+                src = torch.stack([vals.contiguous().view(torch.int32), idx.contiguous().view(torch.int32)])
             dst = torch.empty(2, n, self.size * C, dtype=torch.int32, device=vals.device)
             os_.gather(src, dst)
             return dst[0].view(torch.float32), dst[1]

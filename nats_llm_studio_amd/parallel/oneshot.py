@@ -107,7 +107,7 @@ class OneShotAllReduce:
         are pushed to every peer; the other rows are filled with the peers' -- every rank ends with all n rows."""
         rc = _lib.lib().nls_epx_run(y.data_ptr(), y.stride(0), n, y.shape[1], sel.data_ptr(), per, self.rank,
                                     self.world, self.epeers, self.e_rows, self.egen.data_ptr(), self.err.data_ptr(),
-                                    self.max_spins, _stream(y))
+                                    self.max_spins, int(os.environ.get("NLS_EPX_CHECK", "0") == "1"), _stream(y))
         _lib.check(rc, "nls_epx_run")
 
     def _exchange(self, L, hs, comm, cap: Optional[int] = None):

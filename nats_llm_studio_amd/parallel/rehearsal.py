@@ -106,7 +106,10 @@ def graph_dump_summary(d: str) -> Dict:
                                     if ln.strip() and not ln.startswith("#"))
         out[os.path.basename(f)] = dict(nodes=sum(names.values()), kernels=dict(names.most_common()),
                                         rccl_nodes=sum(c for k, c in names.items()
-                                                       if "nccl" in k.lower() or "rccl" in k.lower()))
+                                                       if "nccl" in k.lower() or "rccl" in k.lower()),
+                                        # PyTorch's own kernels (at::native): none belong in a decode graph
+                                        torch_nodes=sum(c for k, c in names.items()
+                                                        if "at6native" in k or "at::native" in k))
     return out
 
 

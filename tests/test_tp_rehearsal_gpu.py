@@ -8,6 +8,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _epx_checksums(monkeypatch):
+    """Every EP row exchange of these rehearsals self-checks (NLS_EPX_CHECK: per-row payload checksums, a mismatch
+    raises the error word and fails the step), so the first run on real xGMI cannot mix rows silently."""
+    monkeypatch.setenv("NLS_EPX_CHECK", "1")
+
+
 @pytest.fixture(scope="module")
 def models(tmp_path_factory):
     from nats_llm_studio_amd.gguf.synth import write_synthetic_gguf
@@ -34,6 +41,8 @@ def test_tp2_one_gpu_matches_tp1(gpu, models, name, ep, tmp_path):
     assert {f.split("_")[1] for f in dumps} == {"r0", "r1"}, sorted(r["graph_dump"])
     for f, v in dumps.items():
         assert v["nodes"] > 0 and v["rccl_nodes"] == 0, (f, v)
+        # candidate selection, gather and draw are hand-written kernels: no PyTorch kernel in any decode graph
+        assert v["torch_nodes"] == 0, (f, {k: c for k, c in v["kernels"].items() if "native" in k})
     for v in (ref, tp, fol):
         assert "exception" not in v, v
     c = tp["counters"]

@@ -56,8 +56,6 @@ def configs(K, M=1, quant=True):
                     if M >= 128:   # mode 9 (qgemm9.hip): 256 activation rows x 128 / 256 weight rows (8 waves),
                         # 128 weight rows on 4 waves (one per SIMD, 512 registers)
                         c += [(9, 8, 1, ks), (9, 8, 2, ks), (9, 4, 2, ks)]
-                        # mode 11 (hgemm10.hip): mode 10's schedule on the raw tile-blocks, 256 / 128 weight rows
-                        c += [(11, 8, 1, ks), (11, 8, 2, ks)]
         return c
     c = [(0, 8, 1, 1), (0, 4, 1, 1), (0, 8, 2, 1), (0, 4, 2, 1)]
     for waves in (4, 8):
@@ -73,8 +71,9 @@ def dense_configs(K):
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
             + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
-            # mode 13: stream-K over 32 * ks persistent workgroups (hgemm.hip hgemm_sk_kernel)
-            + [(13, wv, 2, ks) for wv in (16, 8) for ks in (4, 8, 16)])
+            # mode 14: 128-row activation blocks x 64 / 96 / 128 weight rows (hgemm.hip launch_dense14)
+            + [(14, wv, rt, ks) for wv, rt in ((4, 2), (4, 3), (4, 4), (8, 2), (8, 4)) for ks in (1, 2)
+               if ks == 1 or nkt // ks >= 4])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
