@@ -36,13 +36,11 @@ using nls_dma::glds16;
 using nls_dma::lds_addr;
 using nls_dma::wait_vm_lgkm0;
 
-template <int WM, int BN, int NWV, int NST = 3, int KG = 1>
+template <int WM, int BN, int NWV, int NST = 3>
 struct HG {
-  static constexpr int NT = 64 * NWV;         // threads per workgroup (4, 8 or 16 waves)
+  static constexpr int NT = 64 * NWV;         // threads per workgroup (8 or 16 waves)
   static constexpr int BM = 64 * WM;          // activation rows per workgroup
-  static constexpr int NWC = NWV / KG;        // waves per K-group (KG 2: waves >= NWC take the second 32-deep
-                                              // half of every K-step; the halves are summed through LDS at the end)
-  static constexpr int WN = NWC / WM;         // waves along N
+  static constexpr int WN = NWV / WM;         // waves along N
   static constexpr int NTW = BN / 16 / WN;    // 16-row weight tiles per wave
   static constexpr int MTW = 4;               // 16-row activation tiles per wave
   static constexpr int XS = BM * 128;         // bytes of one activation stage [BM][64] f16
@@ -52,31 +50,23 @@ struct HG {
   static constexpr int NSW = NST == 2 ? 2 : ((NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2);
   static constexpr int NX = BM / 8 / NWV;     // activation DMA instructions per wave per stage
   static constexpr int NW = BN / 8 / NWV;     // weight DMA instructions per wave per stage
-  static_assert(NX >= 1 && NW >= 1 && NTW >= 1 && NX * 8 * NWV == BM && NW * 8 * NWV == BN &&
-                NTW * 16 * WN == BN && WN * WM == NWC && (KG == 1 || KG == 2), "tile geometry");
-  static constexpr size_t RING = (size_t)NSX * XS + (size_t)NSW * WSB;
-  // K-group partial sums (KG 2) and the epilogue's scratch reuse the drained ring
-  static_assert(KG == 1 || (size_t)NWC * MTW * NTW * 1024 <= RING, "K-group reduce area");
-  // + rinv[BM] (dense RMSNorm consumer, RinvPre) where it fits (not at BM 256 x BN 256: 160 KiB of rings)
-  static constexpr bool RIN = RING + BM * 4 <= 160 * 1024;
-  static constexpr size_t LDS = RING + (RIN ? BM * 4 : 0);
+  static_assert(NX >= 1 && NW >= 1 && NTW >= 1, "tile too small for the wave count");
+  static constexpr size_t LDS = (size_t)NSX * XS + (size_t)NSW * WSB;
 };
 
-template <int WM, int BN, int NWV, int NST, int KG = 1>
-using HGAcc = f32x4[HG<WM, BN, NWV, NST, KG>::MTW][HG<WM, BN, NWV, NST, KG>::NTW];
+template <int WM, int BN, int NWV, int NST>
+using HGAcc = f32x4[HG<WM, BN, NWV, NST>::MTW][HG<WM, BN, NWV, NST>::NTW];
 
-// acc += the tile's product over K-steps [kt0, kt1) (64 columns each); LDS is free again on return. `pre` runs
-// once after the prologue's counted wait, before its barrier (the dense RMSNorm consumer's rinv, RinvPre).
-template <int WM, int BN, int NWV, int NST, int KG, class Pre>
+// acc += the tile's product over K-steps [kt0, kt1) (64 columns each); LDS is free again on return
+template <int WM, int BN, int NWV, int NST>
 DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, uint8_t* lds, const int* xm,
-                  HGAcc<WM, BN, NWV, NST, KG>& acc, Pre&& pre) {
-  typedef HG<WM, BN, NWV, NST, KG> G;
+                  HGAcc<WM, BN, NWV, NST>& acc) {
+  typedef HG<WM, BN, NWV, NST> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, NX = G::NX, NW = G::NW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
-  const int wl = wave % G::NWC, kg = wave / G::NWC;   // compute layout within the K-group; K-group
-  const int wm = wl / WN, wn = wl % WN;
+  const int wm = wave / WN, wn = wave % WN;
   const int nq = kt1 - kt0;
   const int M = a.M;
 
@@ -100,7 +90,7 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
   uint8_t* const Wl = lds + G::NSX * G::XS;
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint32_t xl = base + (uint32_t)(NX * wave) * 1024u;
-  const uint32_t wl_lds = base + G::NSX * G::XS + (uint32_t)(NW * wave) * 1024u;
+  const uint32_t wl = base + G::NSX * G::XS + (uint32_t)(NW * wave) * 1024u;
   auto dma_x = [&](int j) __attribute__((always_inline)) {    // K-step j (clamped) -> x slot j % NSX
     const int koff = min(j, nq - 1) * 64;
     const uint32_t so = (uint32_t)(j % G::NSX) * G::XS;
@@ -111,17 +101,16 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
     const int koff = min(j, nq - 1) * 64;
     const uint32_t so = (uint32_t)(j % G::NSW) * G::WSB;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) glds16(wsrc[i] + koff, wl_lds + so + i * 1024);
+    for (int i = 0; i < NW; ++i) glds16(wsrc[i] + koff, wl + so + i * 1024);
   };
 
-  // one K-step (two 32-deep MFMA K-slices; with KG 2 each K-group takes one of them): each slice's fragments
-  // are requested together (the LDS latency is exposed once per slice), then its MTW * NTW MFMAs
+  // one K-step (two 32-deep MFMA K-slices): each slice's fragments are requested together (the LDS
+  // latency is exposed once per slice), then its MTW * NTW MFMAs
   auto step = [&](int j) __attribute__((always_inline)) {
     const uint8_t* xb = lds + (j % G::NSX) * G::XS;
     const uint8_t* wb = Wl + (j % G::NSW) * G::WSB;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (KG == 2 && t != kg) continue;
       const int co = ((4 * t + g) ^ (r & 7)) << 4;
       f16x8 A[MTW], B[NTW];
 #pragma unroll
@@ -144,7 +133,6 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
       dma_w(1);
       dma_x(1);
       wait_vm_lgkm0<NX + NW>();                 // step 0 landed (step 1 in flight)
-      pre();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       for (int j = 0; j < nq; ++j) {
@@ -161,7 +149,6 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
       dma_w(0);
       dma_x(0);
       wait_vm_lgkm0<0>();
-      pre();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       for (int j = 0; j < nq; ++j) {
@@ -179,7 +166,6 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
       dma_x(0);
       dma_x(1);
       wait_vm_lgkm0<NX>();                      // W(0), X(0) landed (X(1) in flight)
-      pre();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       for (int j = 0; j < nq; ++j) {
@@ -191,42 +177,25 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
         asm volatile("" ::: "memory");
       }
     }
-  } else {
-    pre();
   }
   wait_vm_lgkm0<0>();                           // drain the clamped tail DMAs before LDS reuse / exit
   __syncthreads();
 }
 
-// epilogue of a finished tile: split-K slab (ks > 1) or the launch's epilogue. Only the waves of K-group 0
-// hold results (`act`); every wave of the workgroup calls this (the arg-max / EPI_ADDX reductions barrier).
-// rin: LDS rinv[BM] of a dense RMSNorm consumer (the output row m is scaled by rin[m]), or null.
-template <int WM, int BN, int NWV, int NST, int KG>
+// epilogue of a finished tile: split-K slab (ks > 1) or the launch's epilogue
+template <int WM, int BN, int NWV, int NST>
 DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
-                 const int* ym, HGAcc<WM, BN, NWV, NST, KG>& acc, const float* rin) {
-  typedef HG<WM, BN, NWV, NST, KG> G;
+                 const int* ym, HGAcc<WM, BN, NWV, NST>& acc) {
+  typedef HG<WM, BN, NWV, NST> G;
   constexpr int MTW = G::MTW, NTW = G::NTW, WN = G::WN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
-  const int wl = wave % G::NWC;
-  const bool act = wave < G::NWC;
-  const int wm = wl / WN, wn = wl % WN;
+  const int wm = wave / WN, wn = wave % WN;
   const int M = a.M;
   // ---- lane holds weight rows rbase + 16j + r and activation rows 16i + 4g + e
   const int rbase = row0 + wn * NTW * 16, mbase = wm * 64;
-  if (rin && act) {             // fold the per-row inverse RMS into the accumulators (every epilogue is linear in them)
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float s = rin[mbase + 16 * i + 4 * g + e];
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[i][j][e] *= s;
-      }
-  }
   if (ks > 1) {
-    if (!act) return;
     const int ntot = a.pad;
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
@@ -246,85 +215,35 @@ DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, 
     }
     return;
   }
-  if (a.epi == EPI_ADDX) {
-    // x[b, n] += alpha * acc; hout[b, n] = f16(x); this workgroup's share of sum(x^2) over its BN columns per row
-    // b -> ssq_out[(m0 + b) * ldss + (ycol + row0) / BN] (16 lanes of a row group, then the WN waves via LDS)
-    float* red = reinterpret_cast<float*>(lds);      // [WN][BM] (the ring is drained)
-    if (act) {
-      float ss[MTW][4];
 #pragma unroll
-      for (int i = 0; i < MTW; ++i)
+  for (int j = 0; j < NTW; ++j) {
+    const int row = rbase + 16 * j + r;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ss[i][e] = 0.f;
+    for (int i = 0; i < MTW; ++i) {
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        const int row = rbase + 16 * j + r;
-#pragma unroll
-        for (int i = 0; i < MTW; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int b = mbase + 16 * i + 4 * g + e;
-            if (b < M && row < S.rows) {
-              const size_t off = (size_t)b * a.ldy + S.ycol + row;
-              float* p = reinterpret_cast<float*>(a.y) + off;
-              const float v = *p + acc[i][j][e] * a.alpha;
-              *p = v;
-              a.hout[(size_t)b * a.ldh + S.ycol + row] = (act_t)v;
-              ss[i][e] += v * v;
-            }
-          }
-      }
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = ss[i][e];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-          if (r == 0) red[wn * G::BM + mbase + 16 * i + 4 * g + e] = v;
+      for (int e = 0; e < 4; ++e) {
+        const int b = mbase + 16 * i + 4 * g + e;
+        const float v = acc[i][j][e] * a.alpha;
+        if (a.epi == EPI_ROPE) {
+          // RoPE pair (row, row ^ 1) = lanes r, r ^ 1 (same b)
+          const float pv = __shfl_xor(v, 1, 64);
+          if (b < M && row < S.rows) rope_store1(a, S.ycol + row, a.m0 + b, v, pv);
+          continue;
         }
-    }
-    __syncthreads();
-    const int tile = (S.ycol + row0) / BN;
-    for (int b = threadIdx.x; b < M; b += G::NT) {
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < WN; ++w) v += red[w * G::BM + b];
-      a.ssq_out[(size_t)(a.m0 + b) * a.ldss + tile] = v;
-    }
-    return;
-  }
-  if (act) {
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int row = rbase + 16 * j + r;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int b = mbase + 16 * i + 4 * g + e;
-          const float v = acc[i][j][e] * a.alpha;
-          if (a.epi == EPI_ROPE) {
-            // RoPE pair (row, row ^ 1) = lanes r, r ^ 1 (same b)
-            const float pv = __shfl_xor(v, 1, 64);
-            if (b < M && row < S.rows) rope_store1(a, S.ycol + row, a.m0 + b, v, pv);
-            continue;
+        if (a.epi == EPI_SWIGLU) {
+          // interleaved [g0..g7, u0..u7] per 16 weight rows: the partner row is lane ^ 8 (same b)
+          const float u = __shfl_xor(v, 8, 64);
+          if (r < 8 && b < M && row < S.rows) {
+            const int n = S.ycol + ((row & ~15) >> 1) + (row & 7);
+            reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
           }
-          if (a.epi == EPI_SWIGLU) {
-            // interleaved [g0..g7, u0..u7] per 16 weight rows: the partner row is lane ^ 8 (same b)
-            const float u = __shfl_xor(v, 8, 64);
-            if (r < 8 && b < M && row < S.rows) {
-              const int n = S.ycol + ((row & ~15) >> 1) + (row & 7);
-              reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
-            }
-            continue;
-          }
-          if (b < M && row < S.rows) {
-            const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
-            if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
-            else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
-            else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
-          }
+          continue;
+        }
+        if (b < M && row < S.rows) {
+          const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
+          if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
+          else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
+          else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
         }
       }
     }
@@ -335,91 +254,48 @@ DEVI void hg_epi(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, 
     unsigned long long* red = reinterpret_cast<unsigned long long*>(lds);
     for (int idx = threadIdx.x; idx < G::BM; idx += G::NT) red[idx] = 0ull;
     __syncthreads();
-    if (act) {
 #pragma unroll
-      for (int i = 0; i < MTW; ++i)
+    for (int i = 0; i < MTW; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          unsigned long long k = 0ull;
+      for (int e = 0; e < 4; ++e) {
+        unsigned long long k = 0ull;
 #pragma unroll
-          for (int j = 0; j < NTW; ++j) {
-            const int row = rbase + 16 * j + r;
-            const unsigned long long kj = (row < S.rows) ? argmax_key(acc[i][j][e] * a.alpha, S.ycol + row) : 0ull;
-            k = kj > k ? kj : k;
-          }
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            const unsigned long long ok = __shfl_xor(k, o, 64);
-            k = ok > k ? ok : k;
-          }
-          if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
+        for (int j = 0; j < NTW; ++j) {
+          const int row = rbase + 16 * j + r;
+          const unsigned long long kj = (row < S.rows) ? argmax_key(acc[i][j][e] * a.alpha, S.ycol + row) : 0ull;
+          k = kj > k ? kj : k;
         }
-    }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const unsigned long long ok = __shfl_xor(k, o, 64);
+          k = ok > k ? ok : k;
+        }
+        if (r == 0) atomicMax(red + mbase + 16 * i + 4 * g + e, k);
+      }
     __syncthreads();
     for (int idx = threadIdx.x; idx < M; idx += G::NT) atomicMax(a.argmax + idx, red[idx]);
   }
 }
 
-struct NoPre {
-  DEVI void operator()() const {}
-};
-
-template <int WM, int BN, int NWV, int NST, int KG>
+template <int WM, int BN, int NWV, int NST>
 DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
                      const int* xm, const int* ym) {
-  typedef HG<WM, BN, NWV, NST, KG> G;
-  HGAcc<WM, BN, NWV, NST, KG> acc;
+  typedef HG<WM, BN, NWV, NST> G;
+  HGAcc<WM, BN, NWV, NST> acc;
 #pragma unroll
   for (int i = 0; i < G::MTW; ++i)
 #pragma unroll
     for (int j = 0; j < G::NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nkt = S.K >> 6;
-  const int kt0 = (nkt * kslice) / ks, kt1 = (nkt * (kslice + 1)) / ks;
-  float* rin = nullptr;
-  if constexpr (G::RIN) {
-    if (a.ssq_in && !a.xf) {      // dense RMSNorm consumer: rinv of the block's rows, loads issued ahead of the DMA
-      rin = reinterpret_cast<float*>(lds + G::RING);
-      RinvPre<G::NT, G::BM> rp;
-      rp.issue(a, a.m0, a.M);
-      hg_main<WM, BN, NWV, NST, KG>(S, row0, kt0, kt1, a, lds, xm, acc, [&]() __attribute__((always_inline)) {
-        rp.finish(a, rin, S.K);
-      });
-    } else {
-      hg_main<WM, BN, NWV, NST, KG>(S, row0, kt0, kt1, a, lds, xm, acc, NoPre{});
-    }
-  } else {
-    hg_main<WM, BN, NWV, NST, KG>(S, row0, kt0, kt1, a, lds, xm, acc, NoPre{});
-  }
-  if constexpr (KG == 2) {
-    // K-group 1 hands its partial sums to K-group 0 through the drained ring ([wave][tile][lane] f32x4)
-    constexpr int NACC = G::MTW * G::NTW;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    f32x4* red = reinterpret_cast<f32x4*>(lds);
-    const int wl = wave % G::NWC;
-    if (wave >= G::NWC) {
-#pragma unroll
-      for (int i = 0; i < G::MTW; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NTW; ++j) red[(wl * NACC + i * G::NTW + j) * 64 + lane] = acc[i][j];
-    }
-    __syncthreads();
-    if (wave < G::NWC) {
-#pragma unroll
-      for (int i = 0; i < G::MTW; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NTW; ++j) acc[i][j] += red[(wl * NACC + i * G::NTW + j) * 64 + lane];
-    }
-    __syncthreads();
-  }
-  hg_epi<WM, BN, NWV, NST, KG>(S, row0, kslice, ks, a, ws, lds, ym, acc, rin);
+  hg_main<WM, BN, NWV, NST>(S, row0, (nkt * kslice) / ks, (nkt * (kslice + 1)) / ks, a, lds, xm, acc);
+  hg_epi<WM, BN, NWV, NST>(S, row0, kslice, ks, a, ws, lds, ym, acc);
 }
 
-template <int WM, int BN, int NWV, int NST, int KG>
-__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws,
-                                                                          int ntiles, int nmb) {
+template <int WM, int BN, int NWV, int NST>
+__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+                                                       int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
-  constexpr int BM = HG<WM, BN, NWV, NST, KG>::BM;
+  constexpr int BM = HG<WM, BN, NWV, NST>::BM;
   // (tile, m-block, k-slice) with all m-blocks and k-slices of a tile on one XCD
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
   const int kslice = j % ks;
@@ -439,66 +315,40 @@ __global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegLi
   const int* ym = S.ymap ? S.ymap + m0 : nullptr;
   a.m0 = m0;
   if (!xm) a.x += (size_t)m0 * a.ldx;
-  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX || a.epi == EPI_ADDX) ? 4 : 2;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
   if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-  if (a.hout) a.hout += (size_t)m0 * a.ldh;
   if (a.argmax) a.argmax += m0;
   a.M = min(BM, mrows - m0);
-  hgemm_tile<WM, BN, NWV, NST, KG>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds, xm, ym);
+  hgemm_tile<WM, BN, NWV, NST>(S, (tile - S.tile_begin) * BN, kslice, ks, a, ws, hlds, xm, ym);
 }
 
-template <int WM, int BN, int NWV, int NST, int KG>
+template <int WM, int BN, int NWV, int NST>
 int launch_t(const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
-  typedef HG<WM, BN, NWV, NST, KG> G;
-  if (a.ssq_in && !a.xf && !G::RIN) return -1;        // no room for the rinv rows
+  typedef HG<WM, BN, NWV, NST> G;
   const int nmb = (a.M + G::BM - 1) / G::BM;
   const int grid = ((ntiles + 7) / 8) * 8 * nmb * ks;
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS must be opted into
-    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV, NST, KG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)hgemm_kernel<WM, BN, NWV, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)G::LDS) != hipSuccess)
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV, NST, KG>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles,
-                     nmb);
+  hipLaunchKernelGGL((hgemm_kernel<WM, BN, NWV, NST>), dim3(grid), dim3(G::NT), G::LDS, st, sl, a, ks, ws, ntiles, nmb);
   return (int)hipGetLastError();
 }
 
-// modes 4/5/6: bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at
-// wm 4); nst 2: 2-deep rings (64 KiB at wm 2, bn 128: two workgroups per CU); waves: 8 (2 per SIMD, 64 x 16*bn/128
-// accumulator tile per wave) or 16 (4 per SIMD, half the tile per wave: more waves to cover each other's LDS and
-// barrier waits)
+// bn: weight rows per workgroup (128: 3-deep rings; 256: x 3-deep, W 2-deep, 160 KiB of LDS at
+// wm 4); nst 2: 2-deep rings (64 KiB at wm 2, bn 128: two workgroups per CU); waves: 8 (2 per SIMD, 64 x 16*bn/128 accumulator tile per wave) or 16 (4 per SIMD, half
+// the tile per wave: more waves to cover each other's LDS and barrier waits)
 int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
                  const GemvArgs& a, hipStream_t st) {
 #define NLS_HG(W, B, V, S) \
-  if (wm == W && bn == B && waves == V && nst == S) return launch_t<W, B, V, S, 1>(sl, ntiles, ks, ws, a, st);
+  if (wm == W && bn == B && waves == V && nst == S) return launch_t<W, B, V, S>(sl, ntiles, ks, ws, a, st);
   NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
   NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
   NLS_HG(2, 128, 8, 2)
 #undef NLS_HG
-  return -1;
-}
-
-// mode 14: the narrow-N shapes of a decode batch (Llama-3-8B Q|K|V, o and down at M = 256..512: 48 / 32 weight
-// tiles of 128 rows leave most of the 256 CUs idle at 256-row activation blocks, and split-K pays slab traffic plus
-// a reduce pass). 128-row activation blocks x bn = 64 | 96 | 128 weight rows, so Q|K|V (6,144 rows) and o / down
-// (4,096) fill the chip with ONE workgroup per CU and no split-K:
-//   waves 4: one wave per SIMD, each 64 activation rows x bn/2 weight rows (bn 64 | 96 | 128);
-//   waves 8: two K-groups of 4 waves (kg = wave / 4) take the two 32-deep halves of every K-step -- the same
-//            64 x bn/2 register tile per wave and fragment reads per MFMA as 4 waves, with a partner wave on every
-//            SIMD to cover LDS latency -- summed through LDS before the epilogue (bn 64 | 128).
-// The dense RMSNorm consumer (RinvPre) and the EPI_ADDX producer run on every variant.
-int launch_dense14(int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
-                   hipStream_t st) {
-  if (waves == 4) {
-    if (bn == 64) return launch_t<2, 64, 4, 3, 1>(sl, ntiles, ks, ws, a, st);
-    if (bn == 96) return launch_t<2, 96, 4, 3, 1>(sl, ntiles, ks, ws, a, st);
-    if (bn == 128) return launch_t<2, 128, 4, 3, 1>(sl, ntiles, ks, ws, a, st);
-  } else if (waves == 8) {
-    if (bn == 64) return launch_t<2, 64, 8, 3, 2>(sl, ntiles, ks, ws, a, st);
-    if (bn == 128) return launch_t<2, 128, 8, 3, 2>(sl, ntiles, ks, ws, a, st);
-  }
   return -1;
 }
 

@@ -44,7 +44,7 @@ template <int BN>
 struct H10 {
   static constexpr int AB = BN * KT * 2;     // weight half of a K-tile buffer (32 or 16 KiB)
   static constexpr int TB = AB + BM * KT * 2;
-  static constexpr int LDS = 2 * TB + BM * 4;  // + rinv[BM] of a dense RMSNorm consumer (RinvPre)
+  static constexpr int LDS = 2 * TB;
   static constexpr int RTG = BN / 32;        // 16-row weight tiles per wave group (wr)
   static constexpr int NQH = RTG / 2;        // ... per quadrant half (nq)
   static constexpr int NA = BN / 128;        // DMA instructions per lane of a weight unit (B units: 2)
@@ -79,8 +79,8 @@ DEVI int unit_rt(int u, int idx) {           // idx: row-tile slot of the unit
 // ---- epilogue (mode 8's; shared by modes 10 and 11): lane holds weight rows nb + 16i + 4(l >> 4) + e, activation
 // row mb + 16j + (l & 15)
 template <int BN>
-DEVI void h10_epilogue(f32x4 (&acc)[2 * H10<BN>::NQH][4], const Seg& S, int row0, int kslice, int ks,
-                       const GemvArgs& a, float* ws, const float* rin) {
+DEVI void h10_epilogue(const f32x4 (&acc)[2 * H10<BN>::NQH][4], const Seg& S, int row0, int kslice, int ks,
+                       const GemvArgs& a, float* ws) {
   constexpr int NQH = H10<BN>::NQH;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -88,14 +88,6 @@ DEVI void h10_epilogue(f32x4 (&acc)[2 * H10<BN>::NQH][4], const Seg& S, int row0
   const int M = a.M;
   const int g4 = 4 * (lane >> 4), r16 = lane & 15;
   const int nb = row0 + wr * (BN / 2), mb = wc * 64;
-  if (rin) {             // dense RMSNorm consumer: activation row m of acc[.][j] scaled by rinv[m]
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float sc = rin[mb + 16 * j + r16];
-#pragma unroll
-      for (int i = 0; i < 2 * NQH; ++i) acc[i][j] *= sc;
-    }
-  }
   if (ks > 1 || a.epi == EPI_SLABS) {
 #pragma unroll
     for (int i = 0; i < 2 * NQH; ++i) {
@@ -205,10 +197,6 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   const int nkt = t1 - t0;
   const int M = a.M;
   const act_t* Wd = reinterpret_cast<const act_t*>(S.w);
-  // dense RMSNorm consumer (GemvArgs::ssq_in without xf): the rows' share loads go out ahead of the prologue DMA
-  float* const rin = (a.ssq_in && !a.xf) ? reinterpret_cast<float*>(lds + 2 * TB) : nullptr;
-  RinvPre<512, BM> rp;
-  if (rin) rp.issue(a, a.m0, M);
 
   // ---- DMA: unit u of K-tile T -> buffer T & 1. This wave issues subtiles idx = n * wave + j (j < n; n = 2,
   // or NA for a weight unit) of every unit: row-tile unit_rt(u, idx >> 1), k-step idx & 1. Lane L -> row
@@ -284,7 +272,6 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
     dma(0, 1);
     dma(1, 1);
     wait_vm<C::VM_PRO>();
-    if (rin) rp.finish(a, rin, S.K);
     bar();
     if (wr == 1) bar();
     for (int T = 0; T < nkt; ++T) {
@@ -329,14 +316,12 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
       bar();
     }
     if (wr == 0) bar();                         // barrier counts even again
-  } else if (rin) {
-    rp.finish(a, rin, S.K);
   }
   wait_vm<0>();                                 // drain the clamped tail DMAs
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  h10_epilogue<BN>(acc, S, row0, kslice, ks, a, ws, rin);
+  h10_epilogue<BN>(acc, S, row0, kslice, ks, a, ws);
 }
 
 template <int BN>

@@ -65,25 +65,6 @@ __global__ __launch_bounds__(512) void rmsnorm_kernel(const float* __restrict__ 
   }
 }
 
-// Split-RMSNorm source for the dense large-M path (GemvArgs::ssq_in consumers, RinvPre): row m of the f32 residual
-// x -> xh[m] = f16(x[m]) (the next GEMM's UN-normalised activation operand; its weight copy carries the norm
-// weights) and nss partial sums of squares ssq[m * ldss + j] over the columns [j * D / nss, (j + 1) * D / nss).
-// What an EPI_ADDX GEMM leaves behind, for the rows no GEMM produced (the embedding, a layer-0 input).
-__global__ __launch_bounds__(256) void xprep_kernel(const float* __restrict__ x, long ldx, act_t* __restrict__ xh,
-                                                    long ldh, float* __restrict__ ssq, int ldss, int D, int lps) {
-  const float* xr = x + (size_t)blockIdx.x * ldx;
-  act_t* o = xh + (size_t)blockIdx.x * ldh;
-  typedef act_t act4 __attribute__((ext_vector_type(4)));
-  const int lane = threadIdx.x & 63;
-  for (int c = threadIdx.x; c * 4 < D; c += 256) {     // lps lanes (a power of two <= 64) per share, in one wave
-    const float4 v = *reinterpret_cast<const float4*>(xr + 4 * c);
-    *reinterpret_cast<act4*>(o + 4 * c) = act4{(act_t)v.x, (act_t)v.y, (act_t)v.z, (act_t)v.w};
-    float q = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-    for (int off = 1; off < lps; off <<= 1) q += __shfl_xor(q, off, 64);
-    if ((lane & (lps - 1)) == 0) ssq[(size_t)blockIdx.x * ldss + c / lps] = q;
-  }
-}
-
 // Fused split-K reduce + residual add + RMSNorm (row-parallel projections): the GEMM left
 // ks fp32 partial slabs ws[k][M][D]; x[m] += alpha * sum_k ws[k][m] (fixed order: deterministic),
 // then out[m] = f16(rmsnorm(x[m]) * w). One launch instead of reduce + norm, and x is read once.
@@ -606,16 +587,6 @@ int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, i
   else
     hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, x, ldx, w,
                        (act_t*)out, ldo, D, eps);
-  return (int)hipGetLastError();
-}
-
-// xprep_kernel over M rows of width D into nss shares (D / nss columns each: 4..256, a power of two)
-int nls_xprep(const float* x, long ldx, void* xh, long ldh, float* ssq, int ldss, int nss, int M, int D, void* stream) {
-  if (M < 1 || D % 4 || nss < 1 || D % nss || nss > ldss) return -1;
-  const int cps = D / nss, lps = cps / 4;
-  if (cps % 4 || lps < 1 || lps > 64 || (lps & (lps - 1))) return -1;
-  hipLaunchKernelGGL(xprep_kernel, dim3(M), dim3(256), 0, (hipStream_t)stream, x, ldx, (act_t*)xh, ldh, ssq, ldss, D,
-                     lps);
   return (int)hipGetLastError();
 }
 

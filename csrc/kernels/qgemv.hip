@@ -8,8 +8,6 @@ using namespace nls_gemv;
 namespace nls_hgemm {
 int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntiles, int ks, float* ws,
                  const GemvArgs& a, hipStream_t st);
-int launch_dense14(int bn, int waves, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a,
-                   hipStream_t st);
 }
 namespace nls_hg10 {
 int launch_dense10(int bn, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st);
@@ -57,13 +55,8 @@ struct NlsFuse {
 // mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
 // mode 10: dense f16 GEMM, 256 x 256 tiles, 4 phases per 64-deep K-tile with the two wave groups staggered
 //         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
-// mode 14: dense f16 GEMM for the narrow-N decode shapes (hgemm.hip launch_dense14): 128-row activation blocks x
-//         32 * rt weight rows (rt 2 | 3 | 4 -> 64 | 96 | 128), 4 waves, or 8 waves in two K-groups (rt 2 | 4).
 // (Modes 11-13 -- mode 10 on raw K-quant tiles, mode 9 at 64-row blocks, stream-K -- lost every measured shape in
-//  round 5 and were removed from the build.)
-// Dense modes 4/5/10/14 also run as the CONSUMER of a split RMSNorm (fz->ssq_in without xf: output row m scaled by
-// rinv[m] from the producer's shares, the weights carry the norm weights) and modes 4/5/14 as its PRODUCER
-// (EPI_ADDX: residual add + f16 row + sum-of-squares shares, no split-K).
+//  round 5 and were removed from the build; profiles/streamk_r05.txt, profiles/qgemm11_r05.txt.)
 // mode 9: quantised GEMM on the raw tile-blocks (qgemm9.hip; Q4_K/Q5_K/Q6_K/Q8_0/Q51): 256-row activation
 //         blocks x 16*waves*rt weight rows ((waves, rt) = (4, 2) | (8, 2) | (8, 1)), the mode-8
 //         epilogues, optional split-K.
@@ -75,24 +68,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (!fz) fz = &none;
   const float* xf = fz->xf;
   if (xf && (M > 16 || !fz->nw || (mode != 0 && !(mode == 1 && fz->ssq_in)))) return -1;
-  if (fz->ssq_in && xf && (fz->nss_in < 1 || fz->nss_in > fz->ldss)) return -1;
-  const bool dense_mode = mode == 4 || mode == 5 || mode == 10 || mode == 14;
-  if (fz->ssq_in && !xf) {  // dense RMSNorm consumer (RinvPre): 16-B aligned rows of shares, <= 64 per row
-    if (!dense_mode || fz->nss_in < 4 || fz->nss_in > 64 || fz->nss_in % 4 || fz->ldss % 4 ||
-        fz->nss_in > fz->ldss || ((uintptr_t)fz->ssq_in & 15) || fz->eps <= 0.f)
-      return -1;
-    for (int i = 0; i < nseg; ++i)
-      if (segs[i].xmap || segs[i].ymap || segs[i].mcount) return -1;
-  }
-  if (epi == EPI_ADDX) {    // dense split-RMSNorm producer: residual add into y (f32), f16 row, shares
-    if (!(mode == 4 || mode == 5 || mode == 14) || ks > 1 || nseg != 1 || segs[0].xmap || segs[0].ymap ||
-        segs[0].mcount || argmax || !fz->hout || !fz->ssq_out || fz->onw || fz->xf || segs[0].ycol)
-      return -1;
-    const int bn = mode == 14 ? 32 * rt : (mode == 5 ? 256 : 128);
-    const int nsh = (segs[0].rows + bn - 1) / bn;     // shares per row: what a consumer sums (<= 64)
-    if (fz->ldss < nsh || nsh > 64) return -1;
-  }
-  if (fz->ssq_out && epi != EPI_ADDX) {      // producer of a split RMSNorm: path A residual add, whole tiles of tokens
+  if (fz->ssq_in && (!xf || fz->nss_in < 1 || fz->nss_in > fz->ldss)) return -1;
+  if (fz->ssq_out) {      // producer of a split RMSNorm: path A residual add, whole tiles of tokens
     const int ncols = ((M + 15) / 16) * 16;
     if (mode != 0 || epi != EPI_ADD_F32 || nseg != 1 || segs[0].xmap || segs[0].ymap || segs[0].mcount || argmax ||
         fz->onw || M > 32 || (waves * 64) % ncols || fz->ldss < (segs[0].rows + 16 * rt - 1) / (16 * rt))
@@ -100,7 +77,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A or a dense GEMM without split-K; plain rows,
                            // contiguous Q|K|V segments
-    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10 || mode == 14) && ks <= 1)) || argmax ||
+    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10) && ks <= 1)) || argmax ||
         !fz->pos || !fz->slot ||
         !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 || fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
       return -1;
@@ -125,15 +102,8 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 14 || mode == 7 || mode == 8 || mode == 11 || mode == 12 || mode == 13 ||
-      (mode == 6 && (waves != 8 || rt != 2)))
-    return -1;
-  if (mode == 14) {            // rt 2 | 3 | 4: 64 | 96 | 128 weight rows; 8 waves (two K-groups): rt 2 | 4
-    if (!((waves == 4 && rt >= 2 && rt <= 4) || (waves == 8 && (rt == 2 || rt == 4))) || fz->xf || fz->onw)
-      return -1;
-    for (int i = 0; i < nseg; ++i)
-      if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount) return -1;
-  } else if (mode == 10) {     // rt 1: 256-row weight tiles, rt 2: 128-row
+  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode == 10) {            // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
@@ -164,7 +134,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 14 ? 32 * rt : mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -264,9 +234,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0) {
     if (ks < 1) ks = 1;
     int rc;
-    if (mode == 14)
-      rc = nls_hgemm::launch_dense14(32 * rt, waves, sl, tiles, ks, (float*)ws, a, st);
-    else if (mode == 10)
+    if (mode == 10)
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st, 256);

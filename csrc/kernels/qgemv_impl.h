@@ -26,11 +26,8 @@ namespace nls_gemv {
 // EPI_ARGMAX: fused arg-max keys only, no logits stored (greedy decode)
 // EPI_ROPE: the Q|K|V projection's rows leave the tile rotated (adjacent-pair RoPE, + optional bias)
 //           straight into q (bf16) and the paged K/V cache: no fp32 qkv round trip, no RoPE launch
-// EPI_ADDX: residual add for a dense GEMM (modes 4/14, no split-K) that also leaves the updated row in f16
-//           (hout: the next GEMM's activation operand, un-normalised) and its workgroup's share of sum(x^2) per
-//           row in ssq_out[m * ldss + n_tile] -- the RMSNorm of the next layer input costs no launch (RinvPre)
 enum Epi : int { EPI_F32 = 0, EPI_ACT = 1, EPI_ADD_F32 = 2, EPI_SWIGLU = 3, EPI_SLABS = 4, EPI_ARGMAX = 5,
-                 EPI_ROPE = 6, EPI_ADDX = 7 };
+                 EPI_ROPE = 6 };
 
 struct Seg {
   const uint8_t* w;
@@ -89,39 +86,6 @@ DEVI void ssq_inv(const float* ssq, int ldss, int n, int M, int K, float eps, fl
   }
   __syncthreads();
 }
-
-// Dense consumer of a split RMSNorm (GemvArgs::ssq_in WITHOUT xf; dense modes 4/5/10/14): the GEMM's activation
-// rows are f16(x) -- the UN-normalised residual -- and its f16 weight copy carries the RMSNorm weights folded in
-// (W'[n, k] = W[n, k] * w[k]), so the normalised product is rinv[m] * (x . W'^T) with rinv[m] = 1 / rms(x[m]) from
-// the sum-of-squares shares the producer (an EPI_ADDX GEMM or xprep_kernel) left in ssq_in[m * ldss + j], j < nss_in.
-// issue() loads the block's shares into registers BEFORE the GEMM's DMA prologue (vector-memory ops retire in
-// order, so the prologue's counted wait retires them too and nothing is waited for early); finish() sums them in
-// a fixed order (deterministic) and writes rinv[row] to LDS ahead of the prologue's barrier.
-template <int NT, int BM>
-struct RinvPre {
-  static constexpr int TPR = NT / BM;          // threads per row
-  static constexpr int MAXV = 16 / TPR;        // float4 loads per thread: nss_in <= 64
-  static_assert(TPR >= 1 && TPR <= 16 && (TPR & (TPR - 1)) == 0, "rinv prologue geometry");
-  f32x4 v[MAXV];
-  DEVI void issue(const GemvArgs& a, int m0, int M) {
-    const int row = min((int)threadIdx.x / TPR, M - 1), sub = threadIdx.x % TPR;
-    const f32x4* p = reinterpret_cast<const f32x4*>(a.ssq_in + (size_t)(m0 + row) * a.ldss);
-    const int n4 = a.nss_in >> 2;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int i = c * TPR + sub;
-      v[c] = i < n4 ? p[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  DEVI void finish(const GemvArgs& a, float* rin, int K) {
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) s += (v[c][0] + v[c][1]) + (v[c][2] + v[c][3]);
-#pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) s += __shfl_xor(s, o, 64);
-    if (threadIdx.x % TPR == 0) rin[threadIdx.x / TPR] = rsqrtf(s / (float)K + a.eps);
-  }
-};
 
 // Workgroup ticket: true in exactly one workgroup, the last of `n` to arrive, after which every
 // global store of the others is visible to it (cdna_hip_programming.md Guideline 16: each wave drains

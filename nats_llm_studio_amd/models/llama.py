@@ -69,10 +69,6 @@ _EP_PREFILL = os.environ.get("NLS_EP_PREFILL", "exchange")
 _ROUTER_KERNEL = os.environ.get("NLS_ROUTER_KERNEL", "1") == "1"
 
 
-def _cfgkw(cfg) -> dict:
-    return dict(zip(("mode", "waves", "rt", "ks"), cfg))
-
-
 # device buffers superseded by larger ones; captured hipGraphs may still point at them
 _RETIRED: List[torch.Tensor] = []
 
@@ -147,8 +143,6 @@ class StepBuffers:
     cnt: Optional[torch.Tensor] = None         # int32 tickets of the last-workgroup residual+RMSNorm GEMVs
     ssq: Optional[torch.Tensor] = None         # f32 [pad, ldss] split-RMSNorm partial sums of squares
     ldss: int = 0
-    xh: Optional[torch.Tensor] = None          # f16 [pad, d] un-normalised residual rows (dense large-M path)
-    xss: Optional[torch.Tensor] = None         # f32 [pad, ops.XSS_LD] their sum-of-squares shares
 
 
 class LlamaModel:
@@ -168,14 +162,6 @@ class LlamaModel:
         self.cfg = cfg = ModelConfig.from_gguf(reader.metadata, reader.tensors.keys())
         self.shard = shard
         self.comm = comm
-        # Large-M steps (decode batches >= ops.DENSE_MIN_M rows, prefill chunks) of a single-GPU dense model run
-        # the RMSNorms split between producer and consumer GEMMs (_forward_xnorm): the f16 copies of Q|K|V,
-        # gate|up and the LM head carry their norm weights, the O / down GEMMs leave f16 residual rows plus
-        # sum-of-squares shares in their epilogue and the consumers scale each output row by its inverse RMS -- no
-        # norm launch, no split-K slab pass between the layers. NLS_XNORM=0 keeps separate norm launches.
-        self.xnorm_ok = (shard.size == 1 and not cfg.n_expert and self.device.type == "cuda"
-                         and os.environ.get("NLS_XNORM", "1") == "1")
-        self.xnorm = False          # set once the norm-folded copies exist (expand_dense)
         n = shard.size
         if cfg.n_head % n or cfg.n_kv_head % n:
             raise ValueError(f"TP={n} must divide head counts ({cfg.n_head}/{cfg.n_kv_head})")
@@ -320,9 +306,7 @@ class LlamaModel:
         """Give the dense_matrices() their f16 copies (ops.QWeight.expand_dense) in all-or-nothing
         tiers -- attention/dense FFN/LM head, then (experts=True) the MoE experts -- each only when it
         fits in what is left of `budget_bytes` (None: no limit), so every large-M launch of one kind
-        takes one path. Returns the bytes added (0 if skipped or already expanded). With xnorm_ok the
-        first tier's Q|K|V / gate|up / LM-head copies carry their RMSNorm weights (see _forward_xnorm);
-        each layer's Q|K|V copies share one block (ops.expand_dense_group: one dense segment)."""
+        takes one path. Returns the bytes added (0 if skipped or already expanded)."""
         if self.device.type != "cuda":
             return 0
         added = 0
@@ -333,18 +317,7 @@ class LlamaModel:
                 continue
             if budget_bytes is not None and need > budget_bytes - added:
                 break
-            if not tier:
-                fold = self.xnorm_ok
-                for lw in self.layers:
-                    added += ops.expand_dense_group([sg.w for sg in lw.qkv], lw.attn_norm if fold else None)
-                    added += lw.wo.expand_dense()
-                    if lw.gateup is not None:
-                        added += lw.gateup.expand_dense(lw.ffn_norm if fold else None)
-                        added += lw.down.expand_dense()
-                added += self.lm_head.expand_dense(self.out_norm if fold else None)
-                self.xnorm = fold
-            else:
-                added += sum(w.expand_dense() for w in ws)
+            added += sum(w.expand_dense() for w in ws)
         self.dense_bytes = getattr(self, "dense_bytes", 0) + added
         return added
 
@@ -403,9 +376,6 @@ class LlamaModel:
         if self.shard.size > 1:
             b.part = torch.zeros(pad, cfg.d_model, dtype=torch.float32, device=dev)
         b.cnt = torch.zeros(16, dtype=torch.int32, device=dev)
-        if self.xnorm_ok:
-            b.xh = torch.zeros(pad, cfg.d_model, **act)
-            b.xss = torch.zeros(pad, ops.XSS_LD, **f)
         b.ldss = (cfg.d_model + 15) // 16       # one share per 16-row path-A tile of an O / down GEMV
         b.ssq = torch.zeros(pad * b.ldss, dtype=torch.float32, device=dev)
         b.slot.fill_(-1)
@@ -451,9 +421,6 @@ class LlamaModel:
             # prefill metadata, land under a replaying graph: the 256 x 1K-context fault of this round)
             _RETIRED.append(b.attn_ws)
             b.attn_ws = torch.zeros(need, dtype=torch.float32, device=self.device)
-        if self.xnorm and x.is_cuda and T >= ops.DENSE_MIN_M and b.xh is not None:
-            return self._forward_xnorm(b, kc, vc, T, block_size, n_split, logit_rows, n_logits, qblocks, nqb,
-                                       need_logits)
         fused = self.shard.size == 1            # row-parallel GEMM + residual + next RMSNorm in one pass
         # few-row decode steps: every RMSNorm is folded into the GEMV that consumes it (no norm launches)
         fuse = (T == 1 and x.is_cuda) if self.fuse_norm == "auto" else self.fuse_norm
@@ -573,58 +540,6 @@ class LlamaModel:
                 ops.argmax_reset(b.keys)
             ops.qgemv([Seg(self.lm_head, 0)], b.h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
                       epi="f32" if need_logits else "argmax", norm=nrm(self.out_norm, parts))
-        ops.argmax_unpack(b.keys, n, b.next_ids, rearm=True)
-        b.keys_clean = b.keys.is_cuda
-        return n
-
-    def _forward_xnorm(self, b: StepBuffers, kc, vc, T: int, block_size: int, n_split: int, logit_rows, n_logits,
-                       qblocks, nqb: int, need_logits: bool):
-        """Large-M step with split RMSNorms (dense f16 copies, single GPU, dense FFN): xprep turns the embedding
-        into f16 rows + sum-of-squares shares; per layer Q|K|V (RoPE + KV append epilogue) and gate|up (SwiGLU)
-        run on the un-normalised f16 rows with their norm weights folded into the copies and scale each output
-        row by 1 / rms (ops.qgemv rin=); O and down add into the f32 residual and leave the next f16 rows and
-        shares in their epilogue (ops.qgemv_addx). 4 GEMMs + attention per layer, no norm launch, no split-K
-        reduce pass (the round-5 B=512 step spent 0.59 ms in 64 splitk_add_rmsnorm launches)."""
-        from ..ops import tuning
-        cfg = self.cfg
-        Hq, Hkv, D = self.Hq, self.Hkv, self.D
-        x, xh, xss = b.x, b.xh, b.xss
-        eps = cfg.eps
-        rin = (xss, ops.XSS_LD, ops.xprep(x, xh, xss, T), eps)
-        for L, lw in enumerate(self.layers):
-            ops.qkv_rope_kv(lw.qkv, xh, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
-                            cfg.rope_neox, bias=lw.qkv_bias, cfg=tuning.select_x(lw.qkv, T, "qkv"), rin=rin)
-            if qblocks is not None and nqb > 0 and ops.attention_prefill_ok(Hq, Hkv, D):
-                ops.attention_prefill(b.q, kc[L], vc[L], b.block_tables, qblocks, nqb, b.tok_seq, b.ctx_len, b.ao,
-                                      T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)
-            else:
-                ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
-                              block_size, cfg.attn_softmax_scale, chunk=-_MIN_CHUNK, n_split=n_split,
-                              workspace=b.attn_ws, counters=b.attn_cnt)
-            so = Seg(lw.wo)
-            rin = (xss, ops.XSS_LD, ops.qgemv_addx(so, b.ao, x, xh, xss, T, cfg.residual_scale,
-                                                   tuning.select_x([so], T, "o")), eps)
-            sg = Seg(lw.gateup)
-            ops.qgemv([sg], xh, b.act, T, epi="swiglu", rin=rin, **_cfgkw(tuning.select_x([sg], T, "gateup")))
-            sd = Seg(lw.down)
-            rin = (xss, ops.XSS_LD, ops.qgemv_addx(sd, b.act, x, xh, xss, T, cfg.residual_scale,
-                                                   tuning.select_x([sd], T, "down")), eps)
-        n = T
-        if self.shard.size > 1 or not b.keys_clean:
-            ops.argmax_reset(b.keys)
-        if logit_rows is not None:
-            # a few rows of a prefill chunk: normalise them explicitly, the quantised LM head (its f16 copy is
-            # norm-folded and made for large M)
-            ops.rmsnorm(x, self.out_norm, b.h, T, eps)
-            n = int(n_logits)
-            h = b.h.index_select(0, logit_rows[:n].long())
-            h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
-            ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
-                      epi="f32" if need_logits else "argmax")
-        else:
-            sl = Seg(self.lm_head, 0)
-            ops.qgemv([sl], xh, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
-                      epi="f32" if need_logits else "argmax", rin=rin, **_cfgkw(tuning.select_x([sl], n, "lm_head")))
         ops.argmax_unpack(b.keys, n, b.next_ids, rearm=True)
         b.keys_clean = b.keys.is_cuda
         return n

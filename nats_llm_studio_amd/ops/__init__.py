@@ -20,7 +20,7 @@ from ..gguf.quants import dequantize
 from . import _lib
 from . import transcode
 
-EPI = {"f32": 0, "act": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5, "rope": 6, "addx": 7}
+EPI = {"f32": 0, "act": 1, "add": 2, "swiglu": 3, "slabs": 4, "argmax": 5, "rope": 6}
 import os as _os
 # Path-A row-parallel GEMVs of up to this many rows run the next RMSNorm in their last workgroup.
 # Off by default: measured on MI355X at batch 1 it LENGTHENS the step (2.43 vs 2.25 ms/token) -- the
@@ -163,9 +163,6 @@ class QWeight:
         self._raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1) if self.device.type == "cpu" else None
         self._dense = None
         self.d16: Optional[torch.Tensor] = None    # row-major f16 copy for the large-M GEMM (mode 4)
-        # the copy carries an RMSNorm weight folded in (d16 = W * diag(w)): only the dense RMSNorm consumer
-        # (qgemv(rin=...), un-normalised f16 rows + per-row inverse RMS) may use it
-        self.d16_folded = False
 
     def to_f16(self) -> "QWeight":
         """This matrix re-encoded as tiled F16 (its dequantised values): for a fused launch whose segments
@@ -180,24 +177,13 @@ class QWeight:
         w.d16 = None
         return w
 
-    def expand_dense(self, scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> int:
+    def expand_dense(self) -> int:
         """Keep a dequantised row-major f16 copy next to the quantised tiles (GPU; idempotent).
         Returns the bytes it added. Large-M GEMMs then run on MFMA without in-kernel dequantisation;
-        the copy is the HIP dequant kernel's output, i.e. the very f16 values modes 2/3 feed their MFMAs.
-        `scale` (f32 [K]): fold an RMSNorm weight into the copy (d16 = f16(W * scale), see d16_folded).
-        `out`: a [rows, K] f16 view to write the copy into (expand_dense_group: adjacent matrices in one block)."""
+        the copy is the HIP dequant kernel's output, i.e. the very f16 values modes 2/3 feed their MFMAs."""
         if self.device.type != "cuda" or self.layout != "tiled" or self.d16 is not None:
             return 0
-        if scale is None:
-            d = self.dense(torch.float16)
-        else:
-            d = (self.dense(torch.float32) * scale.float()[None, :]).to(torch.float16)
-            self.d16_folded = True
-        if out is not None:
-            out.copy_(d)
-            self.d16 = out
-        else:
-            self.d16 = d.contiguous()
+        self.d16 = self.dense(torch.float16).contiguous()
         return self.d16.numel() * 2
 
     @property
@@ -266,25 +252,10 @@ def _workspace(dev, n: int) -> torch.Tensor:
     return w
 
 
-def expand_dense_group(ws: Sequence[QWeight], scale: Optional[torch.Tensor] = None) -> int:
-    """f16 copies of matrices that one launch covers (fused Q|K|V) in ONE contiguous block, so the dense GEMM
-    tiles them as a single segment (_seg_arr merges them: no partial tile at each matrix boundary)."""
-    todo = [w for w in ws if w.d16 is None and w.device.type == "cuda" and w.layout == "tiled"]
-    if len(todo) != len(ws) or len({w.K for w in ws}) != 1:
-        return sum(w.expand_dense(scale) for w in ws)
-    blk = torch.empty(sum(w.rows for w in ws), ws[0].K, dtype=torch.float16, device=ws[0].device)
-    r0, added = 0, 0
-    for w in ws:
-        added += w.expand_dense(scale, out=blk[r0:r0 + w.rows])
-        r0 += w.rows
-    return added
-
-
 def dense_ok(segs: Sequence[Seg], M: int) -> bool:
     """May this launch run on the dense f16 GEMM (modes 4-6; the tuning table can still prefer the
-    quantised kernel for the shape)? Never on norm-folded copies: those take the rin= path only."""
-    return M >= DENSE_MIN_M and all(s.w.d16 is not None and not s.w.d16_folded and s.xmap is None
-                                    and s.ymap is None for s in segs)
+    quantised kernel for the shape)?"""
+    return M >= DENSE_MIN_M and all(s.w.d16 is not None and s.xmap is None and s.ymap is None for s in segs)
 
 
 def _contiguous_cols(segs: Sequence[Seg]) -> bool:
@@ -305,36 +276,14 @@ def gemv_config(segs: Sequence[Seg], M: int):
     return tuning.select(segs, M)
 
 
-DENSE_MODES = (4, 5, 6, 10, 14)
-
-
-def _merged_dense(segs: Sequence[Seg]):
-    """Adjacent unmapped segments whose f16 copies are one contiguous block (expand_dense_group) and whose output
-    columns follow each other -> one (ptr, rows, K, ycol) segment; else None."""
-    if len(segs) < 2 or any(s.xmap is not None or s.ymap is not None or s.mcount is not None for s in segs):
-        return None
-    K = segs[0].w.K
-    for a, b in zip(segs, segs[1:]):
-        if (b.w.K != K or b.ycol != a.ycol + a.w.rows
-                or b.w.d16.data_ptr() != a.w.d16.data_ptr() + a.w.rows * K * 2):
-            return None
-    return segs[0].w.d16.data_ptr(), sum(s.w.rows for s in segs), K, segs[0].ycol
-
-
 def _seg_arr(segs: Sequence[Seg], mode: int):
     """ctypes segment list of a launch: modes 4/5 point at the row-major f16 copies (MoE row maps
     included: the dense GEMM gathers/scatters mapped rows like mode 2)."""
-    if mode in DENSE_MODES:
-        if any(s.w.d16 is None for s in segs):
-            raise ValueError(f"{segs[0].w.name}: dense modes {DENSE_MODES} need QWeight.expand_dense()")
-        mg = _merged_dense(segs)
-        if mg is not None:
-            arr = (_lib.NlsSeg * 1)()
-            arr[0] = _lib.NlsSeg(mg[0], None, None, None, 1, mg[1], mg[2], mg[3])
-            return arr
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
-        if mode in DENSE_MODES:
+        if mode in (4, 5, 6, 10):
+            if s.w.d16 is None:
+                raise ValueError(f"{s.w.name}: dense modes (4-6, 10) need QWeight.expand_dense()")
             arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, s.w.rows, s.w.K,
                                  s.ycol)
         else:
@@ -353,12 +302,8 @@ def norm_fusable(M: int, K: int) -> bool:
 
 def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: float = 1.0, epi: str = "f32",
           argmax: Optional[torch.Tensor] = None, waves: int = 0, rt: int = 1, mode: int = -1, ks: int = 1,
-          norm=None, sel=None, rin=None):
+          norm=None, sel=None):
     """y (epilogue) alpha * x[:M] @ W^T for each segment. x: f16 [>=pad16(M), K].
-    rin = (ssq f32 [>=M, ldss], ldss, nss, eps): dense RMSNorm consumer -- x holds UN-normalised rows (f16 of the
-    residual), the segments' f16 copies carry the norm weight (expand_dense(scale)), and output row m is scaled by
-    1 / rms(x[m]) summed from the nss sum-of-squares shares an EPI_ADDX producer (qgemv_addx) or xprep left; the
-    launch config must be a dense mode (4/5/10/14).
     norm = (xf f32 [M, K], w f32 [K], eps[, ssq, ldss, nparts]): the GEMV input is f16(rmsnorm(xf) * w),
     computed inside the kernel (batch <= a few rows; `x` is then ignored on the GPU). With the partial
     sums of squares a qgemv_add_ssq producer left in `ssq`, the kernel skips the reduction pass and the
@@ -424,21 +369,6 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
             raise ValueError(f"qgemv: M={M} rows but x has {x.shape[0]}, y {y.shape[0]}")
         if mode < 0 or waves == 0:
             mode, waves, rt, ks = gemv_config(segs, M) if not mapped else MOE_GEMV
-        folded = any(s.w.d16_folded for s in segs)
-        if rin is not None or (folded and mode in DENSE_MODES):
-            if rin is None or mode not in DENSE_MODES or mapped:
-                raise ValueError(f"{segs[0].w.name}: a norm-folded f16 copy runs only as a dense RMSNorm consumer "
-                                 f"(rin=..., dense mode), got mode {mode}, rin {rin is not None}")
-            ssq, ldss, nss, eps = rin
-            arr = _seg_arr(segs, mode)
-            ws = None
-            if ks > 1:
-                ws = _workspace(x.device, ks * M * sum(s.w.rows for s in segs)).data_ptr()
-            fz = _lib.NlsFuse(ssq_in=ssq.data_ptr(), ldss=int(ldss), nss_in=int(nss), eps=float(eps))
-            _lib.check(L.nls_qgemv_ex(arr, len(arr), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M,
-                                      float(alpha), EPI[epi], _p(argmax), waves, rt, mode, ks, ws, _stream_ptr(x),
-                                      ctypes.byref(fz)), "nls_qgemv_ex(rin)")
-            return y
         if M > 64 and mode == 0:
             # mapped (MoE) rows / path A: chunks of 64 rows
             for m0 in range(0, M, 64):
@@ -451,7 +381,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         if mode != 0 and ks > 1:
             width = segs[0].w.rows if mapped else sum(s.w.rows for s in segs)   # mapped split-K: shared columns
             ws = _workspace(x.device, ks * M * width).data_ptr()
-        rc = L.nls_qgemv(arr, len(arr), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
+        rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
                          EPI[epi], _p(argmax), waves, rt, mode, ks, ws, _stream_ptr(x))
         _lib.check(rc, "nls_qgemv")
         return y
@@ -510,38 +440,6 @@ def qgemv_add_ssq(seg: Seg, xin: torch.Tensor, x: torch.Tensor, M: int, alpha: f
     return None
 
 
-XSS_LD = 64     # row stride (floats) of the split-RMSNorm share buffers of the dense large-M path (<= 64 shares)
-
-
-def qgemv_addx(seg: Seg, xin: torch.Tensor, x: torch.Tensor, xh: torch.Tensor, ssq: torch.Tensor, M: int,
-               alpha: float, cfg) -> int:
-    """Dense split-RMSNorm producer (EPI_ADDX, modes 4/5/14 without split-K): x[:M] += alpha * xin @ W^T (f32
-    residual), xh[:M] = f16(x) (the next dense GEMM's activation rows) and, per row, the workgroups' shares of
-    sum(x^2) in ssq[m * XSS_LD + j]. Returns the number of shares per row (the consumer's nss)."""
-    mode, waves, rt, ks = cfg
-    if mode not in (4, 5, 14) or ks != 1 or seg.ycol or seg.xmap is not None:
-        raise ValueError(f"qgemv_addx: needs an unmapped dense launch without split-K, got {cfg}")
-    bn = 32 * rt if mode == 14 else (256 if mode == 5 else 128)
-    nss = -(-seg.w.rows // bn)
-    if nss > XSS_LD or ssq.stride(0) != XSS_LD or x.shape[0] < M or xh.shape[0] < M:
-        raise ValueError(f"qgemv_addx: {nss} shares per row / buffer shapes")
-    fz = _lib.NlsFuse(hout=xh.data_ptr(), ldh=xh.stride(0), ssq_out=ssq.data_ptr(), ldss=XSS_LD)
-    _lib.check(_lib.lib().nls_qgemv_ex(_seg_arr([seg], mode), 1, xin.data_ptr(), xin.stride(0), x.data_ptr(),
-                                       x.stride(0), M, float(alpha), EPI["addx"], None, waves, rt, mode, 1, None,
-                                       _stream_ptr(x), ctypes.byref(fz)), "nls_qgemv_ex(addx)")
-    return nss
-
-
-def xprep(x: torch.Tensor, xh: torch.Tensor, ssq: torch.Tensor, M: int) -> int:
-    """Split-RMSNorm source rows that no GEMM produced (the embedding output): xh[:M] = f16(x[:M]) and per-row
-    sum-of-squares shares over 64-column chunks (at most XSS_LD per row). Returns the shares per row."""
-    D = x.shape[1]
-    nss = min(XSS_LD, D // 64)
-    _lib.check(_lib.lib().nls_xprep(x.data_ptr(), x.stride(0), xh.data_ptr(), xh.stride(0), ssq.data_ptr(),
-                                    ssq.stride(0), nss, M, D, _stream_ptr(x)), "nls_xprep")
-    return nss
-
-
 def _segs(segs: Sequence[Seg]):
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
@@ -566,12 +464,12 @@ def qgemv_add_rmsnorm(seg: Seg, xin: torch.Tensor, x: torch.Tensor, norm_w: torc
                                                x.stride(0), M, float(alpha), EPI["add"], None, waves, rt, 0, 1, None,
                                                _stream_ptr(x), ctypes.byref(fz)), "nls_qgemv_ex(addnorm)")
             return h
-        if mode not in (0, 13) and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
+        if mode != 0 and ks > 1 and seg.ycol == 0 and seg.w.rows == x.shape[1]:
             L = _lib.lib()
             ws = _workspace(x.device, ks * M * seg.w.rows)
             arr = _seg_arr([seg], mode)
             st = _stream_ptr(x)
-            _lib.check(L.nls_qgemv(arr, len(arr), xin.data_ptr(), xin.stride(0), x.data_ptr(), x.stride(0), M, float(alpha),
+            _lib.check(L.nls_qgemv(arr, 1, xin.data_ptr(), xin.stride(0), x.data_ptr(), x.stride(0), M, float(alpha),
                                    EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
             _lib.check(L.nls_splitk_add_rmsnorm(ws.data_ptr(), ks, M, float(alpha), x.data_ptr(), x.stride(0),
                                                 norm_w.data_ptr(), h.data_ptr(), h.stride(0), x.shape[1], float(eps),
@@ -717,7 +615,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cs: torch.
 def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
                 cs: torch.Tensor, q_out: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, T: int, Hq: int, Hkv: int,
                 D: int, neox: bool = False, cfg=None, bias: Optional[torch.Tensor] = None, norm=None,
-                fuse_rope: bool = True, rin=None):
+                fuse_rope: bool = True):
     """QKV projection + RoPE + paged KV append. A path-A (few-row) launch rotates in the GEMV epilogue
     and writes q / K / V directly (one launch); with a split-K launch config the partial slabs are
     summed inside the RoPE kernel (no separate reduce pass, no fp32 qkv round trip)."""
@@ -746,40 +644,29 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        fin = None
-        if rin is not None:        # dense RMSNorm consumer (un-normalised rows, norm-folded copies)
-            if mode not in DENSE_MODES:
-                raise ValueError(f"qkv_rope_kv(rin=...): dense launch config needed, got {mode}")
-            fin = dict(ssq_in=rin[0].data_ptr(), ldss=int(rin[1]), nss_in=int(rin[2]), eps=float(rin[3]))
-        if (mode in (4, 5, 10, 14) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D
+        if (mode in (4, 5, 10) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D
                 and not neox and fuse_rope and kc.dtype == torch.bfloat16):
             # large-M GEMM on the dense f16 copies with RoPE + KV append in its epilogue (no f32 qkv round trip,
             # no RoPE launch)
             fz = _lib.NlsFuse(pos=pos.data_ptr(), slot=slot.data_ptr(), cs=cs.data_ptr(), bias=_p(bias),
                               q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
-                              Hq=Hq, Hkv=Hkv, D=D, **(fin or {}))
-            arr = _seg_arr(segs, mode)
-            _lib.check(_lib.lib().nls_qgemv_ex(arr, len(arr), h.data_ptr(), h.stride(0), qkv.data_ptr(),
-                                               qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt, mode, 1, None,
-                                               _stream_ptr(h), ctypes.byref(fz)), "nls_qgemv_ex(dense rope)")
+                              Hq=Hq, Hkv=Hkv, D=D)
+            _lib.check(_lib.lib().nls_qgemv_ex(_seg_arr(segs, mode), len(segs), h.data_ptr(), h.stride(0),
+                                               qkv.data_ptr(), qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt,
+                                               mode, 1, None, _stream_ptr(h), ctypes.byref(fz)),
+                       "nls_qgemv_ex(dense rope)")
             return
         if mode != 0 and ks > 1 and contiguous and ncol == (Hq + 2 * Hkv) * D:
             L = _lib.lib()
             ws = _workspace(h.device, ks * T * ncol)
             arr = _seg_arr(segs, mode)
             st = _stream_ptr(h)
-            fz = _lib.NlsFuse(**(fin or {}))
-            _lib.check(L.nls_qgemv_ex(arr, len(arr), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T,
-                                      1.0, EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st, ctypes.byref(fz)),
-                       "nls_qgemv_ex(slabs)")
+            _lib.check(L.nls_qgemv(arr, len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
+                                   EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
             _lib.check(_kv_fn("nls_rope_kv", kc)(ws.data_ptr(), ncol, ks, T * ncol, _p(bias), pos.data_ptr(),
                                                  slot.data_ptr(),
                                      cs.data_ptr(), q_out.data_ptr(), q_out.stride(0), kc.data_ptr(), vc.data_ptr(),
                                      T, Hq, Hkv, D, int(neox), st), "nls_rope_kv")
-            return
-        if rin is not None:
-            qgemv(segs, h, qkv, T, mode=mode, waves=waves, rt=rt, ks=ks, rin=rin)
-            rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox, bias)
             return
     qgemv(segs, h, qkv, T, norm=norm)
     rope_kv(qkv, pos, slot, cs, q_out, kc, vc, T, Hq, Hkv, D, neox, bias)

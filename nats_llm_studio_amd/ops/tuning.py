@@ -53,9 +53,6 @@ def heuristic(segs, M: int):
             return (1, 4, 2, 2) if rows >= 16 * K and K >= 1024 else (1, 4, 2, 1)
         return (0, 4, 2, 1) if len(segs) > 1 else (0, 4, 1, 1)
     if M > 64:
-        # mode 11 (hgemm10.hip's staggered schedule on raw Q4_K / Q6_K tile-blocks) is a tuner candidate only:
-        # it lost every measured Llama-3-8B shape to modes 2 / 9 (LM head M=256: 489 vs 320 us, profiles/
-        # qgemm11_r05.txt)
         if all(int(s.w.type) in (12, 13, 14) for s in segs):
             if M >= 256 and (rows >= 4 * K or K >= 2 * rows):
                 # wide (gate|up, LM head) and down-projection shapes: the quantised GEMM on the raw tile-blocks
@@ -113,32 +110,6 @@ def select_dense(segs, M: int):
     if hit is not None and hit[0] < 0:
         return None
     return hit if hit is not None else dense_heuristic(segs, M)
-
-
-def x_key(segs, M: int, role: str) -> str:
-    return f"x:{role}:{sum(s.w.rows for s in segs)}:{segs[0].w.K}:{_mb(M)}"
-
-
-def select_x(segs, M: int, role: str):
-    """Launch config of a large-M GEMM of the split-RMSNorm path (LlamaModel._forward_xnorm): a dense mode always
-    (the norm-folded copies have no quantised equivalent); o / down are EPI_ADDX producers (modes 4/5/14, no split-K,
-    <= 64 column tiles). Table entries "x:<role>:<rows>:<K>:<Mbucket>" (tools/dense_tune.py --xnorm), else:
-    M <= 512 -- the narrow-N mode-14 tiles that put one workgroup on every CU (Q|K|V 128 x 96, o / down 128 x 64 in
-    two K-groups); larger M and the wide shapes -- the dense table / heuristic."""
-    hit = table().get(x_key(segs, M, role))
-    if hit is not None:
-        return tuple(hit)
-    rows, K = sum(s.w.rows for s in segs), segs[0].w.K
-    if role in ("o", "down"):
-        if M <= 512:
-            return (14, 8, 2, 1) if rows <= 64 * 64 else (14, 8, 4, 1)
-        return (4, 8, 4, 1)          # 256 x 128 tiles
-    if role == "qkv" and M <= 512:
-        return (14, 4, 3, 1) if rows % 96 == 0 else (14, 8, 4, 1)
-    cfg = table().get(dense_key(segs, M))
-    if cfg is None or cfg[0] not in (4, 5, 10, 14):
-        cfg = dense_heuristic(segs, M)
-    return tuple(cfg)
 
 
 # Llama-3-8B Q4_K_M shapes per projection role: the tuned entries an untuned shape of the same role borrows at

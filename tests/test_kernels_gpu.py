@@ -785,11 +785,11 @@ def test_qkv_rope_kv_fused(gpu, cfg, M, bias):
 
 
 @pytest.mark.parametrize("cfg", [(4, 16, 2, 1), (4, 16, 4, 1), (5, 8, 4, 1), (10, 8, 1, 1), (10, 8, 1, 2), (10, 8, 2, 1),
-                                 (14, 4, 3, 1), (14, 8, 4, 1), (14, 4, 2, 2)])
+                                 ])
 @pytest.mark.parametrize("M", [70, 300, 520])
 @pytest.mark.parametrize("bias", [False, True])
 def test_qkv_rope_kv_dense(gpu, cfg, M, bias):
-    """The dense GEMMs on the weights' f16 copies (modes 4/5/10/14) with the RoPE + KV-append epilogue (split-K 1:
+    """The dense GEMMs on the weights' f16 copies (modes 4/5/10) with the RoPE + KV-append epilogue (split-K 1:
     lane pairs rotated in registers; split-K 2: slabs summed by the RoPE kernel)."""
     _qkv_rope_case(gpu, cfg, M, bias, dense=True)
 
@@ -985,157 +985,6 @@ def test_hgemm_dense(gpu, t, M, mode, wm, ks, wv):
     y3 = torch.zeros(pad, rows, device=gpu)
     ops.qgemv([ops.Seg(w)], x, y3, M, mode=2, waves=8, rt=wm, ks=1)
     _close(y3[:M], y[:M], 1e-3)
-
-
-@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
-@pytest.mark.parametrize("M", [65, 300, 520])
-@pytest.mark.parametrize("wv,rt,ks", [(4, 2, 1), (4, 3, 1), (4, 4, 1), (8, 2, 1), (8, 4, 1), (4, 3, 2), (8, 2, 3)])
-def test_hgemm14_dense(gpu, t, M, wv, rt, ks):
-    """Mode 14 (hgemm.hip launch_dense14: 128-row activation blocks x 64 / 96 / 128 weight rows; 8 waves = two
-    K-groups summed through LDS): partial last weight tile (264 rows), partial activation blocks, split-K slabs;
-    f32 store with arg-max keys, residual add with alpha -- against the fp32 torch reference."""
-    rows, K = 264, 768
-    w, Wd = _qw(rows, K, t, gpu)
-    w.expand_dense()
-    x = _x(M, K, gpu)
-    pad = x.shape[0]
-    y = torch.zeros(pad, rows, device=gpu)
-    keys = torch.zeros(pad, dtype=torch.int64, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, mode=14, waves=wv, rt=rt, ks=ks, argmax=keys if ks == 1 else None)
-    ref = x[:M].float().cpu() @ Wd.t()
-    _close(y[:M], ref)
-    if M < pad:
-        assert float(y[M:].abs().max().cpu()) == 0.0
-    if ks == 1:
-        ids = torch.zeros(pad, dtype=torch.int32, device=gpu)
-        ops.argmax_unpack(keys, M, ids)
-        assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
-    base = torch.randn(pad, rows, device=gpu)
-    y2 = base.clone()
-    ops.qgemv([ops.Seg(w)], x, y2, M, alpha=0.5, epi="add", mode=14, waves=wv, rt=rt, ks=ks)
-    _close(y2[:M], base[:M].cpu() + 0.5 * ref)
-
-
-@pytest.mark.parametrize("wv,rt", [(4, 2), (4, 3), (8, 2), (8, 4)])
-def test_hgemm14_swiglu(gpu, wv, rt):
-    """Mode 14 SwiGLU epilogue on interleaved gate/up rows (16-row groups inside 64 / 96 / 128-row tiles)."""
-    K, F = 512, 384
-    rng = np.random.default_rng(19)
-    g_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
-    u_raw = Q.random_blocks(GGMLType.Q4_K, F * K, 0.05, rng)
-    w = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, K), GGMLType.Q4_K, 2 * F, K, gpu)
-    w.expand_dense()
-    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, K)))
-    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, K)))
-    M = 333
-    x = _x(M, K, gpu)
-    y = torch.zeros(x.shape[0], F, dtype=ops.ACT_DTYPE, device=gpu)
-    ops.qgemv([ops.Seg(w)], x, y, M, alpha=0.75, epi="swiglu", mode=14, waves=wv, rt=rt, ks=1)
-    xf = x[:M].float().cpu()
-    _close(y[:M], torch.nn.functional.silu(0.75 * xf @ G.t()) * (0.75 * xf @ U.t()), 3e-2)
-
-
-def _rms_ref(x, w, eps=1e-5):
-    return x * torch.rsqrt(x.pow(2).mean(1, keepdim=True) + eps) * w
-
-
-@pytest.mark.parametrize("M", [100, 256, 520])
-@pytest.mark.parametrize("pcfg", [(14, 8, 2, 1), (14, 4, 2, 1), (14, 8, 4, 1), (4, 8, 4, 1), (4, 16, 2, 1)])
-def test_dense_split_rmsnorm_chain(gpu, M, pcfg):
-    """The split-RMSNorm chain of LlamaModel._forward_xnorm against fp32 torch: xprep (f16 rows + 64-column
-    sum-of-squares shares) -> a norm-folded consumer (output row m scaled by 1/rms from the shares) -> an EPI_ADDX
-    producer (residual add, f16 row, per-tile shares) -> consumers of ITS shares on every dense mode (4 incl.
-    split-K slabs, 10, 14), plain / SwiGLU / arg-max epilogues."""
-    d, K2, eps = 1024, 768, 1e-5
-    x = (torch.randn(M + 64, d) * 0.7).to(gpu)
-    xh = torch.zeros(M + 64, d, dtype=ops.ACT_DTYPE, device=gpu)
-    xss = torch.full((M + 64, ops.XSS_LD), float("nan"), device=gpu)
-    nss = ops.xprep(x, xh, xss, M)
-    assert nss == d // 64
-    _close(xh[:M], x[:M].cpu(), 1e-3)
-    tot = xss[:M, :nss].double().sum(1).cpu()
-    assert torch.allclose(tot, x[:M].double().pow(2).sum(1).cpu(), rtol=1e-4)
-    nw = (torch.rand(d) + 0.5).to(gpu)
-    wc, Wc = _qw(640, d, GGMLType.Q4_K, gpu, 31)
-    wc.expand_dense(nw)
-    assert wc.d16_folded
-    want = _rms_ref(x[:M].cpu(), nw.cpu(), eps) @ Wc.t()
-    rin = (xss, ops.XSS_LD, nss, eps)
-    for c in [(14, 4, 3, 1), (14, 8, 2, 1), (4, 8, 2, 1), (4, 16, 2, 2), (10, 8, 2, 1), (10, 8, 1, 2)]:
-        y = torch.zeros(M + 64, 640, device=gpu)
-        ops.qgemv([ops.Seg(wc)], xh, y, M, rin=rin, **dict(zip(("mode", "waves", "rt", "ks"), c)))
-        _close(y[:M], want, 3e-2)
-    with pytest.raises(ValueError):           # a folded copy never runs without its row scaling
-        ops.qgemv([ops.Seg(wc)], xh, torch.zeros(M + 64, 640, device=gpu), M, mode=4, waves=8, rt=2, ks=1)
-    # producer: x += 0.5 * ao @ Wo^T, xh = f16(x), shares per column tile
-    wo, Wo = _qw(d, K2, GGMLType.Q6_K, gpu, 32)
-    wo.expand_dense()
-    ao = _x(M, K2, gpu, seed=7)
-    x0 = x.clone()
-    n2 = ops.qgemv_addx(ops.Seg(wo), ao, x, xh, xss, M, 0.5, pcfg)
-    ref = x0[:M].cpu() + 0.5 * (ao[:M].float().cpu() @ Wo.t())
-    _close(x[:M], ref)
-    _close(xh[:M], ref, 1e-3)
-    assert float((x[M:] - x0[M:]).abs().max().cpu()) == 0.0
-    tot = xss[:M, :n2].double().sum(1).cpu()
-    assert torch.allclose(tot, ref.double().pow(2).sum(1), rtol=1e-4)
-    rin = (xss, ops.XSS_LD, n2, eps)
-    hn = _rms_ref(ref, nw.cpu(), eps)
-    for c in [(14, 8, 4, 1), (10, 8, 2, 1), (4, 8, 4, 1)]:
-        y = torch.zeros(M + 64, 640, device=gpu)
-        keys = torch.zeros(M + 64, dtype=torch.int64, device=gpu)
-        ops.qgemv([ops.Seg(wc)], xh, y, M, rin=rin, argmax=keys, **dict(zip(("mode", "waves", "rt", "ks"), c)))
-        _close(y[:M], hn @ Wc.t(), 3e-2)
-        ids = torch.zeros(M + 64, dtype=torch.int32, device=gpu)
-        ops.argmax_unpack(keys, M, ids)
-        assert (ids[:M].cpu() == y[:M].argmax(1).cpu().to(torch.int32)).float().mean() > 0.99
-    # SwiGLU consumer on a folded gate|up copy
-    F = 256
-    rng = np.random.default_rng(33)
-    g_raw = Q.random_blocks(GGMLType.Q4_K, F * d, 0.05, rng)
-    u_raw = Q.random_blocks(GGMLType.Q4_K, F * d, 0.05, rng)
-    gu = ops.QWeight(ops.interleave_gate_up(g_raw, u_raw, GGMLType.Q4_K, F, d), GGMLType.Q4_K, 2 * F, d, gpu)
-    gu.expand_dense(nw)
-    G = torch.from_numpy(Q.dequantize(g_raw, 12, (F, d)))
-    U = torch.from_numpy(Q.dequantize(u_raw, 12, (F, d)))
-    for c in [(14, 4, 2, 1), (10, 8, 1, 1), (4, 8, 4, 2)]:
-        y = torch.zeros(M + 64, F, dtype=ops.ACT_DTYPE, device=gpu)
-        ops.qgemv([ops.Seg(gu)], xh, y, M, epi="swiglu", rin=rin, **dict(zip(("mode", "waves", "rt", "ks"), c)))
-        _close(y[:M], torch.nn.functional.silu(hn @ G.t()) * (hn @ U.t()), 3e-2)
-
-
-@pytest.mark.parametrize("cfg", [(14, 4, 3, 1), (14, 8, 4, 1), (4, 16, 2, 1), (10, 8, 1, 1), (14, 4, 2, 2)])
-def test_qkv_rope_kv_dense_rin(gpu, cfg):
-    """Q|K|V as a dense split-RMSNorm consumer: ONE contiguous norm-folded copy (expand_dense_group, merged into a
-    single segment) with the RoPE + KV-append epilogue (split-K: slabs + the RoPE kernel), against
-    rmsnorm -> GEMM -> rope on the CPU."""
-    Hq, Hkv, D, K, M = 4, 2, 128, 512, 300
-    wq, Wq = _qw(Hq * D, K, GGMLType.Q4_K, gpu, 21)
-    wk, Wk = _qw(Hkv * D, K, GGMLType.Q4_K, gpu, 22)
-    wv, Wv = _qw(Hkv * D, K, GGMLType.Q6_K, gpu, 23)
-    nw = (torch.rand(K) + 0.5).to(gpu)
-    ops.expand_dense_group([wq, wk, wv], nw)
-    assert wk.d16.data_ptr() == wq.d16.data_ptr() + wq.rows * K * 2
-    segs = [ops.Seg(wq, 0), ops.Seg(wk, Hq * D), ops.Seg(wv, (Hq + Hkv) * D)]
-    assert ops._merged_dense(segs) is not None
-    x = (torch.randn(M + 64, K) * 0.6).to(gpu)
-    xh = torch.zeros(M + 64, K, dtype=ops.ACT_DTYPE, device=gpu)
-    xss = torch.zeros(M + 64, ops.XSS_LD, device=gpu)
-    rin = (xss, ops.XSS_LD, ops.xprep(x, xh, xss, M), 1e-5)
-    pad = M + 64
-    cs = ops.rope_table(4 * pad, D, 10000.0, gpu)
-    pos = torch.arange(pad, dtype=torch.int32, device=gpu) * 3
-    slot = torch.arange(pad, dtype=torch.int32, device=gpu)
-    qkv = torch.zeros(pad, (Hq + 2 * Hkv) * D, device=gpu)
-    q = torch.zeros(pad, Hq * D, dtype=torch.bfloat16, device=gpu)
-    kc = torch.zeros(pad, Hkv, D, dtype=torch.bfloat16, device=gpu)
-    vc = torch.zeros_like(kc)
-    ops.qkv_rope_kv(segs, xh, qkv, pos, slot, cs, q, kc, vc, M, Hq, Hkv, D, cfg=cfg, rin=rin)
-    qkv_ref = _rms_ref(x[:M].cpu(), nw.cpu()) @ torch.cat([Wq, Wk, Wv]).t()
-    qc, kcc, vcc = q.cpu().zero_(), kc.cpu().zero_(), vc.cpu().zero_()
-    ops.rope_kv(qkv_ref, pos.cpu(), slot.cpu(), cs.cpu(), qc, kcc, vcc, M, Hq, Hkv, D)
-    for a, b in zip((q.cpu(), kc.cpu(), vc.cpu()), (qc, kcc, vcc)):
-        _close(a[:M], b[:M], 3e-2)
 
 
 @pytest.mark.parametrize("mode,ks,wv", [(4, 1, 8), (4, 2, 8), (5, 1, 8), (5, 2, 8), (5, 1, 16), (4, 2, 16)])

@@ -173,8 +173,7 @@ def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
     (models/reference.py: numpy ggml codecs + textbook fp32 decoder, on the GPU; also with the engine's
     storage roundings, to separate kernel error from storage precision) for the two GEMM paths
     production runs at 512 rows: the quantised kernels only (as NLS_DENSE_WEIGHTS=0) and the f16-copy dense
-    kernels with the RMSNorms split between EPI_ADDX producers and norm-folded consumers (LlamaModel._forward_xnorm,
-    modes 4/10/14 per the "x:" / "d:" tuning entries). No library GEMM runs anywhere in the engine."""
+    kernels (modes 4/5/8/10 per the "d:" tuning entries). No library GEMM runs anywhere in the engine."""
     from nats_llm_studio_amd.gguf.reader import GGUFReader
     from nats_llm_studio_amd.models.reference import ReferenceModel
     S = 512
@@ -212,11 +211,10 @@ def test_llama3_8b_logits_vs_fp32_oracle(llama8b, gpu, monkeypatch):
         check(_prefill_logits(llama8b, ids), "quantised")
     llama8b.expand_dense(None)
     gu = ops.Seg(llama8b.layers[0].gateup)
-    assert gu.w.d16 is not None and gu.w.d16_folded and llama8b.xnorm
-    from nats_llm_studio_amd.ops import tuning
-    cfg = tuning.select_x([gu], S, "gateup")
-    assert cfg[0] in ops.DENSE_MODES, cfg              # the gate|up launch runs on the (norm-folded) f16 copy
-    check(_prefill_logits(llama8b, ids), "f16-copy dense, split RMSNorm")
+    assert gu.w.d16 is not None
+    cfg = ops.gemv_config([gu], S)
+    assert cfg[0] in (4, 5, 6, 8, 10), cfg              # the gate|up launch runs on the f16 copy
+    check(_prefill_logits(llama8b, ids), "f16-copy dense")
 
 
 def test_graph_split_workspace_survives_growth(gpu, tiny_models):

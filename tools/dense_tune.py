@@ -59,22 +59,15 @@ def roles(spec):
             "lm_head": ([(14, spec.vocab)], d, "argmax")}
 
 
-def candidates(M, K, epi, rows=None):
+def candidates(M, K, epi):
     out = [(10, 8, rt, ks) for rt in (1, 2) for ks in (1, 2, 3, 4, 6, 8)]
     for mode in (4, 5):
         for waves in (8, 16):
             for wm in ((2, 4) if M >= 192 else (2,)):
                 for ks in (1, 2, 4):
                     out.append((mode, waves, wm, ks))
-    # mode 14: 128-row activation blocks x 64 / 96 / 128 weight rows, 4 waves or two K-groups of 4
-    for waves, rt in ((4, 2), (4, 3), (4, 4), (8, 2), (8, 4)):
-        for ks in (1, 2):
-            out.append((14, waves, rt, ks))
-    if epi in ("argmax", "addx"):
+    if epi == "argmax":
         out = [c for c in out if c[3] == 1]
-    if epi == "addx":          # EPI_ADDX producers: modes 4/5/14, <= 64 column tiles (shares per row)
-        bn = lambda c: 32 * c[2] if c[0] == 14 else (256 if c[0] == 5 else 128)
-        out = [c for c in out if c[0] in (4, 5, 14) and -(-rows // bn(c)) <= 64]
     nkt = K // 64
     out = [c for c in out if nkt // c[3] >= 8]
     return out
@@ -87,10 +80,7 @@ def main():
     ap.add_argument("--roles", default="qkv,o,gateup,down,lm_head")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--emit", action="store_true")
-    ap.add_argument("--modes", default="", help="comma list: time only these modes (e.g. 4,14)")
-    ap.add_argument("--xnorm", action="store_true",
-                    help="time the split-RMSNorm path's launches (LlamaModel._forward_xnorm): norm-folded consumers "
-                         "(rin=) and EPI_ADDX producers (o / down); emits 'x:<role>:...' entries")
+    ap.add_argument("--modes", default="", help="comma list: time only these modes (e.g. 4,10)")
     a = ap.parse_args()
     spec = SPECS[a.model]
     dev = torch.device("cuda:0")
@@ -101,19 +91,18 @@ def main():
         segs, col = [], 0
         for t, rows in segdef:
             w = ops.QWeight(Q.random_blocks(t, rows * K, 0.02, rng), t, rows, K, dev)
+            w.expand_dense()
             segs.append(ops.Seg(w, col))
             col += rows
-        ops.expand_dense_group([sg.w for sg in segs])      # Q|K|V: one block, one dense segment (as the model)
         nbytes = col * K * 2
         ncopy = min(REPS, max(1, -(-(1 << 30) // nbytes)))
         copies = [segs]
         for _ in range(ncopy - 1):
-            cp, blk, r0 = [], torch.cat([sg.w.d16 for sg in segs], 0), 0
+            cp = []
             for s in segs:
                 w = ops.QWeight.__new__(ops.QWeight)
                 w.__dict__.update(s.w.__dict__)
-                w.d16 = blk[r0:r0 + w.rows]
-                r0 += w.rows
+                w.d16 = s.w.d16.clone()
                 cp.append(ops.Seg(w, s.ycol))
             copies.append(cp)
         wcat = [torch.cat([s.w.d16 for s in cp], 0) for cp in copies]
@@ -131,33 +120,9 @@ def main():
                 torch.mm(x[:M], wcat[i % ncopy].t(), out=lib_out[:M])
             t_lib = timed(graph_of(lib), a.rounds)
 
-            xss = torch.zeros(max(M, 64), ops.XSS_LD, device=dev)
-            xin32 = x.float()
-            rin = None
-            if a.xnorm:
-                rin = (xss, ops.XSS_LD, ops.xprep(xin32, x, xss, M), 1e-5)
-                for cp in copies:      # the consumers' copies carry the norm weight (its values do not matter)
-                    for sg in cp:
-                        sg.w.d16_folded = name not in ("o", "down")
-
             def launch(cfg):
                 mode, waves, rt, ks = cfg
-                if a.xnorm and name in ("o", "down"):
-                    xh = torch.zeros(max(M, 64), col, dtype=ops.ACT_DTYPE, device=dev)
-                    xs2 = torch.zeros(max(M, 64), ops.XSS_LD, device=dev)
-
-                    def fn(i):
-                        ops.qgemv_addx(copies[i % ncopy][0], x, y, xh, xs2, M, 1.0, cfg)
-                elif a.xnorm and name == "qkv":
-                    def fn(i):
-                        ops.qgemv(copies[i % ncopy], x, y, M, mode=mode, waves=waves, rt=rt, ks=ks, rin=rin)
-                elif a.xnorm:
-                    def fn(i):
-                        if epi == "argmax":
-                            ops.argmax_reset(keys)
-                        ops.qgemv(copies[i % ncopy], x, y, M, epi=epi, argmax=keys if epi == "argmax" else None,
-                                  mode=mode, waves=waves, rt=rt, ks=ks, rin=rin)
-                elif epi == "add":
+                if epi == "add":
                     def fn(i):
                         ops.qgemv_add_rmsnorm(copies[i % ncopy][0], x, y, nw, hn, M, 1.0, 1e-5, cfg=cfg)
                 elif epi == "argmax":
@@ -170,8 +135,7 @@ def main():
                         ops.qgemv(copies[i % ncopy], x, y, M, epi=epi, mode=mode, waves=waves, rt=rt, ks=ks)
                 return fn
             res = []
-            cepi = "addx" if a.xnorm and name in ("o", "down") else epi
-            for cfg in candidates(M, K, cepi, col):
+            for cfg in candidates(M, K, epi):
                 if a.modes and cfg[0] not in {int(m) for m in a.modes.split(",")}:
                     continue
                 try:
@@ -182,18 +146,17 @@ def main():
             t_best, cfg_best = res[0]
             # correctness of the winner: plain f32 output against the library product
             yy = torch.zeros(max(M, 64), col, device=dev)
-            for sg in segs:
-                sg.w.d16_folded = False
             ops.qgemv(segs, x, yy, M, mode=cfg_best[0], waves=cfg_best[1], rt=cfg_best[2], ks=cfg_best[3])
             torch.mm(x[:M], wcat[0].t(), out=lib_out[:M])
             rel = float((yy[:M] - lib_out[:M].float()).abs().max() / (lib_out[:M].float().abs().max() + 1e-6))
             line = dict(model=a.model, role=name, M=M, rows=col, K=K, lib_us=round(t_lib, 2),
                         lib_TF=round(flop / t_lib / 1e6, 1), hand_us=round(t_best, 2),
                         hand_TF=round(flop / t_best / 1e6, 1), cfg=list(cfg_best), hand_over_lib=round(t_best / t_lib, 3),
-                        maxrel=float(f"{rel:.2e}"), runner_up=[[round(t, 2), list(c)] for t, c in res[1:4]])
+                        maxrel=float(f"{rel:.2e}"), runner_up=[[round(t, 2), list(c)] for t, c in res[1:4]],
+                        all=[[round(t, 2), list(c)] for t, c in res])
             print(json.dumps(line), flush=True)
             rows_out.append(line)
-            emit[tuning.x_key(segs, M, name) if a.xnorm else tuning.dense_key(segs, M)] = list(cfg_best)
+            emit[tuning.dense_key(segs, M)] = list(cfg_best)
         del copies, wcat, segs
         torch.cuda.empty_cache()
     if a.emit:

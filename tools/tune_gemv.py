@@ -70,10 +70,7 @@ def dense_configs(K):
     nkt = K // 64
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
-            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
-            # mode 14: 128-row activation blocks x 64 / 96 / 128 weight rows (hgemm.hip launch_dense14)
-            + [(14, wv, rt, ks) for wv, rt in ((4, 2), (4, 3), (4, 4), (8, 2), (8, 4)) for ks in (1, 2)
-               if ks == 1 or nkt // ks >= 4])
+            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
