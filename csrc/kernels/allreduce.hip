@@ -103,6 +103,15 @@ __device__ __forceinline__ void wt_store4(float* p, float4 v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ... and its reader: agent-scope loads (sc1: no L1, no stale line of this XCD from before the write)
+__device__ __forceinline__ float4 wt_load4(const float* p) {
+  const gu64* q = (const gu64*)p;
+  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)), __uint_as_float((uint32_t)b),
+                     __uint_as_float((uint32_t)(b >> 32)));
+}
+
 // this rank's error word and the peers' (after the 2 x world x cap receive slots)
 __device__ __forceinline__ uint32_t* ar_err_word(uint32_t* buf, int world, long cap) {
   return buf + 2L * world * cap;
@@ -172,6 +181,9 @@ constexpr long AR_OPT_RETAG = 1L << 61;       // fused add+norm: re-tag consumed
 constexpr long AR_OPT_EP_RMW = 1L << 60;      // epoch counters read / written by atomic read-modify-writes
 constexpr long AR_OPT_POLL_RMW = 1L << 59;    // peer granules polled by atomic read-modify-writes (OR 0)
 constexpr long AR_OPT_PROBE = 1L << 58;       // fused add+norm: read every push back (RMW) and log a mismatch
+constexpr long AR_OPT_XCHECK = 1L << 57;      // fused add+norm: the row's normaliser re-sums x^2 from the x it reads
+                                              // and logs a disagreement with the slices' shares (words 32..39)
+constexpr long AR_OPT_XPLAIN = 1L << 56;      // fused add+norm: the normaliser reads x with plain loads (round-5 form)
 constexpr long AR_SPIN_MASK = (1L << 48) - 1;
 
 __device__ __forceinline__ unsigned ep_get(unsigned* p, long opts) {
@@ -474,9 +486,32 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
       const float inv = rsqrtf(tot / (float)D + eps);
       const float* xr = x + (size_t)b * ldx;
       _Float16* hr = h + (size_t)b * ldh;
+      // the other slices' x were written by other workgroups (write-through, agent scope): read them the same way
+      // (agent-scope loads bypass this CU's L1 and any stale line of an earlier kernel's read), not by plain loads
+      const bool plain = max_spins & AR_OPT_XPLAIN;
+      if (max_spins & AR_OPT_XCHECK) {
+        float s2 = 0.f;
+        for (int i = 4 * threadIdx.x; i < D; i += 4 * ARN_THREADS) {
+          const float4 xv = plain ? *reinterpret_cast<const float4*>(xr + i) : wt_load4(xr + i);
+          s2 += xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+        if (threadIdx.x == 0 && fabsf(s2 - tot) > 1e-4f * fabsf(tot) + 1e-6f) {
+          uint32_t* dw = ar_err_word(P.buf[rank], world, cap);
+          if (atomicCAS(dw + 32, 0u, 0xD44u) == 0u) {
+            dw[33] = (uint32_t)b;
+            dw[34] = __float_as_uint(tot);
+            dw[35] = __float_as_uint(s2);
+            dw[36] = ep;
+            dw[37] = (uint32_t)rank;
+            dw[38] = xcc_id();
+          }
+        }
+      }
 #pragma unroll 4
       for (int i = 4 * threadIdx.x; i < D; i += 4 * ARN_THREADS) {
-        const float4 xv = *reinterpret_cast<const float4*>(xr + i);
+        const float4 xv = plain ? *reinterpret_cast<const float4*>(xr + i) : wt_load4(xr + i);
         const float4 wv = *reinterpret_cast<const float4*>(nw + i);
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 o;
@@ -645,9 +680,13 @@ static long ar_opts(long max_spins) {
     if (a && atoi(a)) o |= AR_OPT_POLL_INV;
     if (!b || atoi(b)) o |= AR_OPT_RETAG;      // default on: the simulated-rank tests need it (round 4)
     const char* e = getenv("NLS_AR_PROBE");
+    const char* f = getenv("NLS_AR_XCHECK");
+    const char* g = getenv("NLS_AR_XPLAIN");
     if (c && atoi(c)) o |= AR_OPT_EP_RMW;
     if (d && atoi(d)) o |= AR_OPT_POLL_RMW;
     if (e && atoi(e)) o |= AR_OPT_PROBE;
+    if (f && atoi(f)) o |= AR_OPT_XCHECK;
+    if (g && atoi(g)) o |= AR_OPT_XPLAIN;
     return o;
   }();
   return (max_spins & AR_SPIN_MASK) | opts;

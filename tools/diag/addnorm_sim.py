@@ -38,8 +38,22 @@ def main(world=2, rows=16, D=4096, iters=8):
                                 first_bad_slices=sorted({int(c) // 256 for c in badc[:64].tolist()})[:8]))
         _, tk, _ = g._norm[D]
         tks = tk[:, :rows].tolist()
+        # NLS_AR_XCHECK=1: the normaliser's own re-sum of x^2 vs the slices' shares (words 32..38 of the error area)
+        from nats_llm_studio_amd.ops import _lib
+        xc = []
+        for r in range(world):
+            host = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+            _lib.lib().nls_ar_peek(g.nbufs[r], 2 * world * g.cap + 32, 8, host.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            w = host.tolist()
+            if w[0] == 0xD44:
+                import struct
+                f = lambda u: struct.unpack("f", struct.pack("i", u))[0]
+                xc.append(dict(rank=r, row=w[1], shares=round(f(w[2]), 3), reread=round(f(w[3]), 3), ep=w[4],
+                               xcc=w[6]))
         print(f"call {it} rows {rr} x_ok {x_ok} err {int(g.err.item())} bad {rep[:6]} tickets_nonzero "
-              f"{[[i for i, v in enumerate(t) if v] for t in tks]}", flush=True)
+              f"{[[i for i, v in enumerate(t) if v] for t in tks]} xcheck {xc}", flush=True)
         bad_calls += bool(rep) or not x_ok
     g.close()
     return 1 if bad_calls else 0
