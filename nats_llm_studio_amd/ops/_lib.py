@@ -57,7 +57,6 @@ _SIGS = {
     "nls_epx_err_clear": [c_void_p, c_int, c_int, c_void_p],
     "nls_epx_err_fetch": [c_void_p, c_int, c_int, c_void_p, c_void_p],
     "nls_rmsnorm": [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_int, c_void_p],
-    "nls_xprep": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nls_splitk_add_rmsnorm": [c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int,
                                c_float, c_void_p],
     "nls_rope_kv": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,

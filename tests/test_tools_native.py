@@ -92,3 +92,16 @@ def test_natscore_under_sanitizers(san):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     assert "ThreadSanitizer" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
     assert "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
+def test_kernel_bindings_match_the_built_library():
+    """Every ctypes signature in ops/_lib.py names a symbol the in-tree _kernels.so exports (a binding left
+    behind by a reverted kernel fails the first GPU call of every process, not any CPU test)."""
+    import shutil
+    from nats_llm_studio_amd.ops import _lib
+    if not os.path.exists(_lib.LIB_PATH) or shutil.which("nm") is None:
+        pytest.skip("no built _kernels.so / nm")
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    assert sorted(set(_lib._SIGS) - exported) == []
