@@ -168,11 +168,28 @@ def build_tool(name: str = "nls-nats", src: str = "nls_nats.cpp", extra=(), out_
     return out
 
 
+def build_diag(force: bool = False):
+    """Stand-alone gfx950 probe libraries of tools/diag (csrc/diag/<name>.hip -> tools/diag/_<name>.so)."""
+    outs = []
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    for src in sorted(glob.glob(os.path.join(CSRC, "diag", "*.hip"))):
+        out = os.path.join(ROOT, "tools", "diag", "_" + os.path.basename(src)[:-4] + ".so")
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared"]
+        if force or _stale(out, [src], flags):
+            tmp = out + ".tmp"
+            _run([hipcc, *flags, src, "-o", tmp])
+            os.replace(tmp, out)
+            _write_stamp(out, [src], flags)
+        outs.append(out)
+    return outs
+
+
 def build_all(force: bool = False):
     k = build_kernels(force)
     n = build_natscore(force)
     build_tokcore(force)
     build_tool(force=force)
+    build_diag(force)
     return k, n
 
 

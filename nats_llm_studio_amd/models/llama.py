@@ -488,17 +488,18 @@ class LlamaModel:
             n = int(n_logits)
             h = b.h.index_select(0, logit_rows[:n].long())
             h = torch.cat([h, h.new_zeros((-n) % 16, h.shape[1])]) if n % 16 else h
-        if self.shard.size > 1 or not b.keys_clean:
+        if not b.keys_clean:
             ops.argmax_reset(b.keys)
         # greedy-only steps keep just the fused arg-max keys (no [n, V] logits written)
         ops.qgemv([Seg(self.lm_head, 0)], h, b.logits, n, alpha=1.0 / cfg.logit_scale, argmax=b.keys,
                   epi="f32" if need_logits else "argmax")
+        # the unpack (or the vocab-parallel arg-max) re-arms the keys it read: the next step's arg-max needs no
+        # reset launch (under TP it was the one PyTorch kernel left in the decode graphs)
         if self.shard.size == 1:
-            # the unpack re-arms the keys it read: the next step's arg-max needs no reset launch
             ops.argmax_unpack(b.keys, n, b.next_ids, rearm=True)
-            b.keys_clean = b.keys.is_cuda
         else:
             self.comm.vocab_parallel_argmax(b.keys, n, self.vocab_lo, b.next_ids)
+        b.keys_clean = b.keys.is_cuda
         return n
 
     def _forward_fused_norm(self, b: StepBuffers, kc, vc, T: int, block_size: int, n_split: int, logit_rows,

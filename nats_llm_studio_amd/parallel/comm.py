@@ -117,7 +117,8 @@ class Comm:
         return True
 
     def vocab_parallel_argmax(self, keys: torch.Tensor, n: int, vocab_lo: int, next_ids: torch.Tensor):
-        """Per-rank fused-argmax keys (value<<32 | ~local_idx) -> global greedy ids on every rank."""
+        """Per-rank fused-argmax keys (value<<32 | ~local_idx) -> global greedy ids on every rank. Both paths
+        leave keys[:n] re-armed (the next step's fused arg-max needs no reset launch)."""
         if self._os(keys) is not None:
             # one IPC launch: rebase, exchange, max, unpack and re-arm (no RCCL call in the decode graph)
             self.stats["all_reduce"] += 1
@@ -131,7 +132,7 @@ class Comm:
         self.all_reduce(k, op=dist.ReduceOp.MAX)
         if keys.is_cuda:
             k.bitwise_xor_(_SIGN)
-        ops.argmax_unpack(keys, n, next_ids)
+        ops.argmax_unpack(keys, n, next_ids, rearm=True)
 
     def gather_logits(self, logits: torch.Tensor, n: int, vocab: int, per: int) -> torch.Tensor:
         """Vocab-sharded logits [n, Vs] -> full [n, vocab] on every rank (only when sampling)."""

@@ -1,0 +1,147 @@
+"""Gate for a fence-free small-batch decode (VERDICT r05 "next round" 1): can a stage hand its output to the next
+stage for less than the 6.89 us a dependent batch-1 GEMV costs today (profiles/b1_overlap_r05.txt)?
+
+A chain of L dependent M=1 GEMVs (csrc/diag/chain.hip: 4096 x 4096 4-bit weights, 8 MiB per link, L x 8 MiB >
+the 256 MiB Infinity Cache so every link streams from HBM), captured in a hipGraph and replayed, per link:
+  serial            one launch per link on one stream (today's decode graph structure)
+  ff_branches       one launch per link, links alternating over two graph branches with no edge between them;
+                    each issues its weight loads, then polls the self-tagged x words (no fence)
+  persistent_pf0/1/2 one launch for the chain: weights after the wait / this link's before the wait / the next
+                    link's before this link's wait
+Outputs of every variant must be bit-equal to serial's and close to an fp32 torch reference; error words zero.
+
+    python tools/diag/fencefree_chain.py [L] [reps]
+The probe library is built by nats_llm_studio_amd.build.build_diag (part of build_all) and travels with the tree."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+SRC = os.path.join(ROOT, "csrc", "diag", "chain.hip")
+LIB = os.path.join(HERE, "_chain.so")
+
+
+def build(force=False):
+    sys.path.insert(0, ROOT)
+    from nats_llm_studio_amd.build import build_diag
+    build_diag(force)
+    return LIB
+
+
+def load():
+    L = ctypes.CDLL(LIB)
+    vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+    L.chain_dims.argtypes = [vp]
+    L.chain_init.argtypes = [vp, vp, vp, vp]
+    L.chain_link.argtypes = [vp, vp, vp, ci, vp, ci, cl, vp, vp]
+    L.chain_persistent.argtypes = [vp, vp, vp, ci, vp, ci, cl, vp, vp]
+    return L
+
+
+def decode_link(wbytes, scale, D, NWG, NJ):
+    """uint8 [NWG * NJ * 256 * 16] of one link -> f32 [D, D] (layout of chain.hip: chunk (j, t), byte b, nibble h
+    -> row 16 wg + t // 16, k = 256 (t % 16) + 32 j + 2 b + h)."""
+    import torch
+    b = wbytes.view(NWG, NJ, 16, 16, 16)                       # wg, j, r, c, byte
+    nib = torch.stack([b & 15, b >> 4], -1).to(torch.float32) - 8.0  # wg, j, r, c, byte, h
+    w = nib.permute(0, 2, 3, 1, 4, 5).reshape(D, D)            # (wg, r) x (c, j, byte, h)
+    return w * scale[:, None]
+
+
+def main(L=64, reps=20):
+    import torch
+    build()
+    lib = load()
+    dims = (ctypes.c_int * 4)()
+    lib.chain_dims(dims)
+    D, NWG, NJ, NT = list(dims)
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    W = torch.randint(0, 256, (L, NWG * NJ * NT * 16), dtype=torch.uint8, generator=g).to(dev)
+    scale = (torch.rand(L, D, generator=g) * 0.5 + 0.75) / float(np.sqrt(D * 21.25))
+    scale = scale.to(dev)
+    x0 = torch.randn(D, generator=g).to(torch.float16).to(dev)
+    max_spins = 1 << 17
+
+    def ptr(t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def chk(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed with code {rc}")
+
+    results, outs = {}, {}
+    for variant in ("serial", "ff_branches", "persistent_pf0", "persistent_pf1", "persistent_pf2", "init_only"):
+        X = torch.zeros(L + 1, D, dtype=torch.int32, device=dev)
+        epoch = torch.zeros(1, dtype=torch.int32, device=dev)
+        err = torch.zeros(2, dtype=torch.int32, device=dev)
+        s = [torch.cuda.Stream(dev) for _ in range(2)]
+
+        def body():
+            cur = torch.cuda.current_stream()
+            st = ctypes.c_void_p(cur.cuda_stream)
+            chk(lib.chain_init(ptr(epoch), ptr(X), ptr(x0), st), "chain_init")
+            if variant == "serial":
+                for l in range(L):
+                    chk(lib.chain_link(ptr(W), ptr(scale), ptr(X), l, ptr(epoch), 0, max_spins, ptr(err), st), "link")
+            elif variant == "ff_branches":
+                for k in range(2):
+                    s[k].wait_stream(cur)
+                for l in range(L):
+                    sk = ctypes.c_void_p(s[l % 2].cuda_stream)
+                    chk(lib.chain_link(ptr(W), ptr(scale), ptr(X), l, ptr(epoch), 1, max_spins, ptr(err), sk), "ff")
+                for k in range(2):
+                    cur.wait_stream(s[k])
+            elif variant.startswith("persistent"):
+                pf = int(variant[-1])
+                chk(lib.chain_persistent(ptr(W), ptr(scale), ptr(X), L, ptr(epoch), pf, max_spins, ptr(err), st),
+                    "persistent")
+
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            body()                                   # eager once (also the warm-up)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            body()
+        gr.replay()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            gr.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        results[variant] = float(np.median(ts))
+        e = err.tolist()
+        outs[variant] = (X[L].clone(), e)
+        print(f"{variant:16s} {results[variant]:9.1f} us per replay; err words {e}", flush=True)
+        del gr
+
+    # reference: fp32 GEMV per link, rounded to f16 like the kernels
+    x = x0.float()
+    for l in range(L):
+        x = (decode_link(W[l], scale[l], D, NWG, NJ) @ x).to(torch.float16).float()
+    ser = (outs["serial"][0] & 0xFFFF).to(torch.int16).view(torch.float16).float()
+    rel = float((ser - x).norm() / x.norm())
+    print(f"serial x_L vs fp32 reference: rel err {rel:.2e} (|x_L| rms {float(x.pow(2).mean().sqrt()):.3f})")
+    base = results["init_only"]
+    for v in ("serial", "ff_branches", "persistent_pf0", "persistent_pf1", "persistent_pf2"):
+        same = bool(torch.equal(outs[v][0] & 0xFFFF, outs["serial"][0] & 0xFFFF))
+        per = (results[v] - base) / L
+        print(f"{v:16s} {per:6.2f} us per link ({8.0 * 2**20 / per / 1e6:5.2f} TB/s of weights), "
+              f"x_L bit-equal to serial {same}, err {outs[v][1]}", flush=True)
+    ok = rel < 3e-2 and all(outs[v][1] == [0, 0] for v in outs)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    a = [int(v) for v in sys.argv[1:]]
+    sys.exit(main(*a))
