@@ -75,7 +75,8 @@ DEVI typename RawOf<T>::type raw_lds(const uint8_t* b, int g, int r) {
 }
 
 template <int T, int MT>
-DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds) {
+DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a, float* ws, uint8_t* lds,
+                   const int* xm, const int* ym) {
   constexpr int RT = 2;
   constexpr int BM = MT * 16;
   constexpr int XS = BM * 128;                  // bytes per activation quarter [BM][64] f16
@@ -96,13 +97,15 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 
   // ---- per-lane DMA sources ----------------------------------------------------------------
   // x: instruction i of wave w covers rows 8*(NX*w + i) .. +8; lane -> row + (lane >> 3), physical
-  // chunk lane & 7 <- logical chunk (lane & 7) ^ (row & 7)
+  // chunk lane & 7 <- logical chunk (lane & 7) ^ (row & 7). xm (MoE): block row -> gathered x row, so the
+  // DMA gathers an expert's routed rows straight from the token activations
   const act_t* xsrc[NX];
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
     const int row = 8 * (NX * wave + i) + (lane >> 3);
     const int c = (lane & 7) ^ (row & 7);
-    xsrc[i] = a.x + (size_t)min(row, M - 1) * a.ldx + c * 8;   // rows >= M: clamped, never stored
+    const int lr = min(row, M - 1);                            // rows >= M: clamped, never stored
+    xsrc[i] = a.x + (size_t)(xm ? xm[lr] : lr) * a.ldx + c * 8;
   }
   // raw W: LDS byte b of the packed region <- tile-block b / TB, byte b % TB (TB % 16 == 0)
   const uint8_t* wsrc[NW];
@@ -227,7 +230,11 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int b = 16 * mt + 4 * g + e;
-          if (b < M) ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][e];
+          if (b >= M) continue;
+          if (ym)        // mapped split-K: slab row = the token's y row, columns shared by every expert
+            ws[((size_t)kslice * a.mtot + ym[b]) * ntot + S.ycol + row] = acc[rt][mt][e];
+          else
+            ws[((size_t)kslice * a.mtot + a.m0 + b) * ntot + S.tile_begin_col + row] = acc[rt][mt][e];
         }
     }
     return;
@@ -245,12 +252,12 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
           const float u = __shfl_xor(v, 8, 64);
           if (r < 8 && b < M && row < S.rows) {
             const int n = S.ycol + ((rbase + 16 * rt) >> 1) + r;
-            reinterpret_cast<act_t*>(a.y)[(size_t)b * a.ldy + n] = (act_t)(silu(v) * u);
+            reinterpret_cast<act_t*>(a.y)[(size_t)(ym ? ym[b] : b) * a.ldy + n] = (act_t)(silu(v) * u);
           }
           continue;
         }
         if (b < M && row < S.rows) {
-          const size_t off = (size_t)b * a.ldy + S.ycol + row;
+          const size_t off = (size_t)(ym ? ym[b] : b) * a.ldy + S.ycol + row;
           if (a.epi == EPI_F32) reinterpret_cast<float*>(a.y)[off] = v;
           else if (a.epi == EPI_ADD_F32) reinterpret_cast<float*>(a.y)[off] += v;
           else if (a.epi == EPI_ACT) reinterpret_cast<act_t*>(a.y)[off] = (act_t)v;
@@ -287,9 +294,12 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   }
 }
 
+// MT <= 6 (64 / 96-row blocks: MoE experts at ~64 routed rows) is built for TWO workgroups
+// per CU (<= 256 VGPRs at 4 waves, 52 / 64 KiB of LDS): one workgroup's DMA waits and barriers hide behind the
+// other's MFMAs, where the 128 / 256-row blocks own a CU each.
 template <int MT, int KSET>
-__global__ __launch_bounds__(256, 1) void qmm_dma_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
-                                                         int nmb) {
+__global__ __launch_bounds__(256, MT <= 6 ? 2 : 1) void qmm_dma_kernel(SegList segs, GemvArgs a, int ks, float* ws,
+                                                                        int ntiles, int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
   constexpr int BM = MT * 16;
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
@@ -297,28 +307,34 @@ __global__ __launch_bounds__(256, 1) void qmm_dma_kernel(SegList segs, GemvArgs 
   const int mb = (j / ks) % nmb;
   const int tile = (j / ks / nmb) * 8 + xcd;
   if (tile >= ntiles) return;
-  const int m0 = mb * BM;
-  a.m0 = m0;
-  a.x += (size_t)m0 * a.ldx;
-  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
-  a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
-  if (a.argmax) a.argmax += m0;
-  a.M = min(BM, a.M - m0);
   Seg S = segs.s[0];
 #pragma unroll
   for (int s = 1; s < 8; ++s)
     if (s < segs.nseg && tile >= segs.s[s].tile_begin) S = segs.s[s];
+  const int m0 = mb * BM;
+  // MoE grouped GEMM: the expert's routed-row count lives on the device; m-blocks past it exit before any DMA
+  // (the grid is sized for the worst case, every token on one expert)
+  const int mrows = S.mcount ? min(*S.mcount, a.M) : a.M;
+  if (m0 >= mrows) return;
+  const int* xm = S.xmap ? S.xmap + m0 : nullptr;
+  const int* ym = S.ymap ? S.ymap + m0 : nullptr;
+  a.m0 = m0;
+  if (!xm) a.x += (size_t)m0 * a.ldx;
+  const size_t esz = (a.epi == EPI_F32 || a.epi == EPI_ADD_F32 || a.epi == EPI_ARGMAX) ? 4 : 2;
+  if (!ym) a.y = (char*)a.y + (size_t)m0 * a.ldy * esz;
+  if (a.argmax) a.argmax += m0;
+  a.M = min(BM, mrows - m0);
   const int row0 = (tile - S.tile_begin) * 128;
   if constexpr (KSET == 0) {
     switch (S.type) {
-      case QT_Q4_K: dma_tile<QT_Q4_K, MT>(S, row0, kslice, ks, a, ws, dlds); break;
-      case QT_Q6_K: dma_tile<QT_Q6_K, MT>(S, row0, kslice, ks, a, ws, dlds); break;
+      case QT_Q4_K: dma_tile<QT_Q4_K, MT>(S, row0, kslice, ks, a, ws, dlds, xm, ym); break;
+      case QT_Q6_K: dma_tile<QT_Q6_K, MT>(S, row0, kslice, ks, a, ws, dlds, xm, ym); break;
       default: break;
     }
   } else {
     switch (S.type) {
-      case QT_Q5_K: dma_tile<QT_Q5_K, MT>(S, row0, kslice, ks, a, ws, dlds); break;
-      case QT_Q6_K: dma_tile<QT_Q6_K, MT>(S, row0, kslice, ks, a, ws, dlds); break;
+      case QT_Q5_K: dma_tile<QT_Q5_K, MT>(S, row0, kslice, ks, a, ws, dlds, xm, ym); break;
+      case QT_Q6_K: dma_tile<QT_Q6_K, MT>(S, row0, kslice, ks, a, ws, dlds, xm, ym); break;
       default: break;
     }
   }
@@ -349,6 +365,8 @@ template <int KSET>
 int launch_dma_kset(int mt, const SegList& sl, int ntiles, int ks, float* ws, const GemvArgs& a, hipStream_t st) {
   if (mt == 16) return launch_dma_t<16, KSET>(sl, ntiles, ks, ws, a, st);
   if (mt == 8) return launch_dma_t<8, KSET>(sl, ntiles, ks, ws, a, st);
+  if (mt == 6) return launch_dma_t<6, KSET>(sl, ntiles, ks, ws, a, st);
+  if (mt == 4) return launch_dma_t<4, KSET>(sl, ntiles, ks, ws, a, st);
   return -1;
 }
 

@@ -47,7 +47,8 @@ struct NlsFuse {
 // mode 2: large-M LDS-dequant GEMM (qgemm_impl.h; K-quant types only): 8 waves, `rt` = WM (4: 256-row
 //         activation blocks, 2: 128-row), optional split-K as mode 1.
 // mode 3: large-M LDS-DMA GEMM (qgemm_dma.h; Q4_K/Q5_K/Q6_K only): 4 waves, `rt` = activation
-//         tiles per block (16: 256 rows, 8: 128 rows), optional split-K as mode 1.
+//         tiles per block (16: 256 rows, 8: 128 rows; 6 / 4: 96 / 64 rows at two workgroups per CU, the MoE
+//         expert blocks), mapped rows, optional split-K as mode 1.
 // mode 4: large-M dense f16 GEMM (hgemm.hip): every segment is type F16 with `w` = a ROW-MAJOR
 //         [rows][K] f16 matrix (not the tiled layout); 8 waves, `rt` = WM (4: 256-row activation
 //         blocks, 2: 128-row), optional split-K as mode 1.
@@ -121,7 +122,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16) return -1;
   } else if (mode == 3) {
-    if (waves != 4 || (rt != 8 && rt != 16)) return -1;
+    if (waves != 4 || (rt != 4 && rt != 6 && rt != 8 && rt != 16)) return -1;
   } else if (mode == 2 ? (waves != 8 || (rt != 1 && rt != 2 && rt != 4)) : (rt != 1 && rt != 2)) {
     return -1;
   }
@@ -129,7 +130,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (mode != 0 && ks > 1 && !ws) return -1;
   if (epi == EPI_SLABS && (mode == 0 || ks < 2)) return -1;   // slabs exist only with split-K
   // mapped split-K (MoE down projection at many tokens): slabs indexed by the y row, one reduce
-  bool mks = (mode == 1 || mode == 2 || mode == 4 || mode == 5) && ks > 1 && epi == EPI_F32 && !argmax;
+  bool mks = (mode >= 1 && mode <= 5) && ks > 1 && epi == EPI_F32 && !argmax;
   for (int i = 0; i < nseg && mks; ++i)
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
@@ -138,12 +139,11 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
-    // mapped rows (MoE): path A, or path B / the LDS-dequant / dense GEMMs (modes 1, 2, 4, 5) without
+    // mapped rows (MoE): path A, or path B / the LDS-dequant / LDS-DMA / dense GEMMs (modes 1-5) without
     // arg-max; split-K only as "mapped split-K" (every segment an expert writing the same output
     // columns of its own y rows, f32 store)
     if ((segs[i].xmap || segs[i].ymap || segs[i].mcount) && mode != 0 &&
-        (!(mode == 1 || mode == 2 || mode == 4 || mode == 5) || argmax || epi == EPI_SLABS ||
-         (ks > 1 && !mks)))
+        (!(mode >= 1 && mode <= 5) || argmax || epi == EPI_SLABS || (ks > 1 && !mks)))
       return -1;
     sl.s[i].w = (const uint8_t*)segs[i].w;
     sl.s[i].xmap = segs[i].xmap;

@@ -170,10 +170,14 @@ def test_qgemv_mapped_rows(gpu):
                                                 (150, 1, GGMLType.Q6_K, 2, 8), (200, 2, GGMLType.Q4_K, 5, 8),
                                                 (300, 4, GGMLType.Q5_K, 4, 16), (150, 2, GGMLType.Q6_K, 4, 8),
                                                 (200, 2, GGMLType.Q4_K, 1, 8), (300, 2, GGMLType.Q5_K, 1, 8),
-                                                (150, 1, GGMLType.Q6_K, 1, 4), (40, 2, GGMLType.Q5_K, 1, 8)])
+                                                (150, 1, GGMLType.Q6_K, 1, 4), (40, 2, GGMLType.Q5_K, 1, 8),
+                                                (200, 6, GGMLType.Q4_K, 3, 4), (300, 4, GGMLType.Q5_K, 3, 4),
+                                                (150, 6, GGMLType.Q6_K, 3, 4), (40, 4, GGMLType.Q5_K, 3, 4),
+                                                (300, 8, GGMLType.Q5_K, 3, 4)])
 def test_qgemm_mapped_moe(gpu, T, rt, qt, mode, waves):
     """Grouped MoE GEMM (mapped rows; mode 1 = path B register dequant with per-block active tiles,
-    mode 2 = LDS dequant, modes 4/5 = dense DMA GEMM on the experts' f16 copies): one route over T tokens, SwiGLU
+    mode 2 = LDS dequant, mode 3 = LDS-DMA of the raw blocks with the DMA gathering the routed rows (rt 4 / 6: the
+    64 / 96-row two-workgroups-per-CU blocks), modes 4/5 = dense DMA GEMM on the experts' f16 copies): one route over T tokens, SwiGLU
     gate/up and f32 down over every expert in one launch each, against the per-row fp32 reference."""
     E, k, K, F = 4, 2, 512, 256
     logits = torch.randn(T, E, device=gpu)
