@@ -18,9 +18,13 @@
 // writes only after finishing c). Epochs are kept per SLOT BLOCK (per row slice in the fused add+norm)
 // and a call writes every granule of every block it advances, so at epoch e a slot holds the peer's
 // epoch e - 2 granule or its epoch e granule -- a skipped block keeps its epoch too. The plain all-reduce and
-// the gather never write their own receive slots (see SlotBlocks below); the fused add+norm DOES, by default:
-// it re-tags each consumed granule with the other parity's tag (AR_OPT_RETAG, NLS_AR_RETAG=0 disables), the
-// round-3 protocol, which the simulated-rank test measured as needed (cause not established).
+// the gather never write their own receive slots (see SlotBlocks below), nor does the fused add+norm by default.
+// (Rounds 3-5 re-tagged each consumed granule with the other parity's tag, AR_OPT_RETAG, because the simulated-rank
+// test failed without it. The cause, found in round 6, was elsewhere: the row's normaliser read the other slices'
+// x with PLAIN loads after a one-thread agent-scope acquire, and such a load can still return a pre-add copy of the
+// slice -- "x exact (memory is right), h wrong (normalised from a stale read)". The normaliser now reads x with
+// agent-scope loads (wt_load4, sc1): with the re-tag off the test passes with them and fails with plain reads, the
+// r05 failure reproduced on demand (profiles/ar_retag_cause_r06.txt). NLS_AR_RETAG=1 restores the re-tag.)
 // Eager (non-captured) calls timed out in rounds 3-4 on two ranks sharing ONE GPU: the fused add+norm launched one
 // workgroup per (row, slice), its polling waves filled the GPU and the PEER rank's preceding kernels could not be
 // scheduled until the poll expired (device-clock timestamps of both ranks, profiles/tp_oneshot_eager_r05.txt). The
@@ -177,7 +181,7 @@ __device__ void ar_diag2(uint32_t* mine, int world, long cap, uint4 seen, uint32
 
 // launch-option bits carried above the spin budget (host: ar_opts(), env NLS_AR_POLL_INV / NLS_AR_RETAG)
 constexpr long AR_OPT_POLL_INV = 1L << 62;    // system-scope acquire (L2 invalidate) before every re-poll
-constexpr long AR_OPT_RETAG = 1L << 61;       // fused add+norm: re-tag consumed granules (the round-3 protocol)
+constexpr long AR_OPT_RETAG = 1L << 61;       // fused add+norm: re-tag consumed granules (rounds 3-5; off by default)
 constexpr long AR_OPT_EP_RMW = 1L << 60;      // epoch counters read / written by atomic read-modify-writes
 constexpr long AR_OPT_POLL_RMW = 1L << 59;    // peer granules polled by atomic read-modify-writes (OR 0)
 constexpr long AR_OPT_PROBE = 1L << 58;       // fused add+norm: read every push back (RMW) and log a mismatch
@@ -391,11 +395,9 @@ __global__ __launch_bounds__(ARN_THREADS) void oneshot_ar_addnorm_kernel(
     }
   }
   const unsigned long long t1 = probe_on ? (unsigned long long)wall_clock64() : 0ull;
-  // 2) per item: rank-ordered sum + residual add (bit-identical on every rank); consumed granules get the other
-  //    parity's tag (AR_OPT_RETAG, default on). Every call that advances an item's epoch has the peer write ALL
-  //    of the slice's granules, so the protocol itself does not need the re-tag; the simulated-rank test (all
-  //    ranks in one launch, after other launches on reused buffers) failed without it and passed with it --
-  //    unexplained, kept as the measured-safe default.
+  // 2) per item: rank-ordered sum + residual add (bit-identical on every rank). Every call that advances an item's
+  //    epoch has the peer write ALL of the slice's granules, so the protocol needs no re-tag of consumed granules
+  //    (AR_OPT_RETAG, NLS_AR_RETAG=1, kept as an option; see the header for why rounds 3-5 had it on).
   bool failed = false;   // after one timeout, stop waiting (the error words are raised below)
   for (int t = 0; t < nit; ++t) {
     const AnItem it = an_item(xcd, k, j, t, nblk);
@@ -678,7 +680,7 @@ static long ar_opts(long max_spins) {
     const char* c = getenv("NLS_AR_EP_RMW");
     const char* d = getenv("NLS_AR_POLL_RMW");
     if (a && atoi(a)) o |= AR_OPT_POLL_INV;
-    if (!b || atoi(b)) o |= AR_OPT_RETAG;      // default on: the simulated-rank tests need it (round 4)
+    if (b && atoi(b)) o |= AR_OPT_RETAG;       // default off since round 6 (header comment)
     const char* e = getenv("NLS_AR_PROBE");
     const char* f = getenv("NLS_AR_XCHECK");
     const char* g = getenv("NLS_AR_XPLAIN");

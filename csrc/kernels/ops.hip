@@ -321,6 +321,9 @@ __global__ void argmax_unpack_kernel(unsigned long long* __restrict__ keys, int 
 }
 
 // residual += sum_k w[t,k] * y[t*topk + k]   (MoE combine, deterministic order)
+// SET: resid = alpha * sum instead of +=  (a tensor-parallel rank's partial combine from zero: no fill launch in the
+// decode graph before it)
+template <bool SET>
 __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ y, const float* __restrict__ w,
                                                           int topk, float* __restrict__ resid, long ldr,
                                                           int D, float alpha) {
@@ -328,7 +331,8 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
   for (int i = threadIdx.x; i < D; i += 256) {
     float s = 0.f;
     for (int k = 0; k < topk; ++k) s += w[t * topk + k] * y[((size_t)t * topk + k) * D + i];
-    resid[(size_t)t * ldr + i] += alpha * s;
+    if (SET) resid[(size_t)t * ldr + i] = alpha * s;
+    else resid[(size_t)t * ldr + i] += alpha * s;
   }
 }
 
@@ -728,9 +732,13 @@ int nls_moe_norm_route(const float* x, long ldx, const float* nw, float eps, int
 }
 
 int nls_moe_combine(const float* y, const float* w, int T, int topk, float* resid, long ldr, int D, float alpha,
-                    void* stream) {
-  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr, D,
-                     alpha);
+                    int set, void* stream) {
+  if (set)
+    hipLaunchKernelGGL(moe_combine_kernel<true>, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr, D,
+                       alpha);
+  else
+    hipLaunchKernelGGL(moe_combine_kernel<false>, dim3(T), dim3(256), 0, (hipStream_t)stream, y, w, topk, resid, ldr,
+                       D, alpha);
   return (int)hipGetLastError();
 }
 

@@ -745,9 +745,7 @@ class LlamaModel:
                 # combine locally first, then ONE all-reduce of the combined [n, d] rows (k x fewer bytes
                 # than reducing the per-slot expert outputs): rank 0 adds into the residual, the others
                 # contribute their partial combine from zero (EP: own experts; TP: own FFN slice)
-                if self.shard.rank != 0:
-                    xs.zero_()
-                ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale)
+                ops.moe_combine(m["yexp"], m["topw"], n, k, xs, cfg.residual_scale, set_=self.shard.rank != 0)
                 self.comm.all_reduce(xs)
             elif next_norm is not None and n == T:
                 # one chunk: the combine and the next layer's input RMSNorm share a launch

@@ -981,11 +981,18 @@ def moe_combine_norm(y: torch.Tensor, topw: torch.Tensor, T: int, k: int, resid:
     return rmsnorm(resid, norm_w, h, T, eps)
 
 
-def moe_combine(y: torch.Tensor, topw: torch.Tensor, T: int, k: int, resid: torch.Tensor, alpha: float = 1.0):
+def moe_combine(y: torch.Tensor, topw: torch.Tensor, T: int, k: int, resid: torch.Tensor, alpha: float = 1.0,
+                set_: bool = False):
+    """resid[:T] += alpha * sum_j topw[t, j] * y[t*k + j]; set_: resid[:T] = ... (a partial combine from zero)."""
     D = resid.shape[1]
     if y.is_cuda:
         _lib.check(_lib.lib().nls_moe_combine(y.data_ptr(), topw.data_ptr(), T, k, resid.data_ptr(),
-                                              resid.stride(0), D, float(alpha), _stream_ptr(y)), "nls_moe_combine")
+                                              resid.stride(0), D, float(alpha), int(set_), _stream_ptr(y)),
+                   "nls_moe_combine")
         return
     yy = y[:T * k].float().view(T, k, D)
-    resid[:T] += alpha * (topw[:T * k].view(T, k, 1) * yy).sum(dim=1)
+    c = alpha * (topw[:T * k].view(T, k, 1) * yy).sum(dim=1)
+    if set_:
+        resid[:T] = c
+    else:
+        resid[:T] += c

@@ -76,7 +76,7 @@ _SIGS = {
     "nls_moe_norm_route": [c_void_p, c_long, c_void_p, c_float, c_int, c_void_p, c_void_p, c_long, c_void_p, c_int,
                            c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "nls_router_logits": [c_void_p, c_long, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p],
-    "nls_moe_combine": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p],
+    "nls_moe_combine": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_int, c_void_p],
     "nls_moe_combine_norm": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_float, c_void_p, c_float,
                              c_void_p, c_long, c_void_p],
     "nls_attn_decode": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,

@@ -61,7 +61,10 @@ def main(L=64, reps=20):
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
     W = torch.randint(0, 256, (L, NWG * NJ * NT * 16), dtype=torch.uint8, generator=g).to(dev)
-    scale = (torch.rand(L, D, generator=g) * 0.5 + 0.75) / float(np.sqrt(D * 21.25))
+    # random-sign row scales: (q - 8) has mean -1/2, so equal-sign rows would grow the all-ones direction ~7x per
+    # link (the first run's reference overflowed to NaN); with random signs E[(q-8)^2] = 21.5 keeps |x| ~ 1
+    sign = torch.randint(0, 2, (L, D), generator=g).float() * 2 - 1
+    scale = sign / float(np.sqrt(D * 21.5))
     scale = scale.to(dev)
     x0 = torch.randn(D, generator=g).to(torch.float16).to(dev)
     max_spins = 1 << 17
