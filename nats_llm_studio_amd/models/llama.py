@@ -577,11 +577,21 @@ class LlamaModel:
         rt = 2 if rows < 32 * n_exp else 4
         gu = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_GU", rt)), ks=1)
         dn = dict(mode=2, waves=8, rt=int(os.environ.get("NLS_MOE_RT_DN", rt)), ks=1)
+        kdn = int(os.environ.get("NLS_MOE_KS_DN", "1"))
+        kquant = all(int(w.type) in (12, 13, 14) for w in lw.exp_gateup + lw.exp_down)   # the DMA GEMM's types
+        if kquant and 32 * n_exp <= rows <= 96 * n_exp and os.environ.get("NLS_MOE_DMA", "1") == "1":
+            # ~32-96 routed rows per expert (Mixtral B=128-384): the LDS-DMA GEMM over 96-row blocks at two
+            # workgroups per CU, the DMA gathering each expert's rows, and the down projection split 4 ways
+            # (mapped split-K). Mixtral-8x7B B=256, per launch (profiles/moe_dma_r06.txt): gate|up 335 vs
+            # 369 us, down 168 vs 285 us. (_moe falls back to mode 2 for the down projection when it cannot split.)
+            gu = dict(mode=3, waves=4, rt=6, ks=1)
+            dn = dict(mode=3, waves=4, rt=6, ks=1)
+            kdn = int(os.environ.get("NLS_MOE_KS_DN", "4"))
         if os.environ.get("NLS_MOE_QCFG_GU"):      # explicit (mode, waves, rt) overrides
             gu = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_GU"].split(","))), ks=1)
         if os.environ.get("NLS_MOE_QCFG_DN"):
             dn = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_DN"].split(","))), ks=1)
-        return gu, dn, int(os.environ.get("NLS_MOE_KS_DN", "1"))
+        return gu, dn, kdn
 
     def _ep_a2a(self, T: int) -> bool:
         """Take the all-to-all dispatch / combine (_moe_a2a) for this MoE step? Eager EP steps of
@@ -707,6 +717,8 @@ class LlamaModel:
             if kdn > 1 and len(self.experts) <= 8 and not self.ep and T * k >= 48 * len(self.experts):
                 dn["ks"] = kdn
                 dn_rows = T * k
+            elif dn.get("mode") == 3:
+                dn = dict(mode=2, waves=8, rt=4, ks=1)      # unsplit, the LDS-dequant GEMM is ahead (285 vs 300 us)
         for c0 in range(0, T, step):
             n = min(step, T - c0)
             # few tokens: the route kernel also lists each (token, slot)'s expert and the expert GEMVs
