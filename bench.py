@@ -274,6 +274,9 @@ def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, step
                  ctx=ctx, num_blocks=None if cuda else B * ((need_tokens + 15) // 16 + 1))
     marks = []
     info_mem = dict(dense_gb=round(eng.dense_bytes / 1e9, 2), kv_pool_gb=round(eng.kv_pool_bytes / 1e9, 2))
+    if dev.type == "cuda":
+        # HBM still free after weights, copies and KV pool: what a larger pool / more requests could use
+        info_mem["hbm_free_gb"] = round(torch.cuda.mem_get_info(dev)[0] / 1e9, 1)
 
     def barrier_hook():                 # both sides of the timed region, on every rank
         sync()
@@ -453,6 +456,7 @@ def _reduce_and_report(args, world, dist, torch, dev, elapsed, tokens, info, ran
         "weights_gb_per_rank": info["weights_gb"],
         "dense_weight_copies_gb": info.get("dense_gb"),
         "kv_pool_gb": info.get("kv_pool_gb"),
+        "hbm_free_gb": info.get("hbm_free_gb"),
         "comm": info["comm_stats"],
         "timings_s": info["timings"],
         "kernels_stamp_current": _kernels_current(),
