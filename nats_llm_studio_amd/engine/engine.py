@@ -237,10 +237,13 @@ class Engine:
                 kv_need = (self.max_batch * self.ctx * 2 * self.cfg.n_layer * model.Hkv * model.D * esz
                            if num_blocks is None else 0)
                 budget = max(0, min(int(0.60 * free), int(free - kv_need / max(kv_mem_fraction, 1e-3))))
-                if self.max_batch < ops.DENSE_MIN_M:
-                    # decode never reaches the dense GEMMs at this batch: the copies would serve prompt chunks only,
-                    # so they stay small next to the KV pool (Llama-3-8B: 15 GB, kept; Llama-3-70B: 139 GB, not --
-                    # its prefill runs on the quantised mode-9 GEMMs and the pool gains those bytes)
+                frac = model.dense_decode_fraction(self.max_batch) if hasattr(model, "dense_decode_fraction") else 1.0
+                if frac < 0.5:
+                    # decode (mostly) never takes the dense GEMMs at this batch -- below ops.DENSE_MIN_M, or the tuned
+                    # "d:" entries chose the quantised GEMM: the copies would serve prompt chunks only, so they stay
+                    # small next to the KV pool (Llama-3-8B: 15 GB, kept; Llama-3-70B at B <= 128: 139 GB, not -- 29.40
+                    # vs 29.51 ms/step at B=128 without / with them, 241 vs 104 GB of HBM left, profiles/
+                    # dense_copies_policy_r06.txt; its prefill runs on the quantised mode-9 GEMMs)
                     budget = min(budget, int(0.25 * free))
             self.dense_bytes = model.expand_dense(budget, experts=os.environ.get("NLS_DENSE_EXPERTS", "0") == "1")
             if dense != "1" and self.dense_bytes == 0:

@@ -25,7 +25,7 @@ import torch
 from .. import ops
 from ..gguf.constants import GGMLType, GGML_BLOCK
 from ..gguf.reader import GGUFReader
-from ..ops import QWeight, Seg
+from ..ops import QWeight, Seg, tuning
 from .config import ModelConfig
 
 
@@ -301,6 +301,26 @@ class LlamaModel:
         if not experts:
             out.append(self.lm_head)
         return out
+
+    def dense_decode_fraction(self, M: int) -> float:
+        """Share of a decode step's dense-capable weight bytes whose launch at M rows would take the f16 copies
+        (ops.tuning.select_dense: tuned "d:" entries, -1 = the quantised GEMM measured faster). 0 below
+        ops.DENSE_MIN_M. Llama-3-70B at M = 128: 0 (every shape -1), so its 139 GB of copies would serve prompt
+        chunks only; Llama-3-8B at 512: 1."""
+        if M < ops.DENSE_MIN_M or not self.layers:
+            return 0.0
+        lw = self.layers[0]
+        groups = [list(lw.qkv), [Seg(lw.wo)]]
+        if lw.gateup is not None:
+            groups += [[Seg(lw.gateup)], [Seg(lw.down)]]
+        groups.append([Seg(self.lm_head)])
+        tot = used = 0
+        for segs in groups:
+            b = sum(s.w.dense_bytes for s in segs)
+            tot += b
+            if tuning.select_dense(segs, M) is not None:
+                used += b
+        return used / tot if tot else 0.0
 
     def expand_dense(self, budget_bytes: Optional[int] = None, experts: bool = False) -> int:
         """Give the dense_matrices() their f16 copies (ops.QWeight.expand_dense) in all-or-nothing
@@ -580,13 +600,12 @@ class LlamaModel:
         kdn = int(os.environ.get("NLS_MOE_KS_DN", "1"))
         kquant = all(int(w.type) in (12, 13, 14) for w in lw.exp_gateup + lw.exp_down)   # the DMA GEMM's types
         if kquant and 32 * n_exp <= rows <= 96 * n_exp and os.environ.get("NLS_MOE_DMA", "1") == "1":
-            # ~32-96 routed rows per expert (Mixtral B=128-384): the LDS-DMA GEMM over 96-row blocks at two
-            # workgroups per CU, the DMA gathering each expert's rows, and the down projection split 4 ways
-            # (mapped split-K). Mixtral-8x7B B=256, per launch (profiles/moe_dma_r06.txt): gate|up 335 vs
-            # 369 us, down 168 vs 285 us. (_moe falls back to mode 2 for the down projection when it cannot split.)
+            # ~32-96 routed rows per expert (Mixtral B=128-384): gate|up on the LDS-DMA GEMM over 96-row blocks at
+            # two workgroups per CU, the DMA gathering each expert's rows (286 -> 260 us per launch in the model).
+            # The down projection stays on mode 2 unsplit: in the model (Mixtral-8x7B B=256, one box) 16.45
+            # ms/step vs 16.63 with mode 3 split 4 and 18.24 split 2 (profiles/moe_dma_r06.txt; the isolated
+            # probe's 168 vs 285 us did not carry over -- the model's mode-2 down runs at ~144 us)
             gu = dict(mode=3, waves=4, rt=6, ks=1)
-            dn = dict(mode=3, waves=4, rt=6, ks=1)
-            kdn = int(os.environ.get("NLS_MOE_KS_DN", "4"))
         if os.environ.get("NLS_MOE_QCFG_GU"):      # explicit (mode, waves, rt) overrides
             gu = dict(zip(("mode", "waves", "rt"), (int(v) for v in os.environ["NLS_MOE_QCFG_GU"].split(","))), ks=1)
         if os.environ.get("NLS_MOE_QCFG_DN"):
