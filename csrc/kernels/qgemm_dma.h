@@ -25,6 +25,10 @@
 #pragma once
 #include "qgemv_impl.h"
 
+#ifndef NLS_DMA_NA
+#define NLS_DMA_NA 1     // 0: 96-row blocks multiply every tile (A/B builds)
+#endif
+
 namespace nls_dma {
 using namespace nls_gemv;
 
@@ -147,13 +151,16 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   // quarter is requested up front (2*MT ds_read_b128 in flight) and the weight fragments are
   // dequantised while they land, so the LDS latency is exposed once per quarter, not per MFMA
   // pair (hipcc otherwise issues one read, waits lgkmcnt(0), runs its RT MFMAs, and repeats).
-  auto quarter = [&](int j, int q) __attribute__((always_inline)) {
+  // NA (compile time) = the 16-row activation tiles actually multiplied: a 96-row MoE block holding <= 64 routed
+  // rows skips the padding tiles' LDS reads and MFMAs (their accumulators stay 0 and are never stored)
+  auto quarter = [&](int j, int q, auto nac) __attribute__((always_inline)) {
+    constexpr int NA = decltype(nac)::value;
     const uint8_t* xb = Xs + (j % 3) * XS;
-    f16x8 xa[2][MT];
+    f16x8 xa[2][NA];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int mt = 0; mt < NA; ++mt) {
         const int row = mt * 16 + r, c = 4 * t + g;
         xa[t][mt] = *reinterpret_cast<const f16x8*>(xb + row * 128 + ((c ^ (row & 7)) << 4));
       }
@@ -166,12 +173,12 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < NA; ++mt)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt][mt] = mfma16(xa[t][mt], wf[t][rt], acc[rt][mt]);
   };
 
-  if (nq > 0) {
+  auto main_loop = [&](auto nac) __attribute__((always_inline)) {
     // prologue: W(sb0), X(0), X(1); wait for the first two groups
     dma_w(sb0);
     dma_x(0);
@@ -187,29 +194,37 @@ DEVI void dma_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) prep_sc<T>(raw[rt], g, sc[rt]);
       dma_x(j0 + 2);
-      quarter(j0, 0);
+      quarter(j0, 0, nac);
       wait_vm_lgkm0<NX>();                      // X(j0+1) landed (X(j0+2) in flight)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // ---- q = 1: every wave has its raw regs -> stream the next super-block's weights
       dma_x(j0 + 3);
       dma_w(s + 1);
-      quarter(j0 + 1, 1);
+      quarter(j0 + 1, 1, nac);
       wait_vm_lgkm0<NX + NW>();                 // X(j0+2) landed (X(j0+3), W(s+1) in flight)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // ---- q = 2
       dma_x(j0 + 4);
-      quarter(j0 + 2, 2);
+      quarter(j0 + 2, 2, nac);
       wait_vm_lgkm0<NX + NW>();                 // X(j0+3) landed (W(s+1), X(j0+4) in flight)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // ---- q = 3
       dma_x(j0 + 5);
-      quarter(j0 + 3, 3);
+      quarter(j0 + 3, 3, nac);
       wait_vm_lgkm0<NX>();                      // W(s+1), X(j0+4) landed (X(j0+5) in flight)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+    }
+  };
+  if (nq > 0) {
+    if constexpr (MT == 6 && NLS_DMA_NA) {
+      if (M <= 64) main_loop(std::integral_constant<int, 4>{});
+      else main_loop(std::integral_constant<int, 6>{});
+    } else {
+      main_loop(std::integral_constant<int, MT>{});
     }
   }
   // drain the clamped tail DMAs before anything reuses LDS or the workgroup retires
