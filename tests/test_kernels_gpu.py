@@ -879,7 +879,7 @@ def test_qgemm_lds_swiglu_multiseg(gpu, ks):
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K])
 @pytest.mark.parametrize("M", [65, 256, 300, 520])
-@pytest.mark.parametrize("mt,ks", [(16, 1), (8, 1), (16, 3), (8, 2)])
+@pytest.mark.parametrize("mt,ks", [(16, 1), (8, 1), (16, 3), (8, 2), (6, 1), (6, 2), (4, 1), (4, 3)])
 def test_qgemm_dma(gpu, t, M, mt, ks):
     """Large-M LDS-DMA GEMM (mode 3): activation quarters and raw weight tile-blocks arrive by
     global_load_lds, weights dequantised per wave in registers; partial last 128-row weight tile and

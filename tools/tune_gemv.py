@@ -52,7 +52,7 @@ def configs(K, M=1, quant=True):
             if ks <= max(1, nb // 2):
                 c += [(1, 8, 1, ks), (1, 8, 2, ks)]
                 if quant:
-                    c += [(2, 8, 4, ks), (2, 8, 2, ks), (3, 4, 16, ks), (3, 4, 8, ks)]
+                    c += [(2, 8, 4, ks), (2, 8, 2, ks), (3, 4, 16, ks), (3, 4, 8, ks), (3, 4, 6, ks), (3, 4, 4, ks)]
                     if M >= 128:   # mode 9 (qgemm9.hip): 256 activation rows x 128 / 256 weight rows (8 waves),
                         # 128 weight rows on 4 waves (one per SIMD, 512 registers)
                         c += [(9, 8, 1, ks), (9, 8, 2, ks), (9, 4, 2, ks)]
