@@ -70,7 +70,9 @@ def dense_configs(K):
     nkt = K // 64
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
-            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
+            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
+            # 64-row activation blocks on 4 waves (2-3 workgroups per CU)
+            + [(mode, 4, 1, ks) for mode in (4, 6) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
@@ -160,8 +162,12 @@ def main():
                 qcfg = tuning.select(segs, M)
                 qus = time_cfg(copies, x, y, M, epi, keys, tuple(qcfg))
                 modes = {int(m) for m in args.modes.split(",")} if args.modes else None
-                for cfg in dense_configs(K):
-                    if modes is not None and cfg[0] not in modes:
+                cands = dense_configs(K)
+                cur = tuning.select_dense(segs, M)      # the current entry (e.g. a mode-10 winner of dense_tune.py)
+                if cur is not None and tuple(cur) not in cands:
+                    cands.append(tuple(cur))
+                for cfg in cands:
+                    if modes is not None and cfg[0] not in modes and tuple(cfg) != tuple(cur or ()):
                         continue
                     us = time_cfg(copies, x, y, M, epi, keys, cfg)
                     if us is not None:
