@@ -120,8 +120,11 @@ class GpuTelemetry:
              "n_samples": len(self.samples)}
         if self.err:
             s["error"] = self.err
+        # a timed region shorter than one sampling period (batch-1 runs) has no periodic samples: its begin / end
+        # snapshots stand in, so every record carries the clock it ran at
+        pts = self.samples or [x for x in (self.begin, self.end) if x]
         for f in self.FIELDS:
-            xs = [x[f] for x in self.samples if x.get(f) is not None]
+            xs = [x[f] for x in pts if x.get(f) is not None]
             if xs:
                 s[f] = {"min": min(xs), "mean": round(sum(xs) / len(xs), 1), "max": max(xs)}
         b, e = self.begin or {}, self.end or {}

@@ -82,3 +82,19 @@ def test_service_load_generator_cpu(tiny_models):
     for k in ("validate", "tokenize", "queue", "prefill", "decode", "respond", "total"):
         assert ph[k]["count"] == 8, (k, ph)
     assert out["engine"]["prefill_tokens"] >= 8 * 16
+
+
+def test_gpu_telemetry_summary_without_periodic_samples():
+    """A timed region shorter than the sampling period still reports its clocks (from the begin / end snapshots) and
+    the power-limit residency from the accumulated counters."""
+    from nats_llm_studio_amd.utils.telemetry import GpuTelemetry
+    t = GpuTelemetry.__new__(GpuTelemetry)
+    t.h, t.err, t.samples = object(), None, []
+    t.begin = dict(gfx_mhz=2200, mem_mhz=2000, power_w=600, hotspot_c=50, accumulation_counter=100,
+                   ppt_residency_acc=10, socket_thm_residency_acc=0)
+    t.end = dict(gfx_mhz=2000, mem_mhz=2000, power_w=1200, hotspot_c=52, accumulation_counter=300,
+                 ppt_residency_acc=110, socket_thm_residency_acc=0)
+    s = t.summary()
+    assert s["gfx_mhz"] == {"min": 2000, "mean": 2100.0, "max": 2200}
+    assert s["ppt_limited_frac"] == 0.5 and s["thermal_limited_frac"] == 0.0
+    assert "accumulation_counter" not in s["begin"]
