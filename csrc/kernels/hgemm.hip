@@ -292,7 +292,7 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
 }
 
 template <int WM, int BN, int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, WM == 1 ? 2 : (NST == 2 ? 2 : 1)) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                        int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
   constexpr int BM = HG<WM, BN, NWV, NST>::BM;
@@ -348,10 +348,6 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
   NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
   NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
   NLS_HG(2, 128, 8, 2)
-  // 64-row activation blocks on 4 waves (one per SIMD, 64 x 32 per wave, 104 VGPRs): 72 / 48 KiB of LDS with 3- / 2-deep
-  // rings, two / three workgroups per CU -- the occupancy the quantised mode 3 gained from its 64-row blocks at M = 256-512
-  // (profiles/tune_quant_mode3_r06.txt). (bn 256 at 64 rows spilled 272 B per lane: not built.)
-  NLS_HG(1, 128, 4, 3) NLS_HG(1, 128, 4, 2)
 #undef NLS_HG
   return -1;
 }

@@ -54,7 +54,6 @@ struct NlsFuse {
 //         blocks, 2: 128-row), optional split-K as mode 1.
 // mode 5: mode 4 with 256-row weight tiles (twice the MFMA work per fetched activation byte).
 // mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
-//         (modes 4 / 6 with waves 4, rt 1: 64-row activation blocks, one wave per SIMD, 2-3 workgroups per CU.)
 // mode 10: dense f16 GEMM, 256 x 256 tiles, 4 phases per 64-deep K-tile with the two wave groups staggered
 //         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
 // (Modes 11-13 -- mode 10 on raw K-quant tiles, mode 9 at 64-row blocks, stream-K -- lost every measured shape in
@@ -104,9 +103,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 ||
-      (mode == 6 && !((waves == 8 && rt == 2) || (waves == 4 && rt == 1))))
-    return -1;
+  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
   if (mode == 10) {            // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
@@ -120,10 +117,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     for (int i = 0; i < nseg; ++i)
       if (segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
   } else if (mode >= 4 && mode <= 6) {
-    // rt 4 / 2: 256 / 128-row activation blocks on 8 or 16 waves; rt 1: 64-row blocks on 4 waves
-    if (!(((waves == 8 || waves == 16) && (rt == 2 || rt == 4)) || (waves == 4 && rt == 1 && mode != 5)) || fz->xf ||
-        fz->onw ||
-        (epi == EPI_ROPE && mode == 6))
+    if ((waves != 8 && waves != 16) || (rt != 2 && rt != 4) || fz->xf || fz->onw || (epi == EPI_ROPE && mode == 6))
       return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16) return -1;

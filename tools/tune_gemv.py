@@ -70,9 +70,7 @@ def dense_configs(K):
     nkt = K // 64
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
-            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
-            # 64-row activation blocks on 4 waves (2-3 workgroups per CU)
-            + [(mode, 4, 1, ks) for mode in (4, 6) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
+            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
