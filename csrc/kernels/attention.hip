@@ -322,10 +322,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 // splits' (m, l) across its lanes into per-split weights f_s = 2^(m_s - M) / L (LDS), then each thread
 // sums f_s * O_s for 4 dims of a head over a share of the splits (16-byte loads, all independent) and
 // the shares are added through LDS. smem: >= 16 * 64 + 64 * WAVES * 4 floats.
-template <int WAVES>
+template <int WAVES, int D>
 DEVI void merge_splits(const float* __restrict__ part_o, const float* __restrict__ part_ml, int t, int kh, int G,
                        int Hq, int n_split, int na, act_t* __restrict__ out, long ldo, float* smem) {
-  constexpr int D = 128, NT = 64 * WAVES;
+  constexpr int NT = 64 * WAVES;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* f = smem;                                   // [16 heads][64 splits]
   f32x4* red = reinterpret_cast<f32x4*>(smem + 16 * 64);   // [NT] partial sums
@@ -370,14 +370,19 @@ DEVI void merge_splits(const float* __restrict__ part_o, const float* __restrict
 }
 
 
-template <typename KV, int WAVES>
+// D: head dimension, 128 (Llama / Mistral / Qwen2) or 64 (Granite-3.0): V rows of 2D bytes (D / 8 16-byte chunks, XOR
+// swizzled within the row), 32 / 64 lanes per V row on the loads
+template <typename KV, int WAVES, int D>
 __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
     const __bf16* __restrict__ q, long ldq, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_seq,
     const int* __restrict__ ctx_len, int Hkv, int G, int bs, float scale, int chunk, int n_split,
     act_t* __restrict__ out, long ldo, float* __restrict__ part_o, float* __restrict__ part_ml,
     int* __restrict__ cnt) {
-  constexpr int D = 128, NKK = D / 32, NDT = D / 16, KG = 32;
+  static_assert(D == 128 || D == 64, "head dimension");
+  constexpr int NKK = D / 32, NDT = D / 16, KG = 32;
+  constexpr int NCH = D / 8, LPR = NCH, RPI = 64 / LPR, NVL = KG / RPI;   // V: chunks per row, lanes per row,
+                                                                          // rows per load, loads per 32 keys
   typedef KVRaw<KV> R;
   // per wave: one 32-key V tile (8 KiB; a wave's LDS ops run in order, so the next group's V is written
   // after this group's transposed reads without a second buffer); the space is reused for the cross-wave
@@ -444,12 +449,15 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
     const int blk = lb == 0 ? gblk[0] : (lb == 1 ? gblk[1] : (lb == 2 ? gblk[2] : gblk[3]));
     return ((size_t)((long)blk * bs + pc % bs) * Hkv + kh) * D;
   };
-  // swizzled byte offset of 16-byte chunk ch of V row `row` (256-byte rows): conflict-free for the
-  // transposed reads and the row writes (cdna_hip_programming.md T10, layout (b))
-  auto voff = [](int row, int ch) { return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); };
-  // K of 32 keys: [n-tile][k-step]; V of 32 keys: 8 rows-of-4 per lane (row = 4i + lane / 16, chunk lane % 16)
-  typename R::raw kr[2][NKK], vr[8];
-  auto load = [&](int base, typename R::raw (&K)[2][NKK], typename R::raw (&V)[8]) __attribute__((always_inline)) {
+  // swizzled byte offset of 16-byte chunk ch of V row `row` (2D-byte rows): D = 128 conflict-free for the
+  // transposed reads and the row writes (cdna_hip_programming.md T10, layout (b)); D = 64: chunk ^ (row & 7)
+  auto voff = [](int row, int ch) {
+    if constexpr (D == 128) return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+    else return row * (2 * D) + 16 * (ch ^ (row & (NCH - 1)));
+  };
+  // K of 32 keys: [n-tile][k-step]; V of 32 keys: NVL rows per lane (row = RPI i + lane / LPR, chunk lane % LPR)
+  typename R::raw kr[2][NKK], vr[NVL];
+  auto load = [&](int base, typename R::raw (&K)[2][NKK], typename R::raw (&V)[NVL]) __attribute__((always_inline)) {
     group_blocks(base);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
@@ -458,12 +466,12 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
       for (int kk = 0; kk < NKK; ++kk) K[nt][kk] = R::ld(kc + o0 + kk * 32 + 8 * g);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) V[i] = R::ld(vc + kv_row(base + 4 * i + (lane >> 4), base) + 8 * (lane & 15));
+    for (int i = 0; i < NVL; ++i) V[i] = R::ld(vc + kv_row(base + RPI * i + lane / LPR, base) + 8 * (lane % LPR));
   };
-  auto store_v = [&](int buf, typename R::raw (&V)[8]) __attribute__((always_inline)) {
+  auto store_v = [&](int buf, typename R::raw (&V)[NVL]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      *reinterpret_cast<u32x4*>(Vs + voff(4 * i + (lane >> 4), lane & 15)) = R::bf16(V[i]);
+    for (int i = 0; i < NVL; ++i)
+      *reinterpret_cast<u32x4*>(Vs + voff(RPI * i + lane / LPR, lane % LPR)) = R::bf16(V[i]);
   };
   // wave w takes the 32-key groups w, w + WAVES, ... of the workgroup's range
   const int ngrp_all = end > start ? (end - start + KG - 1) / KG : 0;
@@ -474,7 +482,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   }
   for (int j = 0; j < ngrp; ++j) {
     const int base = start + (j * WAVES + wave) * KG;
-    typename R::raw kn[2][NKK], vn[8];
+    typename R::raw kn[2][NKK], vn[NVL];
     const bool more = j + 1 < ngrp;
     if (more) load(base + WAVES * KG, kn, vn);
     // ---- S^T = K Q^T: s[nt][i] = S[head r][key base + 16 nt + 4 g + i]
@@ -624,7 +632,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_decode_mfma_kernel(
   }
   __syncthreads();
   if (!last) return;
-  merge_splits<WAVES>(part_o, part_ml, t, kh, G, Hq, n_split, na, out, ldo,
+  merge_splits<WAVES, D>(part_o, part_ml, t, kh, G, Hq, n_split, na, out, ldo,
                       reinterpret_cast<float*>(Vsm));
 }
 
@@ -659,30 +667,38 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(T, Hkv, n_split);
-  // D = 128: the MFMA kernel -- one wave per workgroup once the grid fills the chip (>= 1K workgroups),
+  // D = 128 / 64: the MFMA kernel -- one wave per workgroup once the grid fills the chip (>= 1K workgroups),
   // else four waves splitting the workgroup's keys (more K/V in flight per (token, kv head, split): long
   // contexts at small batch). NLS_ATTN_MFMA=0 keeps the VALU kernel.
   static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
-  if (D == 128 && G <= 16 && mf != 0 && block_size >= 16 && n_split <= 64) {
+  if ((D == 128 || D == 64) && G <= 16 && mf != 0 && block_size >= 16 && n_split <= 64) {
     const bool big = (long)T * Hkv * n_split >= 1024;
     // grids of <= 256 workgroups: 8 waves each (one workgroup per CU: 192 VGPRs), so a 256-key context is one
     // pass; up to 1K workgroups: 4 waves (two per CU). NLS_ATTN_MFMA_WAVES=4|8 forces one. The split policy
     // (models/llama.py attn_splits) aims at 256 workgroups at small batch.
     static const int mwf = [] { const char* e = getenv("NLS_ATTN_MFMA_WAVES"); return e ? atoi(e) : 0; }();
     const int mw = mwf == 4 || mwf == 8 ? mwf : ((long)T * Hkv * n_split <= 256 ? 8 : 4);
-#define NLS_ATTN_M(KVT, W)                                                                                     \
-  hipLaunchKernelGGL((attn_decode_mfma_kernel<KVT, W>), grid, dim3(64 * W), 0, st, (const __bf16*)q, ldq,       \
+#define NLS_ATTN_M(KVT, W, DD)                                                                                 \
+  hipLaunchKernelGGL((attn_decode_mfma_kernel<KVT, W, DD>), grid, dim3(64 * W), 0, st, (const __bf16*)q, ldq,   \
                      (const KVT*)kc, (const KVT*)vc, block_tables, bt_stride, tok_seq, ctx_len, Hkv, G, block_size, \
                      scale, chunk, n_split, (act_t*)out, ldo, part_o, part_ml, cnt)
-    if (kv8) {
-      if (big) NLS_ATTN_M(uint8_t, 1); else if (mw == 4) NLS_ATTN_M(uint8_t, 4); else NLS_ATTN_M(uint8_t, 8);
-    } else {
-      if (big) NLS_ATTN_M(__bf16, 1); else if (mw == 4) NLS_ATTN_M(__bf16, 4); else NLS_ATTN_M(__bf16, 8);
+#define NLS_ATTN_MD(DD)                                                                                         \
+    if (kv8) {                                                                                                  \
+      if (big) NLS_ATTN_M(uint8_t, 1, DD); else if (mw == 4) NLS_ATTN_M(uint8_t, 4, DD); else NLS_ATTN_M(uint8_t, 8, DD); \
+    } else {                                                                                                    \
+      if (big) NLS_ATTN_M(__bf16, 1, DD); else if (mw == 4) NLS_ATTN_M(__bf16, 4, DD); else NLS_ATTN_M(__bf16, 8, DD);   \
     }
+    if (D == 128) { NLS_ATTN_MD(128) } else { NLS_ATTN_MD(64) }
+#undef NLS_ATTN_MD
 #undef NLS_ATTN_M
-    if (n_split > 1 && !cnt)      // (the short-context split size of the launched variant)
-      hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
-                         n_split, chunk, block_size, (act_t*)out, ldo, big ? 64 : 32 * mw);
+    if (n_split > 1 && !cnt) {    // (the short-context split size of the launched variant)
+      if (D == 128)
+        hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(T, Hq), dim3(128), 0, st, part_o, part_ml, ctx_len, Hq,
+                           n_split, chunk, block_size, (act_t*)out, ldo, big ? 64 : 32 * mw);
+      else
+        hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(T, Hq), dim3(64), 0, st, part_o, part_ml, ctx_len, Hq,
+                           n_split, chunk, block_size, (act_t*)out, ldo, big ? 64 : 32 * mw);
+    }
     return (int)hipGetLastError();
   }
   // waves per workgroup: 8 (twice the keys in flight per step) while the grid is small -- batch 1 / 16 at

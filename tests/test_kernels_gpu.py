@@ -308,13 +308,15 @@ def test_attention_paged(gpu, D, G, n_split, chunk, fused, kvt):
 @pytest.mark.parametrize("G", [4, 8, 1, 7])
 @pytest.mark.parametrize("n_split,fused", [(1, False), (4, True), (3, False)])
 @pytest.mark.parametrize("kvt", [torch.bfloat16, torch.float8_e4m3fn])
-def test_attention_decode_mfma(gpu, G, n_split, fused, kvt):
-    """The MFMA decode kernel (taken once batch x kv heads x splits >= 1K workgroups, D = 128): G query
-    heads as MFMA columns, V^T through transposed LDS reads; contexts around the 32-key groups (0, 1, 31,
-    32, 33, ...), flash-decoding splits with the fused or the separate combine, bf16 and fp8 caches."""
+@pytest.mark.parametrize("D", [128, 64])
+def test_attention_decode_mfma(gpu, G, n_split, fused, kvt, D):
+    """The MFMA decode kernel (one wave per workgroup once batch x kv heads x splits >= 1K workgroups; D = 128,
+    and since round 6 D = 64 -- Granite-3.0): G query heads as MFMA columns, V^T through transposed LDS reads;
+    contexts around the 32-key groups (0, 1, 31, 32, 33, ...), flash-decoding splits with the fused or the
+    separate combine, bf16 and fp8 caches."""
     if kvt != torch.bfloat16 and G not in (4, 1):
         pytest.skip("fp8 cache: a representative subset")
-    D, Hkv, bs, nblk = 128, 8, 16, 512
+    Hkv, bs, nblk = 8, 16, 512
     Hq = Hkv * G
     ctx = [0, 1, 31, 32, 33, 100, 300, 777] * 16
     T = len(ctx)
