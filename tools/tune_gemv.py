@@ -175,6 +175,8 @@ def main():
                 # [-1]: the quantised GEMM measured faster for this shape and batch bucket
                 table[tuning.dense_key(segs, M)] = list(best) if qus is None or best_us < qus else [-1]
                 tf = 2.0 * M * col * K
+                if qus is None:             # the quantised config failed to launch: the dense one wins by default
+                    qus = float("inf")
                 line = (f"{name:8s} M={M:4d} quant {tuple(qcfg)} {qus:8.2f}us {tf / qus / 1e6:7.1f} TF | dense best={best} "
                         f"{best_us:8.2f}us {tf / best_us / 1e6:7.1f} TF x{qus / best_us:4.2f} | "
                         + " ".join(f"{c}:{u:.1f}" for u, c in res[:4]))
