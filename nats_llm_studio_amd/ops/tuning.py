@@ -86,12 +86,16 @@ def dense_key(segs, M: int) -> str:
 
 
 def dense_heuristic(segs, M: int):
-    """Modes 4/5/6 (dense f16 GEMM): 256-row activation blocks from M >= 192 with 256-row weight tiles
-    (mode 5), then the split-K that minimises (workgroup rounds over the 256 CUs) / ks, with a small
-    per-slice cost."""
-    wm = 4 if M >= 192 else 2
+    """Modes 4/5/6 (dense f16 GEMM) for shapes without a tuned "d:" entry. Decode batches (M < 1024): 128 x 128 tiles
+    on 16 waves (mode 4, wm 2) -- what the tuner picked for nearly every Llama-3-8B / Granite-3.0-2B shape at M = 256 /
+    512, where the r05 rule (256 x 256 tiles from M >= 192) ran Granite's B=512 GEMMs 1.3-1.7x slower
+    (profiles/granite_r06.txt); prefill chunks (M >= 1024): 256-row activation blocks with 256-row weight tiles
+    (mode 5). Then the split-K that minimises (workgroup rounds over the 256 CUs) / ks, with a small per-slice cost."""
+    if M < 1024:
+        mode, bn, wm, waves = (4, 128, 2, 16) if M >= 128 else (4, 128, 2, 8)
+    else:
+        mode, bn, wm, waves = 5, 256, 4, 8
     bm = 64 * wm
-    mode, bn = (5, 256) if M >= 192 else (4, 128)
     tiles = sum((s.w.rows + bn - 1) // bn for s in segs) * ((M + bm - 1) // bm)
     nkt = segs[0].w.K // 64
     best, best_ks = None, 1
@@ -101,7 +105,7 @@ def dense_heuristic(segs, M: int):
         cost = -(-tiles * ks // 256) / ks + 0.03 * ks
         if best is None or cost < best - 1e-9:
             best, best_ks = cost, ks
-    return (mode, 8, wm, best_ks)
+    return (mode, waves, wm, best_ks)
 
 
 def select_dense(segs, M: int):
