@@ -672,7 +672,9 @@ static int attn_decode_impl(const void* q, long ldq, const void* kc, const void*
   // contexts at small batch). NLS_ATTN_MFMA=0 keeps the VALU kernel.
   static const int mf = [] { const char* e = getenv("NLS_ATTN_MFMA"); return e ? atoi(e) : -1; }();
   if ((D == 128 || D == 64) && G <= 16 && mf != 0 && block_size >= 16 && n_split <= 64) {
-    const bool big = (long)T * Hkv * n_split >= 1024;
+    // NLS_ATTN_MFMA_BIG: workgroups from which the one-wave form is taken (default 1024; A/B knob)
+    static const long big_at = [] { const char* e = getenv("NLS_ATTN_MFMA_BIG"); return e ? atol(e) : 1024L; }();
+    const bool big = (long)T * Hkv * n_split >= big_at;
     // grids of <= 256 workgroups: 8 waves each (one workgroup per CU: 192 VGPRs), so a 256-key context is one
     // pass; up to 1K workgroups: 4 waves (two per CU). NLS_ATTN_MFMA_WAVES=4|8 forces one. The split policy
     // (models/llama.py attn_splits) aims at 256 workgroups at small batch.
