@@ -59,8 +59,8 @@ def parse(argv=None):
                     help="after the timed region: N concurrent lmstudio.chat_model requests through NATS (half "
                          "sampled at temperature 0.7) against the same engine; 0 disables")
     ap.add_argument("--serve-tokens", type=int, default=256, help="max_tokens of each --serve-load request")
-    ap.add_argument("--prefill-tokens", type=int, default=int(os.environ.get("NLS_BENCH_PREFILL_TOKENS", "2048")),
-                    help="the engine's prefill chunk (tokens per prefill forward)")
+    ap.add_argument("--prefill-tokens", type=int, default=int(os.environ.get("NLS_BENCH_PREFILL_TOKENS", "4096")),
+                    help="the engine's prefill chunk (tokens per prefill forward; the worker's default; EP: <= 2048)")
     ap.add_argument("--tp-leg", type=int, default=1,
                     help="with --gpus N > 1 and --tp 1: also measure Llama-3-70B over all N ranks (tensor parallel; "
                          "reported as tp_leg); 0 disables")
@@ -261,7 +261,7 @@ def _leg(args, world, rank, local, cuda, dev, model_name, ftype, tp, ep, B, step
     sync()
     t_load = time.time() - t0
 
-    max_prefill = args.prefill_tokens
+    max_prefill = min(args.prefill_tokens, 2048) if ep else args.prefill_tokens
     # sequences prefilled early already decode while later ones prefill: budget those steps too
     prefill_steps = (B * args.prompt_len + max_prefill - 1) // max_prefill
     gen_tokens = warmup + steps + prefill_steps + 8

@@ -160,8 +160,10 @@ class EngineBackend:
                                                                      md.get("tokenizer.ggml.model", "gpt2"))
         bos = tok.tokens[tok.bos_id] if tok.bos_id is not None else ""
         eos = tok.tokens[tok.eos_id] if tok.eos_id is not None else ""
+        # EP: prefill chunks stay within the IPC row exchange's token budget (larger ones take the all-to-all)
+        mp = min(self.cfg.max_prefill_tokens, 2048) if model.ep else self.cfg.max_prefill_tokens
         eng = Engine(model, tok, max_batch=self.cfg.max_batch, ctx=self.cfg.max_ctx or None,
-                     kv_mem_fraction=self.cfg.kv_mem_fraction, max_prefill_tokens=self.cfg.max_prefill_tokens)
+                     kv_mem_fraction=self.cfg.kv_mem_fraction, max_prefill_tokens=mp)
         if eng.use_graphs and os.environ.get("NLS_CAPTURE_AT_LOAD", "1") == "1":
             eng.capture_all()      # every decode bucket's graphs now, not inside the first request burst
         if start:

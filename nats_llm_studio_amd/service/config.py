@@ -48,7 +48,9 @@ class WorkerConfig:
     max_batch: int = 64
     max_ctx: int = 0                   # 0 = model context length
     kv_mem_fraction: float = 0.5
-    max_prefill_tokens: int = 2048
+    # prefill chunk: 4096 tokens (512 burst prompts: TTFT p50 417 vs 462-481 ms at 2048, profiles/service_prefill_chunk_r06.txt);
+    # expert-parallel engines cap it at the EP row exchange's 2048 tokens (backends.py)
+    max_prefill_tokens: int = 4096
     max_loaded_models: int = 1
     default_max_tokens: int = 512
     embedded_server: bool = False      # start an in-process NATS server at nats_url's port
@@ -105,6 +107,7 @@ class WorkerConfig:
         c.max_batch = int(e.get("MAX_BATCH", c.max_batch))
         c.max_ctx = int(e.get("MAX_CTX", c.max_ctx))
         c.kv_mem_fraction = float(e.get("KV_MEM_FRACTION", c.kv_mem_fraction))
+        c.max_prefill_tokens = int(e.get("MAX_PREFILL_TOKENS", c.max_prefill_tokens))
         c.lmstudio_base_url = e.get("LMSTUDIO_BASE_URL", c.lmstudio_base_url)
         c.native_list_models = e.get("NATIVE_LIST_MODELS", "1") not in ("0", "false", "no")
         c.list_refresh_ms = float(e.get("LIST_REFRESH_MS", c.list_refresh_ms))
