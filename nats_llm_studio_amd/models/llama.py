@@ -90,6 +90,20 @@ def _raw_rows(raw: np.ndarray, ggml_type: int, rows: int, K: int, r0: int, r1: i
     return np.asarray(raw).view(np.uint8).reshape(rows, rb)[r0:r1].reshape(-1)
 
 
+def neox_pair_perm(n_heads: int, D: int) -> np.ndarray:
+    """Row order that turns NEOX RoPE pairs (i, i + D/2) of every head into adjacent pairs (2i, 2i + 1): new row
+    2i <- i, 2i + 1 <- i + D/2. Applied to the Q and K projection rows (and biases) at load, it leaves every q.k dot
+    product unchanged (the same permutation on both sides) and lets Qwen2's RoPE run in the Q|K|V GEMV epilogue, which
+    rotates adjacent pairs with pair i's frequency -- the frequency NEOX gives pair (i, i + D/2)."""
+    h = np.stack([np.arange(D // 2), np.arange(D // 2) + D // 2], 1).reshape(-1)
+    return (np.arange(n_heads)[:, None] * D + h[None, :]).reshape(-1)
+
+
+def _raw_perm_rows(raw: np.ndarray, ggml_type: int, rows: int, K: int, perm: np.ndarray) -> np.ndarray:
+    rb = ops.row_bytes(ggml_type, K)
+    return np.ascontiguousarray(np.asarray(raw).view(np.uint8).reshape(rows, rb)[perm]).reshape(-1)
+
+
 def _raw_cols(raw: np.ndarray, ggml_type: int, rows: int, K: int, k0: int, k1: int) -> np.ndarray:
     blk, nbytes = GGML_BLOCK[GGMLType(ggml_type)]
     if k0 % 256 or k1 % 256:
@@ -207,7 +221,7 @@ class LlamaModel:
         self.weight_bytes += w.nbytes
         return w
 
-    def _matrix(self, name, rows_sl=None, cols_sl=None, expert=None, layout="tiled") -> QWeight:
+    def _matrix(self, name, rows_sl=None, cols_sl=None, expert=None, layout="tiled", perm=None) -> QWeight:
         ti = self._t(name)
         shape = ti.np_shape
         raw = ti.data
@@ -223,6 +237,8 @@ class LlamaModel:
         if cols_sl is not None:
             raw = _raw_cols(raw, ti.ggml_type, rows, K, *cols_sl)
             K = cols_sl[1] - cols_sl[0]
+        if perm is not None:
+            raw = _raw_perm_rows(raw, ti.ggml_type, rows, K, perm)
         return self._qw(raw, ti.ggml_type, rows, K, name, layout)
 
     def _vec(self, name) -> torch.Tensor:
@@ -254,10 +270,17 @@ class LlamaModel:
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         self.tok_embd = self._matrix("token_embd.weight", layout="rows")      # gathered, not streamed
         self.layers: List[LayerWeights] = []
+        # NEOX RoPE (Qwen2): Q / K rows reordered so the pairs are adjacent (neox_pair_perm); the kernels then rotate
+        # adjacent pairs, fused into the Q|K|V GEMV / GEMM epilogue like Llama's (NLS_NEOX_PERMUTE=0: the separate
+        # NEOX RoPE launch, original row order)
+        permute = cfg.rope_neox and os.environ.get("NLS_NEOX_PERMUTE", "1") == "1"
+        self.rope_neox = cfg.rope_neox and not permute
+        pq = neox_pair_perm(Hq, D) if permute else None
+        pk = neox_pair_perm(Hkv, D) if permute else None
         for i in range(cfg.n_layer):
             p = f"blk.{i}."
-            wq = self._matrix(p + "attn_q.weight", (r * Hq * D, (r + 1) * Hq * D))
-            wk = self._matrix(p + "attn_k.weight", (r * Hkv * D, (r + 1) * Hkv * D))
+            wq = self._matrix(p + "attn_q.weight", (r * Hq * D, (r + 1) * Hq * D), perm=pq)
+            wk = self._matrix(p + "attn_k.weight", (r * Hkv * D, (r + 1) * Hkv * D), perm=pk)
             wv = self._matrix(p + "attn_v.weight", (r * Hkv * D, (r + 1) * Hkv * D))
             if ops.kernel_set([wq.type, wk.type, wv.type]) is None:   # e.g. Q2_K (-> F16) with a Q3_K V
                 wq, wk, wv = wq.to_f16(), wk.to_f16(), wv.to_f16()
@@ -268,6 +291,8 @@ class LlamaModel:
                 bq = self.reader.dequantized(p + "attn_q.bias").reshape(-1)[r * Hq * D:(r + 1) * Hq * D]
                 bk = self.reader.dequantized(p + "attn_k.bias").reshape(-1)[r * Hkv * D:(r + 1) * Hkv * D]
                 bv = self.reader.dequantized(p + "attn_v.bias").reshape(-1)[r * Hkv * D:(r + 1) * Hkv * D]
+                if permute:
+                    bq, bk = bq[pq], bk[pk]
                 lw.qkv_bias = torch.from_numpy(np.concatenate([bq, bk, bv]).astype(np.float32)).to(self.device)
             if cfg.n_expert:
                 lw.router = self._matrix(p + "ffn_gate_inp.weight")
@@ -454,7 +479,7 @@ class LlamaModel:
             if L > 0 and not fused_prev:
                 ops.rmsnorm(x, lw.attn_norm, b.h, T, cfg.eps)
             ops.qkv_rope_kv(lw.qkv, b.h, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
-                            cfg.rope_neox, bias=lw.qkv_bias)
+                            self.rope_neox, bias=lw.qkv_bias)
             if qblocks is not None and nqb > 0 and ops.attention_prefill_ok(Hq, Hkv, D):
                 ops.attention_prefill(b.q, kc[L], vc[L], b.block_tables, qblocks, nqb, b.tok_seq, b.ctx_len, b.ao,
                                       T, Hq, Hkv, D, block_size, cfg.attn_softmax_scale)
@@ -539,7 +564,7 @@ class LlamaModel:
         parts = None
         for L, lw in enumerate(self.layers):
             ops.qkv_rope_kv(lw.qkv, b.h, b.qkv, b.pos, b.slot, self.cs, b.q, kc[L], vc[L], T, Hq, Hkv, D,
-                            cfg.rope_neox, bias=lw.qkv_bias, norm=nrm(lw.attn_norm, parts))
+                            self.rope_neox, bias=lw.qkv_bias, norm=nrm(lw.attn_norm, parts))
             ops.attention(b.q, kc[L], vc[L], b.block_tables, b.tok_seq, b.ctx_len, b.ao, T, Hq, Hkv, D,
                           block_size, cfg.attn_softmax_scale, chunk=-_MIN_CHUNK, n_split=n_split, workspace=b.attn_ws,
                           counters=b.attn_cnt)
