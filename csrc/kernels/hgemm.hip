@@ -292,7 +292,7 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
 }
 
 template <int WM, int BN, int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+__global__ __launch_bounds__(64 * NWV, (NST == 2 || NWV == 4) ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                        int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
   constexpr int BM = HG<WM, BN, NWV, NST>::BM;
@@ -348,6 +348,7 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
   NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
   NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
   NLS_HG(2, 128, 8, 2)
+  NLS_HG(2, 64, 4, 3) NLS_HG(2, 96, 4, 3) NLS_HG(2, 128, 4, 3)
 #undef NLS_HG
   return -1;
 }

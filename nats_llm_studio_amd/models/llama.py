@@ -362,6 +362,8 @@ class LlamaModel:
                 continue
             if budget_bytes is not None and need > budget_bytes - added:
                 break
+            if not tier:   # each layer's Q|K|V copies as one buffer: one dense segment per launch
+                added += sum(QWeight.expand_dense_group([s.w for s in lw.qkv]) for lw in self.layers)
             added += sum(w.expand_dense() for w in ws)
         self.dense_bytes = getattr(self, "dense_bytes", 0) + added
         return added

@@ -186,6 +186,24 @@ class QWeight:
         self.d16 = self.dense(torch.float16).contiguous()
         return self.d16.numel() * 2
 
+    @staticmethod
+    def expand_dense_group(ws: Sequence["QWeight"]) -> int:
+        """expand_dense for matrices launched together as adjacent output columns (a layer's Q|K|V): their f16
+        copies become consecutive row ranges of ONE buffer, so a dense launch sees a single segment (_seg_arr
+        merges them) -- no partial weight tile at each segment end, e.g. 64 whole 96-row tiles for Llama-3-8B's
+        6144 Q|K|V rows instead of 43 + 11 + 11. Falls back to per-matrix copies when shapes or devices differ."""
+        ws = list(ws)
+        if (len(ws) < 2 or any(w.device.type != "cuda" or w.layout != "tiled" or w.d16 is not None for w in ws)
+                or len({w.K for w in ws}) != 1 or len({str(w.device) for w in ws}) != 1):
+            return sum(w.expand_dense() for w in ws)
+        buf = torch.empty(sum(w.rows for w in ws), ws[0].K, dtype=torch.float16, device=ws[0].device)
+        r0 = 0
+        for w in ws:
+            buf[r0:r0 + w.rows].copy_(w.dense(torch.float16))
+            w.d16 = buf[r0:r0 + w.rows]
+            r0 += w.rows
+        return buf.numel() * 2
+
     @property
     def dense_bytes(self) -> int:
         return self.rows * self.K * 2
@@ -276,19 +294,41 @@ def gemv_config(segs: Sequence[Seg], M: int):
     return tuning.select(segs, M)
 
 
+DENSE_MODES = (4, 5, 6, 7, 10)
+
+
+def _merge_dense(segs: Sequence[Seg]):
+    """[d16 pointer, rows, K, ycol, seg] per launch segment: adjacent unmapped segments whose f16 copies are consecutive
+    rows of one buffer (QWeight.expand_dense_group) and whose output columns are adjacent merge into one."""
+    out = []
+    for s in segs:
+        if s.w.d16 is None:
+            raise ValueError(f"{s.w.name}: dense modes {DENSE_MODES} need QWeight.expand_dense()")
+        p = s.w.d16.data_ptr()
+        plain = s.xmap is None and s.ymap is None and s.mcount is None
+        if out and plain and out[-1][4].xmap is None and out[-1][4].ymap is None and out[-1][4].mcount is None:
+            q, rows, K, ycol, s0 = out[-1]
+            if K == s.w.K and q + rows * K * 2 == p and ycol + rows == s.ycol:
+                out[-1] = [q, rows + s.w.rows, K, ycol, s0]
+                continue
+        out.append([p, s.w.rows, s.w.K, s.ycol, s])
+    return out
+
+
 def _seg_arr(segs: Sequence[Seg], mode: int):
-    """ctypes segment list of a launch: modes 4/5 point at the row-major f16 copies (MoE row maps
-    included: the dense GEMM gathers/scatters mapped rows like mode 2)."""
+    """ctypes segment list of a launch (pass len(arr) as the segment count): the dense modes point at the row-major
+    f16 copies, adjacent copies of one buffer merged into one segment (_merge_dense); MoE row maps included (the
+    dense GEMM gathers/scatters mapped rows like mode 2)."""
+    if mode in DENSE_MODES:
+        merged = _merge_dense(segs)
+        arr = (_lib.NlsSeg * len(merged))()
+        for i, (p, rows, K, ycol, s) in enumerate(merged):
+            arr[i] = _lib.NlsSeg(p, _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, rows, K, ycol)
+        return arr
     arr = (_lib.NlsSeg * len(segs))()
     for i, s in enumerate(segs):
-        if mode in (4, 5, 6, 10):
-            if s.w.d16 is None:
-                raise ValueError(f"{s.w.name}: dense modes (4-6, 10) need QWeight.expand_dense()")
-            arr[i] = _lib.NlsSeg(s.w.d16.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), 1, s.w.rows, s.w.K,
-                                 s.ycol)
-        else:
-            arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows,
-                                 s.w.K, s.ycol)
+        arr[i] = _lib.NlsSeg(s.w.data.data_ptr(), _p(s.xmap), _p(s.ymap), _p(s.mcount), s.w.type, s.w.rows, s.w.K,
+                             s.ycol)
     return arr
 
 
@@ -381,7 +421,7 @@ def qgemv(segs: Sequence[Seg], x: torch.Tensor, y: torch.Tensor, M: int, alpha: 
         if mode != 0 and ks > 1:
             width = segs[0].w.rows if mapped else sum(s.w.rows for s in segs)   # mapped split-K: shared columns
             ws = _workspace(x.device, ks * M * width).data_ptr()
-        rc = L.nls_qgemv(arr, len(segs), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
+        rc = L.nls_qgemv(arr, len(arr), x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), M, float(alpha),
                          EPI[epi], _p(argmax), waves, rt, mode, ks, ws, _stream_ptr(x))
         _lib.check(rc, "nls_qgemv")
         return y
@@ -644,14 +684,15 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        if (mode in (4, 5, 10) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D
+        if (mode in (4, 5, 7, 10) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D
                 and not neox and fuse_rope and kc.dtype == torch.bfloat16):
             # large-M GEMM on the dense f16 copies with RoPE + KV append in its epilogue (no f32 qkv round trip,
             # no RoPE launch)
             fz = _lib.NlsFuse(pos=pos.data_ptr(), slot=slot.data_ptr(), cs=cs.data_ptr(), bias=_p(bias),
                               q_out=q_out.data_ptr(), ldq=q_out.stride(0), kc=kc.data_ptr(), vc=vc.data_ptr(),
                               Hq=Hq, Hkv=Hkv, D=D)
-            _lib.check(_lib.lib().nls_qgemv_ex(_seg_arr(segs, mode), len(segs), h.data_ptr(), h.stride(0),
+            arr = _seg_arr(segs, mode)
+            _lib.check(_lib.lib().nls_qgemv_ex(arr, len(arr), h.data_ptr(), h.stride(0),
                                                qkv.data_ptr(), qkv.stride(0), T, 1.0, EPI["rope"], None, waves, rt,
                                                mode, 1, None, _stream_ptr(h), ctypes.byref(fz)),
                        "nls_qgemv_ex(dense rope)")
@@ -661,7 +702,7 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
             ws = _workspace(h.device, ks * T * ncol)
             arr = _seg_arr(segs, mode)
             st = _stream_ptr(h)
-            _lib.check(L.nls_qgemv(arr, len(segs), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
+            _lib.check(L.nls_qgemv(arr, len(arr), h.data_ptr(), h.stride(0), qkv.data_ptr(), qkv.stride(0), T, 1.0,
                                    EPI["slabs"], None, waves, rt, mode, ks, ws.data_ptr(), st), "nls_qgemv")
             _lib.check(_kv_fn("nls_rope_kv", kc)(ws.data_ptr(), ncol, ks, T * ncol, _p(bias), pos.data_ptr(),
                                                  slot.data_ptr(),

@@ -35,6 +35,11 @@ def table():
             with open(_PATH) as f:
                 _TABLE = {k: tuple(v) for k, v in json.load(f).items()}
         # A/B overrides without editing the table: NLS_TUNING_EXTRA='{"<key>": [..], ...}'
+        # ... or from a file (NLS_TUNING_EXTRA_FILE, e.g. a fresh tune_gemv.py --out table), applied first
+        path = os.environ.get("NLS_TUNING_EXTRA_FILE")
+        if path:
+            with open(path) as f:
+                _TABLE.update({k: tuple(v) for k, v in json.load(f).items()})
         extra = os.environ.get("NLS_TUNING_EXTRA")
         if extra:
             _TABLE.update({k: tuple(v) for k, v in json.loads(extra).items()})

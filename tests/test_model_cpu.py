@@ -189,3 +189,26 @@ def test_tuning_role_fallback_scope(monkeypatch):
     assert tuning.select(qwen_gu, 16) == tuning.heuristic(qwen_gu, 16)
     monkeypatch.setitem(tab, tuning.key(qwen_gu, 16), (0, 4, 1, 1))
     assert tuning.select(qwen_gu, 16) == (0, 4, 1, 1)
+
+
+def test_dense_segment_merge():
+    """Dense launches see one segment per run of f16 copies that are consecutive rows of one buffer with adjacent
+    output columns (a layer's Q|K|V after QWeight.expand_dense_group); separate buffers, gaps in the output columns
+    and mapped (MoE) segments stay apart."""
+    from types import SimpleNamespace as NS
+    from nats_llm_studio_amd import ops
+    K = 64
+    buf = torch.zeros(96 + 32 + 32, K, dtype=torch.float16)
+    q, k, v = (NS(name=n, rows=r, K=K, d16=buf[a:a + r]) for n, r, a in (("q", 96, 0), ("k", 32, 96), ("v", 32, 128)))
+    m = ops._merge_dense([ops.Seg(q, 0), ops.Seg(k, 96), ops.Seg(v, 128)])
+    assert [(x[0], x[1], x[3]) for x in m] == [(buf.data_ptr(), 160, 0)]
+    other = NS(name="o", rows=32, K=K, d16=torch.zeros(32, K, dtype=torch.float16))
+    m = ops._merge_dense([ops.Seg(q, 0), ops.Seg(k, 96), ops.Seg(other, 128)])
+    assert [x[1] for x in m] == [128, 32]
+    m = ops._merge_dense([ops.Seg(q, 0), ops.Seg(k, 100)])            # output columns not adjacent
+    assert [x[1] for x in m] == [96, 32]
+    xm = torch.zeros(4, dtype=torch.int32)
+    m = ops._merge_dense([ops.Seg(q, 0, xm, xm), ops.Seg(k, 96, xm, xm)])
+    assert [x[1] for x in m] == [96, 32] and m[1][4].xmap is xm
+    with pytest.raises(ValueError):
+        ops._merge_dense([ops.Seg(NS(name="n", rows=8, K=K, d16=None), 0)])

@@ -70,7 +70,8 @@ def dense_configs(K):
     nkt = K // 64
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
-            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
+            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
+            + [(7, 4, rt, ks) for rt in (2, 3, 4) for ks in range(1, 5) if ks == 1 or nkt // ks >= 4])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
@@ -145,10 +146,10 @@ def main():
                 w.__dict__.update(s_old.w.__dict__)
                 w.data = s_old.w.data.clone()
         if args.dense:
-            for cp in copies:
+            for cp in copies:       # Q|K|V copies as one buffer, as the model loads them (one merged segment)
                 for s_ in cp:
                     s_.w.d16 = None
-                    s_.w.expand_dense()
+                ops.QWeight.expand_dense_group([s_.w for s_ in cp])
         ncol = col // 2 if epi == "swiglu" else col
         mmax = max(64, max(Ms))
         x = torch.randn(mmax, K, device=dev).to(ops.ACT_DTYPE)
