@@ -243,13 +243,23 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     int rc;
     if (mode == 10)
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
-    else if (mode == 7)
-      rc = nls_hgemm::launch_dense(2, 32 * rt, 4, 3, sl, tiles, ks, (float*)ws, a, st);
+    else if (mode == 7) {
+      static const int nst = [] {   // ring depth: 5 (default) or 3 (NLS_M7_NST=3, A/B)
+        const char* e = getenv("NLS_M7_NST");
+        return e && atoi(e) == 3 ? 3 : 5;
+      }();
+      rc = nls_hgemm::launch_dense(2, 32 * rt, 4, nst, sl, tiles, ks, (float*)ws, a, st);
+    }
     else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st, 256);
-    else if (mode >= 4)
-      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : 3, sl, tiles, ks, (float*)ws, a,
-                                   st);
+    else if (mode >= 4) {
+      static const int m4nst = [] {   // mode 4 at 128-row activation blocks: ring depth 3 (default) or 5 (A/B)
+        const char* e = getenv("NLS_M4_NST");
+        return e && atoi(e) == 5 ? 5 : 3;
+      }();
+      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : (mode == 4 && rt == 2 ? m4nst : 3),
+                                   sl, tiles, ks, (float*)ws, a, st);
+    }
     else if (mode == 3)
       rc = (kset == 0 ? nls_dma::launch_dma_k0 : nls_dma::launch_dma_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 2)
