@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--type", default="Q4_K")
     ap.add_argument("--dense", action="store_true", help="give the weight its f16 copy (mode 4 eligible)")
+    ap.add_argument("--ldx-pad", type=int, default=0, help="activation row stride = K + this (elements)")
     args = ap.parse_args()
     spec = SPECS[args.model]
     d, hd = spec.d_model, spec.head_dim
@@ -47,7 +48,7 @@ def main():
         w.expand_dense()
     segs = [ops.Seg(w, 0)]
     M = args.M
-    x = (torch.randn(M, K, device=dev) * 0.5).to(ops.ACT_DTYPE)
+    x = (torch.randn(M, K + args.ldx_pad, device=dev) * 0.5).to(ops.ACT_DTYPE)[:, :K]
     ncol = rows // 2 if epi == "swiglu" else rows
     y = torch.zeros(M, ncol, dtype=ops.ACT_DTYPE if epi == "swiglu" else torch.float32, device=dev)
     kw = {}
