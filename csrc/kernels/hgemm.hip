@@ -46,9 +46,8 @@ struct HG {
   static constexpr int XS = BM * 128;         // bytes of one activation stage [BM][64] f16
   static constexpr int WSB = BN * 128;        // bytes of one weight stage [BN][64] f16
   static constexpr int NSX = NST;             // activation ring depth
-  // weight ring depth (LDS budget); NST = 2: both rings 2 deep, small enough for 2 workgroups per CU; NST >= 4
-  // (mode 7's one wave per SIMD): both rings NST deep, NST - 2 K-steps of loads in flight behind the one computing
-  static constexpr int NSW = NST == 2 ? 2 : NST >= 4 ? NST : ((NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2);
+  // weight ring depth (LDS budget); NST = 2: both rings 2 deep, small enough for 2 workgroups per CU
+  static constexpr int NSW = NST == 2 ? 2 : ((NSX * XS + 3 * WSB <= 160 * 1024) ? 3 : 2);
   static constexpr int NX = BM / 8 / NWV;     // activation DMA instructions per wave per stage
   static constexpr int NW = BN / 8 / NWV;     // weight DMA instructions per wave per stage
   static_assert(NX >= 1 && NW >= 1 && NTW >= 1, "tile too small for the wave count");
@@ -133,27 +132,7 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
   };
 
   if (nq > 0) {
-    if constexpr (NST >= 4) {
-      // both rings NST deep: steps j+1 .. j+NST-2 in flight while step j computes (HBM latency at one wave per
-      // SIMD is several K-steps of MFMA work)
-      static_assert((NST - 2) * (NX + NW) <= 63, "vmcnt range");
-#pragma unroll
-      for (int p = 0; p < NST - 1; ++p) {
-        dma_w(p);
-        dma_x(p);
-      }
-      wait_vm_lgkm0<(NST - 2) * (NX + NW)>();   // step 0 landed
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      for (int j = 0; j < nq; ++j) {
-        dma_w(j + NST - 1);                     // slots (j-1)%NST were last read in step j-1: retired
-        dma_x(j + NST - 1);
-        step(j);
-        wait_vm_lgkm0<(NST - 2) * (NX + NW)>(); // step j+1 landed
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-    } else if constexpr (G::NSW == 3) {
+    if constexpr (G::NSW == 3) {
       // both rings 3 deep: steps j+1 and j+2 in flight while step j computes
       dma_w(0);
       dma_x(0);
@@ -319,7 +298,7 @@ DEVI void hgemm_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs&
 }
 
 template <int WM, int BN, int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, (NST == 2 || NWV == 4) ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
+__global__ __launch_bounds__(64 * NWV, NST == 2 ? 2 : 1) void hgemm_kernel(SegList segs, GemvArgs a, int ks, float* ws, int ntiles,
                                                        int nmb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t hlds[];
   constexpr int BM = HG<WM, BN, NWV, NST>::BM;
@@ -375,9 +354,6 @@ int launch_dense(int wm, int bn, int waves, int nst, const SegList& sl, int ntil
   NLS_HG(4, 128, 8, 3) NLS_HG(2, 128, 8, 3) NLS_HG(4, 256, 8, 3) NLS_HG(2, 256, 8, 3)
   NLS_HG(4, 128, 16, 3) NLS_HG(2, 128, 16, 3) NLS_HG(4, 256, 16, 3) NLS_HG(2, 256, 16, 3)
   NLS_HG(2, 128, 8, 2)
-  NLS_HG(2, 64, 4, 3) NLS_HG(2, 96, 4, 3) NLS_HG(2, 128, 4, 3)
-  NLS_HG(2, 64, 4, 5) NLS_HG(2, 96, 4, 5) NLS_HG(2, 128, 4, 5)
-  NLS_HG(2, 128, 16, 5) NLS_HG(2, 128, 8, 5)
 #undef NLS_HG
   return -1;
 }

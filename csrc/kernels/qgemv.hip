@@ -54,9 +54,6 @@ struct NlsFuse {
 //         blocks, 2: 128-row), optional split-K as mode 1.
 // mode 5: mode 4 with 256-row weight tiles (twice the MFMA work per fetched activation byte).
 // mode 6: mode 4 at 128-row activation blocks (rt 2) with 2-deep rings: two workgroups per CU.
-// mode 7: narrow dense f16 GEMM (hgemm.hip, 4 waves): 128-row activation blocks x 32*rt weight rows (rt 2/3/4:
-//         64/96/128), one wave per SIMD with a 64 x 16*rt accumulator block: enough workgroups to fill 256 CUs
-//         on the narrow decode shapes (Q|K|V, o at M = 512: 256 tiles) without split-K.
 // mode 10: dense f16 GEMM, 256 x 256 tiles, 4 phases per 64-deep K-tile with the two wave groups staggered
 //         by one barrier (hgemm10.hip); the mode-8 operands and epilogues, optional split-K.
 // (Modes 11-13 -- mode 10 on raw K-quant tiles, mode 9 at 64-row blocks, stream-K -- lost every measured shape in
@@ -81,7 +78,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   }
   if (epi == EPI_ROPE) {   // fused RoPE / KV append: path A or a dense GEMM without split-K; plain rows,
                            // contiguous Q|K|V segments
-    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 7 || mode == 10) && ks <= 1)) || argmax ||
+    if (!(mode == 0 || ((mode == 4 || mode == 5 || mode == 10) && ks <= 1)) || argmax ||
         !fz->pos || !fz->slot ||
         !fz->cs || !fz->q_out || !fz->kc || !fz->vc || fz->D < 2 || fz->D % 2 || fz->Hq < 1 || fz->Hkv < 1)
       return -1;
@@ -106,17 +103,13 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   if (nseg < 1 || nseg > 8 || M < 1 ||
       (waves != 4 && waves != 8 && !(waves == 16 && mode >= 4) && !(waves == 7 && mode == 1 && rt == 1 && M == 1)))
     return -1;
-  if (mode < 0 || mode > 10 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
+  if (mode < 0 || mode > 10 || mode == 7 || mode == 8 || (mode == 6 && (waves != 8 || rt != 2))) return -1;
   if (mode == 10) {            // rt 1: 256-row weight tiles, rt 2: 128-row
     if (waves != 8 || (rt != 1 && rt != 2) || fz->xf || fz->onw || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
       return -1;
     for (int i = 0; i < nseg; ++i)
       if (segs[i].type != QT_F16 || segs[i].xmap || segs[i].ymap || segs[i].mcount || segs[i].ycol % 4) return -1;
-  } else if (mode == 7) {
-    if (waves != 4 || rt < 2 || rt > 4 || fz->xf || fz->onw) return -1;
-    for (int i = 0; i < nseg; ++i)
-      if (segs[i].type != QT_F16) return -1;
   } else if (mode == 9) {
     if (!((waves == 4 && rt == 2) || (waves == 8 && (rt == 2 || rt == 1))) || fz->xf || fz->onw || epi == EPI_ROPE || ldx % 8 ||
         ((epi == EPI_F32 || epi == EPI_ADD_F32 || epi == EPI_ACT) && ldy % 4))
@@ -142,7 +135,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     mks = segs[i].ymap && segs[i].ycol == 0 && segs[i].rows == segs[0].rows;
   SegList sl{};
   int tiles = 0, cols = 0;
-  const int tile_rows = mode == 10 ? 256 / rt : mode == 7 ? 32 * rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
+  const int tile_rows = mode == 10 ? 256 / rt : mode == 9 ? 16 * waves * rt : (mode == 5 ? 256 : (mode >= 2 ? 128 : (mode == 1 ? waves : 1) * rt * 16));
   for (int i = 0; i < nseg; ++i) {
     if (segs[i].K % 256 || segs[i].rows < 1) return -1;
     if (epi == EPI_SWIGLU && segs[i].rows % 16) return -1;
@@ -217,7 +210,7 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     const char* e = getenv("NLS_HG_KROT");
     return e ? atoi(e) : 0;
   }();
-  a.krot = (mode >= 4 && mode <= 7) || mode == 10 ? krot : 0;
+  a.krot = (mode >= 4 && mode <= 6) || mode == 10 ? krot : 0;
   if (fz->sel) tiles = fz->sel_slots * a.sel_tiles;
   a.wr = (const act_t*)fz->wr;
   a.E = fz->E;
@@ -248,23 +241,11 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
     int rc;
     if (mode == 10)
       rc = nls_hg10::launch_dense10(256 / rt, sl, tiles, ks, (float*)ws, a, st);
-    else if (mode == 7) {
-      static const int nst = [] {   // ring depth: 5 (default) or 3 (NLS_M7_NST=3, A/B)
-        const char* e = getenv("NLS_M7_NST");
-        return e && atoi(e) == 3 ? 3 : 5;
-      }();
-      rc = nls_hgemm::launch_dense(2, 32 * rt, 4, nst, sl, tiles, ks, (float*)ws, a, st);
-    }
     else if (mode == 9)
       rc = nls_q9::launch_q9(kset, waves, rt, sl, tiles, ks, (float*)ws, a, st, 256);
-    else if (mode >= 4) {
-      static const int m4nst = [] {   // mode 4 at 128-row activation blocks: ring depth 3 (default) or 5 (A/B)
-        const char* e = getenv("NLS_M4_NST");
-        return e && atoi(e) == 5 ? 5 : 3;
-      }();
-      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : (mode == 4 && rt == 2 ? m4nst : 3),
-                                   sl, tiles, ks, (float*)ws, a, st);
-    }
+    else if (mode >= 4)
+      rc = nls_hgemm::launch_dense(rt, mode == 5 ? 256 : 128, waves, mode == 6 ? 2 : 3, sl, tiles, ks, (float*)ws, a,
+                                   st);
     else if (mode == 3)
       rc = (kset == 0 ? nls_dma::launch_dma_k0 : nls_dma::launch_dma_k1)(rt, sl, tiles, ks, (float*)ws, a, st);
     else if (mode == 2)

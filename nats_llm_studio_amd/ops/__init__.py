@@ -294,7 +294,7 @@ def gemv_config(segs: Sequence[Seg], M: int):
     return tuning.select(segs, M)
 
 
-DENSE_MODES = (4, 5, 6, 7, 10)
+DENSE_MODES = (4, 5, 6, 10)
 
 
 def _merge_dense(segs: Sequence[Seg]):
@@ -684,7 +684,7 @@ def qkv_rope_kv(segs: Sequence[Seg], h: torch.Tensor, qkv: torch.Tensor, pos: to
         mode, waves, rt, ks = cfg or gemv_config(segs, T)
         ncol = sum(s.w.rows for s in segs)
         contiguous = all(s.ycol == sum(x.w.rows for x in segs[:i]) for i, s in enumerate(segs))
-        if (mode in (4, 5, 7, 10) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D
+        if (mode in (4, 5, 10) and ks == 1 and contiguous and ncol == (Hq + 2 * Hkv) * D
                 and not neox and fuse_rope and kc.dtype == torch.bfloat16):
             # large-M GEMM on the dense f16 copies with RoPE + KV append in its epilogue (no f32 qkv round trip,
             # no RoPE launch)

@@ -70,8 +70,7 @@ def dense_configs(K):
     nkt = K // 64
     return ([(mode, wv, wm, ks) for mode in (5, 4) for wv in (8, 16) for wm in (4, 2) for ks in range(1, 9)
              if ks == 1 or nkt // ks >= 4]
-            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4]
-            + [(7, 4, rt, ks) for rt in (2, 3, 4) for ks in range(1, 5) if ks == 1 or nkt // ks >= 4])
+            + [(6, 8, 2, ks) for ks in range(1, 9) if ks == 1 or nkt // ks >= 4])
 
 
 def time_cfg(copies, x, y, M, epi, keys, cfg):
