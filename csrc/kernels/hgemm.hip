@@ -69,8 +69,6 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
   const int wm = wave / WN, wn = wave % WN;
   const int nq = kt1 - kt0;
   const int M = a.M;
-  // K rotation (GemvArgs::krot): this weight tile's first K-step; every m-block / k-slice of the tile shares it
-  const int rot = (a.krot && nq > 0) ? (int)(((long)(row0 / BN + S.tile_begin) * a.krot) % nq) : 0;
 
   // ---- per-lane DMA sources: a DMA group is 8 rows starting at a multiple of 8, lane -> row
   // group_row + (lane >> 3), physical chunk lane & 7 <- logical chunk (lane & 7) ^ (lane >> 3)
@@ -93,18 +91,14 @@ DEVI void hg_main(const Seg& S, int row0, int kt0, int kt1, const GemvArgs& a, u
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint32_t xl = base + (uint32_t)(NX * wave) * 1024u;
   const uint32_t wl = base + G::NSX * G::XS + (uint32_t)(NW * wave) * 1024u;
-  auto kstep = [&](int j) __attribute__((always_inline)) {    // K-step of loop step j (clamped, rotated)
-    const int k = min(j, nq - 1) + rot;
-    return k >= nq ? k - nq : k;
-  };
   auto dma_x = [&](int j) __attribute__((always_inline)) {    // K-step j (clamped) -> x slot j % NSX
-    const int koff = kstep(j) * 64;
+    const int koff = min(j, nq - 1) * 64;
     const uint32_t so = (uint32_t)(j % G::NSX) * G::XS;
 #pragma unroll
     for (int i = 0; i < NX; ++i) glds16(xsrc[i] + koff, xl + so + i * 1024);
   };
   auto dma_w = [&](int j) __attribute__((always_inline)) {    // K-step j (clamped) -> W slot j % NSW
-    const int koff = kstep(j) * 64;
+    const int koff = min(j, nq - 1) * 64;
     const uint32_t so = (uint32_t)(j % G::NSW) * G::WSB;
 #pragma unroll
     for (int i = 0; i < NW; ++i) glds16(wsrc[i] + koff, wl + so + i * 1024);

@@ -197,8 +197,6 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   const int nkt = t1 - t0;
   const int M = a.M;
   const act_t* Wd = reinterpret_cast<const act_t*>(S.w);
-  // K rotation (GemvArgs::krot), shared by every m-block / k-slice of the weight tile
-  const int rot = (a.krot && nkt > 0) ? (int)(((long)(row0 / BN + S.tile_begin) * a.krot) % nkt) : 0;
 
   // ---- DMA: unit u of K-tile T -> buffer T & 1. This wave issues subtiles idx = n * wave + j (j < n; n = 2,
   // or NA for a weight unit) of every unit: row-tile unit_rt(u, idx >> 1), k-step idx & 1. Lane L -> row
@@ -206,8 +204,7 @@ DEVI void h10_tile(const Seg& S, int row0, int kslice, int ks, const GemvArgs& a
   const int lc = (lane & 3) ^ swz(lane >> 2);
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   auto dma = [&](int u, int T) __attribute__((always_inline)) {
-    int Tr = min(T, nkt - 1) + rot;            // clamped: past the end re-stages the last tile (same bytes)
-    const int Tc = t0 + (Tr >= nkt ? Tr - nkt : Tr);
+    const int Tc = t0 + min(T, nkt - 1);       // clamped: past the end re-stages the last tile (same bytes)
     const bool bu = u == 1 || u == 2;
     const uint32_t buf = base + (uint32_t)(T & 1) * TB + (bu ? (uint32_t)C::AB : 0u);
     const int n = bu ? 2 : NA;

@@ -206,11 +206,6 @@ static int qgemv_impl(const NlsSeg* segs, int nseg, const void* x, long ldx, voi
   a.sel = fz->sel;
   a.sel_base = fz->sel_base;
   a.sel_tiles = (segs[0].rows + tile_rows - 1) / tile_rows;
-  static const int krot = [] {   // dense-GEMM K rotation per weight tile (A/B knob, default off)
-    const char* e = getenv("NLS_HG_KROT");
-    return e ? atoi(e) : 0;
-  }();
-  a.krot = (mode >= 4 && mode <= 6) || mode == 10 ? krot : 0;
   if (fz->sel) tiles = fz->sel_slots * a.sel_tiles;
   a.wr = (const act_t*)fz->wr;
   a.E = fz->E;

@@ -64,10 +64,7 @@ struct GemvArgs {
   // device-selected segments (MoE decode, few tokens): workgroup i serves segment sel[i / sel_tiles] -
   // sel_base (out of range or a repeat of an earlier slot: exit), tile i % sel_tiles of it -- only the
   // routed experts' tiles are launched instead of every expert's (most of which would exit at once)
-  const int* sel; int sel_tiles, sel_base;
-  // dense GEMMs (modes 4-7, 10): weight tile t starts its K loop at K-step (t * krot) mod nsteps and wraps, so
-  // the tiles streaming at one instant read different K columns (L2 channel spread; 0 = off, A/B: NLS_HG_KROT)
-  int krot;
+  const int* sel; int sel_tiles, sel_base, pad1;
   // MoE decode (with onw): after the residual update + FFN RMSNorm the last workgroup also computes the router
   // logits hout . wr[e] (wr: the router's f16 copy [E][D]) and the top-k route (route_one) -- the separate
   // norm + router + route launch folded away. counts [E] are zeroed here first.
