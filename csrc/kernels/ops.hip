@@ -68,6 +68,12 @@ __global__ __launch_bounds__(512) void rmsnorm_kernel(const float* __restrict__ 
 // Fused split-K reduce + residual add + RMSNorm (row-parallel projections): the GEMM left
 // ks fp32 partial slabs ws[k][M][D]; x[m] += alpha * sum_k ws[k][m] (fixed order: deterministic),
 // then out[m] = f16(rmsnorm(x[m]) * w). One launch instead of reduce + norm, and x is read once.
+#ifndef NLS_SLAB_RUNTIME
+#define NLS_SLAB_RUNTIME 0   // 1: always the runtime-ks kernels (A/B build tag)
+#endif
+// KS > 0: the split count as a constant -- every slab load of the row is issued before the first add (ks is a
+// runtime loop bound otherwise, and each slab's loads wait for the previous add chain); KS = 0: any ks.
+template <int KS>
 __global__ __launch_bounds__(512) void splitk_add_rmsnorm_kernel(const float* __restrict__ ws, int ks, int M,
                                                                  float alpha, float* __restrict__ x, long ldx,
                                                                  const float* __restrict__ w,
@@ -78,6 +84,7 @@ __global__ __launch_bounds__(512) void splitk_add_rmsnorm_kernel(const float* __
   float* xr = x + (size_t)m * ldx;
   float4 v[4], wv[4];
   float ss = 0.f;
+  const int nk = KS > 0 ? KS : ks;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = (threadIdx.x + j * 512) * 4;
@@ -88,9 +95,19 @@ __global__ __launch_bounds__(512) void splitk_add_rmsnorm_kernel(const float* __
     const int i = (threadIdx.x + j * 512) * 4;
     if (i < D) {
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int k = 0; k < ks; ++k) {
-        const float4 p = *reinterpret_cast<const float4*>(ws + ((size_t)k * M + m) * D + i);
-        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+      if constexpr (KS > 0) {
+        float4 p[KS];
+#pragma unroll
+        for (int k = 0; k < KS; ++k) p[k] = *reinterpret_cast<const float4*>(ws + ((size_t)k * M + m) * D + i);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          acc.x += p[k].x; acc.y += p[k].y; acc.z += p[k].z; acc.w += p[k].w;
+        }
+      } else {
+        for (int k = 0; k < nk; ++k) {
+          const float4 p = *reinterpret_cast<const float4*>(ws + ((size_t)k * M + m) * D + i);
+          acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+        }
       }
       float4 r = *reinterpret_cast<const float4*>(xr + i);
       r.x += alpha * acc.x; r.y += alpha * acc.y; r.z += alpha * acc.z; r.w += alpha * acc.w;
@@ -138,7 +155,7 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 // `ks` > 1: the QKV projection left split-K partial slabs (qkv = ks slabs of [T][ldqkv], stride
 // `slab` floats) and this kernel sums them in fixed order while rotating (fused reduce + RoPE).
-template <typename KV>
+template <typename KV, int KS = 0>     // KS > 0: the slab count as a constant (all slab loads issued first)
 __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, long ldqkv, int ks, long slab,
                                                       const float* __restrict__ bias,
                                                       const int* __restrict__ pos,
@@ -151,10 +168,22 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
   const int t = blockIdx.x;
   const float* row = qkv + (size_t)t * ldqkv;
   auto ld4 = [&](int col) {
-    float4 v = *reinterpret_cast<const float4*>(row + col);
-    for (int k = 1; k < ks; ++k) {
-      const float4 u = *reinterpret_cast<const float4*>(row + (size_t)k * slab + col);
-      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    float4 v;
+    if constexpr (KS > 0) {
+      float4 u[KS];
+#pragma unroll
+      for (int k = 0; k < KS; ++k) u[k] = *reinterpret_cast<const float4*>(row + (size_t)k * slab + col);
+      v = u[0];
+#pragma unroll
+      for (int k = 1; k < KS; ++k) {
+        v.x += u[k].x; v.y += u[k].y; v.z += u[k].z; v.w += u[k].w;
+      }
+    } else {
+      v = *reinterpret_cast<const float4*>(row + col);
+      for (int k = 1; k < ks; ++k) {
+        const float4 u = *reinterpret_cast<const float4*>(row + (size_t)k * slab + col);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
     }
     if (bias) {     // QKV projection bias (Qwen2), added before the rotation
       const float4 u = *reinterpret_cast<const float4*>(bias + col);
@@ -597,8 +626,11 @@ int nls_rmsnorm(const float* x, long ldx, const float* w, void* out, long ldo, i
 int nls_splitk_add_rmsnorm(const float* ws, int ks, int M, float alpha, float* x, long ldx, const float* w,
                            void* out, long ldo, int D, float eps, void* stream) {
   if (D % 4 || D > 8192 || ks < 1) return -1;
-  hipLaunchKernelGGL(splitk_add_rmsnorm_kernel, dim3(M), dim3(512), 0, (hipStream_t)stream, ws, ks, M, alpha, x, ldx,
-                     w, (act_t*)out, ldo, D, eps);
+  const int kc = NLS_SLAB_RUNTIME ? 0 : ks;
+  auto k = kc == 2 ? splitk_add_rmsnorm_kernel<2> : kc == 3 ? splitk_add_rmsnorm_kernel<3>
+         : kc == 4 ? splitk_add_rmsnorm_kernel<4> : kc == 1 ? splitk_add_rmsnorm_kernel<1> : splitk_add_rmsnorm_kernel<0>;
+  hipLaunchKernelGGL(k, dim3(M), dim3(512), 0, (hipStream_t)stream, ws, ks, M, alpha, x, ldx, w, (act_t*)out, ldo, D,
+                     eps);
   return (int)hipGetLastError();
 }
 
@@ -606,7 +638,10 @@ int nls_rope_kv(const float* qkv, long ldqkv, int ks, long slab, const float* bi
                 const float* cs, void* q_out, long ldq, void* kc, void* vc, int T, int Hq, int Hkv, int D, int neox,
                 void* stream) {
   if (ks < 1 || D % 8) return -1;
-  hipLaunchKernelGGL(rope_kv_kernel<__bf16>, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, bias, pos,
+  const int nk = NLS_SLAB_RUNTIME ? 0 : ks;
+  auto k = nk == 1 ? rope_kv_kernel<__bf16, 1> : nk == 2 ? rope_kv_kernel<__bf16, 2> : nk == 3 ? rope_kv_kernel<__bf16, 3>
+         : nk == 4 ? rope_kv_kernel<__bf16, 4> : rope_kv_kernel<__bf16, 0>;
+  hipLaunchKernelGGL(k, dim3(T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, ks, slab, bias, pos,
                      slot, cs, (__bf16*)q_out, ldq, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, D, neox);
   return (int)hipGetLastError();
 }
