@@ -23,7 +23,7 @@ def load(d):
             per = defaultdict(dict)
             for r in csv.DictReader(open(f)):
                 k = r["Kernel_Name"]
-                if not re.search(r"hgemm|hg10", k):
+                if not re.search(r"hgemm|hg10|qgemm9|q9", k):
                     continue
                 per[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
             for disp in per.values():
