@@ -452,6 +452,16 @@ __global__ __launch_bounds__(512) void moe_norm_route_kernel(
   for (int e = threadIdx.x; e < E; e += 512) counts[e] = 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   typedef act_t act4 __attribute__((ext_vector_type(4)));
+  // the router rows do not depend on x: issue their loads first, once for all tokens, so the HBM latency overlaps
+  // the x / norm-weight loads and the norm's block reduction instead of following them
+  act4 w4r[4][E];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = (threadIdx.x + j * 512) * 4;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      w4r[j][e] = i < D ? *reinterpret_cast<const act4*>(wr + (size_t)e * D + i) : act4{0, 0, 0, 0};
+  }
   for (int t = 0; t < T; ++t) {
     const float* xr = x + (size_t)t * ldx;
     float4 v[4], wv[4];
@@ -478,7 +488,7 @@ __global__ __launch_bounds__(512) void moe_norm_route_kernel(
         *reinterpret_cast<act4*>(h + (size_t)t * ldh + i) = r;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          const act4 w4 = *reinterpret_cast<const act4*>(wr + (size_t)e * D + i);
+          const act4 w4 = w4r[j][e];
           acc[e] += (float)r.x * (float)w4.x + (float)r.y * (float)w4.y + (float)r.z * (float)w4.z +
                     (float)r.w * (float)w4.w;
         }
