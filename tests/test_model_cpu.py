@@ -212,3 +212,29 @@ def test_dense_segment_merge():
     assert [x[1] for x in m] == [96, 32] and m[1][4].xmap is xm
     with pytest.raises(ValueError):
         ops._merge_dense([ops.Seg(NS(name="n", rows=8, K=K, d16=None), 0)])
+
+
+def test_tuning_extra_overrides(monkeypatch, tmp_path):
+    """A/B overrides on top of ops/gemv_tuning.json: NLS_TUNING_EXTRA_FILE (a tune_gemv.py --out table) applies first,
+    NLS_TUNING_EXTRA (inline JSON) over it; the table reloads with them and without them."""
+    import json
+    from nats_llm_studio_amd.ops import tuning
+    key = "d:6144:4096:512"
+    f = tmp_path / "extra.json"
+    f.write_text(json.dumps({key: [4, 8, 2, 3], "d:1:2:3": [-1]}))
+    monkeypatch.setattr(tuning, "_TABLE", None)
+    base = dict(tuning.table())
+    try:
+        monkeypatch.setattr(tuning, "_TABLE", None)
+        monkeypatch.setenv("NLS_TUNING_EXTRA_FILE", str(f))
+        t = tuning.table()
+        assert t[key] == (4, 8, 2, 3) and t["d:1:2:3"] == (-1,)
+        monkeypatch.setattr(tuning, "_TABLE", None)
+        monkeypatch.setenv("NLS_TUNING_EXTRA", json.dumps({key: [10, 8, 2, 1]}))
+        t = tuning.table()
+        assert t[key] == (10, 8, 2, 1) and t["d:1:2:3"] == (-1,)
+        assert {k: v for k, v in t.items() if k not in (key, "d:1:2:3")} == {k: v for k, v in base.items() if k != key}
+    finally:
+        monkeypatch.delenv("NLS_TUNING_EXTRA_FILE", raising=False)
+        monkeypatch.delenv("NLS_TUNING_EXTRA", raising=False)
+        monkeypatch.setattr(tuning, "_TABLE", None)
